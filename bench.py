@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 8-config ResNet-50 ImageNet-112 MOP, aggregate img/s.
+
+Workload = the reference's scalability experiment (BASELINE.md §1;
+``cerebro_gpdb/imagenetcat.py:62-67`` ``param_grid_scalability``): 8
+configurations lr{1e-3,1e-4,1e-5,1e-6} x lambda{1e-4,1e-6}, batch 32,
+ResNet-50 at 112x112x3, 1000 classes, Adam, trained by Model Hopper
+Parallelism over 8 data partitions on N GPUs (8/N partitions per GPU).
+
+A *step* = one training iteration of every active configuration on its own
+partition (8 x 32 = 256 images, whatever N is: total work is fixed, so
+scaling is "strong").  Every step is a full fwd + bwd + Adam update.  The
+timed region also contains the sub-epoch boundaries that fall inside it —
+validation (3.9 % of train images, the reference's 50 000 / 1 281 280 ratio)
+and the model hops over xGMI — every ``--steps_per_round`` steps, which is far
+more often than the 5 005-step sub-epochs of the real run (conservative).
+
+Data: synthetic ImageNet-shaped uint8 partitions generated in HBM; random-init
+weights (no datasets/checkpoints offline).
+
+value = (train images in the timed K steps, all GPUs) / max-over-ranks time.
+vs_baseline = value / DA-Cerebro's aggregate img/s at the same worker count
+(289 / 577 / 1002 / 1794 at 1 / 2 / 4 / 8).
+"""
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+BASELINE_IMG_S = {1: 289.0, 2: 577.0, 4: 1002.0, 8: 1794.0}
+TRAIN_IMAGES_PER_EPOCH = 1281280
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps_per_round", type=int, default=20)
+    ap.add_argument("--train_per_partition", type=int, default=8192)
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no_graphs", action="store_true")
+    ap.add_argument("--model", default="resnet50")
+    args = ap.parse_args()
+
+    import torch
+    from cerebro_ds_kpgi_amd.ops import set_backend
+    from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    from cerebro_ds_kpgi_amd.selection import get_msts
+    from cerebro_ds_kpgi_amd.config import catalog as cat
+
+    ctx = init_distributed()
+    N = ctx.world
+    backend = set_backend(args.backend)
+    grid = dict(cat.param_grid_scalability)
+    grid["model"] = [args.model]
+    msts = get_msts(grid)
+    S = len(msts)
+    B = msts[0]["batch_size"]
+    n_train = max(args.train_per_partition, B * args.steps_per_round)
+    n_valid = max(B, int(round(n_train * cat.IMAGENET_VALID_TOTAL / cat.IMAGENET_TRAIN_TOTAL)))
+    opts = EngineOptions(slots_per_gpu=max(1, S // N), scheduler="rotation", n_train=n_train,
+                         n_valid=n_valid, compute_dtype=args.dtype, use_graphs=not args.no_graphs,
+                         verbose=False, ckpt_every="none")
+    eng = MOPEngine(msts, ctx, opts)
+    sync = (torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None))
+
+    # warm-up (includes HIP-graph capture), untimed
+    if args.warmup > 0:
+        eng.run_steps(args.warmup, args.steps_per_round)
+    sync()
+    ctx.barrier()
+    sync()
+    img0 = eng.train_images
+    t0 = time.time()
+    eng.run_steps(args.steps, args.steps_per_round, epoch_start=2)
+    sync()
+    ctx.barrier()
+    sync()
+    dt = time.time() - t0
+    dt_max = ctx.allreduce_max(dt)
+    imgs = sum(ctx.all_gather_object(eng.train_images - img0))
+    value = imgs / dt_max
+    if ctx.rank == 0:
+        base = BASELINE_IMG_S.get(N)
+        out = {
+            "metric": "agg_train_images_per_sec_8cfg_resnet50_mop",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": N,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": args.dtype,
+            "data": "synthetic",
+            "config": {"model": args.model, "global_batch": S * B, "seq_len": None,
+                       "parallelism": "mop{}x{}".format(N, max(1, S // N)),
+                       "configs": S, "batch_per_config": B, "input": "112x112x3",
+                       "partitions": eng.P},
+            "projected_makespan_s": round(S * TRAIN_IMAGES_PER_EPOCH / value, 1),
+            "baseline_makespan_s": {1: 35440, 2: 17754, 4: 10229, 8: 5715}.get(N),
+            "backend": backend,
+            "hop_bytes_rank0": eng.hop_bytes,
+        }
+        print(json.dumps(out))
+        sys.stdout.flush()
+    eng.close()
+    shutdown(ctx)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,83 @@
+"""Minimal packed-model building blocks.
+
+A ``PackedNet`` declares its per-configuration parameters (``ParamSpec``) at
+construction, is ``bind``-ed to an ``Arena`` holding G configurations, and
+runs forward on packed NHWC activations ``[B, H, W, G*C]`` through
+``ops.nn``.  Autograd drives backward; the ops write weight gradients
+straight into the arena.
+"""
+
+import torch
+
+from ..ops import nn as P
+from ..runtime.arena import ModelLayout, ParamRef, ParamSpec
+
+
+class Conv(object):
+    def __init__(self, net, name, cin, cout, k, stride=1, pad=0):
+        self.cin, self.cout, self.k, self.stride, self.pad = cin, cout, k, stride, pad
+        self.w = net.spec(ParamSpec(name + "/kernel", (cout, k, k, cin), "weight",
+                                    fan_in=k * k * cin))
+
+    def out_hw(self, h):
+        return (h + 2 * self.pad - self.k) // self.stride + 1
+
+
+class BN(object):
+    def __init__(self, net, name, c):
+        self.g = net.spec(ParamSpec(name + "/gamma", (c,), "gamma"))
+        self.b = net.spec(ParamSpec(name + "/beta", (c,), "beta"))
+        self.rm = net.spec(ParamSpec(name + "/moving_mean", (c,), "running_mean"))
+        self.rv = net.spec(ParamSpec(name + "/moving_variance", (c,), "running_var"))
+
+
+class Dense(object):
+    def __init__(self, net, name, cin, cout, init="glorot"):
+        self.w = net.spec(ParamSpec(name + "/kernel", (cout, cin), "weight", init=init, fan_in=cin))
+        self.b = net.spec(ParamSpec(name + "/bias", (cout,), "bias"))
+
+
+class PackedNet(object):
+    input_kind = "image"      # image | sparse
+    num_classes = 1000
+    input_hw = 112
+    input_c = 3
+
+    def __init__(self):
+        self._specs = []
+        self.arena = None
+        self.bn_momentum = 0.1
+        self.bn_eps = 1e-5
+
+    def spec(self, s):
+        self._specs.append(s)
+        return s
+
+    def build_layout(self):
+        self.layout = ModelLayout(self._specs)
+        return self.layout
+
+    def bind(self, arena):
+        self.arena = arena
+        self.anchor = torch.zeros((), device=arena.device, requires_grad=True)
+
+    @property
+    def G(self):
+        return self.arena.G
+
+    def ref(self, spec):
+        return ParamRef(self.arena, spec)
+
+    # helpers used by architectures
+    def conv(self, x, c, anchor=False):
+        return P.conv2d(x, self.ref(c.w), c.stride, c.pad, self.anchor if anchor else None)
+
+    def bn(self, x, b, training, relu=True, residual=None):
+        return P.bn_act(x, self.ref(b.g), self.ref(b.b), self.ref(b.rm), self.ref(b.rv),
+                        training, relu, residual, self.bn_momentum, self.bn_eps)
+
+    def dense(self, x, d, relu=False, anchor=False):
+        return P.linear(x, self.ref(d.w), self.ref(d.b), relu, self.anchor if anchor else None)
+
+    def forward(self, x, training):
+        raise NotImplementedError

@@ -1,0 +1,50 @@
+"""MST -> model factory (reference ``create_model_from_mst``,
+``cerebro_gpdb/in_rdbms_helper.py:286-426``; ``TorchTrainer.model_fac``,
+``cerebro_gpdb/run_pytorchddp.py:295-309``).
+
+Configurations that share an architecture *and* a batch size can be packed
+into one horizontally-fused model on a GPU (``pack_key``).
+
+The reference's ``"inceptionresnetv2"`` name silently builds VGG19
+(``in_rdbms_helper.py:314-321``); that quirk is not reproduced.
+"""
+
+from .mlp import PackedConfA, PackedSanity
+from .resnet import PackedResNet
+from .small import PackedMobileNetV2, PackedTinyCNN
+from .vgg import PackedVGG16
+
+MODEL_FACTORIES = {
+    "resnet18": lambda: PackedResNet(18),
+    "resnet34": lambda: PackedResNet(34),
+    "resnet50": lambda: PackedResNet(50),
+    "resnet101": lambda: PackedResNet(101),
+    "resnet152": lambda: PackedResNet(152),
+    "vgg16": lambda: PackedVGG16(),
+    "mobilenetv2": lambda: PackedMobileNetV2(),
+    "confA": lambda: PackedConfA(),
+    "sanity": lambda: PackedSanity(),
+    "tinycnn": lambda: PackedTinyCNN(),
+}
+
+
+def create_model_from_mst(mst):
+    name = mst["model"]
+    if name not in MODEL_FACTORIES:
+        raise ValueError("model {} is not available (have: {})".format(
+            name, sorted(MODEL_FACTORIES)))
+    return MODEL_FACTORIES[name]()
+
+
+def pack_key(mst):
+    return (mst["model"], int(mst["batch_size"]))
+
+
+def dataset_of(model_name):
+    if model_name == "confA":
+        return "criteo"
+    if model_name == "sanity":
+        return "sanity"
+    if model_name == "tinycnn":
+        return "tiny"
+    return "imagenet"

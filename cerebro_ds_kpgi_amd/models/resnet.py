@@ -1,0 +1,89 @@
+"""ResNet-18/34/50/101/152 for ImageNet-112, packed over G configurations.
+
+Architecture = ``keras.applications`` ResNet50 as used by the reference
+(``cerebro_gpdb/resnet50tfk_default.py:161-314``; conv table SURVEY.md §2.8
+K1): ZeroPad(3) -> conv7x7/2 valid -> BN -> ReLU -> ZeroPad(1) ->
+MaxPool3x3/2 valid, bottleneck stages [3, 4, 6, 3] with the stride on the
+block's first 1x1 conv and a 1x1 projection shortcut in each stage's first
+block, global average pool, Dense(1000).  At 112x112 the stage resolutions
+are 28 / 14 / 7 / 4.
+
+Differences (documented, deliberate): convolutions carry no bias — a bias
+followed by BatchNorm is exactly cancelled by the batch-mean subtraction and
+its gradient is identically zero; BN momentum/eps follow the reference's
+PyTorch trainer (0.1 / 1e-5).  Trainable parameters: 25 557 032 (= the
+torchvision count); Keras reports 25 583 592 trainable + 53 120 moving
+statistics = 25 636 712, the difference being the 26 560 conv biases.
+
+ResNet-18/34 (hyperopt grid, ``cerebro_gpdb/imagenetcat.py:100-105``) use
+basic blocks with the same stem; 101/152 bottleneck depths [3,4,23,3] /
+[3,8,36,3] (model-size drill-down).
+"""
+
+from .common import BN, Conv, Dense, PackedNet
+from ..ops import nn as P
+
+_BOTTLENECK = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
+_BASIC = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}
+
+
+class PackedResNet(PackedNet):
+    def __init__(self, depth=50, num_classes=1000, input_hw=112):
+        super(PackedResNet, self).__init__()
+        self.depth = depth
+        self.num_classes = num_classes
+        self.input_hw = input_hw
+        self.bottleneck = depth in _BOTTLENECK
+        # stem: ZeroPad(3) + conv7x7/2 valid == conv7x7/2 pad 3
+        self.conv1 = Conv(self, "conv1", 3, 64, 7, 2, 3)
+        self.bn1 = BN(self, "bn_conv1", 64)
+        self.blocks = []
+        cin = 64
+        stages = _BOTTLENECK[depth] if self.bottleneck else _BASIC[depth]
+        widths = [64, 128, 256, 512]
+        for si, (n, w) in enumerate(zip(stages, widths)):
+            for bi in range(n):
+                stride = 2 if (si > 0 and bi == 0) else 1
+                name = "res{}{}".format(si + 2, chr(ord("a") + bi) if bi < 26 else "z{}".format(bi))
+                blk = {}
+                if self.bottleneck:
+                    cout = 4 * w
+                    blk["c1"] = Conv(self, name + "_branch2a", cin, w, 1, stride, 0)
+                    blk["b1"] = BN(self, name.replace("res", "bn") + "_branch2a", w)
+                    blk["c2"] = Conv(self, name + "_branch2b", w, w, 3, 1, 1)
+                    blk["b2"] = BN(self, name.replace("res", "bn") + "_branch2b", w)
+                    blk["c3"] = Conv(self, name + "_branch2c", w, cout, 1, 1, 0)
+                    blk["b3"] = BN(self, name.replace("res", "bn") + "_branch2c", cout)
+                else:
+                    cout = w
+                    blk["c1"] = Conv(self, name + "_branch2a", cin, w, 3, stride, 1)
+                    blk["b1"] = BN(self, name.replace("res", "bn") + "_branch2a", w)
+                    blk["c2"] = Conv(self, name + "_branch2b", w, w, 3, 1, 1)
+                    blk["b2"] = BN(self, name.replace("res", "bn") + "_branch2b", w)
+                if bi == 0 and (stride != 1 or cin != cout):
+                    blk["cs"] = Conv(self, name + "_branch1", cin, cout, 1, stride, 0)
+                    blk["bs"] = BN(self, name.replace("res", "bn") + "_branch1", cout)
+                self.blocks.append(blk)
+                cin = cout
+        self.feat = cin
+        self.fc = Dense(self, "fc1000", cin, num_classes)
+        self.build_layout()
+
+    def forward(self, x, training):
+        x = self.conv(x, self.conv1, anchor=True)
+        x = self.bn(x, self.bn1, training)
+        x = P.maxpool2d(x, 3, 2, 1)  # ZeroPad(1) + MaxPool 3x3/2 valid (inputs >= 0 post-ReLU)
+        for blk in self.blocks:
+            if "cs" in blk:
+                sc = self.bn(self.conv(x, blk["cs"]), blk["bs"], training, relu=False)
+            else:
+                sc = x
+            h = self.bn(self.conv(x, blk["c1"]), blk["b1"], training)
+            if self.bottleneck:
+                h = self.bn(self.conv(h, blk["c2"]), blk["b2"], training)
+                h = self.bn(self.conv(h, blk["c3"]), blk["b3"], training, relu=True, residual=sc)
+            else:
+                h = self.bn(self.conv(h, blk["c2"]), blk["b2"], training, relu=True, residual=sc)
+            x = h
+        x = P.global_avgpool(x)
+        return self.dense(x, self.fc)

@@ -1,0 +1,51 @@
+"""Kernel backend selection.
+
+``hip``   — our hand-written CDNA4 kernels (``csrc/hip``, loaded by
+            ``ops._hip``); the production path on MI355X.
+``torch`` — plain PyTorch implementations of the same ops; the numerical
+            oracle in tests and the path on CPU (gloo plumbing tests).
+
+``auto`` picks ``hip`` when a GPU is present.  If ``hip`` is requested on a
+GPU and the extension cannot be loaded, it fails loudly: there is no silent
+fallback on a GPU box.  Individual ops can be forced to the oracle with
+``CEREBRO_TORCH_OPS=conv,bn,...`` (used by A/B tests and bring-up).
+"""
+
+import os
+
+import torch
+
+_STATE = {"backend": None}
+_FORCED_TORCH = set(filter(None, os.environ.get("CEREBRO_TORCH_OPS", "").split(",")))
+
+
+def set_backend(name):
+    if name == "auto":
+        name = "hip" if torch.cuda.is_available() else "torch"
+    if name not in ("hip", "torch"):
+        raise ValueError(name)
+    if name == "hip":
+        from . import _hip
+        _hip.lib()  # raises if the extension is missing / broken
+    _STATE["backend"] = name
+    return name
+
+
+def get_backend():
+    if _STATE["backend"] is None:
+        set_backend(os.environ.get("CEREBRO_BACKEND", "auto"))
+    return _STATE["backend"]
+
+
+def use_hip(op, *tensors):
+    if get_backend() != "hip" or op in _FORCED_TORCH:
+        return False
+    from . import _hip
+    if op not in _hip.IMPLEMENTED:
+        return False
+    return all(t.is_cuda for t in tensors if isinstance(t, torch.Tensor))
+
+
+def force_torch_ops(ops):
+    _FORCED_TORCH.clear()
+    _FORCED_TORCH.update(ops)

@@ -1,0 +1,426 @@
+"""Packed (horizontally fused) training ops.
+
+Activation layout is **packed NHWC**: ``[B, H, W, G*C]`` — channel block
+``g`` belongs to configuration ``g`` of the G configurations trained
+together on this GPU.  With that layout
+
+* BatchNorm / ReLU / residual add / pooling over G*C channels are exactly the
+  per-config ops (channels are independent), so they need no group logic,
+* convolutions and linears are *grouped*: config g's weights only see
+  channel block g.
+
+Weights live in the arena (``runtime.arena``), addressed through
+``ParamRef``; backward passes write weight gradients straight into the fp32
+gradient arena instead of returning them to autograd.
+
+Each op dispatches to our HIP kernel (``ops._hip``) or to the PyTorch oracle
+implementation in this file (``ops.backend``).
+"""
+
+import torch
+import torch.nn.functional as F
+
+from .backend import use_hip
+
+
+def _hip():
+    from . import _hip as h
+    return h
+
+
+def _act(z, code):
+    """Activation codes: False/0 = identity, True/1 = ReLU, 6 = ReLU6."""
+    if code == 6:
+        return torch.clamp(z, 0.0, 6.0)
+    if code:
+        return torch.relu(z)
+    return z
+
+
+def _act_grad(dz, y, code):
+    if code == 6:
+        return dz * ((y > 0) & (y < 6))
+    if code:
+        return dz * (y > 0)
+    return dz
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# convolution
+# ---------------------------------------------------------------------------
+
+def _torch_weight(wref):
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    return wref.work().permute(0, 1, 4, 2, 3).reshape(G * cout, cin, kh, kw)
+
+
+class PackedConv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, wref, stride, pad):
+        ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        if use_hip("conv", x):
+            y = _hip().conv2d_fwd(x, wref, stride, pad)
+        else:
+            w = _torch_weight(wref)
+            y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
+        dy = dy.contiguous()
+        dx = None
+        if use_hip("conv", x):
+            h = _hip()
+            if ctx.needs_input_grad[0]:
+                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad)
+            h.conv2d_wgrad(x, dy, wref, stride, pad)
+        else:
+            G = wref.G
+            cout, kh, kw, cin = wref.spec.shape
+            w = _torch_weight(wref)
+            xn, dyn = _nchw(x), _nchw(dy)
+            if ctx.needs_input_grad[0]:
+                dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, G))
+            dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, G)
+            wref.grad().copy_(dw.view(G, cout, cin, kh, kw).permute(0, 1, 3, 4, 2))
+        return dx, None, None, None, None
+
+
+def conv2d(x, wref, stride=1, pad=0, anchor=None):
+    return PackedConv2d.apply(x, anchor, wref, stride, pad)
+
+
+# ---------------------------------------------------------------------------
+# batch norm (+ residual add) (+ ReLU)
+# ---------------------------------------------------------------------------
+
+def _flat_param(ref):
+    return ref.work().reshape(-1).float() if ref.spec.kind in ("gamma", "beta") else ref.master().reshape(-1)
+
+
+class PackedBNAct(torch.autograd.Function):
+    """y = act(BN(x) + residual);  BN statistics per packed channel."""
+
+    @staticmethod
+    def forward(ctx, x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
+        C = x.shape[-1]
+        ctx.refs = (gref, bref)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        if use_hip("bn", x):
+            y, mean, invstd = _hip().bn_act_fwd_train(x, residual, gref, bref, rmref, rvref,
+                                                      relu, momentum, eps)
+        else:
+            x2 = x.reshape(-1, C).float()
+            n = x2.shape[0]
+            mean = x2.mean(0)
+            var = x2.var(0, unbiased=False)
+            invstd = torch.rsqrt(var + eps)
+            with torch.no_grad():
+                rm, rv = rmref.master(), rvref.master()
+                rm.mul_(1 - momentum).add_(mean.view(rm.shape), alpha=momentum)
+                rv.mul_(1 - momentum).add_((var * n / max(n - 1, 1)).view(rv.shape), alpha=momentum)
+            gamma = gref.work().reshape(-1).float()
+            beta = bref.work().reshape(-1).float()
+            z = (x2 - mean) * (invstd * gamma) + beta
+            if residual is not None:
+                z = z + residual.reshape(-1, C).float()
+            z = _act(z, relu)
+            y = z.to(x.dtype).view(x.shape)
+        ctx.save_for_backward(x, y, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd = ctx.saved_tensors
+        gref, bref = ctx.refs
+        dy = dy.contiguous()
+        if use_hip("bn", x):
+            dx, dres = _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res)
+        else:
+            C = x.shape[-1]
+            dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
+            n = dz.shape[0]
+            xhat = (x.reshape(-1, C).float() - mean) * invstd
+            dbeta = dz.sum(0)
+            dgamma = (dz * xhat).sum(0)
+            gamma = gref.work().reshape(-1).float()
+            dx = (gamma * invstd / n) * (n * dz - dbeta - xhat * dgamma)
+            dx = dx.to(x.dtype).view(x.shape)
+            gref.grad().copy_(dgamma.view(gref.grad().shape))
+            bref.grad().copy_(dbeta.view(bref.grad().shape))
+            dres = dz.to(x.dtype).view(x.shape) if ctx.has_res else None
+        return dx, dres, None, None, None, None, None, None, None
+
+
+def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):
+    C = x.shape[-1]
+    if use_hip("bn", x):
+        return _hip().bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, relu, eps)
+    rm = rmref.master().reshape(-1)
+    rv = rvref.master().reshape(-1)
+    scale = gref.work().reshape(-1).float() * torch.rsqrt(rv + eps)
+    shift = bref.work().reshape(-1).float() - rm * scale
+    z = x.reshape(-1, C).float() * scale + shift
+    if residual is not None:
+        z = z + residual.reshape(-1, C).float()
+    return _act(z, relu).to(x.dtype).view(x.shape)
+
+
+def bn_act(x, gref, bref, rmref, rvref, training, relu=True, residual=None,
+           momentum=0.1, eps=1e-5):
+    if training:
+        return PackedBNAct.apply(x, residual, gref, bref, rmref, rvref, relu, momentum, eps)
+    return bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps)
+
+
+# ---------------------------------------------------------------------------
+# bias + activation (conv nets without BN, e.g. VGG)
+# ---------------------------------------------------------------------------
+
+class PackedBiasAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bref, relu):
+        C = x.shape[-1]
+        ctx.bref, ctx.relu = bref, relu
+        if use_hip("bias", x):
+            y = _hip().bias_act_fwd(x, bref, relu)
+        else:
+            z = x.reshape(-1, C).float() + bref.work().reshape(-1).float()
+            if relu:
+                z = torch.relu(z)
+            y = z.to(x.dtype).view(x.shape)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, = ctx.saved_tensors
+        bref = ctx.bref
+        dy = dy.contiguous()
+        if use_hip("bias", y):
+            dx = _hip().bias_act_bwd(dy, y, bref, ctx.relu)
+        else:
+            C = y.shape[-1]
+            dz = dy.reshape(-1, C).float()
+            if ctx.relu:
+                dz = dz * (y.reshape(-1, C) > 0)
+            bref.grad().copy_(dz.sum(0).view(bref.grad().shape))
+            dx = dz.to(dy.dtype).view(dy.shape)
+        return dx, None, None
+
+
+def bias_act(x, bref, relu=True):
+    return PackedBiasAct.apply(x, bref, relu)
+
+
+# ---------------------------------------------------------------------------
+# pooling
+# ---------------------------------------------------------------------------
+
+class MaxPoolHip(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, idx = _hip().maxpool_fwd(x, k, s, p)
+        ctx.save_for_backward(idx)
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, = ctx.saved_tensors
+        return _hip().maxpool_bwd(dy.contiguous(), idx, ctx.xshape), None, None, None
+
+
+def maxpool2d(x, k, s, p=0):
+    if use_hip("pool", x):
+        return MaxPoolHip.apply(x, k, s, p)
+    return _nhwc(F.max_pool2d(_nchw(x), k, s, p))
+
+
+class AvgPoolHip(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.xshape = x.shape
+        return _hip().gavgpool_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _hip().gavgpool_bwd(dy.contiguous(), ctx.xshape)
+
+
+def global_avgpool(x):
+    """[B, H, W, C] -> [B, C]."""
+    if use_hip("pool", x):
+        return AvgPoolHip.apply(x)
+    return x.float().mean(dim=(1, 2)).to(x.dtype)
+
+
+# ---------------------------------------------------------------------------
+# grouped linear (+bias) (+relu)
+# ---------------------------------------------------------------------------
+
+class PackedLinear(torch.autograd.Function):
+    """x [B, G*K] -> y [B, G*N];  config g: y_g = act(x_g W_g^T + b_g)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, wref, bref, relu):
+        ctx.wref, ctx.bref, ctx.relu = wref, bref, relu
+        G = wref.G
+        N, K = wref.spec.shape
+        B = x.shape[0]
+        if use_hip("linear", x):
+            y = _hip().linear_fwd(x, wref, bref, relu)
+        else:
+            xg = x.view(B, G, K).transpose(0, 1)                       # [G, B, K]
+            w = wref.work()                                             # [G, N, K]
+            z = torch.bmm(xg.float(), w.float().transpose(1, 2))        # [G, B, N]
+            if bref is not None:
+                z = z + bref.work().float().unsqueeze(1)
+            if relu:
+                z = torch.relu(z)
+            y = z.transpose(0, 1).reshape(B, G * N).to(x.dtype)
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        wref, bref, relu = ctx.wref, ctx.bref, ctx.relu
+        dy = dy.contiguous()
+        if use_hip("linear", x):
+            dx = _hip().linear_bwd(dy, x, y, wref, bref, relu, ctx.needs_input_grad[0])
+            return dx, None, None, None, None
+        G = wref.G
+        N, K = wref.spec.shape
+        B = x.shape[0]
+        dz = dy.view(B, G, N).float()
+        if relu:
+            dz = dz * (y.view(B, G, N) > 0)
+        dzg = dz.transpose(0, 1)                                        # [G, B, N]
+        xg = x.view(B, G, K).transpose(0, 1).float()                    # [G, B, K]
+        wref.grad().copy_(torch.bmm(dzg.transpose(1, 2), xg))           # [G, N, K]
+        if bref is not None:
+            bref.grad().copy_(dzg.sum(1))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.bmm(dzg, wref.work().float())                    # [G, B, K]
+            dx = dx.transpose(0, 1).reshape(B, G * K).to(x.dtype)
+        return dx, None, None, None, None
+
+
+def linear(x, wref, bref=None, relu=False, anchor=None):
+    return PackedLinear.apply(x, anchor, wref, bref, relu)
+
+
+# ---------------------------------------------------------------------------
+# sparse-input first layer (Criteo confA): embedding-bag over one-hot indices
+# ---------------------------------------------------------------------------
+
+class PackedEmbeddingBag(torch.autograd.Function):
+    """One-hot input with ``nnz`` active columns per row == sum of W columns.
+
+    idx [G, B, nnz] int32 (column ids into the K-wide input), W_g [N, K]:
+    y[b, g*N:(g+1)*N] = act(sum_j W_g[idx[g,b,j], :] + b_g).
+    Weight layout is [K, N] (input-major), which is the Keras ``Dense``
+    kernel layout, so the flat checkpoint blob matches a Dense(7306 -> N)
+    layer and each active input column is one contiguous N-row to gather.
+    """
+
+    @staticmethod
+    def forward(ctx, idx, anchor, wref, bref, relu):
+        ctx.wref, ctx.bref, ctx.relu = wref, bref, relu
+        G = wref.G
+        K, N = wref.spec.shape
+        Gi, B, nnz = idx.shape
+        if use_hip("embbag", idx):
+            y = _hip().embbag_fwd(idx, wref, bref, relu)
+        else:
+            w = wref.work().float()                                     # [G, K, N]
+            rows = torch.stack([w[g][idx[g].long()] for g in range(G)])  # [G, B, nnz, N]
+            z = rows.sum(2) + bref.work().float().unsqueeze(1)
+            if relu:
+                z = torch.relu(z)
+            y = z.transpose(0, 1).reshape(B, G * N).to(wref.arena.compute_dtype)
+        ctx.save_for_backward(idx, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        idx, y = ctx.saved_tensors
+        wref, bref, relu = ctx.wref, ctx.bref, ctx.relu
+        dy = dy.contiguous()
+        if use_hip("embbag", idx):
+            _hip().embbag_bwd(dy, idx, y, wref, bref, relu)
+            return None, None, None, None, None
+        G = wref.G
+        K, N = wref.spec.shape
+        B = dy.shape[0]
+        dz = dy.view(B, G, N).float()
+        if relu:
+            dz = dz * (y.view(B, G, N) > 0)
+        dzg = dz.transpose(0, 1)                                        # [G, B, N]
+        gw = wref.grad()
+        gw.zero_()
+        for g in range(G):
+            flat = idx[g].long().reshape(-1)
+            gw[g].index_add_(0, flat, dzg[g].repeat_interleave(idx.shape[2], 0))
+        bref.grad().copy_(dzg.sum(1))
+        return None, None, None, None, None
+
+
+def embedding_bag(idx, wref, bref, relu=True, anchor=None):
+    return PackedEmbeddingBag.apply(idx, anchor, wref, bref, relu)
+
+
+# ---------------------------------------------------------------------------
+# depthwise conv (MobileNetV2) — packed channels, one filter per channel
+# ---------------------------------------------------------------------------
+
+class PackedDWConv2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, wref, stride, pad):
+        ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        if use_hip("dwconv", x):
+            y = _hip().dwconv_fwd(x, wref, stride, pad)
+        else:
+            C, kh, kw = wref.spec.shape
+            w = wref.work().reshape(wref.G * C, 1, kh, kw)
+            y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * C))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
+        dy = dy.contiguous()
+        if use_hip("dwconv", x):
+            dx = _hip().dwconv_bwd(dy, x, wref, stride, pad, ctx.needs_input_grad[0])
+            return dx, None, None, None, None
+        C, kh, kw = wref.spec.shape
+        GC = wref.G * C
+        w = wref.work().reshape(GC, 1, kh, kw)
+        xn, dyn = _nchw(x), _nchw(dy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, GC))
+        dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, GC)
+        wref.grad().copy_(dw.view(wref.G, C, kh, kw))
+        return dx, None, None, None, None
+
+
+def dwconv2d(x, wref, stride=1, pad=1, anchor=None):
+    return PackedDWConv2d.apply(x, anchor, wref, stride, pad)

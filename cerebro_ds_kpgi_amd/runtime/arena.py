@@ -1,0 +1,237 @@
+"""Flat per-configuration parameter arenas.
+
+One *model state row* holds everything a configuration owns, contiguously:
+
+    [ master fp32 params (trainable) | buffers fp32 (BN running stats) |
+      adam m | adam v | step + pad ]
+
+so a model hop is ONE contiguous buffer -> one RCCL send/recv, and a
+checkpoint is one copy.  A GPU that trains G packed configurations owns a
+``[G, R]`` fp32 state tensor plus:
+
+* ``work``  ``[G, n_train]`` compute-dtype shadow of the master params
+  (bf16 by default), refreshed by the fused optimizer kernel,
+* ``grad``  ``[G, n_train]`` fp32 gradients, written *directly* by the
+  weight-gradient kernels (no autograd AccumulateGrad pass),
+* ``lr``/``wd`` ``[G]`` per-config hyper-parameters on device.
+
+The weight blob order follows the model's layer order and is the same as the
+reference's ``serialize_nd_weights`` flat float32 concatenation
+(``cerebro_gpdb/madlib_keras_wrapper.py:119-131``) for the params of our
+architecture.
+"""
+
+import math
+
+import numpy as np
+import torch
+
+ALIGN = 64  # elements: every tensor starts 256-B aligned in fp32, 128-B in bf16
+
+
+class ParamSpec(object):
+    __slots__ = ("name", "shape", "kind", "init", "fan_in", "offset", "numel")
+
+    def __init__(self, name, shape, kind="weight", init="he", fan_in=None):
+        self.name = name
+        self.shape = tuple(int(s) for s in shape)
+        self.kind = kind          # weight | bias | gamma | beta | running_mean | running_var
+        self.init = init
+        self.fan_in = fan_in
+        self.numel = int(np.prod(self.shape))
+        self.offset = None
+
+    @property
+    def trainable(self):
+        return self.kind not in ("running_mean", "running_var")
+
+
+def _align(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+class ModelLayout(object):
+    """Ordered parameter specs of ONE configuration + their arena offsets."""
+
+    def __init__(self, specs):
+        self.train_specs = [s for s in specs if s.trainable]
+        self.buffer_specs = [s for s in specs if not s.trainable]
+        off = 0
+        for s in self.train_specs:
+            s.offset = off
+            off += _align(s.numel)
+        self.n_train = off
+        for s in self.buffer_specs:
+            s.offset = off
+            off += _align(s.numel)
+        self.n_master = off
+        self.by_name = {s.name: s for s in specs}
+        self.specs = list(specs)
+
+    @property
+    def num_params(self):
+        """Trainable parameter count (unpadded)."""
+        return sum(s.numel for s in self.train_specs)
+
+    def row_len(self, with_optimizer=True):
+        if not with_optimizer:
+            return self.n_master
+        return self.n_master + 2 * self.n_train + ALIGN
+
+    # offsets of the sections inside a state row
+    @property
+    def off_m(self):
+        return self.n_master
+
+    @property
+    def off_v(self):
+        return self.n_master + self.n_train
+
+    @property
+    def off_step(self):
+        return self.n_master + 2 * self.n_train
+
+
+def init_row(layout, master_row, seed):
+    """Deterministic per-config initialisation of one master row (fp32 tensor).
+
+    Drawn on the row's device so every rank produces the same initial weights
+    for the same seed without a host round trip.
+    """
+    dev = master_row.device
+    g = torch.Generator(device=dev if dev.type == "cuda" else "cpu")
+    g.manual_seed(int(seed))
+    master_row.zero_()
+    for s in layout.specs:
+        view = master_row[s.offset:s.offset + s.numel]
+        if s.kind in ("weight",):
+            fan_in = s.fan_in if s.fan_in else int(np.prod(s.shape[1:]))
+            if s.init == "he":
+                std = math.sqrt(2.0 / fan_in)
+            elif s.init == "glorot":
+                fan_out = s.shape[0]
+                std = math.sqrt(2.0 / (fan_in + fan_out))
+            else:
+                std = float(s.init)
+            view.normal_(0.0, std, generator=g)
+        elif s.kind in ("gamma", "running_var"):
+            view.fill_(1.0)
+        else:  # bias, beta, running_mean
+            view.fill_(0.0)
+
+
+class Arena(object):
+    """State of G packed configurations of one architecture on one device."""
+
+    def __init__(self, layout, G, device, compute_dtype=torch.bfloat16, trainable=True):
+        self.layout = layout
+        self.G = G
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        R = layout.row_len(True)
+        self.state = torch.zeros(G, R, dtype=torch.float32, device=self.device)
+        L = layout
+        self.master = self.state[:, :L.n_master]
+        self.params = self.state[:, :L.n_train]
+        self.m = self.state[:, L.off_m:L.off_m + L.n_train]
+        self.v = self.state[:, L.off_v:L.off_v + L.n_train]
+        self.step = self.state[:, L.off_step:L.off_step + 1]
+        # a "home" arena only parks states between rounds: no work/grad copies
+        if compute_dtype == torch.float32 or not trainable:
+            self.work = self.params
+        else:
+            self.work = torch.zeros(G, L.n_train, dtype=compute_dtype, device=self.device)
+        self.grad = (torch.zeros(G, L.n_train, dtype=torch.float32, device=self.device)
+                     if trainable else None)
+        self.lr = torch.zeros(G, dtype=torch.float32, device=self.device)
+        self.wd = torch.zeros(G, dtype=torch.float32, device=self.device)
+        self.model_ids = [None] * G
+
+    # ---- views -----------------------------------------------------------
+    def _view(self, base, spec):
+        return base[:, spec.offset:spec.offset + spec.numel].view(self.G, *spec.shape)
+
+    def work_view(self, spec):
+        return self._view(self.work, spec)
+
+    def master_view(self, spec):
+        return self._view(self.master, spec)
+
+    def grad_view(self, spec):
+        return self._view(self.grad, spec)
+
+    # ---- state management -------------------------------------------------
+    def init_model(self, row, seed):
+        init_row(self.layout, self.master[row], seed)
+        self.m[row].zero_()
+        self.v[row].zero_()
+        self.step[row].zero_()
+        self.sync_work(row)
+
+    def sync_work(self, row=None):
+        if self.work is self.params:
+            return
+        if row is None:
+            self.work.copy_(self.params)
+        else:
+            self.work[row].copy_(self.params[row])
+
+    def reset_optimizer(self, row=None):
+        sl = slice(None) if row is None else slice(row, row + 1)
+        self.m[sl].zero_()
+        self.v[sl].zero_()
+        self.step[sl].zero_()
+
+    def set_hparams(self, row, lr, wd):
+        self.lr[row] = float(lr)
+        self.wd[row] = float(wd)
+
+    def row_weights_f32(self, row):
+        """Unpadded flat float32 weight blob (serialize_nd_weights order)."""
+        parts = [self.master[row, s.offset:s.offset + s.numel] for s in self.layout.specs]
+        return torch.cat(parts).detach().cpu().numpy().astype(np.float32)
+
+    def load_row_weights_f32(self, row, blob):
+        blob = np.asarray(blob, dtype=np.float32)
+        off = 0
+        for s in self.layout.specs:
+            self.master[row, s.offset:s.offset + s.numel].copy_(
+                torch.from_numpy(blob[off:off + s.numel]).to(self.device))
+            off += s.numel
+        assert off == blob.size, "weight blob size mismatch: {} vs {}".format(off, blob.size)
+        self.sync_work(row)
+
+
+class ParamRef(object):
+    """Handle to one parameter of all G packed configs (passed to ops)."""
+    __slots__ = ("arena", "spec")
+
+    def __init__(self, arena, spec):
+        self.arena = arena
+        self.spec = spec
+
+    @property
+    def G(self):
+        return self.arena.G
+
+    def work(self):
+        return self.arena.work_view(self.spec)
+
+    def grad(self):
+        return self.arena.grad_view(self.spec)
+
+    def master(self):
+        return self.arena.master_view(self.spec)
+
+    # raw addressing for HIP kernels: base pointer + per-config stride (elements)
+    def work_ptr(self):
+        w = self.arena.work
+        return w.data_ptr() + self.spec.offset * w.element_size(), w.stride(0)
+
+    def grad_ptr(self):
+        g = self.arena.grad
+        return g.data_ptr() + self.spec.offset * g.element_size(), g.stride(0)
+
+    def master_ptr(self):
+        m = self.arena.master
+        return m.data_ptr() + self.spec.offset * m.element_size(), m.stride(0)

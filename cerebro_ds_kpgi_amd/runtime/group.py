@@ -1,0 +1,202 @@
+"""Pack groups: the per-GPU execution unit of the MOP runtime.
+
+All configurations with the same (architecture, batch size) form a pack
+group.  On every GPU a group owns
+
+* a *home* arena with one state row per member config (where a config's
+  state parks between rounds and from where it is shipped on a hop), and
+* a *working* arena holding the G configs that train on this GPU in the
+  current round, packed into ONE horizontally-fused model: every kernel
+  launch trains all G at once, each on its own data partition.
+
+A training step (gather -> forward -> fused loss -> backward -> fused Adam)
+has static shapes and device-side cursors, so after a few eager steps it is
+captured once in a HIP graph and replayed for the rest of the run.
+(Reference equivalents: the per-sub-epoch ``train_fn`` / ``fit_step_ctq``
+jobs, ``run_cerebro_standalone_helper.py:270-289``, ``ctq.py:110-121``.)
+"""
+
+import time
+
+import torch
+
+from ..data.store import gather_batch, input_buffers
+from ..models import create_model_from_mst
+from ..ops.loss import eval_metrics, softmax_ce
+from ..ops.optim import adam_step
+from .arena import Arena
+
+
+class PackGroup(object):
+    def __init__(self, key, model_ids, msts, store, device, compute_dtype, seed_base,
+                 use_graphs=True, l2=True, warmup_eager=3, init=True):
+        self.key = key
+        self.arch, self.batch_size = key
+        self.model_ids = list(model_ids)
+        self.home_row = {m: i for i, m in enumerate(self.model_ids)}
+        self.msts = msts
+        self.store = store
+        self.device = torch.device(device)
+        self.dtype = compute_dtype
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self.l2 = l2
+        self.warmup_eager = warmup_eager
+        proto = create_model_from_mst({"model": self.arch})
+        self.layout = proto.layout
+        self.home = Arena(self.layout, len(self.model_ids), device, compute_dtype, trainable=False)
+        if init:
+            for m in self.model_ids:
+                self.home.init_model(self.home_row[m], seed_base + m)
+        self._work = {}   # G -> _Working
+        self.current = None
+
+    def add_models(self, model_ids, seed):
+        """Grow the home arena for configs proposed mid-run (hyperopt)."""
+        new = [m for m in model_ids if m not in self.home_row]
+        if not new:
+            return
+        old = self.home
+        self.model_ids.extend(new)
+        self.home_row = {m: i for i, m in enumerate(self.model_ids)}
+        self.home = Arena(self.layout, len(self.model_ids), self.device, self.dtype,
+                          trainable=False)
+        self.home.state[:old.G].copy_(old.state)
+        for m in new:
+            self.home.init_model(self.home_row[m], seed * 100 + m)
+        del old
+
+    # ------------------------------------------------------------------
+    def state_row(self, m):
+        return self.home.state[self.home_row[m]]
+
+    def working(self, G):
+        w = self._work.get(G)
+        if w is None:
+            w = _Working(self, G)
+            self._work[G] = w
+        return w
+
+    def begin_round(self, jobs, recv_into=None):
+        """jobs: list of (model_id, local_partition_index).  Returns the
+        working set; rows whose state arrives by a hop are filled by the
+        caller through ``recv_buffer``."""
+        G = len(jobs)
+        w = self.working(G)
+        w.assign(jobs)
+        self.current = w
+        return w
+
+    def end_round(self, hop_optimizer_state=True):
+        """Park the trained states back in the home arena."""
+        w = self.current
+        for row, (m, _) in enumerate(w.jobs):
+            self.home.state[self.home_row[m]].copy_(w.arena.state[row])
+        self.current = None
+
+
+class _Working(object):
+    def __init__(self, group, G):
+        self.group = group
+        self.G = G
+        g = group
+        self.arena = Arena(g.layout, G, g.device, g.dtype, trainable=True)
+        self.net = create_model_from_mst({"model": g.arch})
+        self.net.bind(self.arena)
+        B = g.batch_size
+        self.x, self.y = input_buffers(g.store, G, B, g.dtype)
+        self.part_of_row = torch.zeros(G, dtype=torch.int32, device=g.device)
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=g.device)
+        self.acc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
+        self.vx, self.vy = input_buffers(g.store, G, B, g.dtype)
+        self.vcursor = torch.zeros(1, dtype=torch.int32, device=g.device)
+        self.vacc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
+        self.graph = None
+        self.eager_steps = 0
+        self.jobs = []
+
+    def assign(self, jobs):
+        self.jobs = list(jobs)
+        parts = torch.tensor([p for _, p in jobs], dtype=torch.int32)
+        self.part_of_row.copy_(parts)
+        for row, (m, _) in enumerate(jobs):
+            mst = self.group.msts[m]
+            self.arena.set_hparams(row, mst["learning_rate"], mst["lambda_value"])
+
+    def recv_buffer(self, row, with_optimizer=True):
+        st = self.arena.state[row]
+        return st if with_optimizer else st[:self.group.layout.n_master]
+
+    def load_local(self, row, m):
+        self.arena.state[row].copy_(self.group.state_row(m))
+
+    def prepare(self, hop_optimizer_state):
+        if not hop_optimizer_state:
+            self.arena.reset_optimizer()
+        self.arena.sync_work()
+        self.cursor.zero_()
+        self.acc.zero_()
+        self.vacc.zero_()
+
+    # ------------------------------------------------------------------
+    def _step(self):
+        g = self.group
+        gather_batch(g.store, True, self.part_of_row, self.cursor, g.batch_size, self.x, self.y)
+        logits = self.net.forward(self.x, True)
+        loss = softmax_ce(logits, self.y, self.acc, self.G)
+        loss.sum().backward()
+        adam_step(self.arena, l2=g.l2)
+        self.cursor.add_(1)
+
+    def train_steps(self, nsteps):
+        done = 0
+        if not self.group.use_graphs:
+            for _ in range(nsteps):
+                self._step()
+            return nsteps
+        if self.graph is None:
+            # eager warm-up on a side stream (real steps), then capture once
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                while self.eager_steps < self.group.warmup_eager and done < nsteps:
+                    self._step()
+                    self.eager_steps += 1
+                    done += 1
+            torch.cuda.current_stream().wait_stream(s)
+            if done >= nsteps:
+                return done
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._step()
+        while done < nsteps:
+            self.graph.replay()
+            done += 1
+        return done
+
+    def validate(self, nsteps):
+        g = self.group
+        self.vcursor.zero_()
+        with torch.no_grad():
+            for _ in range(nsteps):
+                gather_batch(g.store, False, self.part_of_row, self.vcursor, g.batch_size,
+                             self.vx, self.vy)
+                logits = self.net.forward(self.vx, False)
+                eval_metrics(logits, self.vy, self.vacc, self.G)
+                self.vcursor.add_(1)
+
+    def read_metrics(self):
+        """(train, valid) per row: dict(loss, top1, top5, n) — one host sync."""
+        both = torch.stack([self.acc, self.vacc]).cpu()
+        out = []
+        for row in range(self.G):
+            rec = {}
+            for name, a in (("train", both[0, row]), ("valid", both[1, row])):
+                n = max(float(a[3]), 1.0)
+                rec[name] = {"loss": float(a[0]) / n, "top1": float(a[1]) / n,
+                             "top5": float(a[2]) / n, "n": int(a[3])}
+            out.append(rec)
+        return out
+
+
+def now():
+    return time.time()

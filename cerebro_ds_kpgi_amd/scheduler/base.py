@@ -1,0 +1,121 @@
+"""MOP scheduling core: (model, worker) visit bookkeeping + invariants.
+
+Model Hopper Parallelism: data partitions ("workers" here are
+*virtual workers* = one data partition each) never move; S configurations
+hop between them.  A *sub-epoch* is one (model, worker) visit; an *epoch* is
+complete when every model has visited every worker once.  Invariants that
+every policy must hold (reference ``cerebro_gpdb/ctq.py:448-508``):
+
+1. each (model, worker) pair is trained exactly once per epoch,
+2. a model is on at most one worker at a time,
+3. a worker trains at most one model at a time.
+
+``InvariantMonitor`` enforces them at runtime (scheduler
+invariant assertions) for every scheduler and in the simulator.
+"""
+
+
+class SchedulerInvariantError(RuntimeError):
+    pass
+
+
+class InvariantMonitor(object):
+    def __init__(self, models, workers):
+        self.models = list(models)
+        self.workers = list(workers)
+        self.reset()
+
+    def reset(self):
+        self.done = set()
+        self.model_on = {}    # model -> worker
+        self.worker_has = {}  # worker -> model
+
+    def start(self, model, worker):
+        if model in self.model_on:
+            raise SchedulerInvariantError(
+                "model {} already running on worker {}".format(model, self.model_on[model]))
+        if worker in self.worker_has:
+            raise SchedulerInvariantError(
+                "worker {} already running model {}".format(worker, self.worker_has[worker]))
+        if (model, worker) in self.done:
+            raise SchedulerInvariantError("pair {} trained twice in one epoch".format((model, worker)))
+        self.model_on[model] = worker
+        self.worker_has[worker] = model
+
+    def finish(self, model, worker):
+        if self.model_on.get(model) != worker:
+            raise SchedulerInvariantError("finish of a job that is not running: {}".format((model, worker)))
+        del self.model_on[model]
+        del self.worker_has[worker]
+        self.done.add((model, worker))
+
+    def check_epoch_complete(self, models=None):
+        models = self.models if models is None else models
+        missing = [(m, w) for m in models for w in self.workers if (m, w) not in self.done]
+        if missing:
+            raise SchedulerInvariantError("epoch incomplete, missing {}".format(missing[:8]))
+        if self.model_on:
+            raise SchedulerInvariantError("jobs still running at epoch end: {}".format(self.model_on))
+
+
+class MOPScheduler(object):
+    """Base class.  Subclasses implement ``assign(worker)``.
+
+    ``models`` is a list of model ids, ``workers`` a list of virtual-worker
+    (partition) ids.  Models may be added between epochs (hyperopt) and
+    removed (early stop) via ``add_models`` / ``remove_models``.
+    """
+
+    lockstep = False
+
+    def __init__(self, models, workers, seed=2018):
+        self.models = list(models)
+        self.workers = list(workers)
+        self.seed = seed
+        self.epoch = 0
+        self.monitor = InvariantMonitor(self.models, self.workers)
+        self.idle_models = set()
+        self.idle_workers = set()
+
+    # -- epoch lifecycle --------------------------------------------------
+    def start_epoch(self, epoch):
+        self.epoch = epoch
+        self.monitor = InvariantMonitor(self.models, self.workers)
+        self.idle_models = set(self.models)
+        self.idle_workers = set(self.workers)
+        self.pending = [(m, w) for m in self.models for w in self.workers]
+
+    def epoch_done(self):
+        return not self.pending and not self.monitor.model_on
+
+    def add_models(self, models):
+        for m in models:
+            if m not in self.models:
+                self.models.append(m)
+
+    def remove_models(self, models):
+        self.models = [m for m in self.models if m not in set(models)]
+
+    # -- job lifecycle ----------------------------------------------------
+    def assign(self, worker):
+        raise NotImplementedError
+
+    def _start(self, model, worker):
+        self.monitor.start(model, worker)
+        self.pending.remove((model, worker))
+        self.idle_models.discard(model)
+        self.idle_workers.discard(worker)
+
+    def complete(self, model, worker):
+        self.monitor.finish(model, worker)
+        self.idle_models.add(model)
+        self.idle_workers.add(worker)
+
+    def assign_all_idle(self):
+        """Offer every idle worker a job (worker order = id order, like CTQ's loop)."""
+        out = []
+        for w in sorted(self.idle_workers):
+            m = self.assign(w)
+            if m is not None:
+                out.append((m, w))
+        return out

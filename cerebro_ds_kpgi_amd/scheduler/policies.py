@@ -1,0 +1,131 @@
+"""Scheduling policies.
+
+* ``RotationScheduler`` — UDAF / MADlib ``fit_multiple_model`` semantics
+  (reference ``hetero_simluator.ipynb`` cell 2 ``rotate`` /
+  ``UDAFSimulator.generate_schedule``): at sub-epoch ``s`` worker ``i`` trains
+  ``rotate(models, i)[s]``; every sub-epoch ends at a global barrier.  On a
+  ring of partitions this is a *ring shift*: each model moves to the next
+  partition, so across GPUs it is one xGMI neighbour send per GPU.
+* ``GreedyScheduler`` — CTQ / Cerebro semantics (reference
+  ``cerebro_gpdb/ctq.py:247-261,448-508``): per epoch, all (model, worker)
+  pairs in a seeded shuffled order; an idle worker takes the first pair whose
+  worker matches and whose model is idle.  Work-conserving, event driven (no
+  busy-wait: the runtime calls ``assign`` on completion events).
+* ``TaskParallelScheduler`` — Hyperopt-Spark semantics: one
+  model per worker for the whole epoch over the *replicated* dataset.
+"""
+
+import random
+
+from .base import MOPScheduler
+
+
+def rotate(seq, n):
+    """Rotate right by n (reference notebook ``rotate``: ``l[-n:] + l[:-n]``)."""
+    n = n % len(seq) if seq else 0
+    return seq[-n:] + seq[:-n] if n else list(seq)
+
+
+class RotationScheduler(MOPScheduler):
+    lockstep = True
+
+    def start_epoch(self, epoch):
+        super(RotationScheduler, self).start_epoch(epoch)
+        L = max(len(self.models), len(self.workers))
+        slots = list(self.models) + [None] * (L - len(self.models))
+        self.rounds = []
+        for s in range(L):
+            rnd = {}
+            for i, w in enumerate(self.workers):
+                m = rotate(slots, i)[s]
+                if m is not None:
+                    rnd[w] = m
+            self.rounds.append(rnd)
+        self.subepoch = 0
+
+    def assign(self, worker):
+        if self.subepoch >= len(self.rounds):
+            return None
+        m = self.rounds[self.subepoch].get(worker)
+        if m is None or m not in self.idle_models or (m, worker) not in self.pending:
+            return None
+        self._start(m, worker)
+        return m
+
+    def next_round(self):
+        """Lock-step API: the full {worker: model} map of the next sub-epoch."""
+        if self.subepoch >= len(self.rounds):
+            return None
+        rnd = self.rounds[self.subepoch]
+        for w, m in sorted(rnd.items()):
+            self._start(m, w)
+        return dict(rnd)
+
+    def finish_round(self, rnd):
+        for w, m in rnd.items():
+            self.complete(m, w)
+        self.subepoch += 1
+
+
+class GreedyScheduler(MOPScheduler):
+    def __init__(self, models, workers, seed=2018, shuffle=True):
+        super(GreedyScheduler, self).__init__(models, workers, seed)
+        self.shuffle = shuffle
+        self.rng = random.Random(seed)
+
+    def start_epoch(self, epoch):
+        super(GreedyScheduler, self).start_epoch(epoch)
+        if self.shuffle:
+            self.rng.shuffle(self.pending)
+
+    def assign(self, worker):
+        if worker not in self.idle_workers:
+            return None
+        for m, w in self.pending:
+            if w == worker and m in self.idle_models:
+                self._start(m, w)
+                return m
+        return None
+
+
+class TaskParallelScheduler(MOPScheduler):
+    """Each job = one model trained on *all* partitions (replicated data).
+
+    Bookkeeping is per (model, "ALL") so the invariants still apply.
+    """
+
+    ALL = "ALL"
+
+    def start_epoch(self, epoch):
+        super(TaskParallelScheduler, self).start_epoch(epoch)
+        self.pending_models = list(self.models)
+        self.running = {}
+        self.pending = []
+
+    def epoch_done(self):
+        return not self.pending_models and not self.running
+
+    def assign(self, worker):
+        if worker in self.running or not self.pending_models:
+            return None
+        m = self.pending_models.pop(0)
+        self.running[worker] = m
+        self.idle_workers.discard(worker)
+        self.idle_models.discard(m)
+        return m
+
+    def complete(self, model, worker):
+        assert self.running.get(worker) == model
+        del self.running[worker]
+        self.idle_workers.add(worker)
+        self.idle_models.add(model)
+
+
+def make_scheduler(name, models, workers, seed=2018, shuffle=True):
+    if name == "rotation":
+        return RotationScheduler(models, workers, seed)
+    if name == "greedy":
+        return GreedyScheduler(models, workers, seed, shuffle=shuffle)
+    if name == "task":
+        return TaskParallelScheduler(models, workers, seed)
+    raise ValueError("unknown scheduler {}".format(name))

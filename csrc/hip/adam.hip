@@ -1,0 +1,83 @@
+// Fused multi-configuration Adam over the flat arena.
+//
+// One launch updates all G configs: grid.y = config row, each thread owns 8
+// consecutive parameters (two 16-B loads per operand).  Per-row lr / lambda
+// and the step counter live on device, so the update is HIP-graph
+// capturable.  Semantics = torch.optim.Adam(lr, weight_decay=lambda):
+//   g += wd * p;  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
+//   p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)
+// and the bf16 compute shadow of p is written in the same pass.
+// Bytes/param: read p,m,v,g (16) + write p,m,v (12) + bf16 shadow (2).
+#include "common.h"
+
+__global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G) {
+  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < G) state[g * row_stride + off_step] += 1.0f;
+}
+
+template <bool WRITE_BF16>
+__global__ __launch_bounds__(256) void adam_kernel(
+    float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
+    int64_t off_v, int64_t off_step, const float* __restrict__ grad, int64_t grad_stride,
+    bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
+    const float* __restrict__ wd, float b1, float b2, float eps, int l2) {
+  const int g = blockIdx.y;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n_train) return;
+  float* row = state + g * row_stride;
+  const float t = row[off_step];
+  const float bc1 = 1.f - __powf(b1, t);
+  const float bc2 = 1.f - __powf(b2, t);
+  const float step_size = lr[g] / bc1;
+  const float inv_sqrt_bc2 = rsqrtf(bc2);
+  const float lam = l2 ? wd[g] : 0.f;
+
+  float4* pp = reinterpret_cast<float4*>(row + i);
+  float4* mp = reinterpret_cast<float4*>(row + off_m + i);
+  float4* vp = reinterpret_cast<float4*>(row + off_v + i);
+  const float4* gp = reinterpret_cast<const float4*>(grad + g * grad_stride + i);
+  float4 p[2] = {pp[0], pp[1]}, m[2] = {mp[0], mp[1]}, v[2] = {vp[0], vp[1]};
+  const float4 gr[2] = {gp[0], gp[1]};
+  float* pf = reinterpret_cast<float*>(p);
+  float* mf = reinterpret_cast<float*>(m);
+  float* vf = reinterpret_cast<float*>(v);
+  const float* gf = reinterpret_cast<const float*>(gr);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float gk = gf[k] + lam * pf[k];
+    mf[k] = b1 * mf[k] + (1.f - b1) * gk;
+    vf[k] = b2 * vf[k] + (1.f - b2) * gk * gk;
+    float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
+    pf[k] -= step_size * mf[k] / denom;
+  }
+  pp[0] = p[0]; pp[1] = p[1];
+  mp[0] = m[0]; mp[1] = m[1];
+  vp[0] = v[0]; vp[1] = v[1];
+  if (WRITE_BF16) {
+    uint4 o;
+    o.x = pack_bf2(pf[0], pf[1]);
+    o.y = pack_bf2(pf[2], pf[3]);
+    o.z = pack_bf2(pf[4], pf[5]);
+    o.w = pack_bf2(pf[6], pf[7]);
+    *reinterpret_cast<uint4*>(work + g * work_stride + i) = o;
+  }
+}
+
+CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
+                          int64_t off_v, int64_t off_step, const float* grad,
+                          int64_t grad_stride, bf16_t* work, int64_t work_stride,
+                          const float* lr, const float* wd, int G, float b1, float b2,
+                          float eps, int l2, hipStream_t stream) {
+  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  dim3 grid(cer_blocks(n_train / 8, 256), G);
+  if (work)
+    adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
+                                                 off_step, grad, grad_stride, work, work_stride,
+                                                 lr, wd, b1, b2, eps, l2);
+  else
+    adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
+                                                  off_step, grad, grad_stride, nullptr, 0, lr,
+                                                  wd, b1, b2, eps, l2);
+  return (int)hipGetLastError();
+}

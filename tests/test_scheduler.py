@@ -1,0 +1,116 @@
+"""Scheduler invariants + simulator parity with the reference notebook.
+
+Golden numbers: ``cerebro_gpdb/hetero_simluator.ipynb`` cell 6 recorded
+output (48 configs, 38 fast + 10 slow, scale 7.9427, seed 2020, W = 1..8).
+"""
+
+import itertools
+import random
+
+import numpy as np
+import pytest
+
+from cerebro_ds_kpgi_amd.scheduler import (GreedyScheduler, RotationScheduler,
+                                           SchedulerInvariantError, TaskParallelScheduler,
+                                           predict_greedy_runtime, predict_rotation_runtime,
+                                           rotate, simulate_greedy, simulate_rotation)
+
+S = 7.942693044033185
+NB_RUNTIMES = [1, 1, 1, 1, 1, 1, S, 1, 1, 1, 1, 1, 1, 1, S, 1, 1, 1, S, 1, 1, 1, 1, 1, 1, 1, 1,
+               S, 1, S, 1, 1, 1, S, 1, 1, S, 1, 1, 1, 1, S, 1, 1, 1, S, S, 1.0]
+NB_UDAF = [117.42693044033184, 166.02578174856416, 207.68194001276322, 249.33809827696234,
+           270.1661774090619, 290.99425654116146, 304.8796426292278, 318.7650287172942]
+NB_CTQ = [117.42693044033187, 117.42693044033189, 117.42693044033187, 117.42693044033189,
+          120.36962348436506, 124.36962348436506, 117.42693044033187, 120.36962348436506]
+
+
+def test_rotate_matches_reference_definition():
+    assert rotate([0, 1, 2, 3], 1) == [3, 0, 1, 2]
+    assert rotate([0, 1, 2, 3], 0) == [0, 1, 2, 3]
+    assert rotate([0, 1, 2, 3], 5) == [3, 0, 1, 2]
+
+
+def test_simulator_parity_with_notebook():
+    arr = np.array(NB_RUNTIMES)
+    random.seed(2020)
+    random.shuffle(arr)
+    for W in range(1, 9):
+        assert simulate_rotation(list(arr), W) == pytest.approx(NB_UDAF[W - 1], rel=1e-12)
+        assert simulate_greedy(list(arr), W) == pytest.approx(NB_CTQ[W - 1], rel=1e-12)
+
+
+def test_analytic_predictions():
+    assert predict_rotation_runtime(1, 48, S, 0.8) == pytest.approx(114.64985322271856)
+    assert predict_greedy_runtime(48, float(np.mean(NB_RUNTIMES))) == pytest.approx(117.42693044033186)
+
+
+@pytest.mark.parametrize("S_models,W", [(8, 8), (8, 2), (3, 5), (10, 4), (1, 1)])
+def test_rotation_covers_every_pair_once(S_models, W):
+    sch = RotationScheduler(list(range(S_models)), list(range(W)))
+    sch.start_epoch(1)
+    seen = []
+    while True:
+        rnd = sch.next_round()
+        if rnd is None:
+            break
+        # one model per worker, one worker per model
+        assert len(set(rnd.values())) == len(rnd)
+        seen += [(m, w) for w, m in rnd.items()]
+        sch.finish_round(rnd)
+    assert sorted(seen) == sorted(itertools.product(range(S_models), range(W)))
+    sch.monitor.check_epoch_complete()
+    assert len(sch.rounds) == max(S_models, W)
+
+
+def test_rotation_is_ring_shift():
+    sch = RotationScheduler(list(range(8)), list(range(8)))
+    sch.start_epoch(1)
+    r0 = sch.next_round()
+    sch.finish_round(r0)
+    r1 = sch.next_round()
+    inv0 = {m: w for w, m in r0.items()}
+    inv1 = {m: w for w, m in r1.items()}
+    assert all(inv1[m] == (inv0[m] + 1) % 8 for m in range(8))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2018])
+def test_greedy_event_driven_invariants(seed):
+    rng = random.Random(seed)
+    runtimes = [rng.choice([1, 3, 8]) for _ in range(12)]
+    t, jobs = simulate_greedy(runtimes, 5, rng=random.Random(seed), return_jobs=True)
+    assert len(jobs) == 12 * 5
+    # no overlap on a worker or for a model
+    for key in ("dist_key", "model_key"):
+        by = {}
+        for j in jobs:
+            by.setdefault(j[key], []).append((j["start_time"], j["end_time"]))
+        for iv in by.values():
+            iv.sort()
+            for a, b in zip(iv, iv[1:]):
+                assert a[1] <= b[0] + 1e-12
+    assert t >= sum(runtimes) * 5 / 5 - 1e-9
+
+
+def test_invariant_monitor_rejects_violations():
+    sch = GreedyScheduler([0, 1], [0, 1], shuffle=False)
+    sch.start_epoch(1)
+    sch.monitor.start(0, 0)
+    with pytest.raises(SchedulerInvariantError):
+        sch.monitor.start(0, 1)
+    with pytest.raises(SchedulerInvariantError):
+        sch.monitor.start(1, 0)
+    with pytest.raises(SchedulerInvariantError):
+        sch.monitor.check_epoch_complete()
+
+
+def test_task_parallel_each_model_once():
+    sch = TaskParallelScheduler(list(range(5)), list(range(2)))
+    sch.start_epoch(1)
+    done = []
+    while not sch.epoch_done():
+        for w in (0, 1):
+            m = sch.assign(w)
+            if m is not None:
+                done.append(m)
+                sch.complete(m, w)
+    assert sorted(done) == list(range(5))
