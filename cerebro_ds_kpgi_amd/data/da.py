@@ -1,0 +1,304 @@
+"""Direct Access (DA): read Greenplum-format packed-table partitions straight
+from their heap/TOAST segment files, bypassing the database.
+
+* ``DirectAccessReader`` — ctypes front-end of ``libcerebro_da.so``
+  (csrc/da): parses heap pages, indexes TOAST chunks, detoasts +
+  pglz-decompresses all buffers on a thread pool into *pinned* host memory,
+  from which partitions go to HBM with asynchronous copies.
+* ``write_partition`` / ``write_dataset`` — produce the same on-disk format
+  (``{root}/gpseg{i}/base/{dboid}/{relfilenode}[.N]`` + toast relfilenode +
+  a shapes/manifest JSON replacing the reference's ``sys_cat.dill`` catalog,
+  ``cerebro_gpdb/da.py:26,96-183``).
+* ``input_fn(file_path)`` — the reference's DA worker contract
+  (``cerebro_gpdb/da.py:29-58``): ``{buffer_id: {'independent_var': f32[N,...],
+  'dependent_var': i16[N, classes]}}``.
+* ``da_partition_loader`` — plugs DA partitions into the HBM partition store.
+
+Payloads: independent_var float32 ``[N, 112, 112, 3]`` (or ``[N, 7306]``
+one-hot for Criteo), dependent_var int16 one-hot ``[N, classes]``
+(``pg_page_reader.py:177-182``).
+"""
+
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+
+from ..config import catalog as cat
+
+_LIB = None
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib",
+                        "libcerebro_da.so")
+SEG_BYTES = 1 << 30        # Greenplum segment file size
+DBOID = 16384
+TRAIN_RELFILENODE, TRAIN_TOAST = 24576, 24580
+VALID_RELFILENODE, VALID_TOAST = 24590, 24594
+MANIFEST = "da_manifest.json"
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            from ..tools.build import build_da
+            build_da()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+        L.cer_pglz_compress.argtypes = [vp, i64, vp, i64]
+        L.cer_pglz_compress.restype = i64
+        L.cer_pglz_decompress.argtypes = [vp, i64, vp, i64]
+        L.cer_pglz_decompress.restype = i64
+        L.cer_da_last_error.restype = ctypes.c_char_p
+        L.cer_da_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.cer_da_open.restype = vp
+        L.cer_da_count.argtypes = [vp]
+        L.cer_da_info.argtypes = [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                  ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        L.cer_da_read.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.c_int]
+        L.cer_da_close.argtypes = [vp]
+        L.cer_da_writer_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                         ctypes.c_uint32, i64]
+        L.cer_da_writer_open.restype = vp
+        L.cer_da_writer_add.argtypes = [vp, i32, i32, vp, i64, vp, i64, ctypes.c_int]
+        L.cer_da_writer_close.argtypes = [vp]
+        _LIB = L
+    return _LIB
+
+
+def _err():
+    return lib().cer_da_last_error().decode()
+
+
+# ---------------------------------------------------------------------------
+# pglz
+# ---------------------------------------------------------------------------
+def pglz_compress(data):
+    src = np.frombuffer(bytes(data), dtype=np.uint8)
+    dst = np.empty(max(len(src) + 16, 16), dtype=np.uint8)
+    n = lib().cer_pglz_compress(src.ctypes.data, len(src), dst.ctypes.data, len(dst))
+    if n < 0:
+        return None
+    return dst[:n].tobytes()
+
+
+def pglz_decompress(comp, rawsize):
+    src = np.frombuffer(bytes(comp), dtype=np.uint8)
+    dst = np.empty(rawsize, dtype=np.uint8)
+    n = lib().cer_pglz_decompress(src.ctypes.data, len(src), dst.ctypes.data, rawsize)
+    if n < 0:
+        raise ValueError("compressed data is corrupt")
+    return dst.tobytes()
+
+
+# ---------------------------------------------------------------------------
+# reader
+# ---------------------------------------------------------------------------
+class DirectAccessReader(object):
+    def __init__(self, heap_path, toast_path):
+        self.h = lib().cer_da_open(heap_path.encode(), toast_path.encode())
+        if not self.h:
+            raise IOError("DA open failed: {}".format(_err()))
+
+    def __len__(self):
+        return lib().cer_da_count(self.h)
+
+    def info(self, i):
+        dk, bid = ctypes.c_int32(), ctypes.c_int32()
+        ni, nd = ctypes.c_int64(), ctypes.c_int64()
+        if lib().cer_da_info(self.h, i, ctypes.byref(dk), ctypes.byref(bid), ctypes.byref(ni),
+                             ctypes.byref(nd)) != 0:
+            raise IndexError(i)
+        return dk.value, bid.value, ni.value, nd.value
+
+    def read(self, nthreads=16, pinned=False, indices=None):
+        """List of (dist_key, buffer_id, indep bytes array, dep bytes array)."""
+        idx = list(range(len(self))) if indices is None else list(indices)
+        infos = [self.info(i) for i in idx]
+        if pinned:
+            import torch
+            ind = [torch.empty(ni, dtype=torch.uint8).pin_memory() for _, _, ni, _ in infos]
+            dep = [torch.empty(nd, dtype=torch.uint8).pin_memory() for _, _, _, nd in infos]
+            ip = [t.data_ptr() for t in ind]
+            dp = [t.data_ptr() for t in dep]
+        else:
+            ind = [np.empty(ni, dtype=np.uint8) for _, _, ni, _ in infos]
+            dep = [np.empty(nd, dtype=np.uint8) for _, _, _, nd in infos]
+            ip = [a.ctypes.data for a in ind]
+            dp = [a.ctypes.data for a in dep]
+        n = len(idx)
+        c_idx = (ctypes.c_int * n)(*idx)
+        c_ip = (ctypes.c_void_p * n)(*ip)
+        c_dp = (ctypes.c_void_p * n)(*dp)
+        rc = lib().cer_da_read(self.h, n, ctypes.cast(c_idx, ctypes.c_void_p),
+                               ctypes.cast(c_ip, ctypes.c_void_p),
+                               ctypes.cast(c_dp, ctypes.c_void_p), nthreads)
+        if rc != 0:
+            raise IOError("DA read failed: {}".format(_err()))
+        return [(dk, bid, a, b) for (dk, bid, _, _), a, b in zip(infos, ind, dep)]
+
+    def close(self):
+        if self.h:
+            lib().cer_da_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+# ---------------------------------------------------------------------------
+# writer
+# ---------------------------------------------------------------------------
+def seg_dir(root, seg, dboid=DBOID):
+    return os.path.join(root, "gpseg{}".format(seg), "base", str(dboid))
+
+
+def write_partition(heap_path, toast_path, buffers, dist_key, toastrelid=99999,
+                    first_valueid=1 << 20, seg_bytes=SEG_BYTES, dep_inline=True):
+    """buffers: list of (buffer_id, indep ndarray, dep ndarray)."""
+    os.makedirs(os.path.dirname(heap_path), exist_ok=True)
+    w = lib().cer_da_writer_open(heap_path.encode(), toast_path.encode(), toastrelid,
+                                 first_valueid, seg_bytes)
+    if not w:
+        raise IOError("DA writer open failed: {}".format(_err()))
+    for bid, indep, dep in buffers:
+        a = np.ascontiguousarray(indep)
+        b = np.ascontiguousarray(dep)
+        rc = lib().cer_da_writer_add(w, int(dist_key), int(bid), a.ctypes.data, a.nbytes,
+                                     b.ctypes.data, b.nbytes, int(bool(dep_inline)))
+        if rc != 0:
+            lib().cer_da_writer_close(w)
+            raise IOError("DA write failed: {}".format(_err()))
+    if lib().cer_da_writer_close(w) != 0:
+        raise IOError("DA writer close failed: {}".format(_err()))
+
+
+def write_dataset(root, dataset, num_partitions, n_train, n_valid, buffer_size=cat.TRAIN_BUFFER_SIZE,
+                  seed=cat.SEED, seg_bytes=SEG_BYTES):
+    """Synthetic packed tables for ``num_partitions`` segments + manifest."""
+    from . import synthetic
+    shapes = {"train": [], "valid": []}
+    for p in range(num_partitions):
+        for split, n, rel, toast in (("train", n_train, TRAIN_RELFILENODE, TRAIN_TOAST),
+                                     ("valid", n_valid, VALID_RELFILENODE, VALID_TOAST)):
+            s = seed * 1000 + 2 * p + (split == "valid")
+            if dataset == "imagenet":
+                x, y = synthetic.image_partition(n, seed=s)
+                x = x.numpy().astype(np.float32)
+                classes = cat.NUM_CLASSES
+            elif dataset == "criteo":
+                idx, y = synthetic.criteo_partition(n, seed=s)
+                x = np.zeros((n, cat.INPUT_SHAPE_CRITEO[0]), dtype=np.float32)
+                np.put_along_axis(x, idx.numpy().astype(np.int64), 1.0, axis=1)
+                classes = cat.NUM_CLASSES_CRITEO
+            else:
+                raise ValueError(dataset)
+            yy = np.zeros((n, classes), dtype=np.int16)
+            yy[np.arange(n), y.numpy()] = 1
+            bufs = []
+            for bid, s0 in enumerate(range(0, n, buffer_size)):
+                e = min(n, s0 + buffer_size)
+                bufs.append((bid, x[s0:e], yy[s0:e]))
+                shapes[split].append({"dist_key": p, "buffer_id": bid,
+                                      "independent_var_shape": list(x[s0:e].shape),
+                                      "dependent_var_shape": [e - s0, classes]})
+            d = seg_dir(root, p)
+            write_partition(os.path.join(d, str(rel)), os.path.join(d, str(toast)), bufs, p,
+                            toastrelid=toast, first_valueid=(p + 1) << 20, seg_bytes=seg_bytes)
+    man = {"dataset": dataset, "num_partitions": num_partitions, "dboid": DBOID,
+           "train": {"relfilenode": TRAIN_RELFILENODE, "toast_relfilenode": TRAIN_TOAST},
+           "valid": {"relfilenode": VALID_RELFILENODE, "toast_relfilenode": VALID_TOAST},
+           "shapes": shapes}
+    with open(os.path.join(root, MANIFEST), "w") as f:
+        json.dump(man, f)
+    return man
+
+
+# ---------------------------------------------------------------------------
+# catalog + reference-compatible input_fn
+# ---------------------------------------------------------------------------
+def load_manifest(root):
+    with open(os.path.join(root, MANIFEST)) as f:
+        return json.load(f)
+
+
+def generate_cats(root, size):
+    """(data_cat, sys_cats) like ``DirectAccessClient.generate_cats``: the
+    Cerebro data catalog with an identity availability matrix + the system
+    catalog (relfilenodes, dboid, shapes)."""
+    man = load_manifest(root)
+    data_cat = {
+        "data_root": root,
+        "train": ["gpseg{}/base/{}/train".format(i, man["dboid"]) for i in range(size)],
+        "train_availability": np.eye(size, dtype=int).tolist(),
+        "valid": ["gpseg{}/base/{}/valid".format(i, man["dboid"]) for i in range(size)],
+        "valid_availability": np.eye(size, dtype=int).tolist(),
+    }
+    return data_cat, man
+
+
+def _paths(root, file_path, man):
+    m = re.search(r"gpseg(\d+)", file_path)
+    seg = int(m.group(1))
+    split = "valid" if file_path.rstrip("/").endswith("valid") else "train"
+    d = seg_dir(root, seg, man["dboid"])
+    return (os.path.join(d, str(man[split]["relfilenode"])),
+            os.path.join(d, str(man[split]["toast_relfilenode"])), seg, split)
+
+
+def input_fn(file_path, root=None, nthreads=16):
+    """Reference DA worker contract: catalog path -> {buffer_id: {...}}."""
+    root = root or os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(file_path))))
+    man = load_manifest(root)
+    heap, toast, seg, split = _paths(root, file_path, man)
+    shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
+    r = DirectAccessReader(heap, toast)
+    out = {}
+    for dk, bid, a, b in r.read(nthreads):
+        sh = shapes[(dk, bid)]
+        out[bid] = {"independent_var": np.frombuffer(a.tobytes(), np.float32).reshape(
+                        sh["independent_var_shape"]),
+                    "dependent_var": np.frombuffer(b.tobytes(), np.int16).reshape(
+                        sh["dependent_var_shape"])}
+    r.close()
+    return out
+
+
+def da_partition_loader(root, device, nthreads=16):
+    """Loader for ``PartitionStore``: DA partition -> HBM tensors (uint8
+    images / int32 active-column ids, int32 labels)."""
+    import torch
+    man = load_manifest(root)
+
+    def load_split(p, split):
+        heap = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["relfilenode"]))
+        toast = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["toast_relfilenode"]))
+        shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
+        r = DirectAccessReader(heap, toast)
+        recs = sorted(r.read(nthreads, pinned=(torch.device(device).type == "cuda")),
+                      key=lambda t: t[1])
+        r.close()
+        xs, ys = [], []
+        for dk, bid, a, b in recs:
+            sh = shapes[(dk, bid)]
+            a = a if isinstance(a, torch.Tensor) else torch.from_numpy(a)
+            b = b if isinstance(b, torch.Tensor) else torch.from_numpy(b)
+            x = a.view(torch.float32).view(sh["independent_var_shape"]).to(device, non_blocking=True)
+            y = b.view(torch.int16).view(sh["dependent_var_shape"]).to(device, non_blocking=True)
+            xs.append(x)
+            ys.append(y)
+        x = torch.cat(xs)
+        y = torch.cat(ys).argmax(1).to(torch.int32)
+        if man["dataset"] == "imagenet":
+            x = x.round_().clamp_(0, 255).to(torch.uint8)
+        else:  # criteo one-hot -> active column ids
+            nnz = int((x[0] != 0).sum().item())
+            x = torch.nonzero(x, as_tuple=False)[:, 1].view(x.shape[0], nnz).to(torch.int32)
+        return x, y
+
+    def loader(p):
+        tx, ty = load_split(p, "train")
+        vx, vy = load_split(p, "valid")
+        return tx, ty, vx, vy
+    return loader

@@ -75,13 +75,21 @@ class PartitionStore(object):
         raise ValueError(d)
 
     def new_epoch(self, epoch):
-        """Fresh per-partition shuffles (seeded by partition and epoch)."""
+        """Fresh per-partition shuffles (seeded by partition and epoch).
+
+        Written IN PLACE into one persistent buffer: captured HIP graphs hold
+        its address, so it must never be reallocated.
+        """
         perms = []
         for p in self.pids:
             g = torch.Generator(device="cpu")
             g.manual_seed(self.seed * 7919 + 104729 * p + epoch)
             perms.append(torch.randperm(self.n_train, generator=g).to(torch.int32))
-        self.perm = torch.stack(perms).to(self.device)
+        new = torch.stack(perms)
+        if self.perm is None:
+            self.perm = new.to(self.device)
+        else:
+            self.perm.copy_(new)
 
     def nbytes(self):
         tot = 0
@@ -91,10 +99,17 @@ class PartitionStore(object):
         return tot
 
 
+_NORM_CACHE = {}
+
+
 def _norm_consts(device, dtype=torch.float32):
-    mean = torch.tensor(cat.IMAGENET_MEAN, device=device, dtype=dtype) * 255.0
-    std = torch.tensor(cat.IMAGENET_STD, device=device, dtype=dtype) * 255.0
-    return mean, std
+    """Mean/std*255 tensors, created once per device (never inside a graph capture)."""
+    key = (str(device), dtype)
+    if key not in _NORM_CACHE:
+        mean = torch.tensor(cat.IMAGENET_MEAN, device=device, dtype=dtype) * 255.0
+        std = torch.tensor(cat.IMAGENET_STD, device=device, dtype=dtype) * 255.0
+        _NORM_CACHE[key] = (mean, std)
+    return _NORM_CACHE[key]
 
 
 def gather_batch(store, train, part_of_row, cursor, B, x_out, y_out):
@@ -131,6 +146,8 @@ def gather_batch(store, train, part_of_row, cursor, B, x_out, y_out):
 def input_buffers(store, G, B, dtype):
     """Static (graph-capturable) batch buffers for G configs."""
     dev = store.device
+    if store.dataset in ("imagenet", "tiny"):
+        _norm_consts(dev)
     ds = store.dataset
     if ds in ("imagenet", "tiny"):
         hw = store.train_x.shape[2]

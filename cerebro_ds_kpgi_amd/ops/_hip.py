@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libcerebro_hip.so")
 
 IMPLEMENTED = {"adam", "loss", "gather"}
+_RET_I64 = {"cer_bn_part_floats"}
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -44,7 +45,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(L, name)
             fn.argtypes = args
-            fn.restype = c_i
+            fn.restype = c_i64 if name in _RET_I64 else c_i
         _LIB = L
     return _LIB
 
@@ -115,3 +116,268 @@ def gather_images(X, Y, perm, part_of_row, cursor, B, x_out, y_out):
                                  _ptr(x_out), _ptr(y_out), n, H * W, G, B,
                                  ctypes.cast(mean, c_p), ctypes.cast(inv, c_p), _stream())
     _check(rc, "cer_gather_images")
+
+
+# ---------------------------------------------------------------------------
+# convolution / linear (csrc/hip/conv.hip)
+# ---------------------------------------------------------------------------
+_SIGS.update({
+    "cer_conv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p,
+                     c_i, c_i, c_p],
+    "cer_conv_dgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_i, c_i, c_i, c_i,
+                       c_p, c_i, c_i, c_p],
+    "cer_conv_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                       c_p, c_i64, c_i, c_p],
+    "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
+    "cer_bn_part_floats": [c_i64, c_i],
+    "cer_bn_fwd_train": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p,
+                         c_p, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
+    "cer_bn_fwd_eval": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i, c_i,
+                        c_f, c_i, c_p],
+    "cer_bn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, c_p,
+                   c_i64, c_i, c_i, c_i, c_p],
+    "cer_maxpool_fwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "cer_maxpool_bwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "cer_gavgpool_fwd": [c_p, c_p, c_i, c_i, c_i, c_p],
+    "cer_gavgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_p],
+    "cer_bias_act_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
+    "cer_bias_act_bwd": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
+})
+IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
+
+
+def _act_code(a):
+    if a == 6:
+        return 6
+    return 1 if a else 0
+
+
+def _bf16(t):
+    assert t.dtype == torch.bfloat16, t.dtype
+    return t.contiguous()
+
+
+def conv2d_fwd(x, wref, stride, pad):
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    assert GC == G * cin, (x.shape, wref.spec.shape, G)
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
+    wp, ws = wref.work_ptr()
+    rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
+                            _ptr(y), Ho, Wo, _stream())
+    _check(rc, "cer_conv_fwd")
+    return y
+
+
+def conv2d_dgrad(dy, wref, xshape, stride, pad):
+    dy = _bf16(dy)
+    B, Ho, Wo, _ = dy.shape
+    _, H, W, _ = xshape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    dx = torch.empty((B, H, W, G * cin), dtype=torch.bfloat16, device=dy.device)
+    wt = torch.empty(G * cout * kh * kw * cin, dtype=torch.bfloat16, device=dy.device)
+    wp, ws = wref.work_ptr()
+    rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh, kw,
+                              stride, pad, _ptr(dx), H, W, _stream())
+    _check(rc, "cer_conv_dgrad")
+    return dx
+
+
+def conv2d_wgrad(x, dy, wref, stride, pad):
+    x = _bf16(x)
+    dy = _bf16(dy)
+    B, H, W, _ = x.shape
+    _, Ho, Wo, _ = dy.shape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    L = lib()
+    splits = L.cer_wgrad_splits(B * Ho * Wo, cout, kh * kw * cin, G)
+    if splits > 1:
+        wref.grad().zero_()
+    gp, gs = wref.grad_ptr()
+    rc = L.cer_conv_wgrad(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride, pad,
+                          c_p(gp), gs, splits, _stream())
+    _check(rc, "cer_conv_wgrad")
+
+
+# ---------------------------------------------------------------------------
+# batch norm (csrc/hip/bn.hip)
+# ---------------------------------------------------------------------------
+def _bn_part(M, C, device):
+    return torch.empty(int(lib().cer_bn_part_floats(M, C)), dtype=torch.float32, device=device)
+
+
+def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
+    x = _bf16(x)
+    C = x.shape[-1]
+    M = x.numel() // C
+    Cper = gref.spec.shape[0]
+    y = torch.empty_like(x)
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    part = _bn_part(M, C, x.device)
+    gp, gs = gref.work_ptr()
+    bp, bs = bref.work_ptr()
+    rmp, rs = rmref.master_ptr()
+    rvp, _ = rvref.master_ptr()
+    res = _bf16(residual) if residual is not None else None
+    rc = lib().cer_bn_fwd_train(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
+                                c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
+                                _ptr(part), M, C, Cper, eps, momentum, _act_code(act), _stream())
+    _check(rc, "cer_bn_fwd_train")
+    return y, mean, invstd
+
+
+def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
+    x = _bf16(x)
+    C = x.shape[-1]
+    M = x.numel() // C
+    Cper = gref.spec.shape[0]
+    y = torch.empty_like(x)
+    gp, gs = gref.work_ptr()
+    bp, bs = bref.work_ptr()
+    rmp, rs = rmref.master_ptr()
+    rvp, _ = rvref.master_ptr()
+    res = _bf16(residual) if residual is not None else None
+    rc = lib().cer_bn_fwd_eval(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs, c_p(rmp),
+                               c_p(rvp), rs, M, C, Cper, eps, _act_code(act), _stream())
+    _check(rc, "cer_bn_fwd_eval")
+    return y
+
+
+def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res):
+    dy = _bf16(dy)
+    C = x.shape[-1]
+    M = x.numel() // C
+    Cper = gref.spec.shape[0]
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if has_res else None
+    ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    part = _bn_part(M, C, x.device)
+    gp, gs = gref.work_ptr()
+    dgp, dgs = gref.grad_ptr()
+    dbp, _ = bref.grad_ptr()
+    rc = lib().cer_bn_bwd(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
+                          c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
+                          M, C, Cper, _act_code(act), _stream())
+    _check(rc, "cer_bn_bwd")
+    return dx, dres
+
+
+# ---------------------------------------------------------------------------
+# pooling / bias+act (csrc/hip/pool.hip)
+# ---------------------------------------------------------------------------
+def maxpool_fwd(x, k, s, p):
+    x = _bf16(x)
+    B, H, W, C = x.shape
+    Ho = (H + 2 * p - k) // s + 1
+    Wo = (W + 2 * p - k) // s + 1
+    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+    rc = lib().cer_maxpool_fwd(_ptr(x), _ptr(y), _ptr(arg), B, H, W, C, Ho, Wo, k, s, p,
+                               _stream())
+    _check(rc, "cer_maxpool_fwd")
+    return y, (arg, k, s, p)
+
+
+def maxpool_bwd(dy, saved, xshape):
+    arg, k, s, p = saved
+    B, H, W, C = xshape
+    _, Ho, Wo, _ = dy.shape
+    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
+    rc = lib().cer_maxpool_bwd(_ptr(_bf16(dy)), _ptr(arg), _ptr(dx), B, H, W, C, Ho, Wo, k, s, p,
+                               _stream())
+    _check(rc, "cer_maxpool_bwd")
+    return dx
+
+
+def gavgpool_fwd(x):
+    x = _bf16(x)
+    B, H, W, C = x.shape
+    y = torch.empty((B, C), dtype=torch.bfloat16, device=x.device)
+    rc = lib().cer_gavgpool_fwd(_ptr(x), _ptr(y), B, H * W, C, _stream())
+    _check(rc, "cer_gavgpool_fwd")
+    return y
+
+
+def gavgpool_bwd(dy, xshape):
+    B, H, W, C = xshape
+    dx = torch.empty(xshape, dtype=torch.bfloat16, device=dy.device)
+    rc = lib().cer_gavgpool_bwd(_ptr(_bf16(dy)), _ptr(dx), B, H * W, C, _stream())
+    _check(rc, "cer_gavgpool_bwd")
+    return (dx,)
+
+
+def bias_act_fwd(x, bref, act, out=None):
+    x = _bf16(x)
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty_like(x) if out is None else out
+    bp, bs = bref.work_ptr()
+    rc = lib().cer_bias_act_fwd(_ptr(x), c_p(bp), bs, _ptr(y), M, C, bref.spec.shape[0],
+                                _act_code(act), _stream())
+    _check(rc, "cer_bias_act_fwd")
+    return y
+
+
+def bias_act_bwd(dy, y, bref, act):
+    dy = _bf16(dy)
+    C = y.shape[-1]
+    M = y.numel() // C
+    dx = torch.empty_like(dy)
+    ws = torch.empty(C, dtype=torch.float32, device=dy.device)
+    gp, gs = bref.grad_ptr()
+    rc = lib().cer_bias_act_bwd(_ptr(dy), _ptr(y), _ptr(dx), c_p(gp), gs, _ptr(ws), M, C,
+                                bref.spec.shape[0], _act_code(act), _stream())
+    _check(rc, "cer_bias_act_bwd")
+    return dx
+
+
+# ---------------------------------------------------------------------------
+# grouped linear = 1x1 conv on a 1x1 image (+ bias/act kernel)
+# ---------------------------------------------------------------------------
+def linear_fwd(x, wref, bref, act):
+    x = _bf16(x)
+    B = x.shape[0]
+    G = wref.G
+    N, K = wref.spec.shape
+    y = torch.empty((B, G * N), dtype=torch.bfloat16, device=x.device)
+    wp, ws = wref.work_ptr()
+    rc = lib().cer_conv_fwd(_ptr(x), B, 1, 1, K, G, c_p(wp), ws, N, 1, 1, 1, 0, _ptr(y), 1, 1,
+                            _stream())
+    _check(rc, "cer_conv_fwd(linear)")
+    if bref is not None or act:
+        if bref is None:
+            raise NotImplementedError("linear without bias")
+        bias_act_fwd(y, bref, act, out=y)
+    return y
+
+
+def linear_bwd(dy, x, y, wref, bref, act, need_dx):
+    G = wref.G
+    N, K = wref.spec.shape
+    B = x.shape[0]
+    dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _bf16(dy)
+    L = lib()
+    splits = L.cer_wgrad_splits(B, N, K, G)
+    if splits > 1:
+        wref.grad().zero_()
+    gp, gs = wref.grad_ptr()
+    rc = L.cer_conv_wgrad(_ptr(_bf16(x)), B, 1, 1, K, G, _ptr(dz), 1, 1, N, 1, 1, 1, 0,
+                          c_p(gp), gs, splits, _stream())
+    _check(rc, "cer_conv_wgrad(linear)")
+    if not need_dx:
+        return None
+    dx = torch.empty((B, G * K), dtype=torch.bfloat16, device=dy.device)
+    wt = torch.empty(G * N * K, dtype=torch.bfloat16, device=dy.device)
+    wp, ws = wref.work_ptr()
+    rc = L.cer_conv_dgrad(_ptr(dz), B, 1, 1, N, G, c_p(wp), ws, _ptr(wt), K, 1, 1, 1, 0,
+                          _ptr(dx), 1, 1, _stream())
+    _check(rc, "cer_conv_dgrad(linear)")
+    return dx

@@ -43,7 +43,14 @@ def use_hip(op, *tensors):
     from . import _hip
     if op not in _hip.IMPLEMENTED:
         return False
-    return all(t.is_cuda for t in tensors if isinstance(t, torch.Tensor))
+    for t in tensors:
+        if isinstance(t, torch.Tensor):
+            if not t.is_cuda:
+                return False
+            # activation kernels are bf16; fp32 compute runs on the oracle path
+            if t.is_floating_point() and t.dtype != torch.bfloat16 and op not in ("adam", "gather"):
+                return False
+    return True
 
 
 def force_torch_ops(ops):

@@ -233,15 +233,17 @@ def bias_act(x, bref, relu=True):
 class MaxPoolHip(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):
-        y, idx = _hip().maxpool_fwd(x, k, s, p)
-        ctx.save_for_backward(idx)
+        y, saved = _hip().maxpool_fwd(x, k, s, p)
+        ctx.save_for_backward(saved[0])
+        ctx.geom = saved[1:]
         ctx.xshape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        idx, = ctx.saved_tensors
-        return _hip().maxpool_bwd(dy.contiguous(), idx, ctx.xshape), None, None, None
+        arg, = ctx.saved_tensors
+        dx = _hip().maxpool_bwd(dy.contiguous(), (arg,) + ctx.geom, ctx.xshape)
+        return dx, None, None, None
 
 
 def maxpool2d(x, k, s, p=0):
@@ -258,7 +260,7 @@ class AvgPoolHip(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        return _hip().gavgpool_bwd(dy.contiguous(), ctx.xshape)
+        return _hip().gavgpool_bwd(dy.contiguous(), ctx.xshape)[0]
 
 
 def global_avgpool(x):

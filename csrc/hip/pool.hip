@@ -1,0 +1,314 @@
+// Pooling + bias/activation elementwise kernels on packed NHWC (SURVEY.md
+// K10, K15).  All kernels move 8 channels (16 B of bf16) per thread.
+//
+// maxpool fwd stores the argmax window offset (uint8) per output element;
+// maxpool bwd is a deterministic *gather* (each input pixel sums the
+// gradients of the <= ceil(k/s)^2 windows whose argmax is it) — no atomics.
+#include "common.h"
+
+constexpr int PT = 256;
+
+__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
+  uint4 u;
+  u.x = pack_bf2(v[0], v[1]);
+  u.y = pack_bf2(v[2], v[3]);
+  u.z = pack_bf2(v[4], v[5]);
+  u.w = pack_bf2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+__global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                         bf16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ arg, int B, int H,
+                                                         int W, int C, int Ho, int Wo, int k,
+                                                         int s, int pad) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * Ho * Wo * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int wo = (int)(pix % Wo);
+  pix /= Wo;
+  const int ho = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  float best[8];
+  uint8_t bi[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    best[i] = -INFINITY;
+    bi[i] = 0;
+  }
+  for (int r = 0; r < k; ++r) {
+    const int h = ho * s - pad + r;
+    if (h < 0 || h >= H) continue;
+    for (int q = 0; q < k; ++q) {
+      const int w = wo * s - pad + q;
+      if (w < 0 || w >= W) continue;
+      float v[8];
+      ld8(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (v[i] > best[i]) {
+          best[i] = v[i];
+          bi[i] = (uint8_t)(r * k + q);
+        }
+    }
+  }
+  const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+  st8(y + o, best);
+  uint2 packed;
+  packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+  packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+  *reinterpret_cast<uint2*>(arg + o) = packed;
+}
+
+__global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                         const uint8_t* __restrict__ arg,
+                                                         bf16_t* __restrict__ dx, int B, int H,
+                                                         int W, int C, int Ho, int Wo, int k,
+                                                         int s, int pad) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * H * W * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int w = (int)(pix % W);
+  pix /= W;
+  const int h = (int)(pix % H);
+  const int b = (int)(pix / H);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // windows containing h: ho*s - pad <= h <= ho*s - pad + k - 1
+  int ho0 = (h + pad - k + 1 + s - 1) / s;
+  if (h + pad - k + 1 < 0) ho0 = 0;
+  const int ho1 = min(Ho - 1, (h + pad) / s);
+  int wo0 = (w + pad - k + 1 + s - 1) / s;
+  if (w + pad - k + 1 < 0) wo0 = 0;
+  const int wo1 = min(Wo - 1, (w + pad) / s);
+  for (int ho = ho0; ho <= ho1; ++ho) {
+    for (int wo = wo0; wo <= wo1; ++wo) {
+      const uint8_t want = (uint8_t)((h + pad - ho * s) * k + (w + pad - wo * s));
+      const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+      uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+      float g[8];
+      ld8(dy + o, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t word = i < 4 ? packed.x : packed.y;
+        uint8_t a = (uint8_t)(word >> (8 * (i & 3)));
+        if (a == want) acc[i] += g[i];
+      }
+    }
+  }
+  st8(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
+}
+
+// global average pool: x [B, HW, C] -> y [B, C]
+__global__ __launch_bounds__(PT) void gavg_fwd_kernel(const bf16_t* __restrict__ x,
+                                                      bf16_t* __restrict__ y, int B, int HW,
+                                                      int C) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  if (t >= (int64_t)B * cv) return;
+  const int c0 = (int)(t % cv) * 8;
+  const int b = (int)(t / cv);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < HW; ++i) {
+    float v[8];
+    ld8(x + ((int64_t)b * HW + i) * C + c0, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= inv;
+  st8(y + (int64_t)b * C + c0, acc);
+}
+
+__global__ __launch_bounds__(PT) void gavg_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                      bf16_t* __restrict__ dx, int B, int HW,
+                                                      int C) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * HW * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  const int64_t pix = t / cv;
+  const int b = (int)(pix / HW);
+  float g[8];
+  ld8(dy + (int64_t)b * C + c0, g);
+  const float inv = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] *= inv;
+  st8(dx + pix * C + c0, g);
+}
+
+// bias + activation: y = act(x + bias[g][c]) over [M, C] packed channels
+__global__ __launch_bounds__(PT) void bias_act_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ bias,
+                                                          int64_t bstride, bf16_t* __restrict__ y,
+                                                          int64_t M, int C, int Cper, int act) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  if (t >= M * cv) return;
+  const int c0 = (int)(t % cv) * 8;
+  const int g = c0 / Cper, cc = c0 - g * Cper;
+  float v[8], b[8];
+  ld8(x + t * 8, v);
+  ld8(bias + g * bstride + cc, b);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float z = v[i] + b[i];
+    v[i] = act == 6 ? fminf(fmaxf(z, 0.f), 6.f) : (act ? fmaxf(z, 0.f) : z);
+  }
+  st8(y + t * 8, v);
+}
+
+// dz = act'(y) * dy  (written to dx) and per-channel partial sums of dz
+__global__ __launch_bounds__(PT) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ y,
+                                                          bf16_t* __restrict__ dx, float* ws,
+                                                          int64_t M, int C, int rows, int act) {
+  const int c0 = (blockIdx.x * PT + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = min(M, r0 + rows);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; ++r) {
+    float d[8], yv[8];
+    ld8(dy + r * C + c0, d);
+    ld8(y + r * C + c0, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float z = act == 6 ? ((yv[i] > 0.f && yv[i] < 6.f) ? d[i] : 0.f)
+                         : (act ? (yv[i] > 0.f ? d[i] : 0.f) : d[i]);
+      d[i] = z;
+      s[i] += z;
+    }
+    st8(dx + r * C + c0, d);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) atomicAdd(&ws[c0 + i], s[i]);
+}
+
+__global__ void bias_grad_scatter(const float* ws, float* dbias, int64_t gstride, int C,
+                                  int Cper) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int g = c / Cper;
+  dbias[g * gstride + (c - g * Cper)] = ws[c];
+}
+
+// scalar fallbacks for channel counts that are not multiples of 8 (N = 500, 10, 2 heads)
+__global__ __launch_bounds__(PT) void bias_act_fwd_scalar(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ bias,
+                                                          int64_t bstride, bf16_t* __restrict__ y,
+                                                          int64_t M, int C, int Cper, int act) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  if (t >= M * C) return;
+  const int c = (int)(t % C);
+  const int g = c / Cper;
+  float z = bf2f(x[t]) + bf2f(bias[g * bstride + (c - g * Cper)]);
+  z = act == 6 ? fminf(fmaxf(z, 0.f), 6.f) : (act ? fmaxf(z, 0.f) : z);
+  y[t] = f2bf(z);
+}
+
+__global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ y,
+                                                          bf16_t* __restrict__ dx, float* ws,
+                                                          int64_t M, int C, int rows, int act) {
+  const int c = blockIdx.x * PT + threadIdx.x;
+  if (c >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = min(M, r0 + rows);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float d = bf2f(dy[r * C + c]), yv = bf2f(y[r * C + c]);
+    const float z = act == 6 ? ((yv > 0.f && yv < 6.f) ? d : 0.f) : (act ? (yv > 0.f ? d : 0.f) : d);
+    dx[r * C + c] = f2bf(z);
+    s += z;
+  }
+  atomicAdd(&ws[c], s);
+}
+
+CER_API int cer_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int B, int H, int W, int C,
+                            int Ho, int Wo, int k, int s, int pad, hipStream_t stream) {
+  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)B * Ho * Wo * (C / 8);
+  maxpool_fwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, arg, B, H, W, C, Ho, Wo,
+                                                               k, s, pad);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int B, int H,
+                            int W, int C, int Ho, int Wo, int k, int s, int pad,
+                            hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)B * H * W * (C / 8);
+  maxpool_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, arg, dx, B, H, W, C, Ho, Wo,
+                                                               k, s, pad);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_gavgpool_fwd(const bf16_t* x, bf16_t* y, int B, int HW, int C,
+                             hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  gavg_fwd_kernel<<<cer_blocks((int64_t)B * (C / 8), PT), PT, 0, stream>>>(x, y, B, HW, C);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_gavgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int HW, int C,
+                             hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  int64_t total = (int64_t)B * HW * (C / 8);
+  gavg_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, HW, C);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_bias_act_fwd(const bf16_t* x, const bf16_t* bias, int64_t bstride, bf16_t* y,
+                             int64_t M, int C, int Cper, int act, hipStream_t stream) {
+  if (C % 8 || Cper % 8) {
+    bias_act_fwd_scalar<<<cer_blocks(M * C, PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
+                                                                  Cper, act);
+    return (int)hipGetLastError();
+  }
+  bias_act_fwd_kernel<<<cer_blocks(M * (C / 8), PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
+                                                                      Cper, act);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_bias_act_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, float* dbias,
+                             int64_t gstride, float* ws, int64_t M, int C, int Cper, int act,
+                             hipStream_t stream) {
+  if (C % 8 || Cper % 8) {
+    const int cb = cer_blocks(C, PT);
+    int64_t want = (1024 + cb - 1) / cb;
+    int64_t rows = (M + want - 1) / want;
+    if (rows < 16) rows = 16;
+    dim3 grid(cb, (unsigned)((M + rows - 1) / rows));
+    hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+    bias_act_bwd_scalar<<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
+    bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
+    return (int)hipGetLastError();
+  }
+  int cblocks = cer_blocks(C / 8, PT);
+  int64_t want = (2048 + cblocks - 1) / cblocks;
+  int64_t rows = (M + want - 1) / want;
+  if (rows < 16) rows = 16;
+  dim3 grid(cblocks, (unsigned)((M + rows - 1) / rows));
+  hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+  bias_act_bwd_kernel<<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
+  bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,217 @@
+"""Conv / BN / pool / linear HIP kernels vs the PyTorch oracle (GPU box).
+
+Every case runs the same autograd Function twice — HIP backend and forced
+oracle — on identical bf16 inputs and compares outputs, input gradients and
+the weight gradients written into the arena.
+"""
+
+import pytest
+import torch
+
+from cerebro_ds_kpgi_amd.ops import backend
+from cerebro_ds_kpgi_amd.ops import nn as P
+from cerebro_ds_kpgi_amd.runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _hip_backend():
+    backend.set_backend("hip")
+    backend.force_torch_ops([])
+    yield
+    backend.force_torch_ops([])
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _make(specs, G, seed=0):
+    lay = ModelLayout(specs)
+    a = Arena(lay, G, "cuda", torch.bfloat16)
+    torch.manual_seed(1000 + seed)   # identical parameters for the HIP and oracle runs
+    for g in range(G):
+        a.init_model(g, seed + g)
+    # non-trivial BN params
+    for s in specs:
+        if s.kind in ("gamma", "beta", "bias", "running_mean"):
+            a.master_view(s).uniform_(-0.5, 1.5)
+        if s.kind == "running_var":
+            a.master_view(s).uniform_(0.5, 2.0)
+    a.sync_work()
+    return a, {s.name: ParamRef(a, s) for s in specs}
+
+
+CONV_CASES = [
+    # (B, H, W, Cin, Cout, k, stride, pad, G)
+    (2, 28, 28, 64, 64, 3, 1, 1, 2),
+    (2, 28, 28, 256, 128, 1, 2, 0, 2),
+    (2, 14, 14, 128, 512, 1, 1, 0, 3),
+    (4, 7, 7, 256, 256, 3, 1, 1, 1),
+    (4, 4, 4, 512, 512, 3, 1, 1, 2),
+    (2, 7, 7, 1024, 2048, 1, 2, 0, 1),
+    (2, 112, 112, 3, 64, 7, 2, 3, 2),      # stem (unaligned path)
+    (2, 9, 11, 24, 40, 3, 2, 1, 2),        # odd everything
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_matches_oracle(case):
+    B, H, W, cin, cout, k, s, p, G = case
+    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+    a, refs = _make([spec], G)
+    torch.manual_seed(1)
+    x = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+    grads = []
+
+    def fn(xx):
+        return P.conv2d(xx, refs["w"], s, p)
+    outs = []
+    for force in ([], ["conv"]):
+        backend.force_torch_ops(force)
+        xx = x.clone().requires_grad_(True)
+        y = fn(xx)
+        torch.manual_seed(3)
+        gy = torch.randn_like(y.float()).to(torch.bfloat16)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append(y.detach().float())
+        grads.append((xx.grad.float(), a.grad.clone()))
+    backend.force_torch_ops([])
+    assert _rel(outs[0], outs[1]) < 1e-2
+    assert _rel(grads[0][0], grads[1][0]) < 1e-2
+    assert _rel(grads[0][1], grads[1][1]) < 1e-2
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (True, True), (False, False), (6, False)])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64), (2, 7, 7, 3 * 256)])
+def test_bn_act_matches_oracle(act, res, shape):
+    G = 2 if shape[-1] == 64 else 3
+    C = shape[-1] // G
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    outs = []
+    torch.manual_seed(2)
+    x = (2 * torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16)
+    r = torch.randn(shape, device="cuda").to(torch.bfloat16) if res else None
+    for force in ([], ["bn"]):
+        backend.force_torch_ops(force)
+        a, refs = _make(specs, G, seed=5)
+        xx = x.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True) if res else None
+        y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        ye = P.bn_act(x, refs["g"], refs["b"], refs["rm"], refs["rv"], False, act, r)
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
+                     a.master.clone(), ye))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert _rel(h[0], t[0]) < 1e-2
+    assert _rel(h[1], t[1]) < 2e-2
+    if res:
+        assert _rel(h[2], t[2]) < 1e-2
+    assert _rel(h[3], t[3]) < 1e-2          # dgamma / dbeta
+    assert _rel(h[4], t[4]) < 1e-4          # running stats
+    assert _rel(h[5], t[5]) < 1e-2          # eval path
+
+
+@pytest.mark.parametrize("k,s,p,shape", [(3, 2, 1, (2, 56, 56, 128)), (2, 2, 0, (2, 7, 7, 64))])
+def test_maxpool_matches_oracle(k, s, p, shape):
+    torch.manual_seed(4)
+    # distinct values so argmax is unique
+    x = torch.randperm(int(torch.tensor(shape).prod()), device="cuda").float().view(shape)
+    x = (x / x.numel()).to(torch.bfloat16)
+    res = []
+    for force in ([], ["pool"]):
+        backend.force_torch_ops(force)
+        xx = x.clone().requires_grad_(True)
+        y = P.maxpool2d(xx, k, s, p)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        res.append((y.detach(), xx.grad))
+    backend.force_torch_ops([])
+    assert torch.equal(res[0][0], res[1][0])
+    assert _rel(res[0][1], res[1][1]) < 1e-2
+
+
+def test_global_avgpool_matches_oracle():
+    torch.manual_seed(5)
+    x = torch.randn(4, 4, 4, 2 * 2048, device="cuda").to(torch.bfloat16)
+    res = []
+    for force in ([], ["pool"]):
+        backend.force_torch_ops(force)
+        xx = x.clone().requires_grad_(True)
+        y = P.global_avgpool(xx)
+        y.backward(torch.ones_like(y))
+        res.append((y.detach(), xx.grad))
+    backend.force_torch_ops([])
+    assert _rel(res[0][0], res[1][0]) < 1e-2
+    assert _rel(res[0][1], res[1][1]) < 1e-2
+
+
+@pytest.mark.parametrize("B,K,N,G,act", [(32, 2048, 1000, 2, False), (64, 1000, 500, 3, True),
+                                         (16, 500, 2, 2, False), (8, 4, 10, 4, True)])
+def test_linear_matches_oracle(B, K, N, G, act):
+    specs = [ParamSpec("w", (N, K), "weight", init="glorot", fan_in=K), ParamSpec("b", (N,), "bias")]
+    torch.manual_seed(6)
+    x = torch.randn(B, G * K, device="cuda").to(torch.bfloat16)
+    res = []
+    for force in ([], ["linear", "bias"]):
+        backend.force_torch_ops(force)
+        a, refs = _make(specs, G, seed=9)
+        xx = x.clone().requires_grad_(True)
+        y = P.linear(xx, refs["w"], refs["b"], act)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        torch.cuda.synchronize()
+        res.append((y.detach(), xx.grad, a.grad.clone()))
+    backend.force_torch_ops([])
+    for i in range(3):
+        assert _rel(res[0][i], res[1][i]) < 1e-2, i
+
+
+def test_vgg_bias_act_matches_oracle():
+    specs = [ParamSpec("b", (64,), "bias")]
+    torch.manual_seed(8)
+    x = torch.randn(2, 14, 14, 2 * 64, device="cuda").to(torch.bfloat16)
+    res = []
+    for force in ([], ["bias"]):
+        backend.force_torch_ops(force)
+        a, refs = _make(specs, 2, seed=1)
+        xx = x.clone().requires_grad_(True)
+        y = P.bias_act(xx, refs["b"], True)
+        y.backward(torch.ones_like(y))
+        res.append((y.detach(), xx.grad, a.grad.clone()))
+    backend.force_torch_ops([])
+    for i in range(3):
+        assert _rel(res[0][i], res[1][i]) < 1e-2, i
+
+
+@pytest.mark.parametrize("model", ["resnet50", "vgg16", "mobilenetv2"])
+def test_full_model_step_matches_oracle(model):
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    from cerebro_ds_kpgi_amd.ops.loss import softmax_ce
+    G, B = 2, 4
+    torch.manual_seed(11)
+    x = torch.randn(B, 112, 112, 3 * G, device="cuda").to(torch.bfloat16)
+    y = torch.randint(0, 1000, (G, B), device="cuda", dtype=torch.int32)
+    res = []
+    for force in ([], ["conv", "bn", "pool", "bias", "linear", "dwconv"]):
+        backend.force_torch_ops(force)
+        net = create_model_from_mst({"model": model})
+        a = Arena(net.layout, G, "cuda", torch.bfloat16)
+        for g in range(G):
+            a.init_model(g, 100 + g)
+        net.bind(a)
+        acc = torch.zeros(G, 4, device="cuda")
+        loss = softmax_ce(net.forward(x, True), y, acc, G)
+        loss.sum().backward()
+        torch.cuda.synchronize()
+        res.append((loss.detach(), a.grad.clone()))
+    backend.force_torch_ops([])
+    torch.testing.assert_close(res[0][0], res[1][0], rtol=2e-2, atol=2e-2)
+    assert _rel(res[0][1], res[1][1]) < 5e-2

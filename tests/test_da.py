@@ -1,0 +1,152 @@
+"""Direct-Access reader: pglz codec + heap/TOAST page round trips.
+
+The reference ships no test vectors; its format is what its Python reader
+parses (``cerebro_gpdb/pg_page_reader.py``), so golden checks here are
+(a) hand-built pglz streams following the documented control-byte format and
+(b) writer -> reader round trips covering the edge cases named in SURVEY.md
+§4: inline-compressed dependent_var, a partial last TOAST chunk, values
+spanning many chunks and multi-segment (``relfilenode.N``) files.
+"""
+
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from cerebro_ds_kpgi_amd.data import da
+
+
+def test_pglz_hand_built_stream():
+    # ctrl 0b00000010: literal 'a', then match off=1 len=5 -> "aaaaaa"
+    stream = bytes([0b00000010, ord("a"), 0x02, 0x01])
+    assert da.pglz_decompress(stream, 6) == b"aaaaaa"
+    # long match (len 18 + ext byte): literal 'x', match off=1 len=18+7=25
+    stream = bytes([0b10, ord("x"), 0x0F, 0x01, 7])
+    assert da.pglz_decompress(stream, 26) == b"x" * 26
+    # two literals, match off=2 len=4 -> "abab" + "ab"
+    stream = bytes([0b100, ord("a"), ord("b"), 0x01, 0x02])
+    assert da.pglz_decompress(stream, 6) == b"ababab"
+
+
+def test_pglz_corruption_detected():
+    stream = bytes([0b10, ord("a"), 0x02, 0x01])
+    with pytest.raises(ValueError):
+        da.pglz_decompress(stream, 7)          # underrun: rawsize too large
+    with pytest.raises(ValueError):
+        da.pglz_decompress(stream + b"zz", 6)  # input not fully consumed
+    with pytest.raises(ValueError):
+        da.pglz_decompress(bytes([0b1, 0x00, 0x05]), 3)  # offset beyond output
+
+
+@pytest.mark.parametrize("kind", ["zeros", "random", "images", "text"])
+def test_pglz_roundtrip(kind):
+    rng = np.random.RandomState(0)
+    if kind == "zeros":
+        raw = bytes(100000)
+    elif kind == "random":
+        raw = rng.randint(0, 256, 5000).astype(np.uint8).tobytes()
+    elif kind == "images":
+        raw = rng.randint(0, 8, (64, 64, 3)).astype(np.float32).tobytes()
+    else:
+        raw = (b"model hopper parallelism " * 400)
+    comp = da.pglz_compress(raw)
+    if comp is None:
+        assert kind == "random"
+        return
+    assert da.pglz_decompress(comp, len(raw)) == raw
+    if kind in ("zeros", "text"):
+        assert len(comp) < len(raw) / 10
+
+
+def _bufs(rng, nbuf, n_img, hw=8, classes=10):
+    out = []
+    for b in range(nbuf):
+        x = rng.randint(0, 256, (n_img, hw, hw, 3)).astype(np.float32)
+        y = np.zeros((n_img, classes), np.int16)
+        y[np.arange(n_img), rng.randint(0, classes, n_img)] = 1
+        out.append((b, x, y))
+    return out
+
+
+@pytest.mark.parametrize("dep_inline", [True, False])
+def test_page_roundtrip(tmp_path, dep_inline):
+    rng = np.random.RandomState(1)
+    bufs = _bufs(rng, 5, 37)
+    heap, toast = str(tmp_path / "24576"), str(tmp_path / "24580")
+    da.write_partition(heap, toast, bufs, dist_key=3, dep_inline=dep_inline)
+    r = da.DirectAccessReader(heap, toast)
+    assert len(r) == 5
+    got = r.read(nthreads=4)
+    for (dk, bid, a, b), (bid0, x, y) in zip(sorted(got, key=lambda t: t[1]), bufs):
+        assert dk == 3 and bid == bid0
+        assert np.array_equal(np.frombuffer(a.tobytes(), np.float32).reshape(x.shape), x)
+        assert np.array_equal(np.frombuffer(b.tobytes(), np.int16).reshape(y.shape), y)
+
+
+def test_multi_segment_files_and_many_chunks(tmp_path):
+    rng = np.random.RandomState(2)
+    bufs = _bufs(rng, 6, 200, hw=16)   # ~600 KB per buffer, random -> ~74 chunks each
+    heap, toast = str(tmp_path / "h"), str(tmp_path / "t")
+    da.write_partition(heap, toast, bufs, dist_key=0, seg_bytes=4 * 32768)
+    assert os.path.exists(toast + ".1") and os.path.exists(toast + ".5")
+    r = da.DirectAccessReader(heap, toast)
+    got = {bid: (a, b) for _, bid, a, b in r.read(nthreads=3)}
+    for bid, x, y in bufs:
+        assert np.array_equal(np.frombuffer(got[bid][0].tobytes(), np.float32).reshape(x.shape), x)
+
+
+def test_page_layout_matches_reference_parser(tmp_path):
+    """Decode our heap page with the reference's documented struct layouts."""
+    rng = np.random.RandomState(3)
+    heap, toast = str(tmp_path / "h"), str(tmp_path / "t")
+    da.write_partition(heap, toast, _bufs(rng, 2, 5), dist_key=7, dep_inline=False)
+    page = open(heap, "rb").read(32768)
+    lsn, tli, flags, lower, upper, special, psv, prune = struct.unpack("@qHHHHHHI", page[:24])
+    assert special == 32768 and (lower - 24) % 4 == 0
+    lp = struct.unpack("@I", page[24:28])[0]
+    bits = "{:032b}".format(lp)
+    lp_len, lp_flags, lp_off = int(bits[:15], 2), int(bits[15:17], 2), int(bits[17:], 2)
+    assert lp_flags == 1
+    item = page[lp_off:lp_off + lp_len]
+    t_hoff = struct.unpack("@IIIHHHHHB", item[:23])[-1]
+    tup = item[t_hoff:]
+    assert struct.unpack("@I", tup[:4])[0] == 7                       # __dist_key__
+    ind = struct.unpack("@BBBBiiII", tup[4:24])
+    assert ind[0] == 0x80                                            # 1B_E external
+    assert ind[4] == 5 * 8 * 8 * 3 * 4 + 4                           # va_rawsize
+    assert struct.unpack("@I", tup[-4:])[0] in (0, 1)                # buffer_id
+
+
+def test_corrupt_toast_detected(tmp_path):
+    rng = np.random.RandomState(4)
+    heap, toast = str(tmp_path / "h"), str(tmp_path / "t")
+    da.write_partition(heap, toast, _bufs(rng, 1, 50), dist_key=0)
+    data = bytearray(open(toast, "rb").read())
+    data[-100] ^= 0xFF   # flip bytes inside the first-written chunk's payload
+    data[-101] ^= 0x5A
+    open(toast, "wb").write(bytes(data))
+    r = da.DirectAccessReader(heap, toast)
+    try:
+        out = r.read()
+        # corruption inside literal bytes can decode "successfully" but differently
+        assert out is not None
+    except IOError as e:
+        assert "corrupt" in str(e) or "size" in str(e)
+
+
+def test_dataset_writer_and_input_fn(tmp_path):
+    root = str(tmp_path / "gp")
+    man = da.write_dataset(root, "imagenet", 2, n_train=12, n_valid=5, buffer_size=5)
+    data_cat, sys_cat = da.generate_cats(root, 2)
+    assert data_cat["train_availability"] == [[1, 0], [0, 1]]
+    out = da.input_fn(os.path.join(root, data_cat["train"][1]))
+    assert sorted(out) == [0, 1, 2]
+    assert out[0]["independent_var"].shape == (5, 112, 112, 3)
+    assert out[2]["dependent_var"].shape == (2, 1000)
+    loader = da.da_partition_loader(root, "cpu")
+    tx, ty, vx, vy = loader(1)
+    assert tx.shape == (12, 112, 112, 3) and tx.dtype.is_floating_point is False
+    from cerebro_ds_kpgi_amd.data import synthetic
+    x_ref, y_ref = synthetic.image_partition(12, seed=2018 * 1000 + 2)
+    assert (tx == x_ref).all() and (ty == y_ref).all()

@@ -45,11 +45,12 @@ def test_adam_matches_torch():
     torch.testing.assert_close(a.work.float(), b.work.float(), rtol=1e-2, atol=1e-3)
 
 
-@pytest.mark.parametrize("N,G,B", [(1000, 8, 32), (2, 4, 64), (10, 3, 8)])
-def test_softmax_ce_matches_torch(N, G, B):
+@pytest.mark.parametrize("N,G,B,dt", [(1000, 8, 32, torch.bfloat16), (1000, 8, 32, torch.float32),
+                                      (2, 4, 64, torch.float32), (10, 3, 8, torch.bfloat16)])
+def test_softmax_ce_matches_torch(N, G, B, dt):
     from cerebro_ds_kpgi_amd.ops.loss import softmax_ce
     torch.manual_seed(1)
-    z = (3 * torch.randn(B, G * N, device="cuda")).to(torch.bfloat16)
+    z = (3 * torch.randn(B, G * N, device="cuda")).to(dt)
     y = torch.randint(0, N, (G, B), device="cuda", dtype=torch.int32)
     acc1 = torch.zeros(G, 4, device="cuda")
     acc2 = torch.zeros(G, 4, device="cuda")
@@ -61,7 +62,10 @@ def test_softmax_ce_matches_torch(N, G, B):
     l2 = softmax_ce(z2, y, acc2, G)
     (l2 * torch.arange(1, G + 1, device="cuda")).sum().backward()
     torch.testing.assert_close(l1, l2, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(acc1, acc2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(acc1[:, 0], acc2[:, 0], rtol=1e-4, atol=1e-3)
+    # top-k counts: exact for fp32; bf16 logits can tie (tie order is arbitrary)
+    tol = 0 if dt == torch.float32 else 1
+    assert (acc1[:, 1:] - acc2[:, 1:]).abs().max().item() <= tol
     torch.testing.assert_close(z1.grad.float(), z2.grad.float(), rtol=2e-2, atol=2e-4)
 
 
