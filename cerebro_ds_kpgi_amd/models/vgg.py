@@ -44,9 +44,9 @@ class PackedVGG16(PackedNet):
         first = True
         for blk in self.convs:
             for conv, bias in blk:
-                x = self.conv(x, conv, anchor=first)
+                x = P.conv2d_bias_act(x, self.ref(conv.w), self.ref(bias), conv.stride, conv.pad,
+                                      act=1, anchor=self.anchor if first else None)
                 first = False
-                x = P.bias_act(x, self.ref(bias), relu=True)
             x = P.maxpool2d(x, 2, 2, 0)
         B, H, W, GC = x.shape
         G = self.G

@@ -123,7 +123,7 @@ def gather_images(X, Y, perm, part_of_row, cursor, B, x_out, y_out):
 # ---------------------------------------------------------------------------
 _SIGS.update({
     "cer_conv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p,
-                     c_i, c_i, c_p],
+                     c_i, c_i, c_p, c_i64, c_i, c_p],
     "cer_conv_dgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_i, c_i, c_i, c_i,
                        c_p, c_i, c_i, c_p],
     "cer_conv_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
@@ -157,7 +157,8 @@ def _bf16(t):
     return t.contiguous()
 
 
-def conv2d_fwd(x, wref, stride, pad):
+def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
+    """y = act(conv(x, W) + b): bias and activation fused in the GEMM epilogue."""
     x = _bf16(x)
     B, H, W, GC = x.shape
     G = wref.G
@@ -167,8 +168,9 @@ def conv2d_fwd(x, wref, stride, pad):
     Wo = (W + 2 * pad - kw) // stride + 1
     y = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
+    bp, bs = bref.work_ptr() if bref is not None else (0, 0)
     rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
-                            _ptr(y), Ho, Wo, _stream())
+                            _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
     _check(rc, "cer_conv_fwd")
     return y
 
@@ -349,13 +351,10 @@ def linear_fwd(x, wref, bref, act):
     N, K = wref.spec.shape
     y = torch.empty((B, G * N), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
+    bp, bs = bref.work_ptr() if bref is not None else (0, 0)
     rc = lib().cer_conv_fwd(_ptr(x), B, 1, 1, K, G, c_p(wp), ws, N, 1, 1, 1, 0, _ptr(y), 1, 1,
-                            _stream())
+                            c_p(bp), bs, _act_code(act), _stream())
     _check(rc, "cer_conv_fwd(linear)")
-    if bref is not None or act:
-        if bref is None:
-            raise NotImplementedError("linear without bias")
-        bias_act_fwd(y, bref, act, out=y)
     return y
 
 

@@ -78,12 +78,15 @@ class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, = ctx.saved_tensors
+        return PackedConv2d.backward_core(ctx, x, dy.contiguous(), ctx.needs_input_grad[0])
+
+    @staticmethod
+    def backward_core(ctx, x, dy, need_dx):
         wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
-        dy = dy.contiguous()
         dx = None
         if use_hip("conv", x):
             h = _hip()
-            if ctx.needs_input_grad[0]:
+            if need_dx:
                 dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad)
             h.conv2d_wgrad(x, dy, wref, stride, pad)
         else:
@@ -91,7 +94,7 @@ class PackedConv2d(torch.autograd.Function):
             cout, kh, kw, cin = wref.spec.shape
             w = _torch_weight(wref)
             xn, dyn = _nchw(x), _nchw(dy)
-            if ctx.needs_input_grad[0]:
+            if need_dx:
                 dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, G))
             dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, G)
             wref.grad().copy_(dw.view(G, cout, cin, kh, kw).permute(0, 1, 3, 4, 2))
@@ -100,6 +103,35 @@ class PackedConv2d(torch.autograd.Function):
 
 def conv2d(x, wref, stride=1, pad=0, anchor=None):
     return PackedConv2d.apply(x, anchor, wref, stride, pad)
+
+
+class PackedConvBiasAct(torch.autograd.Function):
+    """y = act(conv(x) + b) — BN-free conv layers (VGG); bias + activation are
+    fused into the HIP GEMM epilogue (one bf16 rounding, no extra pass)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, wref, bref, stride, pad, act):
+        ctx.wref, ctx.bref, ctx.stride, ctx.pad, ctx.act = wref, bref, stride, pad, act
+        if use_hip("conv", x) and use_hip("bias", x):
+            y = _hip().conv2d_fwd(x, wref, stride, pad, bref, act)
+        else:
+            w = _torch_weight(wref)
+            z = F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G)
+            z = z.float() + bref.work().reshape(1, -1, 1, 1).float()
+            y = _nhwc(_act(z, act).to(x.dtype))
+        ctx.save_for_backward(x, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y = ctx.saved_tensors
+        dz = PackedBiasAct.backward_core(dy.contiguous(), y, ctx.bref, ctx.act)
+        dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
+        return dx, None, None, None, None, None, None
+
+
+def conv2d_bias_act(x, wref, bref, stride=1, pad=0, act=1, anchor=None):
+    return PackedConvBiasAct.apply(x, anchor, wref, bref, stride, pad, act)
 
 
 # ---------------------------------------------------------------------------
@@ -208,18 +240,17 @@ class PackedBiasAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         y, = ctx.saved_tensors
-        bref = ctx.bref
-        dy = dy.contiguous()
+        return PackedBiasAct.backward_core(dy.contiguous(), y, ctx.bref, ctx.relu), None, None
+
+    @staticmethod
+    def backward_core(dy, y, bref, act):
+        """dz = act'(y) * dy; dbias = sum_rows dz written into the arena."""
         if use_hip("bias", y):
-            dx = _hip().bias_act_bwd(dy, y, bref, ctx.relu)
-        else:
-            C = y.shape[-1]
-            dz = dy.reshape(-1, C).float()
-            if ctx.relu:
-                dz = dz * (y.reshape(-1, C) > 0)
-            bref.grad().copy_(dz.sum(0).view(bref.grad().shape))
-            dx = dz.to(dy.dtype).view(dy.shape)
-        return dx, None, None
+            return _hip().bias_act_bwd(dy, y, bref, act)
+        C = y.shape[-1]
+        dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), act)
+        bref.grad().copy_(dz.sum(0).view(bref.grad().shape))
+        return dz.to(dy.dtype).view(dy.shape)
 
 
 def bias_act(x, bref, relu=True):

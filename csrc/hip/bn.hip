@@ -146,17 +146,42 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
 // ---------------------------------------------------------------------------
 // stage 2: finalize
 // ---------------------------------------------------------------------------
-__global__ void bn_finalize_fwd(const float* __restrict__ part, int slabs, float* __restrict__ ws,
-                                float* mean_out, float* invstd_out, float* rmean, float* rvar,
-                                int64_t rstat_stride, int64_t M, int C, int Cper, float eps,
-                                float momentum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// one block = 32 channels x 8 slab lanes; lanes strided over slabs, LDS tree
+constexpr int FIN_C = 32, FIN_L = 8;
+
+__device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int slabs, int C,
+                                          float* a_out, float* b_out) {
+  __shared__ float sa[FIN_L][FIN_C], sb[FIN_L][FIN_C];
+  const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
+  const int c = blockIdx.x * FIN_C + cl;
   float a = 0.f, b = 0.f;
-  for (int k = 0; k < slabs; ++k) {
-    a += part[(int64_t)k * 2 * C + c];
-    b += part[(int64_t)k * 2 * C + C + c];
+  if (c < C)
+    for (int k = ln; k < slabs; k += FIN_L) {
+      a += part[(int64_t)k * 2 * C + c];
+      b += part[(int64_t)k * 2 * C + C + c];
+    }
+  sa[ln][cl] = a;
+  sb[ln][cl] = b;
+  __syncthreads();
+  if (ln == 0) {
+#pragma unroll
+    for (int k = 1; k < FIN_L; ++k) {
+      a += sa[k][cl];
+      b += sb[k][cl];
+    }
   }
+  *a_out = a;
+  *b_out = b;
+}
+
+__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_fwd(
+    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
+    float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, int64_t M, int C,
+    int Cper, float eps, float momentum) {
+  float a, b;
+  sum_slabs(part, slabs, C, &a, &b);
+  const int c = blockIdx.x * FIN_C + threadIdx.x;
+  if (threadIdx.x >= FIN_C || c >= C) return;
   const float inv_m = 1.f / (float)M;
   const float mu = a * inv_m;
   const float var = fmaxf(b * inv_m - mu * mu, 0.f);
@@ -173,15 +198,13 @@ __global__ void bn_finalize_fwd(const float* __restrict__ part, int slabs, float
   *rv = (1.f - momentum) * *rv + momentum * unb;
 }
 
-__global__ void bn_finalize_bwd(const float* __restrict__ part, int slabs, float* __restrict__ ws,
-                                float* dgamma, float* dbeta, int64_t gstride, int C, int Cper) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, b = 0.f;
-  for (int k = 0; k < slabs; ++k) {
-    a += part[(int64_t)k * 2 * C + c];
-    b += part[(int64_t)k * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
+    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* dgamma,
+    float* dbeta, int64_t gstride, int C, int Cper) {
+  float a, b;
+  sum_slabs(part, slabs, C, &a, &b);
+  const int c = blockIdx.x * FIN_C + threadIdx.x;
+  if (threadIdx.x >= FIN_C || c >= C) return;
   ws[c] = a;
   ws[C + c] = b;
   const int g = c / Cper, cc = c - g * Cper;
@@ -278,7 +301,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
 // ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
-constexpr int RED_TARGET = 1024, RED_MIN_ROWS = 32;
+constexpr int RED_TARGET = 512, RED_MIN_ROWS = 64;
 constexpr int APPLY_TARGET = 2048, APPLY_MIN_ROWS = 16;
 
 // floats of scratch the partials need (part[slabs][2][C])
@@ -303,7 +326,7 @@ CER_API int cer_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
                                           rrows, 0, mp);
-  bn_finalize_fwd<<<cer_blocks(C, 256), 256, 0, stream>>>(part, (int)rg.y, ws, mean_out,
+  bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
                                                           M, C, Cper, eps, momentum);
   bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
@@ -339,7 +362,7 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   bn_partials<1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows, act, mp);
-  bn_finalize_bwd<<<cer_blocks(C, 256), 256, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
+  bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
   bn_apply_bwd<<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws,
                                         Strided{gamma, gamma_stride}, dx, dres, M, C, Cper, arows,

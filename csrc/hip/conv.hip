@@ -53,6 +53,9 @@ struct NTParams {
   bf16_t* out;            // [M][ldc] with config block at g*N
   int ldc;
   int M, N, K;
+  const bf16_t* bias;     // optional fused epilogue: out = act(acc + bias[g][n])
+  int64_t bias_gstride;
+  int act;                // 0 none, 1 relu, 6 relu6
 };
 
 struct WGParams {
@@ -246,8 +249,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
     __syncthreads();
   }
 
-  // epilogue: stage the bf16 tile in LDS, then 16-B coalesced stores
+  // epilogue: (bias + act in fp32, one rounding), stage the bf16 tile in
+  // LDS, then 16-B coalesced stores
   constexpr int LDE = BN + 8;
+  float bcol[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + 16 * j + fr;
+    bcol[j] = (p.bias && n < p.N) ? bf2f(p.bias[(int64_t)cfg * p.bias_gstride + n]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -256,7 +266,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
       for (int e = 0; e < 4; ++e) {
         const int r = wm * TM + 16 * i + 4 * fc + e;
         const int c = wn * TN + 16 * j + fr;
-        lds[r * LDE + c] = f2bf(acc[i][j][e]);
+        float v = acc[i][j][e] + bcol[j];
+        v = p.act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (p.act ? fmaxf(v, 0.f) : v);
+        lds[r * LDE + c] = f2bf(v);
       }
   __syncthreads();
   constexpr int CPR = BN / 8;
@@ -492,8 +504,12 @@ static int run_nt(const NTParams& p, int G, hipStream_t stream) {
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
-                         bf16_t* y, int Ho, int Wo, hipStream_t stream) {
+                         bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
+                         int act, hipStream_t stream) {
   NTParams p;
+  p.bias = bias;
+  p.bias_gstride = bias_gstride;
+  p.act = act;
   p.a = GatherGeom{x, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad};
   p.dgrad = 0;
   p.w = w;
@@ -515,6 +531,9 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   dim3 tg(((Cout + 31) / 32) * ((Cin + 31) / 32), T, G);
   transpose_w_kernel<<<tg, 256, 0, stream>>>(w, w_gstride, wt, Cout, T, Cin);
   NTParams p;
+  p.bias = nullptr;
+  p.bias_gstride = 0;
+  p.act = 0;
   p.a = GatherGeom{dy, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad};
   p.dgrad = 1;
   p.w = wt;

@@ -15,6 +15,6 @@ echo "== bench torch"; date
 timeout -k 10 500 python bench.py --steps 30 --warmup 10 --steps_per_round 10 --backend torch > gpurun_out/bench_torch.log 2>&1 || { echo "bench torch failed"; tail -30 gpurun_out/bench_torch.log; exit 1; }
 tail -1 gpurun_out/bench_torch.log
 echo "== rocprof"; date
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o prof -- python3 bench.py --steps 20 --warmup 10 --steps_per_round 10 > gpurun_out/prof3.log 2>&1
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o prof -- python3 bench.py --steps 20 --warmup 10 --steps_per_round 10 > gpurun_out/prof4.log 2>&1
 echo "rocprof rc=$?"
-find gpurun_out/prof3 -name "*stats*"
+find gpurun_out/prof4 -name "*stats*"

@@ -54,6 +54,9 @@ CONV_CASES = [
     (2, 7, 7, 1024, 2048, 1, 2, 0, 1),
     (2, 112, 112, 3, 64, 7, 2, 3, 2),      # stem (unaligned path)
     (2, 9, 11, 24, 40, 3, 2, 1, 2),        # odd everything
+    (8, 28, 28, 256, 512, 1, 1, 0, 4),     # 128x128 NT tiles (>= 512 tiles)
+    (8, 28, 28, 128, 128, 3, 1, 1, 8),     # 128x128 NT fwd + dgrad, 3x3
+    (16, 14, 14, 512, 256, 1, 2, 0, 8),    # strided 1x1 with big tiles
 ]
 
 
@@ -192,26 +195,38 @@ def test_vgg_bias_act_matches_oracle():
 
 
 @pytest.mark.parametrize("model", ["resnet50", "vgg16", "mobilenetv2"])
-def test_full_model_step_matches_oracle(model):
+def test_full_model_step_vs_fp32_reference(model):
+    """Whole-model fwd+bwd.  Gradients of a freshly initialised deep net are
+    chaotic (a 1e-3 input perturbation moves even the fp32 reference's
+    gradient by ~80 %, see scripts/debug/grad_sens.py), so the criterion is
+    relative: against an fp32 PyTorch reference, our bf16 HIP path must be no
+    worse than PyTorch's own bf16 path (loss and gradient error)."""
     from cerebro_ds_kpgi_amd.models import create_model_from_mst
     from cerebro_ds_kpgi_amd.ops.loss import softmax_ce
-    G, B = 2, 4
+    G, B = 2, 8
     torch.manual_seed(11)
-    x = torch.randn(B, 112, 112, 3 * G, device="cuda").to(torch.bfloat16)
+    x = torch.randn(B, 112, 112, 3 * G, device="cuda")
     y = torch.randint(0, 1000, (G, B), device="cuda", dtype=torch.int32)
-    res = []
-    for force in ([], ["conv", "bn", "pool", "bias", "linear", "dwconv"]):
+    every = ["conv", "bn", "pool", "bias", "linear", "dwconv", "loss", "adam", "gather"]
+
+    def run(force, dtype):
         backend.force_torch_ops(force)
         net = create_model_from_mst({"model": model})
-        a = Arena(net.layout, G, "cuda", torch.bfloat16)
+        a = Arena(net.layout, G, "cuda", dtype)
         for g in range(G):
             a.init_model(g, 100 + g)
         net.bind(a)
         acc = torch.zeros(G, 4, device="cuda")
-        loss = softmax_ce(net.forward(x, True), y, acc, G)
+        loss = softmax_ce(net.forward(x.to(dtype), True), y, acc, G)
         loss.sum().backward()
         torch.cuda.synchronize()
-        res.append((loss.detach(), a.grad.clone()))
-    backend.force_torch_ops([])
-    torch.testing.assert_close(res[0][0], res[1][0], rtol=2e-2, atol=2e-2)
-    assert _rel(res[0][1], res[1][1]) < 5e-2
+        backend.force_torch_ops([])
+        return loss.detach(), a.grad.clone()
+    l32, g32 = run(every, torch.float32)
+    lh, gh = run([], torch.bfloat16)
+    lt, gt = run(every, torch.bfloat16)
+    err_h = ((gh - g32).norm() / g32.norm()).item()
+    err_t = ((gt - g32).norm() / g32.norm()).item()
+    assert torch.isfinite(gh).all()
+    assert (lh - l32).abs().max() <= max(3 * (lt - l32).abs().max().item(), 0.05)
+    assert err_h <= 1.15 * err_t + 0.02, (err_h, err_t)
