@@ -1,0 +1,80 @@
+"""Summarise a rocprofv3 SQLite output (``--kernel-trace --stats``) as markdown.
+
+    python -m cerebro_ds_kpgi_amd.tools.prof_summary gpurun_out/prof4 > profiles/x.md
+
+Groups kernels into the framework's op families (conv fwd/dgrad/wgrad, BN,
+pooling, optimizer, loss, data, torch glue) and reports time per step.
+"""
+
+import glob
+import os
+import re
+import sqlite3
+import sys
+
+FAMILIES = [
+    ("conv/linear GEMM (MFMA, NT: fwd+dgrad)", r"igemm_nt"),
+    ("conv/linear wgrad (MFMA, TN)", r"igemm_wgrad"),
+    ("weight transpose (dgrad)", r"transpose_w"),
+    ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),
+    ("pooling", r"maxpool|gavg"),
+    ("bias/act", r"bias_act|bias_grad"),
+    ("adam (fused, flat arena)", r"adam"),
+    ("softmax-CE + metrics", r"softmax_ce"),
+    ("batch gather (HBM store)", r"gather_images"),
+    ("memset/copy (runtime)", r"__amd_rocclr|fillBuffer|copyBuffer"),
+    ("torch elementwise glue", r"at::native"),
+]
+
+
+def find_db(path):
+    if path.endswith(".db"):
+        return path
+    dbs = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
+    if not dbs:
+        raise SystemExit("no .db under {}".format(path))
+    return dbs[0]
+
+
+def summarize(path, steps=None, title=None):
+    con = sqlite3.connect(find_db(path))
+    rows = list(con.execute("select name, total_calls, total_duration, average from top_kernels"))
+    total = sum(r[2] for r in rows)
+    fam = {}
+    for name, calls, dur, avg in rows:
+        key = "other"
+        for label, pat in FAMILIES:
+            if re.search(pat, name):
+                key = label
+                break
+        f = fam.setdefault(key, [0, 0.0])
+        f[0] += calls
+        f[1] += dur
+    out = []
+    out.append("# {}".format(title or "rocprofv3 kernel summary"))
+    out.append("")
+    out.append("source: `{}`; total GPU kernel time {:.1f} ms{}".format(
+        os.path.relpath(find_db(path)), total / 1000.0,
+        "" if not steps else " over {} steps = {:.2f} ms/step".format(steps, total / 1000.0 / steps)))
+    out.append("")
+    out.append("| family | calls | time (ms) | share |")
+    out.append("|---|---:|---:|---:|")
+    for label, (calls, dur) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        out.append("| {} | {} | {:.2f} | {:.1f}% |".format(label, calls, dur / 1000.0,
+                                                         100.0 * dur / total))
+    out.append("")
+    out.append("## top kernels")
+    out.append("")
+    out.append("| kernel | calls | total (ms) | avg (us) | share |")
+    out.append("|---|---:|---:|---:|---:|")
+    for name, calls, dur, avg in rows[:25]:
+        short = name if len(name) < 90 else name[:87] + "..."
+        out.append("| `{}` | {} | {:.2f} | {:.1f} | {:.1f}% |".format(
+            short.replace("|", "\\|"), calls, dur / 1000.0, avg, 100.0 * dur / total))
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    title = sys.argv[3] if len(sys.argv) > 3 else None
+    sys.stdout.write(summarize(sys.argv[1], steps, title))
