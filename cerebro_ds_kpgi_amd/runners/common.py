@@ -1,0 +1,116 @@
+"""Shared driver for every ``run_*`` entry point.
+
+Each reference approach maps onto one engine of this framework:
+
+=================================  ============================================
+reference approach                  here
+=================================  ============================================
+DA-Cerebro / Cerebro standalone     MOP, greedy randomized scheduler
+                                    (``--da`` reads Greenplum-format pages)
+UDAF (``madlib_keras_fit_multiple``) MOP, lock-step rotation scheduler
+CTQ                                 MOP, greedy scheduler (seeded shuffle)
+MA (``madlib_keras_fit``)           ``MAEngine`` (RCCL weighted averaging)
+PyTorch DDP / DA-DDP                ``DDPEngine`` (RCCL gradient all-reduce)
+Hyperopt-Spark                      MOP ``task`` scheduler + TPE batches
+*-Hyperopt over MOP                 MOP + async TPE ``mst_eval_fn``
+=================================  ============================================
+
+Timing follows ``runner_helper.sh``: ``global.log`` gets the Start/End lines
+and ``TOTAL EXECUTION TIME OVER ALL MST {s}``; data loading (ETL) is timed
+and reported separately (the reference's ``DA`` vs ``DA_w_ETL``).
+"""
+
+import json
+import os
+import time
+
+from ..ops import set_backend
+from ..parallel import init_distributed, shutdown
+from ..runtime.baselines import DDPEngine, MAEngine
+from ..runtime.engine import EngineOptions, MOPEngine
+from ..selection import hyperopt_helper as hh
+from ..utils.cli import main_prepare
+from ..utils.logging import GlobalLog, logs
+
+
+def _loader(args, device):
+    if not getattr(args, "da", False):
+        return None
+    from ..data import da
+    root = args.da_root or os.path.join(args.logs_root or "/tmp", "da_data")
+    if not os.path.exists(os.path.join(root, da.MANIFEST)):
+        raise SystemExit("--da needs a DA dataset at --da_root (create one with "
+                         "python -m cerebro_ds_kpgi_amd.tools.make_da_data)")
+    return da.da_partition_loader(root, device)
+
+
+def _opts(args, scheduler, loader):
+    return EngineOptions(
+        slots_per_gpu=args.slots_per_gpu, scheduler=scheduler,
+        n_train=args.train_per_partition, n_valid=args.valid_per_partition,
+        compute_dtype=args.compute_dtype, hop_optimizer_state=args.hop_optimizer_state,
+        l2=(args.l2_mode == "adam_wd"), logs_root=args.logs_root, models_root=args.models_root,
+        seed=2018, shuffle=args.shuffle or scheduler == "greedy", fault_inject=args.fault_inject,
+        dataset=("criteo" if args.criteo else None), store_loader=loader)
+
+
+def run_approach(approach, argv=None, shuffle=True):
+    args, msts = main_prepare(argv, shuffle=shuffle, verbose=True)
+    if not args.run:
+        logs("nothing to do (pass --run)")
+        return None
+    ctx = init_distributed(backend=args.dist_backend)
+    set_backend(args.backend)
+    exp = approach
+    glog = None
+    if ctx.rank == 0 and args.logs_root:
+        glog = GlobalLog(os.path.dirname(os.path.abspath(args.logs_root)) or ".", exp)
+        glog.start()
+    t0 = time.time()
+    loader = _loader(args, ctx.device)
+    tpe_state = None
+    if args.hyperopt and approach not in ("ma", "ddp"):
+        # initial batch proposed by TPE (model ids == trial order)
+        tpe_state = hh.init_hyperopt(args=args)
+        msts = tpe_state[1]
+    if approach in ("ma",):
+        eng = MAEngine(msts, ctx, _opts(args, "rotation", loader))
+    elif approach in ("ddp",):
+        eng = DDPEngine(msts, ctx, _opts(args, "rotation", loader))
+    else:
+        sched = {"udaf": "rotation", "ctq": "greedy", "cerebro": args.scheduler,
+                 "task": "task"}[approach]
+        eng = MOPEngine(msts, ctx, _opts(args, sched, loader))
+    etl = getattr(eng, "data_load_time", 0.0)
+    mst_eval = None
+    if isinstance(eng, MOPEngine):
+        if tpe_state is not None:
+            hp, _, trials, domain, rand, _ = tpe_state
+            mst_eval = hh.mst_eval_fn_hyperopt(args.num_epochs, hp, trials, domain,
+                                               args.max_num_config, rand, len(msts))
+        else:
+            mst_eval = hh.mst_eval_fn(args.num_epochs)
+        epochs = 10 ** 6 if args.hyperopt else args.num_epochs
+        eng.run(epochs, mst_eval_fn=mst_eval)
+    else:
+        eng.run(args.num_epochs)
+    train_s = time.time() - t0
+    images = eng.train_images
+    if ctx.initialized:
+        images = sum(ctx.all_gather_object(images))
+    if ctx.rank == 0:
+        makespan = glog.end() if glog else train_s
+        summary = {"approach": approach, "gpus": ctx.world, "configs": len(eng.msts),
+                   "epochs": args.num_epochs, "makespan_s": makespan, "etl_s": etl,
+                   "train_images": images, "agg_img_per_s": images / max(train_s, 1e-9),
+                   "mst_state": {str(k): v for k, v in eng.mst_state.items()}}
+        logs("SUMMARY {}".format(json.dumps({k: v for k, v in summary.items()
+                                              if k != "mst_state"})))
+        if args.logs_root:
+            os.makedirs(args.logs_root, exist_ok=True)
+            with open(os.path.join(args.logs_root, "summary.json"), "w") as f:
+                json.dump(summary, f, indent=1, default=str)
+    if hasattr(eng, "close"):
+        eng.close()
+    shutdown(ctx)
+    return eng

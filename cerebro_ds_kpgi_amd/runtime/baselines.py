@@ -1,0 +1,167 @@
+"""Comparison baselines on the same runtime.
+
+* ``MAEngine`` — model averaging, the reference's in-DB MA approach
+  (``madlib_keras_fit``; ``cerebro_gpdb/run_imagenet.py:46-108``, merge format
+  ``madlib_keras_wrapper.py:37-116``): every epoch each GPU trains every
+  config on its local partition starting from the same weights, then the
+  weights (and BN statistics) are averaged weighted by image count — an
+  RCCL all-reduce of ``count * w`` and ``count``.  The optimizer is rebuilt
+  every epoch, as a MADlib fit transition does.
+* ``DDPEngine`` — synchronous data parallel per config (the reference's
+  PyTorch DDP baseline, ``cerebro_gpdb/run_pytorchddp.py:204-519``): each
+  step every GPU computes gradients on its own partition's batch and the flat
+  gradient arena is all-reduced (one bucket per pack group) before the fused
+  Adam step.  Per-rank batch = the MST's batch size (reference default;
+  ``--pytorchddp_sanity`` divides it by the world size).
+* Task parallelism (Hyperopt-Spark, D6) is ``MOPEngine`` with
+  ``scheduler="task"``: data replicated on every GPU, whole models per GPU.
+
+All three reuse the pack groups (packed configs, HIP kernels, HIP graphs).
+"""
+
+import collections
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..data.store import PartitionStore
+from ..models import dataset_of, pack_key
+from ..utils.keys import model_key
+from .engine import default_sizes
+from .group import PackGroup
+
+
+class _GroupEngine(object):
+    """Shared setup: one local partition per GPU, every config on every GPU."""
+
+    mode = "base"
+
+    def __init__(self, msts, ctx, opts):
+        self.msts = [dict(m) for m in msts]
+        self.ctx = ctx
+        self.o = opts
+        self.device = ctx.device
+        self.dataset = opts.dataset or dataset_of(self.msts[0]["model"])
+        self.P = ctx.world
+        self.my_parts = [ctx.rank]
+        n_tr, n_va = default_sizes(self.dataset, self.P)
+        self.n_train = opts.n_train or n_tr
+        self.n_valid = opts.n_valid or n_va
+        self.dtype = torch.bfloat16 if opts.compute_dtype == "bf16" else torch.float32
+        self.store = PartitionStore(self.dataset, self.my_parts, self.n_train, self.n_valid,
+                                    self.device, seed=opts.seed, loader=opts.store_loader)
+        by_key = collections.defaultdict(list)
+        for m in range(len(self.msts)):
+            by_key[pack_key(self.msts[m])].append(m)
+        self.groups = {k: PackGroup(k, ms, self.msts, self.store, self.device, self.dtype,
+                                    seed_base=opts.seed * 100,
+                                    use_graphs=opts.use_graphs and self.mode != "ddp",
+                                    l2=opts.l2)
+                       for k, ms in by_key.items()}
+        self.mst_state = {m: {"train_loss": [], "valid_loss": [], "train_top5_error": [],
+                              "valid_top5_error": [], "state": "RUNNING"}
+                          for m in range(len(self.msts))}
+        self.jobs_info = {}
+        self.train_images = 0
+
+    def _record(self, epoch, per_model):
+        for m, rec in per_model.items():
+            st = self.mst_state[m]
+            st["train_loss"].append(rec["train"]["loss"])
+            st["valid_loss"].append(rec["valid"]["loss"])
+            st["train_top5_error"].append(1 - rec["train"]["top5"])
+            st["valid_top5_error"].append(1 - rec["valid"]["top5"])
+            self.jobs_info.setdefault(epoch, {})[(model_key(m, self.msts[m]), "ALL")] = rec
+
+    def _gather_metrics(self, w):
+        """Average the per-rank metrics (weighted by sample counts)."""
+        mets = w.read_metrics()
+        allm = self.ctx.all_gather_object(mets)
+        out = []
+        for row in range(w.G):
+            rec = {}
+            for ph in ("train", "valid"):
+                n = sum(r[row][ph]["n"] for r in allm) or 1
+                rec[ph] = {k: sum(r[row][ph][k] * r[row][ph]["n"] for r in allm) / n
+                           for k in ("loss", "top1", "top5")}
+                rec[ph]["n"] = n
+            out.append(rec)
+        return out
+
+    def close(self):
+        pass
+
+
+class MAEngine(_GroupEngine):
+    mode = "ma"
+
+    def run(self, num_epochs):
+        t0 = time.time()
+        for epoch in range(1, num_epochs + 1):
+            self.store.new_epoch(epoch)
+            per_model = {}
+            for key, grp in self.groups.items():
+                jobs = [(m, 0) for m in grp.model_ids]
+                w = grp.begin_round(jobs)
+                for row, (m, _) in enumerate(jobs):
+                    w.load_local(row, m)
+                w.prepare(hop_optimizer_state=False)      # fresh optimizer per fit iteration
+                B = grp.batch_size
+                steps = self.n_train // B
+                w.train_steps(steps)
+                self.train_images += steps * B * w.G
+                w.validate(max(1, self.n_valid // B))
+                mets = self._gather_metrics(w)
+                self._average(w, steps * B)
+                grp.end_round()
+                for row, (m, _) in enumerate(jobs):
+                    per_model[m] = mets[row]
+            self._record(epoch, per_model)
+        return time.time() - t0
+
+    def _average(self, w, count):
+        """w <- sum_r count_r * w_r / sum_r count_r over ranks (params + BN stats)."""
+        if not self.ctx.initialized:
+            return
+        master = w.arena.master
+        cnt = torch.tensor([float(count)], device=master.device)
+        master.mul_(float(count))
+        dist.all_reduce(master)
+        dist.all_reduce(cnt)
+        master.div_(cnt)
+        w.arena.sync_work()
+
+
+class DDPEngine(_GroupEngine):
+    mode = "ddp"
+
+    def run(self, num_epochs):
+        t0 = time.time()
+        world = self.ctx.world
+
+        def allreduce_grads(arena):
+            if self.ctx.initialized:
+                dist.all_reduce(arena.grad)
+                arena.grad.div_(world)
+        for epoch in range(1, num_epochs + 1):
+            self.store.new_epoch(epoch)
+            per_model = {}
+            for key, grp in self.groups.items():
+                jobs = [(m, 0) for m in grp.model_ids]
+                w = grp.begin_round(jobs)
+                for row, (m, _) in enumerate(jobs):
+                    w.load_local(row, m)
+                w.prepare(hop_optimizer_state=True)
+                w.grad_hook = allreduce_grads
+                B = grp.batch_size
+                steps = self.n_train // B
+                w.train_steps(steps)
+                self.train_images += steps * B * w.G
+                w.validate(max(1, self.n_valid // B))
+                mets = self._gather_metrics(w)
+                grp.end_round()
+                for row, (m, _) in enumerate(jobs):
+                    per_model[m] = mets[row]
+            self._record(epoch, per_model)
+        return time.time() - t0

@@ -57,6 +57,7 @@ class EngineOptions(object):
         self.verbose = kw.get("verbose", True)
         self.dataset = kw.get("dataset", None)
         self.store_loader = kw.get("store_loader", None)
+        self.partitions = kw.get("partitions", 0)
 
 
 def default_sizes(dataset, P):
@@ -77,10 +78,19 @@ class MOPEngine(object):
         self.device = ctx.device
         S = len(self.msts)
         self.dataset = opts.dataset or dataset_of(self.msts[0]["model"])
-        V = opts.slots_per_gpu or max(1, S // ctx.world)
-        self.V = V
-        self.P = V * ctx.world
-        self.my_parts = list(range(ctx.rank * V, (ctx.rank + 1) * V))
+        self.task_parallel = opts.scheduler == "task"
+        if self.task_parallel:
+            # Hyperopt-Spark semantics: every GPU holds the WHOLE dataset (P
+            # partitions replicated; the full ImageNet-112 uint8 fits in HBM)
+            # and trains whole models; no hops.
+            self.P = opts.partitions or 8
+            self.V = self.P
+            self.my_parts = list(range(self.P))
+        else:
+            V = opts.slots_per_gpu or max(1, S // ctx.world)
+            self.V = V
+            self.P = V * ctx.world
+            self.my_parts = list(range(ctx.rank * V, (ctx.rank + 1) * V))
         n_tr, n_va = default_sizes(self.dataset, self.P)
         self.n_train = opts.n_train or n_tr
         self.n_valid = opts.n_valid or n_va
@@ -128,7 +138,12 @@ class MOPEngine(object):
                 self.group_of[m] = self.groups[key]
 
     def owner(self, p):
+        if self.task_parallel:
+            return (p // self.P) % self.ctx.world
         return p // self.V
+
+    def local_part(self, p):
+        return p % self.P if self.task_parallel else self.store.local[p]
 
     def log(self, msg):
         if self.o.verbose and self.ctx.rank == 0:
@@ -143,8 +158,8 @@ class MOPEngine(object):
         moves = plan_moves(holder, dest)
         validate_plan(moves, self.ctx.world)
         # working sets per group on this rank
-        mine = sorted(((m, self.store.local[p]) for p, m in rnd.items() if self.owner(p) == rank),
-                      key=lambda t: t[1])
+        mine = sorted(((m, self.local_part(p)) for p, m in rnd.items() if self.owner(p) == rank),
+                      key=lambda t: (t[1], t[0]))
         per_group = collections.defaultdict(list)
         for m, lp in mine:
             per_group[self.group_of[m].key].append((m, lp))
@@ -314,7 +329,18 @@ class MOPEngine(object):
         self.writer.flush()
         return time.time() - t0
 
+    def _run_task_epoch(self, epoch, active, max_steps=None):
+        """Task parallel: models are pinned to ranks round-robin; in round r
+        every rank trains all its models on (its replica of) partition r.
+        Round keys are pseudo-partitions m * P + r (see ``owner``)."""
+        for r in range(self.P):
+            rnd = {m * self.P + r: m for m in active}
+            self.run_round(rnd, epoch, max_steps)
+
     def _run_epoch_rounds(self, epoch, max_steps=None):
+        if self.task_parallel:
+            self._run_task_epoch(epoch, list(self.sched.models), max_steps)
+            return
         if self.sched.lockstep:
             while True:
                 rnd = self.sched.next_round()

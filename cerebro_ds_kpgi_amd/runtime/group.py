@@ -113,6 +113,8 @@ class _Working(object):
         self.graph = None
         self.eager_steps = 0
         self.jobs = []
+        # called between backward and the optimizer (DDP gradient all-reduce)
+        self.grad_hook = None
 
     def assign(self, jobs):
         self.jobs = list(jobs)
@@ -144,6 +146,8 @@ class _Working(object):
         logits = self.net.forward(self.x, True)
         loss = softmax_ce(logits, self.y, self.acc, self.G)
         loss.sum().backward()
+        if self.grad_hook is not None:
+            self.grad_hook(self.arena)
         adam_step(self.arena, l2=g.l2)
         self.cursor.add_(1)
 

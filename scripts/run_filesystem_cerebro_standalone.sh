@@ -1,0 +1,7 @@
+#!/bin/bash
+# Cerebro standalone (reference run_filesystem_cerebro_standalone.sh)
+EXP_NAME=e2e_filesystem_cerebro_standalone
+source "$(dirname "$0")/runner_helper.sh" "$@"
+PRINT_START
+LAUNCH run_filesystem_cerebro_standalone --logs_root "$LOG_DIR/$EXP_NAME" --models_root "$MODEL_DIR" --run --num_epochs "$EPOCHS" --size "$SIZE" --scheduler greedy $OPTIONS 2>&1 | tee "$LOG_DIR/$EXP_NAME/client.log"
+PRINT_END

@@ -1,0 +1,77 @@
+"""Entry points, schedule() facade, baselines and async TPE over MOP (CPU)."""
+
+import json
+import os
+
+import pytest
+
+os.environ.setdefault("CEREBRO_BACKEND", "torch")
+
+
+def _ctx():
+    from cerebro_ds_kpgi_amd.parallel import init_distributed
+    return init_distributed(device_type="cpu")
+
+
+def _tiny(n=2, lrs=(1e-3, 1e-2, 3e-3, 2e-3)):
+    return [{"learning_rate": lrs[i], "lambda_value": 1e-4, "batch_size": 8, "model": "tinycnn"}
+            for i in range(n)]
+
+
+def test_run_mop_cli_writes_global_log(tmp_path):
+    from cerebro_ds_kpgi_amd.runners import run_mop
+    logs = tmp_path / "run_logs" / "cerebro"
+    run_mop.main(["--run", "--tiny", "--num_epochs", "1", "--train_per_partition", "32",
+                  "--valid_per_partition", "16", "--compute_dtype", "fp32", "--backend", "torch",
+                  "--logs_root", str(logs), "--models_root", str(tmp_path / "models")])
+    g = (tmp_path / "run_logs" / "global.log").read_text().splitlines()
+    assert g[0].startswith("udaf, Start time:") and g[1].startswith("udaf, End time:")
+    assert g[2].startswith("udaf, TOTAL EXECUTION TIME OVER ALL MST ")
+    summ = json.loads((logs / "summary.json").read_text())
+    assert summ["configs"] == 2 and summ["train_images"] == 2 * 2 * 32
+
+
+def test_schedule_facade_grid_search(tmp_path):
+    from cerebro_ds_kpgi_amd.api import schedule
+    from cerebro_ds_kpgi_amd.selection.hyperopt_helper import mst_eval_fn
+    state = schedule(data_set_name="tiny", initial_msts=_tiny(3), mst_eval_fn=mst_eval_fn(2),
+                     ckpt_root=str(tmp_path / "ck"), log_files_root=str(tmp_path / "lg"),
+                     ctx=_ctx(), n_train=32, n_valid=16, compute_dtype="fp32", verbose=False,
+                     slots_per_gpu=2)
+    assert all(len(s["train_loss"]) == 2 and s["state"] == "COMPLETED" for s in state.values())
+
+
+def test_async_tpe_over_mop():
+    """Cerebro-hyperopt contract: configs finishing their epochs report to TPE
+    and new configs join the running MOP until max_num_config."""
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    from cerebro_ds_kpgi_amd.selection import hyperopt_helper as hh
+    grid = {"learning_rate": [1e-4, 1e-1], "lambda_value": [1e-4], "batch_size": [8, 8],
+            "model": ["tinycnn"]}
+
+    class A:
+        size = 2
+    hp, msts, trials, domain, rand, _ = hh.init_hyperopt(grid, A())
+    eng = MOPEngine(msts, _ctx(), EngineOptions(n_train=32, n_valid=16, compute_dtype="fp32",
+                                                verbose=False, ckpt_every="none",
+                                                slots_per_gpu=2))
+    fn = hh.mst_eval_fn_hyperopt(1, hp, trials, domain, 6, rand, 2, param_grid=grid)
+    eng.run(10, mst_eval_fn=fn)
+    assert len(eng.msts) == 6
+    assert all(s["state"] == "COMPLETED" for s in eng.mst_state.values())
+    assert len(trials.completed()) == 6
+
+
+@pytest.mark.parametrize("engine", ["ma", "ddp", "task"])
+def test_baseline_engines_train(engine):
+    from cerebro_ds_kpgi_amd.runtime.baselines import DDPEngine, MAEngine
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    o = EngineOptions(n_train=64, n_valid=16, compute_dtype="fp32", verbose=False,
+                      ckpt_every="none", scheduler="task" if engine == "task" else "rotation",
+                      partitions=2)
+    cls = {"ma": MAEngine, "ddp": DDPEngine, "task": MOPEngine}[engine]
+    eng = cls(_tiny(2), _ctx(), o)
+    eng.run(3)
+    for st in eng.mst_state.values():
+        assert len(st["train_loss"]) == 3
+        assert st["train_loss"][-1] < st["train_loss"][0]
