@@ -182,7 +182,9 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad):
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
     dx = torch.empty((B, H, W, G * cin), dtype=torch.bfloat16, device=dy.device)
-    wt = torch.empty(G * cout * kh * kw * cin, dtype=torch.bfloat16, device=dy.device)
+    # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
+    n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
+    wt = torch.empty(n_wt, dtype=torch.bfloat16, device=dy.device)
     wp, ws = wref.work_ptr()
     rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh, kw,
                               stride, pad, _ptr(dx), H, W, _stream())
@@ -374,7 +376,7 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     if not need_dx:
         return None
     dx = torch.empty((B, G * K), dtype=torch.bfloat16, device=dy.device)
-    wt = torch.empty(G * N * K, dtype=torch.bfloat16, device=dy.device)
+    wt = torch.empty(G * N * K if (N % 8 or K % 8) else 1, dtype=torch.bfloat16, device=dy.device)
     wp, ws = wref.work_ptr()
     rc = L.cer_conv_dgrad(_ptr(dz), B, 1, 1, N, G, c_p(wp), ws, _ptr(wt), K, 1, 1, 1, 0,
                           _ptr(dx), 1, 1, _stream())
