@@ -51,7 +51,10 @@ def _opts(args, scheduler, loader):
         compute_dtype=args.compute_dtype, hop_optimizer_state=args.hop_optimizer_state,
         l2=(args.l2_mode == "adam_wd"), logs_root=args.logs_root, models_root=args.models_root,
         seed=2018, shuffle=args.shuffle or scheduler == "greedy", fault_inject=args.fault_inject,
-        dataset=("criteo" if args.criteo else None), store_loader=loader)
+        dataset=("criteo" if args.criteo else None), store_loader=loader,
+        trace=args.trace, resume=args.resume, max_retries=args.max_retries,
+        heartbeat=args.heartbeat,
+        ckpt_every=args.ckpt_every or ("subepoch" if args.best_model_run else "epoch"))
 
 
 def run_approach(approach, argv=None, shuffle=True):
@@ -67,6 +70,10 @@ def run_approach(approach, argv=None, shuffle=True):
         glog = GlobalLog(os.path.dirname(os.path.abspath(args.logs_root)) or ".", exp)
         glog.start()
     t0 = time.time()
+    mon = None
+    if args.trace and args.logs_root and ctx.local_rank == 0:
+        from ..utils.sysmon import SysMonitor
+        mon = SysMonitor(os.path.join(args.logs_root, "sys_logs")).start()
     loader = _loader(args, ctx.device)
     tpe_state = None
     if args.hyperopt and approach not in ("ma", "ddp"):
@@ -112,5 +119,7 @@ def run_approach(approach, argv=None, shuffle=True):
                 json.dump(summary, f, indent=1, default=str)
     if hasattr(eng, "close"):
         eng.close()
+    if mon is not None:
+        mon.stop()
     shutdown(ctx)
     return eng

@@ -18,11 +18,28 @@ Per round (= one sub-epoch on every partition):
 
 Epoch end: per-config train/valid summaries, ``mst_eval_fn`` (grid stopper or
 async TPE) and checkpoints in the CTQ layout.
+
+Failure handling (the reference only re-raises,
+``ctq.py:411-423``):
+
+* a *recoverable* job failure (``SoftFault``, e.g. an unreadable partition)
+  on one rank fails only that rank's (config, partition) pairs: the other
+  ranks' results commit, the failed pairs roll back to their pre-round
+  state (still parked in the previous holder's home row) and are re-run as
+  a sub-round, up to ``max_retries`` times;
+* a crash ends the job; with ``ckpt_every="subepoch"`` every round ends with
+  a consistent checkpoint + ``resume.json`` and ``resume=True`` (``--resume``)
+  continues from the next unfinished round of the interrupted epoch
+  (epoch-level resume with ``ckpt_every="epoch"``);
+* ``fault_inject="r:k[:soft|:exit]"`` raises (or soft-fails, or hard-exits)
+  rank r at sub-epoch k — the tests' injection hook.
 """
 
 import collections
+import json
 import math
 import os
+import pickle
 import time
 
 import torch
@@ -34,7 +51,9 @@ from ..parallel.hop import execute_moves, plan_moves, validate_plan
 from ..scheduler import make_scheduler
 from ..utils.keys import model_key, mst_2_str
 from ..utils.logging import logs
-from .checkpoint import AsyncWriter, ckpt_path, dump_infos, state_to_host, write_checkpoint
+from ..utils.trace import Tracer
+from .checkpoint import (AsyncWriter, ckpt_path, dump_infos, host_to_state, read_checkpoint,
+                         state_to_host, write_checkpoint)
 from .group import PackGroup
 
 
@@ -58,6 +77,17 @@ class EngineOptions(object):
         self.dataset = kw.get("dataset", None)
         self.store_loader = kw.get("store_loader", None)
         self.partitions = kw.get("partitions", 0)
+        self.trace = kw.get("trace", False)
+        self.max_retries = kw.get("max_retries", 2)
+        self.resume = kw.get("resume", False)
+        self.heartbeat = kw.get("heartbeat", 0)     # watchdog timeout (s); 0 = off
+
+
+class SoftFault(RuntimeError):
+    """A recoverable job failure: the failed pairs are requeued."""
+
+
+RESUME_FILE = "resume.json"
 
 
 def default_sizes(dataset, P):
@@ -116,6 +146,12 @@ class MOPEngine(object):
         self.hop_bytes = 0
         self.hop_time = 0.0
         self.epoch = 0
+        self.failures = []
+        self._fired = set()
+        self.tracer = Tracer(ctx.rank, enabled=opts.trace)
+        self._sync = torch.cuda.synchronize if self.device.type == "cuda" else None
+        self._metrics_path = (os.path.join(opts.logs_root, "metrics.jsonl")
+                              if opts.logs_root and ctx.rank == 0 else "")
         if ctx.rank == 0 and opts.logs_root:
             write_manifest(os.path.join(opts.logs_root, "manifest.json"),
                            make_data_catalog(self.dataset, self.P, ctx.world),
@@ -196,17 +232,25 @@ class MOPEngine(object):
         spec = self.o.fault_inject
         if not spec:
             return
-        r, k = [int(v) for v in spec.split(":")]
-        if r == self.ctx.rank and k == self.round_idx:
-            raise RuntimeError("FAULT INJECTED at rank {} sub-epoch {}".format(r, k))
+        f = spec.split(":")
+        r, k = int(f[0]), int(f[1])
+        kind = f[2] if len(f) > 2 else "raise"
+        if r != self.ctx.rank or k != self.round_idx or (r, k) in self._fired:
+            return
+        self._fired.add((r, k))
+        msg = "FAULT INJECTED at rank {} sub-epoch {}".format(r, k)
+        if kind == "soft":
+            raise SoftFault(msg)
+        if kind == "exit":
+            logs(msg + " (process exit)")
+            os._exit(3)
+        raise RuntimeError(msg)
 
-    def run_round(self, rnd, epoch, max_steps=None):
-        t_start = time.time()
-        per_group, moves = self._hop_and_load(rnd)
-        t_hop = time.time()
-        self._fault_check()
+    def _train_local(self, per_group, max_steps):
+        """Train + validate every local pack group; returns (results, images)."""
         results = []
         trained = 0
+        tr = self.tracer
         for key, jobs in per_group.items():
             grp = self.groups[key]
             w = grp.current
@@ -215,44 +259,113 @@ class MOPEngine(object):
             steps = self.n_train // B
             if max_steps is not None:
                 steps = min(steps, max_steps)
-            w.train_steps(steps)
+            with tr.span("train", sync=self._sync, arch=key[0], G=w.G, steps=steps):
+                w.train_steps(steps)
             trained += steps * B * w.G
             vsteps = self.n_valid // B
             if max_steps is not None:
                 # shortened sub-epoch (bench): keep the valid/train ratio
                 full = max(self.n_train // B, 1)
                 vsteps = max(1, int(math.ceil(vsteps * steps / full)))
-            w.validate(vsteps)
-            mets = w.read_metrics()
+            with tr.span("valid", sync=self._sync, arch=key[0], G=w.G, steps=vsteps):
+                w.validate(vsteps)
+                mets = w.read_metrics()
             for row, (m, lp) in enumerate(jobs):
                 results.append({"model": m, "dist_key": self.store.pids[lp], "metrics": mets[row],
-                                "steps": steps, "batch": B})
-            grp.end_round()
+                                "steps": steps, "batch": B, "partition": lp})
+        return results, trained
+
+    def run_round(self, rnd, epoch, max_steps=None):
+        """One sub-epoch; failed (config, partition) pairs are requeued."""
+        pending = dict(rnd)
+        trained = 0
+        for attempt in range(self.o.max_retries + 1):
+            failed, images = self._attempt(pending, epoch, max_steps, attempt)
+            trained += images
+            if not failed:
+                break
+            pending = failed
+        else:
+            raise RuntimeError("sub-epoch {} failed {} times; giving up".format(
+                self.round_idx, self.o.max_retries + 1))
+        self.round_idx += 1
+        return trained
+
+    def _attempt(self, rnd, epoch, max_steps, attempt):
+        tr = self.tracer
+        prev_holder = dict(self.holder)
+        t_start = time.time()
+        with tr.span("hop", sync=self._sync, round=self.round_idx, attempt=attempt):
+            per_group, moves = self._hop_and_load(rnd)
+        t_hop = time.time()
+        error = None
+        results, trained = [], 0
+        try:
+            self._fault_check()
+            results, trained = self._train_local(per_group, max_steps)
+        except SoftFault as e:
+            error = str(e)
+        if error is None:
+            for key in per_group:
+                self.groups[key].end_round()
+        else:
+            # drop the working copies: the pre-round states are still parked
+            # in the previous holders' home rows
+            for key in per_group:
+                self.groups[key].current = None
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         t_end = time.time()
-        self.train_images += trained
         local = {"rank": self.ctx.rank, "results": results, "t_start": t_start, "t_hop": t_hop,
-                 "t_end": t_end}
-        gathered = self.ctx.all_gather_object(local)
+                 "t_end": t_end, "error": error}
+        with tr.span("report", round=self.round_idx):
+            gathered = self.ctx.all_gather_object(local)
+        failed = {}
         for g in gathered:
+            if g["error"] is not None:
+                for p, m in rnd.items():
+                    if self.owner(p) == g["rank"]:
+                        failed[p] = m
+                        self.holder[m] = prev_holder[m]
+                        fj = {"status": "FAILED", "epoch": epoch, "subepoch": self.round_idx,
+                              "attempt": attempt, "rank": g["rank"], "partition": p,
+                              "model_key": model_key(m, self.msts[m]), "error": g["error"]}
+                        self.failures.append(fj)
+                        self.log("JOB FAILED {} on partition {} (rank {}): {} -> requeued".format(
+                            fj["model_key"], p, g["rank"], g["error"]))
+                continue
             for r in g["results"]:
-                m = r["model"]
-                mets = r["metrics"]
-                job = {"status": "SUCCESS", "epoch": epoch, "dist_key": r["dist_key"],
-                       "model_key": model_key(m, self.msts[m]),
-                       "loss_train": mets["train"]["loss"], "metric_train": mets["train"]["top5"],
-                       "loss_valid": mets["valid"]["loss"], "metric_valid": mets["valid"]["top5"],
-                       "top1_train": mets["train"]["top1"], "top1_valid": mets["valid"]["top1"],
-                       "n_train": mets["train"]["n"], "n_valid": mets["valid"]["n"],
-                       "start_time": g["t_start"], "end_time": g["t_end"],
-                       "init_time": 0.0, "train_time": g["t_end"] - g["t_hop"],
-                       "valid_time": 0.0, "exit_time": 0.0, "hop_time": g["t_hop"] - g["t_start"],
-                       "subepoch": self.round_idx}
-                self.jobs_info.setdefault(epoch, {})[(job["model_key"], r["dist_key"])] = job
-                self.models_info[job["model_key"]].append(job)
-        self.round_idx += 1
-        return trained
+                self._record_job(epoch, g, r)
+        if error is not None:
+            trained = 0
+        self.train_images += trained
+        return failed, trained
+
+    def _record_job(self, epoch, g, r):
+        m = r["model"]
+        mets = r["metrics"]
+        job = {"status": "SUCCESS", "epoch": epoch, "dist_key": r["dist_key"],
+               "model_key": model_key(m, self.msts[m]),
+               "loss_train": mets["train"]["loss"], "metric_train": mets["train"]["top5"],
+               "loss_valid": mets["valid"]["loss"], "metric_valid": mets["valid"]["top5"],
+               "top1_train": mets["train"]["top1"], "top1_valid": mets["valid"]["top1"],
+               "n_train": mets["train"]["n"], "n_valid": mets["valid"]["n"],
+               "start_time": g["t_start"], "end_time": g["t_end"],
+               "init_time": 0.0, "train_time": g["t_end"] - g["t_hop"],
+               "valid_time": 0.0, "exit_time": 0.0, "hop_time": g["t_hop"] - g["t_start"],
+               "subepoch": self.round_idx, "rank": g["rank"]}
+        self.jobs_info.setdefault(epoch, {})[(job["model_key"], r["dist_key"])] = job
+        self.models_info[job["model_key"]].append(job)
+        if self._metrics_path:
+            rec = {"epoch": epoch, "subepoch": self.round_idx, "cfg": job["model_key"],
+                   "partition": r["dist_key"], "rank": g["rank"],
+                   "loss": job["loss_train"], "top1": job["top1_train"],
+                   "top5": job["metric_train"], "valid_loss": job["loss_valid"],
+                   "valid_top1": job["top1_valid"], "valid_top5": job["metric_valid"],
+                   "img_s": job["n_train"] / max(job["train_time"], 1e-9),
+                   "hop_ms": job["hop_time"] * 1e3}
+            with open(self._metrics_path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
 
     # ------------------------------------------------------------------
     def _epoch_summary(self, epoch):
@@ -282,11 +395,13 @@ class MOPEngine(object):
             st["train_top1_error"].append(1 - a["t1"] / nt)
             st["valid_top1_error"].append(1 - a["v1"] / nv)
 
-    def checkpoint_all(self, epoch):
+    def checkpoint_all(self, epoch, models=None):
+        """Queue async checkpoints of the configs parked on this rank."""
         if not self.o.models_root:
             return
         os.makedirs(self.o.models_root, exist_ok=True)
-        for m in range(len(self.msts)):
+        ids = range(len(self.msts)) if models is None else models
+        for m in ids:
             h = self.holder[m]
             if h is None:
                 h = 0
@@ -295,68 +410,163 @@ class MOPEngine(object):
             grp = self.group_of[m]
             weights, opt = state_to_host(grp.layout, grp.state_row(m))
             path = ckpt_path(self.o.models_root, m, self.msts[m])
-            meta = {"epoch": epoch, "model_key": model_key(m, self.msts[m]),
-                    "mst": self.msts[m], "mst_str": mst_2_str(self.msts[m])}
+            meta = {"epoch": epoch, "subepoch": self.round_idx,
+                    "model_key": model_key(m, self.msts[m]),
+                    "mst": self.msts[m], "mst_str": mst_2_str(self.msts[m]),
+                    "partitions_visited": sorted(
+                        j["dist_key"] for j in self.jobs_info.get(epoch, {}).values()
+                        if j["model_key"] == model_key(m, self.msts[m]))}
             self.writer.submit(lambda p=path, w=weights, o=opt, mt=meta, L=grp.layout:
                                write_checkpoint(p, L, w, o, mt))
+
+    def _commit(self, epoch, rounds_done, epoch_done, sched_rng):
+        """Consistent restart point: every rank's checkpoint writes are on
+        disk before rank 0 publishes ``resume.json`` (atomic rename)."""
+        if not self.o.models_root:
+            return
+        with self.tracer.span("checkpoint", epoch=epoch, rounds=rounds_done):
+            self.writer.flush()
+            self.ctx.barrier()
+            if self.ctx.rank == 0:
+                if self.o.logs_root:
+                    dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
+                st = {"epoch": epoch, "rounds_done": rounds_done, "epoch_done": epoch_done,
+                      "round_idx": self.round_idx, "msts": self.msts,
+                      "states": {str(m): self.mst_state[m]["state"] for m in self.mst_state},
+                      "sched_rng": sched_rng, "failures": self.failures}
+                path = os.path.join(self.o.models_root, RESUME_FILE)
+                with open(path + ".tmp", "w") as f:
+                    json.dump(st, f, default=str)
+                os.replace(path + ".tmp", path)
+
+    def _resume(self):
+        """Load ``resume.json`` + checkpoints; returns (epoch, rounds_to_skip, rng)."""
+        path = os.path.join(self.o.models_root or "", RESUME_FILE)
+        if not self.o.models_root or not os.path.exists(path):
+            self.log("RESUME: no {} under models_root; starting fresh".format(RESUME_FILE))
+            return 1, 0, None
+        with open(path) as f:
+            st = json.load(f)
+        if len(st["msts"]) > len(self.msts):
+            self.add_msts(st["msts"][len(self.msts):])
+        for m in range(len(self.msts)):
+            weights, opt, _ = read_checkpoint(ckpt_path(self.o.models_root, m, self.msts[m]))
+            grp = self.group_of[m]
+            host_to_state(grp.layout, weights, opt, grp.state_row(m))
+            self.holder[m] = None            # every rank now holds the same copy
+            self.mst_state[m]["state"] = st["states"].get(str(m), "RUNNING")
+        lr = self.o.logs_root
+        if lr and os.path.exists(os.path.join(lr, "jobs_info.pkl")):
+            # files this framework wrote itself (dump_infos)
+            with open(os.path.join(lr, "jobs_info.pkl"), "rb") as f:
+                self.jobs_info = pickle.load(f)
+            with open(os.path.join(lr, "models_info.pkl"), "rb") as f:
+                self.models_info = collections.defaultdict(list, pickle.load(f))
+        for e in sorted(self.jobs_info):
+            if e < st["epoch"] or st["epoch_done"]:
+                self._epoch_summary(e)
+        self.round_idx = st["round_idx"]
+        self.failures = list(st.get("failures", []))
+        self.log("RESUME: epoch {} after {} sub-epochs{}".format(
+            st["epoch"], st["rounds_done"], " (epoch complete)" if st["epoch_done"] else ""))
+        if st["epoch_done"]:
+            return st["epoch"] + 1, 0, None
+        return st["epoch"], st["rounds_done"], st.get("sched_rng")
 
     def run(self, num_epochs, mst_eval_fn=None):
         """Full semantic run: ``num_epochs`` MOP epochs (reference ``schedule``)."""
         t0 = time.time()
-        for epoch in range(1, num_epochs + 1):
-            active = [m for m in range(len(self.msts)) if self.mst_state[m]["state"] == "RUNNING"]
-            if not active:
-                break
-            self.epoch = epoch
-            self.sched.models = list(active)
-            self.sched.start_epoch(epoch)
-            self.store.new_epoch(epoch)
-            self.log("EPOCH:{}".format(epoch))
-            self._run_epoch_rounds(epoch)
-            self._epoch_summary(epoch)
-            if self.ctx.rank == 0 and self.o.logs_root:
-                dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
-            if self.o.ckpt_every != "none":
-                self.checkpoint_all(epoch)
-            if mst_eval_fn is not None:
-                decision = mst_eval_fn(self.mst_state) if self.ctx.rank == 0 else None
-                decision = self.ctx.broadcast_object(decision)
-                stop, _, new_msts = decision
-                for m in stop:
-                    self.mst_state[m]["state"] = "COMPLETED"
-                if new_msts:
-                    self.add_msts(new_msts)
-        self.writer.flush()
+        first, skip, rng = (self._resume() if self.o.resume else (1, 0, None))
+        hb = self._start_heartbeat()
+        try:
+            for epoch in range(first, num_epochs + 1):
+                active = [m for m in range(len(self.msts))
+                          if self.mst_state[m]["state"] == "RUNNING"]
+                if not active:
+                    break
+                self.epoch = epoch
+                self.sched.models = list(active)
+                if rng is not None:
+                    self.sched.set_rng_state(rng)
+                rng_at_start = self.sched.rng_state()
+                self.sched.start_epoch(epoch)
+                self.store.new_epoch(epoch)
+                self.log("EPOCH:{}".format(epoch))
+                self._run_epoch_rounds(epoch, skip=skip, rng=rng_at_start)
+                skip, rng = 0, None
+                self._epoch_summary(epoch)
+                if self.ctx.rank == 0 and self.o.logs_root:
+                    dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
+                if mst_eval_fn is not None:
+                    decision = mst_eval_fn(self.mst_state) if self.ctx.rank == 0 else None
+                    decision = self.ctx.broadcast_object(decision)
+                    stop, _, new_msts = decision
+                    for m in stop:
+                        self.mst_state[m]["state"] = "COMPLETED"
+                    if new_msts:
+                        self.add_msts(new_msts)
+                if self.o.ckpt_every != "none":
+                    self.checkpoint_all(epoch)
+                    self._commit(epoch, -1, True, None)
+            self.writer.flush()
+        finally:
+            if hb is not None:
+                hb.stop()
         return time.time() - t0
 
-    def _run_task_epoch(self, epoch, active, max_steps=None):
+    def _start_heartbeat(self):
+        if not getattr(self.o, "heartbeat", 0) or not self.ctx.initialized:
+            return None
+        from ..parallel.health import Heartbeat, default_store
+        store = default_store()
+        if store is None:
+            return None
+        return Heartbeat(store, self.ctx.rank, self.ctx.world, timeout=self.o.heartbeat,
+                         logs_root=self.o.logs_root).start()
+
+    def _after_round(self, epoch, rnd, rounds_done, rng):
+        if self.o.ckpt_every == "subepoch":
+            self.checkpoint_all(epoch, models=sorted(set(rnd.values())))
+            self._commit(epoch, rounds_done, False, rng)
+
+    def _run_task_epoch(self, epoch, active, max_steps=None, skip=0, rng=None):
         """Task parallel: models are pinned to ranks round-robin; in round r
         every rank trains all its models on (its replica of) partition r.
         Round keys are pseudo-partitions m * P + r (see ``owner``)."""
-        for r in range(self.P):
+        for r in range(skip, self.P):
             rnd = {m * self.P + r: m for m in active}
             self.run_round(rnd, epoch, max_steps)
+            self._after_round(epoch, rnd, r + 1, rng)
 
-    def _run_epoch_rounds(self, epoch, max_steps=None):
+    def _run_epoch_rounds(self, epoch, max_steps=None, skip=0, rng=None):
         if self.task_parallel:
-            self._run_task_epoch(epoch, list(self.sched.models), max_steps)
+            self._run_task_epoch(epoch, list(self.sched.models), max_steps, skip, rng)
             return
+        k = 0
         if self.sched.lockstep:
             while True:
                 rnd = self.sched.next_round()
                 if rnd is None:
                     break
-                self.run_round(rnd, epoch, max_steps)
+                if k >= skip:
+                    self.run_round(rnd, epoch, max_steps)
                 self.sched.finish_round(rnd)
+                k += 1
+                if k > skip:
+                    self._after_round(epoch, rnd, k, rng)
         else:
             while not self.sched.epoch_done():
                 pairs = self.sched.assign_all_idle()
                 if not pairs:
                     raise RuntimeError("scheduler stalled")
                 rnd = {w: m for m, w in pairs}
-                self.run_round(rnd, epoch, max_steps)
+                if k >= skip:
+                    self.run_round(rnd, epoch, max_steps)
                 for m, w in pairs:
                     self.sched.complete(m, w)
+                k += 1
+                if k > skip:
+                    self._after_round(epoch, rnd, k, rng)
         self.sched.monitor.check_epoch_complete(self.sched.models)
 
     def add_msts(self, new_msts):
@@ -402,3 +612,5 @@ class MOPEngine(object):
 
     def close(self):
         self.writer.close()
+        if self.o.trace and self.o.logs_root:
+            self.tracer.dump(os.path.join(self.o.logs_root, "traces"))

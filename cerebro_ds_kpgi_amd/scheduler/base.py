@@ -96,6 +96,19 @@ class MOPScheduler(object):
     def remove_models(self, models):
         self.models = [m for m in self.models if m not in set(models)]
 
+    # -- resume support ---------------------------------------------------
+    def rng_state(self):
+        """JSON-able RNG state (None for deterministic policies)."""
+        rng = getattr(self, "rng", None)
+        if rng is None:
+            return None
+        v, internal, gauss = rng.getstate()
+        return [v, list(internal), gauss]
+
+    def set_rng_state(self, state):
+        if state is not None and getattr(self, "rng", None) is not None:
+            self.rng.setstate((state[0], tuple(state[1]), state[2]))
+
     # -- job lifecycle ----------------------------------------------------
     def assign(self, worker):
         raise NotImplementedError

@@ -84,10 +84,18 @@ def get_main_parser():
     p.add_argument("--backend", choices=["auto", "hip", "torch"], default="auto",
                    help="kernel backend: our HIP kernels or the PyTorch oracle")
     p.add_argument("--dist_backend", choices=["auto", "nccl", "gloo"], default="auto")
-    p.add_argument("--resume", action="store_true", help="resume from jobs_info in logs_root")
+    p.add_argument("--resume", action="store_true",
+                   help="resume from models_root/resume.json (+ jobs_info in logs_root)")
     p.add_argument("--fault_inject", type=str, default="",
-                   help="'rank:subepoch' — raise inside that sub-epoch (fault-injection tests)")
-    p.add_argument("--trace", action="store_true", help="write chrome-trace spans")
+                   help="'rank:subepoch[:soft|:exit]' — fail that sub-epoch (fault-injection tests)")
+    p.add_argument("--ckpt_every", choices=["epoch", "subepoch", "none"], default="",
+                   help="checkpoint cadence (default: subepoch with --best_model_run, else epoch)")
+    p.add_argument("--max_retries", type=int, default=2,
+                   help="requeues of a (config, partition) pair after a recoverable failure")
+    p.add_argument("--heartbeat", type=float, default=0.0,
+                   help="watchdog timeout in seconds for worker heartbeats (0 = off)")
+    p.add_argument("--trace", action="store_true",
+                   help="write chrome-trace spans (logs_root/traces) and 1 Hz system telemetry")
     p.add_argument("--da", action="store_true", help="read partitions through the Direct-Access page reader")
     p.add_argument("--da_root", type=str, default="", help="root of GP-format segment files")
     return p

@@ -1,0 +1,176 @@
+"""Failure detection, requeue, resume and observability.
+
+* a soft failure on one rank requeues only that rank's (config, partition)
+  pairs; the run ends bit-identical to a fault-free run,
+* a crash mid-epoch + ``resume=True`` from sub-epoch checkpoints ends
+  bit-identical to an uninterrupted run (rotation and greedy schedulers),
+* the heartbeat watchdog flags a silent rank,
+* chrome-trace spans, per-job metrics JSONL and the system sampler.
+"""
+
+import json
+import os
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from test_distributed import _free_port, _msts
+
+
+def _opts(outdir, **kw):
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions
+    base = dict(n_train=64, n_valid=16, compute_dtype="fp32", verbose=False,
+                models_root=os.path.join(outdir, "models"), logs_root=os.path.join(outdir, "logs"))
+    base.update(kw)
+    return EngineOptions(**base)
+
+
+def _states(eng):
+    return {m: eng.group_of[m].state_row(m).clone() for m in range(len(eng.msts))
+            if eng.holder[m] in (None, eng.ctx.rank)}
+
+
+def _run_soft(rank, world, port, outdir, fault):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "CEREBRO_BACKEND": "torch", "CEREBRO_QUIET": "1"})
+    torch.set_num_threads(1)
+    from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
+    from cerebro_ds_kpgi_amd.runtime.engine import MOPEngine
+    ctx = init_distributed(device_type="cpu")
+    eng = MOPEngine(_msts(), ctx, _opts(outdir, ckpt_every="none", fault_inject=fault))
+    eng.run(2)
+    torch.save(_states(eng), os.path.join(outdir, "states_{}.pt".format(rank)))
+    if rank == 0:
+        with open(os.path.join(outdir, "out.json"), "w") as f:
+            json.dump({"failures": eng.failures, "images": eng.train_images,
+                       "mst_state": {str(k): v for k, v in eng.mst_state.items()}}, f)
+    eng.close()
+    shutdown(ctx)
+
+
+def _launch_soft(tmp, fault):
+    os.makedirs(tmp, exist_ok=True)
+    mp.spawn(_run_soft, args=(2, _free_port(), tmp, fault), nprocs=2, join=True)
+    st = {}
+    for r in range(2):
+        st.update(torch.load(os.path.join(tmp, "states_{}.pt".format(r)), weights_only=True))
+    with open(os.path.join(tmp, "out.json")) as f:
+        return st, json.load(f)
+
+
+def test_soft_fault_requeues_only_failed_pairs(tmp_path):
+    ref, ref_out = _launch_soft(str(tmp_path / "ref"), "")
+    got, out = _launch_soft(str(tmp_path / "flt"), "1:1:soft")
+    fails = out["failures"]
+    # rank 1 owns partitions 2 and 3 -> exactly those two pairs failed once
+    assert sorted(f["partition"] for f in fails) == [2, 3]
+    assert all(f["rank"] == 1 and f["subepoch"] == 1 and f["attempt"] == 0 for f in fails)
+    assert out["mst_state"] == ref_out["mst_state"]
+    assert set(got) == set(ref)
+    for m in ref:
+        assert torch.equal(got[m], ref[m]), m
+
+
+def _engine(outdir, scheduler, **kw):
+    from cerebro_ds_kpgi_amd.parallel import DistContext
+    from cerebro_ds_kpgi_amd.runtime.engine import MOPEngine
+    return MOPEngine(_msts(), DistContext(), _opts(outdir, scheduler=scheduler,
+                                                   shuffle=True, **kw))
+
+
+@pytest.mark.parametrize("scheduler", ["rotation", "greedy"])
+def test_crash_then_resume_matches_uninterrupted(tmp_path, scheduler, monkeypatch):
+    monkeypatch.setenv("CEREBRO_BACKEND", "torch")
+    monkeypatch.setenv("CEREBRO_QUIET", "1")
+    torch.set_num_threads(2)
+    ref = _engine(str(tmp_path / "ref"), scheduler, ckpt_every="none")
+    ref.run(2)
+    want = _states(ref)
+    ref.close()
+
+    d = str(tmp_path / "run")
+    eng = _engine(d, scheduler, ckpt_every="subepoch", fault_inject="0:6")   # epoch 2, round 3
+    with pytest.raises(RuntimeError, match="FAULT INJECTED"):
+        eng.run(2)
+    eng.close()
+    with open(os.path.join(d, "models", "resume.json")) as f:
+        st = json.load(f)
+    assert st["epoch"] == 2 and st["rounds_done"] == 2 and not st["epoch_done"]
+
+    eng2 = _engine(d, scheduler, ckpt_every="subepoch", resume=True)
+    eng2.run(2)
+    got = _states(eng2)
+    for m in want:
+        assert torch.equal(got[m], want[m]), (scheduler, m)
+    for m in range(len(ref.msts)):
+        for k in ("train_loss", "valid_loss"):
+            assert eng2.mst_state[m][k] == pytest.approx(ref.mst_state[m][k], rel=1e-6)
+    eng2.close()
+
+
+def test_epoch_resume_skips_finished_epochs(tmp_path, monkeypatch):
+    monkeypatch.setenv("CEREBRO_BACKEND", "torch")
+    monkeypatch.setenv("CEREBRO_QUIET", "1")
+    d = str(tmp_path)
+    eng = _engine(d, "rotation", ckpt_every="epoch")
+    eng.run(1)
+    eng.close()
+    eng2 = _engine(d, "rotation", ckpt_every="epoch", resume=True)
+    eng2.run(2)
+    assert eng2.round_idx == 8          # 4 rounds of epoch 1 restored + 4 run
+    assert all(len(eng2.mst_state[m]["train_loss"]) == 2 for m in range(4))
+    eng2.close()
+
+
+def test_heartbeat_watchdog_flags_silent_rank(tmp_path):
+    from torch.distributed import HashStore
+    from cerebro_ds_kpgi_amd.parallel.health import Heartbeat
+    store = HashStore()
+    seen = []
+    w0 = Heartbeat(store, 0, 2, interval=0.05, timeout=0.4, logs_root=str(tmp_path),
+                   on_failure=seen.append)
+    w1 = Heartbeat(store, 1, 2, interval=0.05, timeout=0.4)
+    w1.start()
+    w0.start()
+    time.sleep(0.3)
+    assert not seen and w0.check() == []
+    w1.stop()                      # rank 1 goes silent
+    deadline = time.time() + 5
+    while not seen and time.time() < deadline:
+        time.sleep(0.05)
+    w0.stop()
+    assert seen == [[1]]
+    with open(os.path.join(str(tmp_path), "failed_workers.json")) as f:
+        assert json.load(f)["lost"] == [1]
+
+
+def test_trace_spans_and_metrics_jsonl(tmp_path, monkeypatch):
+    monkeypatch.setenv("CEREBRO_BACKEND", "torch")
+    monkeypatch.setenv("CEREBRO_QUIET", "1")
+    d = str(tmp_path)
+    eng = _engine(d, "rotation", ckpt_every="none", trace=True)
+    eng.run(1)
+    eng.close()
+    with open(os.path.join(d, "logs", "traces", "trace_rank0.json")) as f:
+        ev = json.load(f)["traceEvents"]
+    names = {e["name"] for e in ev}
+    assert {"hop", "train", "valid", "report"} <= names
+    assert sum(e["name"] == "train" for e in ev) == 4
+    with open(os.path.join(d, "logs", "metrics.jsonl")) as f:
+        rows = [json.loads(l) for l in f]
+    assert len(rows) == 16
+    assert {r["partition"] for r in rows} == {0, 1, 2, 3}
+    assert all(r["img_s"] > 0 and r["loss"] > 0 for r in rows)
+
+
+def test_sysmon_sampler(tmp_path):
+    from cerebro_ds_kpgi_amd.utils.sysmon import SysMonitor, summarize
+    mon = SysMonitor(str(tmp_path), interval=0.05, gpus=False).start()
+    time.sleep(0.3)
+    mon.stop()
+    s = summarize(mon.path)
+    assert s["seconds"] > 0 and s["cpu_util_mean"] is not None
+    assert s["disk_read_gb"] >= 0 and s["net_gb"] >= 0

@@ -75,3 +75,22 @@ def test_baseline_engines_train(engine):
     for st in eng.mst_state.values():
         assert len(st["train_loss"]) == 3
         assert st["train_loss"][-1] < st["train_loss"][0]
+
+
+def test_log_analyzer_breakdown(tmp_path):
+    """--trace run -> analyzer reproduces makespan + breakdown categories."""
+    from cerebro_ds_kpgi_amd.runners import run_da_cerebro_standalone as r
+    from cerebro_ds_kpgi_amd.tools import log_analyzer as la
+    logs = tmp_path / "run_logs" / "da"
+    r.main(["--run", "--tiny", "--num_epochs", "2", "--train_per_partition", "32",
+            "--valid_per_partition", "16", "--compute_dtype", "fp32", "--backend", "torch",
+            "--trace", "--logs_root", str(logs), "--models_root", str(tmp_path / "models")])
+    res = la.main(["--logs_root", str(logs), "--json", str(tmp_path / "a.json")])
+    assert res["exp"] and res["makespan_s"] > 0
+    bd = res["breakdown"]
+    assert set(bd["gpu_seconds"]) == set(la.CATEGORIES)
+    assert bd["gpu_seconds"]["train_valid"] > 0 and sorted(bd["per_epoch"]) == [1, 2]
+    assert abs(sum(bd["fraction"].values()) - 1.0) < 1e-6 or bd["gpu_seconds"]["idle"] == 0
+    assert {"hop", "train", "valid"} <= set(res["trace_seconds"])
+    assert res["best"]["epochs"] == [1, 2]
+    assert list(res["system"].values())[0]["seconds"] >= 0
