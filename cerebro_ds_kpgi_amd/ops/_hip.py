@@ -129,6 +129,7 @@ _SIGS.update({
     "cer_conv_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                        c_p, c_i64, c_i, c_p],
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
+    "cer_conv_set_variant": [c_i, c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_bn_fwd_train": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p,
                          c_p, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
@@ -157,6 +158,66 @@ def _bf16(t):
     return t.contiguous()
 
 
+# Kernel-variant autotuning (the MIOpen "find" step, done by the framework):
+# every conv problem is timed once under each of the 6 kernel variants
+# (register-staged / LDS-DMA ring x 64x64 / 128x128 / 128x64 tiles) on its
+# first eager call and the fastest is pinned for all later calls, including
+# HIP-graph capture.  CER_CONV_TUNE=0 keeps the built-in heuristic.
+NVARIANTS = 6
+_TUNED = {}
+_PINNED = {}
+
+
+def _tune_enabled():
+    return os.environ.get("CER_CONV_TUNE", "1") != "0"
+
+
+def _select(op, key, launch):
+    if op in _PINNED:
+        lib().cer_conv_set_variant(op, _PINNED[op])
+        return
+    v = _TUNED.get((op, key))
+    if v is None:
+        v = -1
+        if _tune_enabled() and not torch.cuda.is_current_stream_capturing():
+            v = _autotune(op, launch)
+        _TUNED[(op, key)] = v
+    lib().cer_conv_set_variant(op, v)
+
+
+def _autotune(op, launch, reps=3):
+    L = lib()
+    best, best_v = None, -1
+    for v in range(NVARIANTS):
+        L.cer_conv_set_variant(op, v)
+        launch()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            launch()
+        e.record()
+        e.synchronize()
+        t = s.elapsed_time(e)
+        if best is None or t < best:
+            best, best_v = t, v
+    return best_v
+
+
+def tuned_variants():
+    """{(op, problem key): variant} chosen so far (for logs / profiles)."""
+    return dict(_TUNED)
+
+
+def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,
+                     act):
+    def launch():
+        rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
+                                _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
+        _check(rc, "cer_conv_fwd")
+    _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    launch()
+
+
 def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     """y = act(conv(x, W) + b): bias and activation fused in the GEMM epilogue."""
     x = _bf16(x)
@@ -169,10 +230,21 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     y = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
-    rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
-                            _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
-    _check(rc, "cer_conv_fwd")
+    _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs, act)
     return y
+
+
+def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W):
+    # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
+    n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
+    wt = torch.empty(n_wt, dtype=torch.bfloat16, device=dy.device)
+
+    def launch():
+        rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
+                                  kw, stride, pad, _ptr(dx), H, W, _stream())
+        _check(rc, "cer_conv_dgrad")
+    _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W), launch)
+    launch()
 
 
 def conv2d_dgrad(dy, wref, xshape, stride, pad):
@@ -182,14 +254,33 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad):
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
     dx = torch.empty((B, H, W, G * cin), dtype=torch.bfloat16, device=dy.device)
-    # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
-    n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
-    wt = torch.empty(n_wt, dtype=torch.bfloat16, device=dy.device)
     wp, ws = wref.work_ptr()
-    rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh, kw,
-                              stride, pad, _ptr(dx), H, W, _stream())
-    _check(rc, "cer_conv_dgrad")
+    _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W)
     return dx
+
+
+def conv_set_variant(op, v):
+    """Pin a conv kernel variant (tuning): op 0 fwd / 1 dgrad / 2 wgrad; v -1 = unpin."""
+    if v < 0:
+        _PINNED.pop(int(op), None)
+    else:
+        _PINNED[int(op)] = int(v)
+    lib().cer_conv_set_variant(int(op), int(v))
+
+
+def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref):
+    gp, gs = wref.grad_ptr()
+
+    def launch():
+        L = lib()
+        splits = L.cer_wgrad_splits(B * Ho * Wo, cout, kh * kw * cin, G)
+        if splits > 1:
+            wref.grad().zero_()
+        rc = L.cer_conv_wgrad(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride,
+                              pad, c_p(gp), gs, splits, _stream())
+        _check(rc, "cer_conv_wgrad")
+    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    launch()
 
 
 def conv2d_wgrad(x, dy, wref, stride, pad):
@@ -199,14 +290,7 @@ def conv2d_wgrad(x, dy, wref, stride, pad):
     _, Ho, Wo, _ = dy.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
-    L = lib()
-    splits = L.cer_wgrad_splits(B * Ho * Wo, cout, kh * kw * cin, G)
-    if splits > 1:
-        wref.grad().zero_()
-    gp, gs = wref.grad_ptr()
-    rc = L.cer_conv_wgrad(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride, pad,
-                          c_p(gp), gs, splits, _stream())
-    _check(rc, "cer_conv_wgrad")
+    _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref)
 
 
 # ---------------------------------------------------------------------------
@@ -354,9 +438,7 @@ def linear_fwd(x, wref, bref, act):
     y = torch.empty((B, G * N), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
-    rc = lib().cer_conv_fwd(_ptr(x), B, 1, 1, K, G, c_p(wp), ws, N, 1, 1, 1, 0, _ptr(y), 1, 1,
-                            c_p(bp), bs, _act_code(act), _stream())
-    _check(rc, "cer_conv_fwd(linear)")
+    _conv_fwd_launch(x, B, 1, 1, K, G, wp, ws, N, 1, 1, 1, 0, y, 1, 1, bp, bs, act)
     return y
 
 
@@ -365,20 +447,10 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     N, K = wref.spec.shape
     B = x.shape[0]
     dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _bf16(dy)
-    L = lib()
-    splits = L.cer_wgrad_splits(B, N, K, G)
-    if splits > 1:
-        wref.grad().zero_()
-    gp, gs = wref.grad_ptr()
-    rc = L.cer_conv_wgrad(_ptr(_bf16(x)), B, 1, 1, K, G, _ptr(dz), 1, 1, N, 1, 1, 1, 0,
-                          c_p(gp), gs, splits, _stream())
-    _check(rc, "cer_conv_wgrad(linear)")
+    _conv_wgrad_launch(_bf16(x), B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref)
     if not need_dx:
         return None
     dx = torch.empty((B, G * K), dtype=torch.bfloat16, device=dy.device)
-    wt = torch.empty(G * N * K if (N % 8 or K % 8) else 1, dtype=torch.bfloat16, device=dy.device)
     wp, ws = wref.work_ptr()
-    rc = L.cer_conv_dgrad(_ptr(dz), B, 1, 1, N, G, c_p(wp), ws, _ptr(wt), K, 1, 1, 1, 0,
-                          _ptr(dx), 1, 1, _stream())
-    _check(rc, "cer_conv_dgrad(linear)")
+    _conv_dgrad_launch(dz, B, 1, 1, N, G, wp, ws, K, 1, 1, 1, 0, dx, 1, 1)
     return dx

@@ -89,14 +89,56 @@ def bench_shape(shape, G, iters):
     return out
 
 
+VARIANTS = {0: "reg64", 1: "reg128", 2: "reg128x64", 3: "dma64", 4: "dma128", 5: "dma128x64"}
+
+
+def sweep(shapes, G, iters):
+    """Time every kernel variant of every op on every shape (HIP only)."""
+    out = []
+    for shape, count in shapes.items():
+        B, H, W, cin, cout, k, st, pad = shape
+        if cin % 8:
+            continue
+        spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+        a = Arena(ModelLayout([spec]), G, "cuda", torch.bfloat16)
+        for g in range(G):
+            a.init_model(g, g)
+        ref = ParamRef(a, spec)
+        x = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+        Ho = (H + 2 * pad - k) // st + 1
+        Wo = (W + 2 * pad - k) // st + 1
+        dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(torch.bfloat16)
+        row = {"shape": shape, "count": count}
+        ops = {0: lambda: _hip.conv2d_fwd(x, ref, st, pad),
+               1: lambda: _hip.conv2d_dgrad(dy, ref, x.shape, st, pad),
+               2: lambda: _hip.conv2d_wgrad(x, dy, ref, st, pad)}
+        for op, fn in ops.items():
+            for v in VARIANTS:
+                _hip.conv_set_variant(op, v)
+                row["{}:{}".format(op, VARIANTS[v])] = _time(fn, iters)
+            _hip.conv_set_variant(op, -1)
+            row["{}:auto".format(op)] = _time(fn, iters)
+        out.append(row)
+        print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()}),
+              flush=True)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--G", type=int, default=8)
     ap.add_argument("--B", type=int, default=32)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
+    ap.add_argument("--sweep", action="store_true", help="time every kernel variant per shape")
     a = ap.parse_args(argv)
     backend.set_backend("hip")
+    if a.sweep:
+        rows = sweep(resnet50_shapes(a.B), a.G, a.iters)
+        if a.json:
+            with open(a.json, "w") as f:
+                json.dump(rows, f, indent=1, default=str)
+        return
     rows = []
     tot = collections.defaultdict(float)
     for shape, count in resnet50_shapes(a.B).items():

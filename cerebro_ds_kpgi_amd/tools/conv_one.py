@@ -1,0 +1,28 @@
+"""Run one packed conv shape's fwd / dgrad / wgrad a few times (profiling target).
+
+    python -m cerebro_ds_kpgi_amd.tools.conv_one --shape 32,7,7,256,256,3,1,1 --G 8 --iters 20
+"""
+
+import argparse
+
+import torch
+
+from ..ops import backend
+from .bench_conv import bench_shape
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="32,7,7,256,256,3,1,1")
+    ap.add_argument("--G", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args(argv)
+    backend.set_backend("hip")
+    shape = tuple(int(v) for v in a.shape.split(","))
+    r = bench_shape(shape, a.G, a.iters)
+    torch.cuda.synchronize()
+    print(shape, {k: round(v, 1) for k, v in r["tflops"].items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -13,7 +13,8 @@ import sqlite3
 import sys
 
 FAMILIES = [
-    ("conv/linear GEMM (MFMA, NT: fwd+dgrad)", r"igemm_nt"),
+    ("conv/linear GEMM (MFMA, NT: fwd)", r"igemm_nt"),
+    ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad"),
     ("conv/linear wgrad (MFMA, TN)", r"igemm_wgrad"),
     ("weight transpose (dgrad)", r"transpose_w"),
     ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),

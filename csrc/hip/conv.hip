@@ -1,5 +1,5 @@
 // Grouped implicit-GEMM convolution / linear on MFMA for packed NHWC
-// (SURVEY.md K4-K6, K8).  G configs are trained at once: blockIdx.z = config
+// (SURVEY.md K4-K6, K8).  G configs are trained at once: work item -> config
 // g, whose activations are channel block g of the packed tensor and whose
 // weights sit at w + g*w_gstride in the arena.
 //
@@ -68,12 +68,13 @@ struct GatherGeom {
   int Hs, Ws;         // gathered tensor spatial dims
   int Hm, Wm;         // GEMM row grid (pixels of the GEMM's M dimension)
   int kh, kw, st, pad;
-  FastDiv dWm, dHm, dCg, dkw;
+  uint32_t bytes;     // size of src in bytes (buffer-load range); 0 = too big for 32-bit offsets
+  FastDiv dWm, dHm, dCg, dkw, dst;
 };
 
 struct NTParams {
   GatherGeom a;
-  int dgrad;              // 0: hi = y*st - pad + r ; 1: (y + pad - r) / st if divisible
+  int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
   const bf16_t* w;        // [N][K] per config
   int64_t w_gstride;
   bf16_t* out;            // [M][ldc] with config block at g*N
@@ -93,21 +94,48 @@ struct WGParams {
   int64_t dw_gstride;
   int Mred, N, K;
   int m_per_split;
+  int splits;
 };
 
-static GatherGeom make_geom(const bf16_t* src, int Ctot, int Cg, int Hs, int Ws, int Hm, int Wm,
-                            int kh, int kw, int st, int pad) {
-  GatherGeom g{src, Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad, {}, {}, {}, {}};
+static GatherGeom make_geom(const bf16_t* src, int B, int Ctot, int Cg, int Hs, int Ws, int Hm,
+                            int Wm, int kh, int kw, int st, int pad) {
+  GatherGeom g{src, Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad, 0u, {}, {}, {}, {}, {}};
+  const uint64_t bytes = (uint64_t)B * Hs * Ws * Ctot * sizeof(bf16_t);
+  g.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   g.dWm = make_div((uint32_t)Wm);
   g.dHm = make_div((uint32_t)Hm);
   g.dCg = make_div((uint32_t)Cg);
   g.dkw = make_div((uint32_t)kw);
+  g.dst = make_div((uint32_t)st);
   return g;
 }
 
 // ---------------------------------------------------------------------------
 // gather helpers
 // ---------------------------------------------------------------------------
+// Gather modes.  The fast modes (8-channel aligned operands) are branch-free:
+// every 16-B chunk is one buffer_load whose byte offset is set past the
+// descriptor's range for padding taps / out-of-range rows, so the hardware
+// returns zeros.
+enum { GM_SLOW = 0, GM_FWD = 1, GM_DG1 = 2, GM_DGS = 3 };
+//  GM_FWD : hi = y*st - pad + r                (forward, wgrad, strided-1x1 dgrad)
+//  GM_DG1 : hi = y + pad - r                   (stride-1 dgrad)
+//  GM_DGS : hi = (y + pad - r) / st if exact   (strided k x k dgrad)
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  // inputs made provably wave-uniform so the descriptor lives in SGPRs
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+}
+
 struct RowPos {
   int b, y, x;
   bool ok;
@@ -125,6 +153,53 @@ __device__ __forceinline__ RowPos decode_row(int m, int M, const GatherGeom& g) 
   return p;
 }
 
+// per-row state of the fast gather: tap-(0,0) coordinates and pixel index
+struct RowA {
+  int hy, wx, pix;
+};
+
+template <int GM>
+__device__ __forceinline__ RowA row_init(const GatherGeom& g, int m, int M) {
+  const RowPos p = decode_row(m, M, g);
+  RowA a;
+  if (GM == GM_FWD) {
+    a.hy = p.y * g.st - g.pad;
+    a.wx = p.x * g.st - g.pad;
+  } else {
+    a.hy = p.y + g.pad;
+    a.wx = p.x + g.pad;
+  }
+  a.pix = (GM == GM_DGS) ? p.b * g.Hs : (p.b * g.Hs + a.hy) * g.Ws + a.wx;
+  if (!p.ok) a.hy = -(1 << 29);  // every tap out of range
+  return a;
+}
+
+// byte offset of channel c of tap (r, s) for a row, or OOB (-> zeros)
+template <int GM>
+__device__ __forceinline__ uint32_t a_off(const GatherGeom& g, const RowA& a, int r, int s, int c) {
+  int hi, wi;
+  uint32_t pix;
+  if (GM == GM_FWD) {
+    hi = a.hy + r;
+    wi = a.wx + s;
+    pix = (uint32_t)a.pix + (uint32_t)(r * g.Ws + s);
+  } else if (GM == GM_DG1) {
+    hi = a.hy - r;
+    wi = a.wx - s;
+    pix = (uint32_t)a.pix - (uint32_t)(r * g.Ws + s);
+  } else {
+    const int hn = a.hy - r, wn = a.wx - s;
+    const uint32_t hq = fdiv((uint32_t)max(hn, 0), g.dst), wq = fdiv((uint32_t)max(wn, 0), g.dst);
+    const bool exact = (hn >= 0) & (wn >= 0) & ((int)hq * g.st == hn) & ((int)wq * g.st == wn);
+    hi = exact ? (int)hq : -1;
+    wi = (int)wq;
+    pix = ((uint32_t)a.pix + hq) * (uint32_t)g.Ws + wq;
+  }
+  const bool ok = ((unsigned)hi < (unsigned)g.Hs) & ((unsigned)wi < (unsigned)g.Ws);
+  return ok ? (pix * (uint32_t)g.Ctot + (uint32_t)c) * 2u : OOB;
+}
+
+// --- generic (unaligned) path ------------------------------------------------
 // source pixel offset (elements, without channel) or -1 when the tap is padding
 __device__ __forceinline__ int64_t src_pixel(const GatherGeom& g, const RowPos& p, int r, int s,
                                              int dgrad) {
@@ -156,7 +231,7 @@ __device__ __forceinline__ uint4 pack8(const uint16_t* e) {
   return v;
 }
 
-// generic per-element gather (channel counts not multiple of 8, e.g. the stem)
+// per-element gather (channel counts not multiple of 8, e.g. the stem)
 __device__ __forceinline__ uint4 gather_chunk_slow(const GatherGeom& g, int cfg, const RowPos& p,
                                                    int k0, int K, int dgrad) {
   uint16_t e[8];
@@ -196,6 +271,15 @@ __device__ __forceinline__ void kpos_advance(const GatherGeom& g, KPos& kp) {
   }
 }
 
+// XCD-aware work order: the dispatcher deals consecutive block ids round-robin
+// to the 8 XCDs (each with a private L2); remap so every XCD walks one
+// contiguous range of (config, tile) work -> a config's weights and input
+// rows stay in one L2.  Bijective for any grid size.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, local = bid >> 3, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
 // ---------------------------------------------------------------------------
 // NT LDS tile: [rows][64] bf16, 128-B rows, 16-B chunk c stored at
 // c ^ ((row >> 1) & 7)  (conflict-free for the MFMA ds_read_b128 pattern)
@@ -230,7 +314,42 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
   }
 }
 
-template <int BM, int BN, bool ALIGNED>
+// Epilogue staging for the NT / NN kernels.  Their MFMAs take the weight
+// fragment as the FIRST operand, so a lane's accumulator holds 4 consecutive
+// output channels of one output row, C[16i + fr][16j + 4fc + e]: bias + act
+// in fp32, one rounding, one 8-B LDS write per fragment.
+template <int BM, int BN>
+__device__ __forceinline__ void stage_c(const NTParams& p, bf16_t* lds,
+                                        const f32x4 (&acc)[BM / 32][BN / 32], int cfg, int n0,
+                                        int wm, int wn, int lane) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16, LDE = BN + 8;
+  const int fr = lane & 15, fc = lane >> 4;
+  float bc[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+      bc[j][e] = (p.bias && n < p.N) ? bf2f(p.bias[(int64_t)cfg * p.bias_gstride + n]) : 0.f;
+    }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bc[j][e];
+        v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
+      }
+      uint2 pk;
+      pk.x = pack_bf2(v[0], v[1]);
+      pk.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(lds + (wm * TM + 16 * i + fr) * LDE + wn * TN + 16 * j + 4 * fc) = pk;
+    }
+}
+
+template <int BM, int BN, int GM>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   constexpr int CPR = BK / 8;                                  // 16-B chunks per row
@@ -242,9 +361,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
 #define SA(buf) (lds + (buf) * (BM * BK))
 #define SB(buf) (lds + 2 * BM * BK + (buf) * (BN * BK))
 
-  const int cfg = blockIdx.z;
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -253,29 +374,33 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.Cg;
 
   RowPos rows[A_CH];
+  RowA rowa[A_CH];
+  __amdgpu_buffer_rsrc_t rA, rB;
+  if constexpr (GM != GM_SLOW) {
+    rA = make_rsrc(abase, p.a.bytes);
+    rB = make_rsrc(wbase, (uint32_t)p.N * (uint32_t)p.K * 2u);
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
+    for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
+  } else {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
+  }
   KPos kp = kpos_init(p.a, 8 * my_chunk);
   uint4 ra[A_CH], rb[B_CH];
 
   auto load_tiles = [&](int kt) {
     const int k0 = kt * BK + 8 * my_chunk;
-    if (ALIGNED) {
+    if constexpr (GM != GM_SLOW) {
       const bool kok = k0 < p.K;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (kok) {
-          const int64_t off = src_pixel(p.a, rows[i], kp.r, kp.s, p.dgrad);
-          if (off >= 0) v = *reinterpret_cast<const uint4*>(abase + off + kp.c);
-        }
-        ra[i] = v;
+        const uint32_t off = a_off<GM>(p.a, rowa[i], kp.r, kp.s, kp.c);
+        ra[i] = bload(rA, kok ? off : OOB);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const int n = n0 + (tid + NTHREADS * i) / CPR;
-        rb[i] = (kok && n < p.N) ? *reinterpret_cast<const uint4*>(wbase + (int64_t)n * p.K + k0)
-                                 : make_uint4(0, 0, 0, 0);
+        rb[i] = bload(rB, (kok && n < p.N) ? (uint32_t)(n * p.K + k0) * 2u : OOB);
       }
       kpos_advance(p.a, kp);
     } else {
@@ -328,33 +453,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < KT) store_tiles(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue: (bias + act in fp32, one rounding), stage the bf16 tile in
-  // LDS, then 16-B coalesced stores
+  // epilogue: stage the bf16 tile in LDS, then 16-B coalesced stores
   constexpr int LDE = BN + 8;
-  float bcol[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * TN + 16 * j + fr;
-    bcol[j] = (p.bias && n < p.N) ? bf2f(p.bias[(int64_t)cfg * p.bias_gstride + n]) : 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = wm * TM + 16 * i + 4 * fc + e;
-        const int c = wn * TN + 16 * j + fr;
-        float v = acc[i][j][e] + bcol[j];
-        v = p.act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (p.act ? fmaxf(v, 0.f) : v);
-        lds[r * LDE + c] = f2bf(v);
-      }
+  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
@@ -385,7 +492,7 @@ __device__ __forceinline__ bf16x8 tn_frag(const bf16_t* tile, int row0, int col_
   return __builtin_bit_cast(bf16x8, t);
 }
 
-template <int BM, int BN, bool ALIGNED>
+template <int BM, int BN, int GM>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;           // 16-B chunks per tile row
@@ -393,11 +500,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
   constexpr int A_RSTEP = NTHREADS / A_CPR, B_RSTEP = NTHREADS / B_CPR;
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
 
-  const int cfg = blockIdx.z;
   const int tiles_k = (p.K + BN - 1) / BN;
-  const int tn_ = blockIdx.x / tiles_k, tk = blockIdx.x % tiles_k;
+  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / (tiles * p.splits);
+  const int rem = work - cfg * tiles * p.splits;
+  const int split = rem / tiles, tile = rem - split * tiles;
+  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
   const int n0 = tn_ * BM, k0 = tk * BN;
-  const int ms = blockIdx.y * p.m_per_split;
+  const int ms = split * p.m_per_split;
   const int me = min(p.Mred, ms + p.m_per_split);
   if (ms >= me) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -413,40 +524,45 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
   uint4 ra[A_CH], rb[B_CH];
   const bf16_t* dyb = p.dy + (int64_t)cfg * p.N;
   const bf16_t* xb = p.x.src + (int64_t)cfg * p.x.Cg;
+  __amdgpu_buffer_rsrc_t rDY, rX;
+  if constexpr (GM != GM_SLOW) {
+    rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 2u);
+    rX = make_rsrc(xb, p.x.bytes);
+  }
 
   auto load_tiles = [&](int mt) {
     const int mbase = ms + mt * BK;
+    if constexpr (GM != GM_SLOW) {
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (m < me && n < p.N) {
-        const bf16_t* src = dyb + (int64_t)m * p.ldy + n;
-        if (ALIGNED && n + 8 <= p.N) {
-          v = *reinterpret_cast<const uint4*>(src);
-        } else {
-          uint16_t e[8];
+      for (int i = 0; i < A_CH; ++i) {
+        const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
+        ra[i] = bload(rDY, (m < me && n < p.N) ? (uint32_t)(m * p.ldy + n) * 2u : OOB);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const RowA ra_ = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
+        const uint32_t off = a_off<GM_FWD>(p.x, ra_, bk.r, bk.s, bk.c);
+        rb[i] = bload(rX, b_kok ? off : OOB);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
+        uint16_t e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (m < me && n < p.N) {
+          const bf16_t* src = dyb + (int64_t)m * p.ldy + n;
 #pragma unroll
           for (int t = 0; t < 8; ++t) e[t] = (n + t < p.N) ? src[t] : 0;
-          v = pack8(e);
         }
+        ra[i] = pack8(e);
       }
-      ra[i] = v;
-    }
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int m = mbase + b_row0 + B_RSTEP * i;
-      const RowPos pos = decode_row(m, me, p.x);
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (b_kok && pos.ok) {
-        if (ALIGNED) {
-          const int64_t off = src_pixel(p.x, pos, bk.r, bk.s, 0);
-          if (off >= 0) v = *reinterpret_cast<const uint4*>(xb + off + bk.c);
-        } else {
-          v = gather_chunk_slow(p.x, cfg, pos, kk0, p.K, 0);
-        }
+      for (int i = 0; i < B_CH; ++i) {
+        const int m = mbase + b_row0 + B_RSTEP * i;
+        const RowPos pos = decode_row(m, me, p.x);
+        rb[i] = (b_kok && pos.ok) ? gather_chunk_slow(p.x, cfg, pos, kk0, p.K, 0)
+                                  : make_uint4(0, 0, 0, 0);
       }
-      rb[i] = v;
     }
   };
   auto store_tiles = [&](int buf) {
@@ -494,7 +610,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
 
   float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
   const int fr = lane & 15, fc = lane >> 4;
-  const bool split = gridDim.y > 1;
+  const bool split_k = p.splits > 1;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -505,7 +621,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
         const int k = k0 + wb * TN + 16 * j + fr;
         if (n < p.N && k < p.K) {
           float* d = dwb + (int64_t)n * p.K + k;
-          if (split)
+          if (split_k)
             atomicAdd(d, acc[i][j][e]);
           else
             *d = acc[i][j][e];
@@ -519,8 +635,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
 // B = W read as [k = (tap, cout)] x [cin] rows straight from the arena (TN-
 // style LDS, ds_read_b64_tr_b16) -> no per-step weight transpose.
 //   dx[m, c] = sum_{tap, n} dy~[m, (tap, n)] * W[n][tap][c]
+// GM_DG1 (stride 1, and the strided-1x1 case on the dy grid) or GM_DGS.
 // ---------------------------------------------------------------------------
-template <int BM, int BN>
+template <int BM, int BN, int GM>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T, FastDiv dCout) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   constexpr int CPR = BK / 8;
@@ -531,9 +648,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   constexpr int LDS_ELEMS = TILE_ELEMS > EPI_ELEMS ? TILE_ELEMS : EPI_ELEMS;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 
-  const int cfg = blockIdx.z;
   const int tiles_n = (p.N + BN - 1) / BN;
-  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -543,10 +662,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   const bf16_t* wbase = p.w + (int64_t)cfg * p.w_gstride;
   const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.Cg;
   const int b_col = 8 * (tid % B_CPR), b_row0 = tid / B_CPR;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(abase, p.a.bytes);
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(wbase, (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 2u);
 
-  RowPos rows[A_CH];
+  RowA rowa[A_CH];
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
+  for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   KPos kp = kpos_init(p.a, 8 * my_chunk);
   uint4 ra[A_CH], rb[B_CH];
 
@@ -555,25 +676,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
     const bool kok = k0 < p.K;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kok) {
-        const int64_t off = src_pixel(p.a, rows[i], kp.r, kp.s, p.dgrad);
-        if (off >= 0) v = *reinterpret_cast<const uint4*>(abase + off + kp.c);
-      }
-      ra[i] = v;
+      const uint32_t off = a_off<GM>(p.a, rowa[i], kp.r, kp.s, kp.c);
+      ra[i] = bload(rA, kok ? off : OOB);
     }
     kpos_advance(p.a, kp);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int k = kt * BK + b_row0 + B_RSTEP * i;
       const int c = n0 + b_col;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (k < p.K && c < Cin) {
-        const int tap = (int)fdiv((uint32_t)k, dCout);
-        const int n = k - tap * Cout;
-        v = *reinterpret_cast<const uint4*>(wbase + ((int64_t)n * T + tap) * Cin + c);
-      }
-      rb[i] = v;
+      const int tap = (int)fdiv((uint32_t)k, dCout);
+      const int n = k - tap * Cout;
+      rb[i] = bload(rW, (k < p.K && c < Cin) ? (uint32_t)((n * T + tap) * Cin + c) * 2u : OOB);
     }
   };
   auto store_tiles = [&](int buf) {
@@ -615,25 +728,373 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < KT) store_tiles(cur ^ 1);
     __syncthreads();
   }
   constexpr int LDE = BN + 8;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        lds[(wm * TM + 16 * i + 4 * fc + e) * LDE + wn * TN + 16 * j + fr] = f2bf(acc[i][j][e]);
+  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
 #undef SA
 #undef SB
+
+// ===========================================================================
+// Pipelined kernels (8/64-channel aligned operands): operand tiles go
+// global -> LDS by LDS-DMA (buffer_load ... lds, 1 KiB per wave-instruction,
+// padding / out-of-range chunks zero-filled by the descriptor range check)
+// into an S-stage LDS ring.  One raw barrier per 64-deep K-step, a counted
+// vmcnt keeps the next stage's DMA in flight across it (S = 3: two K-steps of
+// loads overlap each K-step's MFMAs), no VGPR staging, no ds_write pass.
+// The LDS images are the same swizzled layouts as above; the swizzle is
+// applied to the per-lane SOURCE address because a DMA piece lands
+// lane-linearly in LDS.
+// ===========================================================================
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, bf16_t* dst, uint32_t voff,
+                                       uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// 16-B column index (global) of LDS slot col16 of a TN tile row (tn_off swizzle)
+template <int COLS>
+__device__ __forceinline__ int tn_col16(int row, int col16) {
+  int sw;
+  if (COLS == 128)
+    sw = (row & 3) | (((row >> 3) & 1) << 2);
+  else
+    sw = ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return col16 ^ (2 * sw);
+}
+
+// NT-image MFMA step over one 64-deep stage: A [BM][64], B [BN][64]
+template <int BM, int BN>
+__device__ __forceinline__ void mma_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn, int lane,
+                                       f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc + 4 * kk));
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 16 * j + fr, fc + 4 * kk));
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+}
+
+// A as NT image, B as TN image (dgrad)
+template <int BM, int BN>
+__device__ __forceinline__ void mma_nn(const bf16_t* sa, const bf16_t* sb, int wm, int wn, int lane,
+                                       f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc + 4 * kk));
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = tn_frag<BN>(sb, 32 * kk, wn * TN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+  }
+}
+
+// both TN images (wgrad)
+template <int BM, int BN>
+__device__ __forceinline__ void mma_tn(const bf16_t* sa, const bf16_t* sb, int wm, int wn, int lane,
+                                       f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[FM], bfr[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) af[i] = tn_frag<BM>(sa, 32 * kk, wm * TM + 16 * i, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) bfr[j] = tn_frag<BN>(sb, 32 * kk, wn * TN + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// S-stage ring driver: issue(t, stage) queues tile t's DMA pieces (LPW per
+// wave), mma(stage) consumes one stage.
+template <int S, int LPW, typename Issue, typename Mma>
+__device__ __forceinline__ void ring_loop(int KT, Issue&& issue, Mma&& mma) {
+  issue(0, 0);
+  if (S > 2 && KT > 1) issue(1, 1);
+  int st = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    if (S > 2 && kt + 1 < KT)
+      wait_vm<LPW>();          // tile kt landed; tile kt+1 stays in flight
+    else
+      wait_vm<0>();
+    lds_barrier();             // tile kt visible to all waves; stage (kt-1) % S free
+    const int nxt = kt + S - 1;
+    if (nxt < KT) issue(nxt, (st + S - 1) % S);
+    mma(st);
+    st = (st + 1 == S) ? 0 : st + 1;
+  }
+  lds_barrier();               // every wave done reading before LDS is reused
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void zero_acc(f32x4 (&acc)[BM / 32][BN / 32]) {
+#pragma unroll
+  for (int i = 0; i < BM / 32; ++i)
+#pragma unroll
+    for (int j = 0; j < BN / 32; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// forward: y = act(im2col(x) W^T + b); requires Cg % 64 == 0
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
+  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int EPI = BM * (BN + 8);
+  constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.Cg, p.a.bytes);
+  const auto rB = make_rsrc(p.w + (int64_t)cfg * p.w_gstride, (uint32_t)p.N * (uint32_t)p.K * 2u);
+
+  RowA arow[AJ];
+  int achan[AJ];
+  uint32_t boff[BJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    const int row = (wid * AJ + j) * 8 + (lane >> 3);
+    achan[j] = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    arow[j] = row_init<GM_FWD>(p.a, m0 + row, p.M);
+  }
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    const int row = (wid * BJ + j) * 8 + (lane >> 3);
+    const int n = n0 + row;
+    boff[j] = n < p.N ? (uint32_t)(n * p.K + 8 * ((lane & 7) ^ ((row >> 1) & 7))) * 2u : OOB;
+  }
+  int tr = 0, ts = 0, tc = 0;  // tap / channel of the next K tile to issue (uniform)
+  auto issue = [&](int kt, int st) {
+    bf16_t* sa = lds + st * STAGE;
+    bf16_t* sb = sa + BM * BK;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+      glds16(rA, sa + (wid * AJ + j) * 512, a_off<GM_FWD>(p.a, arow[j], tr, ts, tc + achan[j]), 0);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) glds16(rB, sb + (wid * BJ + j) * 512, boff[j], (uint32_t)kt * (BK * 2));
+    tc += BK;
+    if (tc == p.a.Cg) {
+      tc = 0;
+      if (++ts == p.a.kw) {
+        ts = 0;
+        ++tr;
+      }
+    }
+  };
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  ring_loop<S, LPW>(p.K / BK, issue, [&](int st) {
+    mma_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+  });
+
+  constexpr int LDE = BN + 8;
+  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  __syncthreads();
+  store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
+}
+
+// dgrad: dx = col2im(dy) * W; requires Cout % 64 == 0, Cin % 8 == 0
+template <int BM, int BN, int S, int GM>
+__global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
+  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int EPI = BM * (BN + 8);
+  constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
+  constexpr int BROWS = 512 / BN, BC16 = BN / 8;   // rows / 16-B columns per B piece
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int Cout = p.a.Cg, Cin = p.N;
+  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.Cg, p.a.bytes);
+  const auto rW = make_rsrc(p.w + (int64_t)cfg * p.w_gstride,
+                            (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 2u);
+
+  RowA arow[AJ];
+  int achan[AJ];
+  uint32_t boff[BJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    const int row = (wid * AJ + j) * 8 + (lane >> 3);
+    achan[j] = 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    arow[j] = row_init<GM>(p.a, m0 + row, p.M);
+  }
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    const int row = (wid * BJ + j) * BROWS + lane / BC16;
+    const int c = n0 + 8 * tn_col16<BN>(row, lane % BC16);
+    boff[j] = c < Cin ? (uint32_t)(row * T * Cin + c) * 2u : OOB;
+  }
+  int tr = 0, ts = 0, tc = 0;
+  auto issue = [&](int kt, int st) {
+    bf16_t* sa = lds + st * STAGE;
+    bf16_t* sb = sa + BM * BK;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+      glds16(rA, sa + (wid * AJ + j) * 512, a_off<GM>(p.a, arow[j], tr, ts, tc + achan[j]), 0);
+    const uint32_t wso = (uint32_t)(tc * T + tr * p.a.kw + ts) * (uint32_t)Cin * 2u;
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) glds16(rW, sb + (wid * BJ + j) * 512, boff[j], wso);
+    tc += BK;
+    if (tc == Cout) {
+      tc = 0;
+      if (++ts == p.a.kw) {
+        ts = 0;
+        ++tr;
+      }
+    }
+  };
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  ring_loop<S, LPW>(p.K / BK, issue, [&](int st) {
+    mma_nn<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+  });
+
+  constexpr int LDE = BN + 8;
+  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  __syncthreads();
+  store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
+}
+
+// wgrad: dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]; requires Cin % 8 == 0, Cout % 8 == 0
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(NTHREADS, 2) void pipe_wg(WGParams p) {
+  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int AROWS = 512 / BM, AC16 = BM / 8, BROWS = 512 / BN, BC16 = BN / 8;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
+
+  const int tiles_k = (p.K + BN - 1) / BN;
+  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int cfg = work / (tiles * p.splits);
+  const int rem = work - cfg * tiles * p.splits;
+  const int split = rem / tiles, tile = rem - split * tiles;
+  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
+  const int n0 = tn_ * BM, k0 = tk * BN;
+  const int ms = split * p.m_per_split;
+  const int me = min(p.Mred, ms + p.m_per_split);
+  if (ms >= me) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const auto rDY = make_rsrc(p.dy + (int64_t)cfg * p.N, (uint32_t)p.Mred * (uint32_t)p.ldy * 2u);
+  const auto rX = make_rsrc(p.x.src + (int64_t)cfg * p.x.Cg, p.x.bytes);
+
+  int arow[AJ];
+  uint32_t aoff[AJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    arow[j] = (wid * AJ + j) * AROWS + lane / AC16;
+    const int n = n0 + 8 * tn_col16<BM>(arow[j], lane % AC16);
+    aoff[j] = n < p.N ? (uint32_t)(arow[j] * p.ldy + n) * 2u : OOB;
+  }
+  int brow[BJ];
+  KPos bk[BJ];
+  bool bok[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    brow[j] = (wid * BJ + j) * BROWS + lane / BC16;
+    const int k = k0 + 8 * tn_col16<BN>(brow[j], lane % BC16);
+    bok[j] = k < p.K;
+    bk[j] = kpos_init(p.x, bok[j] ? k : 0);
+  }
+  auto issue = [&](int mt, int st) {
+    bf16_t* sa = lds + st * STAGE;
+    bf16_t* sb = sa + BM * BK;
+    const int mbase = ms + mt * BK, lim = me - mbase;
+    const uint32_t so = (uint32_t)mbase * (uint32_t)p.ldy * 2u;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) glds16(rDY, sa + (wid * AJ + j) * 512, arow[j] < lim ? aoff[j] : OOB, so);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const RowA ra = row_init<GM_FWD>(p.x, mbase + brow[j], me);
+      const uint32_t off = a_off<GM_FWD>(p.x, ra, bk[j].r, bk[j].s, bk[j].c);
+      glds16(rX, sb + (wid * BJ + j) * 512, bok[j] ? off : OOB, 0);
+    }
+  };
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  ring_loop<S, LPW>((me - ms + BK - 1) / BK, issue, [&](int st) {
+    mma_tn<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+  });
+
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
+  const int fr = lane & 15, fc = lane >> 4;
+  const bool split_k = p.splits > 1;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wm * TM + 16 * i + 4 * fc + e;
+        const int k = k0 + wn * TN + 16 * j + fr;
+        if (n < p.N && k < p.K) {
+          float* d = dwb + (int64_t)n * p.K + k;
+          if (split_k)
+            atomicAdd(d, acc[i][j][e]);
+          else
+            *d = acc[i][j][e];
+        }
+      }
+}
 
 // ---------------------------------------------------------------------------
 // per-config weight transpose for dgrad: W[N][T][C] -> Wt[C][T][N]
@@ -664,22 +1125,74 @@ __global__ __launch_bounds__(256) void transpose_w_kernel(const bf16_t* __restri
 // ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
+// Kernel variants: (staging kind) x (tile).  kind 0 = register-staged
+// double buffer, 1 = LDS-DMA ring; tile 0 = 64x64, 1 = 128x128, 2 = 128x64
+// (BM x BN; for wgrad BM tiles Cout, BN tiles K).  v = 3 * kind + tile.
+// cer_conv_set_variant(op, v) pins a variant per op (0 fwd, 1 dgrad, 2 wgrad)
+// for tuning; -1 = the built-in choice.
+static int g_variant[3] = {-1, -1, -1};
+
+CER_API void cer_conv_set_variant(int op, int v) {
+  if (op >= 0 && op < 3) g_variant[op] = v;
+}
+
+static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
+
+// built-in choice (from the per-shape sweep of tools/bench_conv --sweep)
+static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
+  if (g_variant[op] >= 0) {
+    const int v = g_variant[op];
+    return (v >= 3 && !pipe_ok) ? v - 3 : v;
+  }
+  int tile;
+  if (op == 2) {
+    tile = ntiles(N, K, 128, 128) * G >= 256 ? 1 : 0;
+  } else if (N <= 64) {
+    tile = ntiles(M, N, 128, 64) * G >= 512 ? 2 : 0;
+  } else {
+    tile = ntiles(M, N, 128, 128) * G >= 512 ? 1 : 0;
+  }
+  return tile;
+}
+
+static void tile_dims(int v, int& bm, int& bn) {
+  const int t = v % 3;
+  bm = t == 0 ? 64 : 128;
+  bn = t == 1 ? 128 : 64;
+}
+
 template <int BM, int BN>
-static int launch_nt(const NTParams& p, int G, bool aligned, hipStream_t stream) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, G);
-  if (aligned)
-    igemm_nt<BM, BN, true><<<grid, NTHREADS, 0, stream>>>(p);
-  else
-    igemm_nt<BM, BN, false><<<grid, NTHREADS, 0, stream>>>(p);
-  return (int)hipGetLastError();
+static void launch_nt_t(const NTParams& p, int G, int kind, bool fast, hipStream_t stream) {
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G));
+  if (kind == 1) {
+    if (p.K / BK >= 3)
+      pipe_nt<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      pipe_nt<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
+  } else if (fast) {
+    igemm_nt<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+  } else {
+    igemm_nt<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+  }
+}
+
+// fast = 8-channel aligned operands addressed by 32-bit buffer offsets
+static bool nt_fast(const NTParams& p) {
+  return p.dgrad == 0 && (p.a.Cg % 8 == 0) && (p.a.Ctot % 8 == 0) && (p.K % 8 == 0) &&
+         p.a.bytes != 0 && (uint64_t)p.N * p.K * 2 < (1ull << 31);
 }
 
 static int run_nt(const NTParams& p, int G, hipStream_t stream) {
-  const bool aligned = (p.a.Cg % 8 == 0) && (p.a.Ctot % 8 == 0) && (p.K % 8 == 0);
-  const long big = (long)((p.M + 127) / 128) * ((p.N + 127) / 128) * G;
-  if (big >= 512) return launch_nt<128, 128>(p, G, aligned, stream);
-  return launch_nt<64, 64>(p, G, aligned, stream);
+  const bool fast = nt_fast(p);
+  const bool pipe_ok = fast && p.a.Cg % 64 == 0;
+  const int v = fast ? choose(0, p.M, p.N, p.K, G, pipe_ok) : choose(0, p.M, p.N, p.K, G, false) % 3;
+  const int kind = v / 3;
+  switch (v % 3) {
+    case 0: launch_nt_t<64, 64>(p, G, kind, fast, stream); break;
+    case 1: launch_nt_t<128, 128>(p, G, kind, fast, stream); break;
+    default: launch_nt_t<128, 64>(p, G, kind, fast, stream); break;
+  }
+  return (int)hipGetLastError();
 }
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
@@ -687,7 +1200,7 @@ CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
                          int act, hipStream_t stream) {
   NTParams p;
-  p.a = make_geom(x, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
+  p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
   p.dgrad = 0;
   p.w = w;
   p.w_gstride = w_gstride;
@@ -706,11 +1219,29 @@ CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
 }
 
 template <int BM, int BN>
-static int launch_nn(const NTParams& p, int G, int T, hipStream_t stream) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, G);
-  igemm_nn_dgrad<BM, BN><<<grid, NTHREADS, 0, stream>>>(p, T, make_div((uint32_t)p.a.Cg));
-  return (int)hipGetLastError();
+static void launch_nn_t(const NTParams& p, int G, int T, int kind, bool strided,
+                        hipStream_t stream) {
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G));
+  if (kind == 1) {
+    const bool s3 = p.K / BK >= 3;
+    if (strided) {
+      if (s3)
+        pipe_nn<BM, BN, 3, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T);
+      else
+        pipe_nn<BM, BN, 2, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T);
+    } else {
+      if (s3)
+        pipe_nn<BM, BN, 3, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T);
+      else
+        pipe_nn<BM, BN, 2, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T);
+    }
+    return;
+  }
+  const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if (strided)
+    igemm_nn_dgrad<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+  else
+    igemm_nn_dgrad<BM, BN, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
 }
 
 // dx = dgrad(dy, W).  Aligned channels: NN kernel (weights read in place, no
@@ -733,29 +1264,38 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   p.ldc = G * Cin;
   p.N = Cin;
   p.K = T * Cout;
-  const bool aligned = (Cout % 8 == 0) && (Cin % 8 == 0);
+  const bool aligned = (Cout % 8 == 0) && (Cin % 8 == 0) &&
+                       (uint64_t)B * Ho * Wo * G * Cout * 2 < (1ull << 31) &&
+                       (uint64_t)Cout * T * Cin * 2 < (1ull << 31);
   if (aligned) {
     p.w = w;
     p.w_gstride = w_gstride;
+    bool strided = false;
     if (kh == 1 && kw == 1 && pad == 0 && st > 1) {
       // rows (b, ho, wo) of dy map to dx pixels (b, ho*st, wo*st); others get 0
-      hipMemsetAsync(dx, 0, sizeof(bf16_t) * (size_t)B * H * W * G * Cin, stream);
-      p.a = make_geom(dy, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0);
+      (void)hipMemsetAsync(dx, 0, sizeof(bf16_t) * (size_t)B * H * W * G * Cin, stream);
+      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0);
       p.dgrad = 0;
       p.M = B * Ho * Wo;
       p.o_st = st;
     } else {
-      p.a = make_geom(dy, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
+      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
       p.dgrad = 1;
       p.M = B * H * W;
+      strided = st > 1;
     }
-    const long big = (long)((p.M + 127) / 128) * ((p.N + 127) / 128) * G;
-    if (big >= 512) return launch_nn<128, 128>(p, G, T, stream);
-    return launch_nn<64, 64>(p, G, T, stream);
+    const int v = choose(1, p.M, p.N, p.K, G, Cout % 64 == 0);
+    const int kind = v / 3;
+    switch (v % 3) {
+      case 0: launch_nn_t<64, 64>(p, G, T, kind, strided, stream); break;
+      case 1: launch_nn_t<128, 128>(p, G, T, kind, strided, stream); break;
+      default: launch_nn_t<128, 64>(p, G, T, kind, strided, stream); break;
+    }
+    return (int)hipGetLastError();
   }
   dim3 tg(((Cout + 31) / 32) * ((Cin + 31) / 32), T, G);
   transpose_w_kernel<<<tg, 256, 0, stream>>>(w, w_gstride, wt, Cout, T, Cin);
-  p.a = make_geom(dy, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
+  p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
   p.dgrad = 1;
   p.w = wt;
   p.w_gstride = (int64_t)Cout * T * Cin;
@@ -763,21 +1303,42 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   return run_nt(p, G, stream);
 }
 
-template <int BM, int BN>
-static int launch_wg(WGParams p, int G, bool aligned, int splits, hipStream_t stream) {
-  const int tiles = ((p.N + BM - 1) / BM) * ((p.K + BN - 1) / BN);
-  p.m_per_split = ((p.Mred + splits - 1) / splits + BK - 1) / BK * BK;
-  splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
-  dim3 grid(tiles, splits, G);
-  if (aligned)
-    igemm_wgrad<BM, BN, true><<<grid, NTHREADS, 0, stream>>>(p);
-  else
-    igemm_wgrad<BM, BN, false><<<grid, NTHREADS, 0, stream>>>(p);
-  return (int)hipGetLastError();
+static int wg_variant(int N, int K, int G, bool fast) {
+  const int v = choose(2, 0, N, K, G, fast);
+  return fast ? v : v % 3;
 }
 
-static bool wgrad_big(int N, int K, int G) {
-  return ((long)((N + 127) / 128) * ((K + 127) / 128) * G) >= 256;
+static int wg_splits(int Mred, int N, int K, int G, int v) {
+  int bm, bn;
+  tile_dims(v, bm, bn);
+  const long tiles = ntiles(N, K, bm, bn) * G;
+  long want = (1024 + tiles - 1) / tiles;          // aim for ~1024 blocks
+  long maxs = (Mred + 511) / 512;                  // >= 512 rows per split
+  long s = want < maxs ? want : maxs;
+  return (int)(s < 1 ? 1 : s);
+}
+
+template <int BM, int BN>
+static void launch_wg_t(WGParams p, int G, int kind, bool fast, int splits, hipStream_t stream) {
+  p.m_per_split = ((p.Mred + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
+  p.splits = splits;
+  dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
+  if (kind == 1) {
+    if (p.m_per_split / BK >= 3)
+      pipe_wg<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      pipe_wg<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
+  } else if (fast) {
+    igemm_wgrad<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+  } else {
+    igemm_wgrad<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+  }
+}
+
+static bool wg_fast(int Cin, int Cout, const WGParams& p) {
+  return (Cin % 8 == 0) && (Cout % 8 == 0) && p.x.bytes != 0 &&
+         (uint64_t)p.Mred * p.ldy * 2 < (1ull << 31);
 }
 
 // dw must be zeroed by the caller when more than one split is used (splits > 1)
@@ -786,7 +1347,7 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
                            int pad, float* dw, int64_t dw_gstride, int splits,
                            hipStream_t stream) {
   WGParams p;
-  p.x = make_geom(x, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
+  p.x = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
   p.dy = dy;
   p.ldy = G * Cout;
   p.dw = dw;
@@ -794,17 +1355,20 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
-  const bool aligned = (Cin % 8 == 0) && (Cout % 8 == 0);
-  if (wgrad_big(p.N, p.K, G)) return launch_wg<128, 128>(p, G, aligned, splits, stream);
-  return launch_wg<64, 64>(p, G, aligned, splits, stream);
+  const bool fast = wg_fast(Cin, Cout, p);
+  const int v = wg_variant(p.N, p.K, G, fast);
+  const int kind = v / 3;
+  switch (v % 3) {
+    case 0: launch_wg_t<64, 64>(p, G, kind, fast, splits, stream); break;
+    case 1: launch_wg_t<128, 128>(p, G, kind, fast, splits, stream); break;
+    default: launch_wg_t<128, 64>(p, G, kind, fast, splits, stream); break;
+  }
+  return (int)hipGetLastError();
 }
 
-// the split count the host should use (and whether dw needs zeroing)
+// the split count the host should use (and whether dw needs zeroing); the
+// variant is re-derived exactly as cer_conv_wgrad will (fast path assumed
+// when channels are 8-aligned)
 CER_API int cer_wgrad_splits(int Mred, int N, int K, int G) {
-  const int bm = wgrad_big(N, K, G) ? 128 : 64;
-  const long tiles = (long)((N + bm - 1) / bm) * ((K + bm - 1) / bm) * G;
-  long want = (1024 + tiles - 1) / tiles;          // aim for ~1024 blocks
-  long maxs = (Mred + 511) / 512;                  // >= 512 rows per split
-  long s = want < maxs ? want : maxs;
-  return (int)(s < 1 ? 1 : s);
+  return wg_splits(Mred, N, K, G, wg_variant(N, K, G, true));
 }

@@ -57,6 +57,9 @@ CONV_CASES = [
     (8, 28, 28, 256, 512, 1, 1, 0, 4),     # 128x128 NT tiles (>= 512 tiles)
     (8, 28, 28, 128, 128, 3, 1, 1, 8),     # 128x128 NT fwd + dgrad, 3x3
     (16, 14, 14, 512, 256, 1, 2, 0, 8),    # strided 1x1 with big tiles
+    (4, 14, 14, 64, 128, 3, 2, 1, 2),      # strided 3x3 (ResNet-18 style) dgrad
+    (2, 10, 10, 16, 32, 5, 1, 2, 2),       # 16 channels: several taps per K tile
+    (3, 6, 5, 8, 8, 3, 1, 0, 3),           # no padding, tiny
 ]
 
 
@@ -230,3 +233,25 @@ def test_full_model_step_vs_fp32_reference(model):
     assert torch.isfinite(gh).all()
     assert (lh - l32).abs().max() <= max(3 * (lt - l32).abs().max().item(), 0.05)
     assert err_h <= 1.15 * err_t + 0.02, (err_h, err_t)
+
+
+VARIANT_CASES = [
+    (2, 14, 14, 64, 128, 3, 2, 1, 2),
+    (4, 7, 7, 128, 64, 1, 1, 0, 3),
+    (2, 9, 11, 24, 40, 3, 1, 1, 2),
+    (2, 12, 12, 64, 64, 3, 1, 1, 2),
+]
+
+
+@pytest.mark.parametrize("variant", range(6))
+@pytest.mark.parametrize("case", VARIANT_CASES)
+def test_conv_variant_matches_oracle(case, variant):
+    """Every pinned kernel variant (staging x tile) of fwd / dgrad / wgrad."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    for op in range(3):
+        _hip.conv_set_variant(op, variant)
+    try:
+        test_conv_matches_oracle(case)
+    finally:
+        for op in range(3):
+            _hip.conv_set_variant(op, -1)
