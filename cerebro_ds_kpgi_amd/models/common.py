@@ -76,6 +76,15 @@ class PackedNet(object):
         return P.bn_act(x, self.ref(b.g), self.ref(b.b), self.ref(b.rm), self.ref(b.rv),
                         training, relu, residual, self.bn_momentum, self.bn_eps)
 
+    def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False):
+        """act(BN(conv(x)) + residual); in training the conv epilogue feeds BN
+        its batch statistics (ops.nn.PackedConvBNAct)."""
+        if not training:
+            return self.bn(self.conv(x, c, anchor), b, training, relu, residual)
+        return P.conv_bn_act(x, self.ref(c.w), self.ref(b.g), self.ref(b.b), self.ref(b.rm),
+                             self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
+                             self.bn_eps, self.anchor if anchor else None)
+
     def dense(self, x, d, relu=False, anchor=False):
         return P.linear(x, self.ref(d.w), self.ref(d.b), relu, self.anchor if anchor else None)
 

@@ -70,20 +70,19 @@ class PackedResNet(PackedNet):
         self.build_layout()
 
     def forward(self, x, training):
-        x = self.conv(x, self.conv1, anchor=True)
-        x = self.bn(x, self.bn1, training)
+        x = self.conv_bn(x, self.conv1, self.bn1, training, anchor=True)
         x = P.maxpool2d(x, 3, 2, 1)  # ZeroPad(1) + MaxPool 3x3/2 valid (inputs >= 0 post-ReLU)
         for blk in self.blocks:
             if "cs" in blk:
-                sc = self.bn(self.conv(x, blk["cs"]), blk["bs"], training, relu=False)
+                sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False)
             else:
                 sc = x
-            h = self.bn(self.conv(x, blk["c1"]), blk["b1"], training)
+            h = self.conv_bn(x, blk["c1"], blk["b1"], training)
             if self.bottleneck:
-                h = self.bn(self.conv(h, blk["c2"]), blk["b2"], training)
-                h = self.bn(self.conv(h, blk["c3"]), blk["b3"], training, relu=True, residual=sc)
+                h = self.conv_bn(h, blk["c2"], blk["b2"], training)
+                h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc)
             else:
-                h = self.bn(self.conv(h, blk["c2"]), blk["b2"], training, relu=True, residual=sc)
+                h = self.conv_bn(h, blk["c2"], blk["b2"], training, relu=True, residual=sc)
             x = h
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

@@ -26,9 +26,9 @@ class PackedTinyCNN(PackedNet):
         self.build_layout()
 
     def forward(self, x, training):
-        x = self.bn(self.conv(x, self.c1, anchor=True), self.b1, training)
+        x = self.conv_bn(x, self.c1, self.b1, training, anchor=True)
         x = P.maxpool2d(x, 2, 2, 0)
-        x = self.bn(self.conv(x, self.c2), self.b2, training)
+        x = self.conv_bn(x, self.c2, self.b2, training)
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)
 
@@ -71,16 +71,16 @@ class PackedMobileNetV2(PackedNet):
         self.build_layout()
 
     def forward(self, x, training):
-        x = self.bn(self.conv(x, self.stem, anchor=True), self.stem_bn, training, relu=6)
+        x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True)
         for blk in self.blocks:
             h = x
             if "exp" in blk:
-                h = self.bn(self.conv(h, blk["exp"]), blk["exp_bn"], training, relu=6)
+                h = self.conv_bn(h, blk["exp"], blk["exp_bn"], training, relu=6)
             h = P.dwconv2d(h, self.ref(blk["dw"]), blk["stride"], 1)
             h = self.bn(h, blk["dw_bn"], training, relu=6)
-            h = self.bn(self.conv(h, blk["proj"]), blk["proj_bn"], training, relu=False,
-                        residual=x if blk["res"] else None)
+            h = self.conv_bn(h, blk["proj"], blk["proj_bn"], training, relu=False,
+                             residual=x if blk["res"] else None)
             x = h
-        x = self.bn(self.conv(x, self.head), self.head_bn, training, relu=6)
+        x = self.conv_bn(x, self.head, self.head_bn, training, relu=6)
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libcerebro_hip.so")
 
 IMPLEMENTED = {"adam", "loss", "gather"}
-_RET_I64 = {"cer_bn_part_floats"}
+_RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats"}
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -131,6 +131,11 @@ _SIGS.update({
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
     "cer_bn_part_floats": [c_i64, c_i],
+    "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
+                           c_p, c_i, c_i, c_p, c_p, c_p],
+    "cer_conv_stats_floats": [c_i64, c_i],
+    "cer_bn_fwd_train_part": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
+                              c_p, c_p, c_i, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
     "cer_bn_fwd_train": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p,
                          c_p, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
     "cer_bn_fwd_eval": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i, c_i,
@@ -234,6 +239,34 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     return y
 
 
+def conv2d_fwd_stats(x, wref, stride, pad):
+    """z = conv(x, W) plus the BN (sum, sum^2) per-slab partials of z, computed
+    in the GEMM epilogue.  Returns (z, part, nslab)."""
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    assert GC == G * cin, (x.shape, wref.spec.shape, G)
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    z = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
+    C = G * cout
+    M = B * Ho * Wo
+    part = torch.empty(int(lib().cer_conv_stats_floats(M, C)), dtype=torch.float32,
+                       device=x.device)
+    nslab = ctypes.c_int(0)
+    wp, ws = wref.work_ptr()
+
+    def launch():
+        rc = lib().cer_conv_fwd_stats(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride,
+                                      pad, _ptr(z), Ho, Wo, _ptr(part), ctypes.byref(nslab),
+                                      _stream())
+        _check(rc, "cer_conv_fwd_stats")
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    launch()
+    return z, part, nslab.value
+
+
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W):
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -319,6 +352,30 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
                                 c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
                                 _ptr(part), M, C, Cper, eps, momentum, _act_code(act), _stream())
     _check(rc, "cer_bn_fwd_train")
+    return y, mean, invstd
+
+
+def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, eps, part,
+                          nslab):
+    """BN forward from conv-epilogue partials (cer_conv_fwd_stats)."""
+    x = _bf16(x)
+    C = x.shape[-1]
+    M = x.numel() // C
+    Cper = gref.spec.shape[0]
+    y = torch.empty_like(x)
+    mean = torch.empty(C, dtype=torch.float32, device=x.device)
+    invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+    ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    gp, gs = gref.work_ptr()
+    bp, bs = bref.work_ptr()
+    rmp, rs = rmref.master_ptr()
+    rvp, _ = rvref.master_ptr()
+    res = _bf16(residual) if residual is not None else None
+    rc = lib().cer_bn_fwd_train_part(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
+                                     c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
+                                     _ptr(part), int(nslab), M, C, Cper, eps, momentum,
+                                     _act_code(act), _stream())
+    _check(rc, "cer_bn_fwd_train_part")
     return y, mean, invstd
 
 

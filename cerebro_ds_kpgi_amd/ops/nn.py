@@ -63,15 +63,18 @@ def _torch_weight(wref):
     return wref.work().permute(0, 1, 4, 2, 3).reshape(G * cout, cin, kh, kw)
 
 
+def _conv_forward(x, wref, stride, pad):
+    if use_hip("conv", x):
+        return _hip().conv2d_fwd(x, wref, stride, pad)
+    w = _torch_weight(wref)
+    return _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G))
+
+
 class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
-        if use_hip("conv", x):
-            y = _hip().conv2d_fwd(x, wref, stride, pad)
-        else:
-            w = _torch_weight(wref)
-            y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G))
+        y = _conv_forward(x, wref, stride, pad)
         ctx.save_for_backward(x)
         return y
 
@@ -142,35 +145,38 @@ def _flat_param(ref):
     return ref.work().reshape(-1).float() if ref.spec.kind in ("gamma", "beta") else ref.master().reshape(-1)
 
 
+def _bn_forward_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
+    C = x.shape[-1]
+    if use_hip("bn", x):
+        return _hip().bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps)
+    x2 = x.reshape(-1, C).float()
+    n = x2.shape[0]
+    mean = x2.mean(0)
+    var = x2.var(0, unbiased=False)
+    invstd = torch.rsqrt(var + eps)
+    with torch.no_grad():
+        rm, rv = rmref.master(), rvref.master()
+        rm.mul_(1 - momentum).add_(mean.view(rm.shape), alpha=momentum)
+        rv.mul_(1 - momentum).add_((var * n / max(n - 1, 1)).view(rv.shape), alpha=momentum)
+    gamma = gref.work().reshape(-1).float()
+    beta = bref.work().reshape(-1).float()
+    z = (x2 - mean) * (invstd * gamma) + beta
+    if residual is not None:
+        z = z + residual.reshape(-1, C).float()
+    z = _act(z, relu)
+    return z.to(x.dtype).view(x.shape), mean, invstd
+
+
 class PackedBNAct(torch.autograd.Function):
     """y = act(BN(x) + residual);  BN statistics per packed channel."""
 
     @staticmethod
     def forward(ctx, x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
-        C = x.shape[-1]
         ctx.refs = (gref, bref)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        if use_hip("bn", x):
-            y, mean, invstd = _hip().bn_act_fwd_train(x, residual, gref, bref, rmref, rvref,
-                                                      relu, momentum, eps)
-        else:
-            x2 = x.reshape(-1, C).float()
-            n = x2.shape[0]
-            mean = x2.mean(0)
-            var = x2.var(0, unbiased=False)
-            invstd = torch.rsqrt(var + eps)
-            with torch.no_grad():
-                rm, rv = rmref.master(), rvref.master()
-                rm.mul_(1 - momentum).add_(mean.view(rm.shape), alpha=momentum)
-                rv.mul_(1 - momentum).add_((var * n / max(n - 1, 1)).view(rv.shape), alpha=momentum)
-            gamma = gref.work().reshape(-1).float()
-            beta = bref.work().reshape(-1).float()
-            z = (x2 - mean) * (invstd * gamma) + beta
-            if residual is not None:
-                z = z + residual.reshape(-1, C).float()
-            z = _act(z, relu)
-            y = z.to(x.dtype).view(x.shape)
+        y, mean, invstd = _bn_forward_train(x, residual, gref, bref, rmref, rvref, relu, momentum,
+                                            eps)
         ctx.save_for_backward(x, y, mean, invstd)
         return y
 
@@ -178,23 +184,70 @@ class PackedBNAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, mean, invstd = ctx.saved_tensors
         gref, bref = ctx.refs
-        dy = dy.contiguous()
-        if use_hip("bn", x):
-            dx, dres = _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res)
-        else:
-            C = x.shape[-1]
-            dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
-            n = dz.shape[0]
-            xhat = (x.reshape(-1, C).float() - mean) * invstd
-            dbeta = dz.sum(0)
-            dgamma = (dz * xhat).sum(0)
-            gamma = gref.work().reshape(-1).float()
-            dx = (gamma * invstd / n) * (n * dz - dbeta - xhat * dgamma)
-            dx = dx.to(x.dtype).view(x.shape)
-            gref.grad().copy_(dgamma.view(gref.grad().shape))
-            bref.grad().copy_(dbeta.view(bref.grad().shape))
-            dres = dz.to(x.dtype).view(x.shape) if ctx.has_res else None
+        dx, dres = _bn_backward(ctx, dy.contiguous(), x, y, mean, invstd, gref, bref)
         return dx, dres, None, None, None, None, None, None, None
+
+
+class PackedConvBNAct(torch.autograd.Function):
+    """y = act(BN(conv(x)) + residual) in training mode — the ResNet unit.
+
+    HIP path: the convolution's GEMM epilogue also emits the per-channel
+    (sum, sum^2) partials of its bf16 output, so BN skips its statistics pass
+    over z (finalize + apply only).  Backward = BN backward, then the conv's
+    dgrad / wgrad on the BN input gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
+                momentum, eps):
+        ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        ctx.refs = (gref, bref)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        if use_hip("conv", x) and use_hip("bn", x):
+            h = _hip()
+            z, part, nslab = h.conv2d_fwd_stats(x, wref, stride, pad)
+            y, mean, invstd = h.bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, relu,
+                                                      momentum, eps, part, nslab)
+        else:
+            z = _conv_forward(x, wref, stride, pad)
+            y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,
+                                                momentum, eps)
+        ctx.save_for_backward(x, z, y, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, mean, invstd = ctx.saved_tensors
+        gref, bref = ctx.refs
+        dy = dy.contiguous()
+        dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
+        dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
+        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+
+
+def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
+    if use_hip("bn", x):
+        return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res)
+    C = x.shape[-1]
+    dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
+    n = dz.shape[0]
+    xhat = (x.reshape(-1, C).float() - mean) * invstd
+    dbeta = dz.sum(0)
+    dgamma = (dz * xhat).sum(0)
+    gamma = gref.work().reshape(-1).float()
+    dx = (gamma * invstd / n) * (n * dz - dbeta - xhat * dgamma)
+    dx = dx.to(x.dtype).view(x.shape)
+    gref.grad().copy_(dgamma.view(gref.grad().shape))
+    bref.grad().copy_(dbeta.view(bref.grad().shape))
+    dres = dz.to(x.dtype).view(x.shape) if ctx.has_res else None
+    return dx, dres
+
+
+def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
+                momentum=0.1, eps=1e-5, anchor=None):
+    return PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
+                                 relu, momentum, eps)
 
 
 def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):

@@ -1,9 +1,12 @@
 """Summarise a rocprofv3 SQLite output (``--kernel-trace --stats``) as markdown.
 
-    python -m cerebro_ds_kpgi_amd.tools.prof_summary gpurun_out/prof4 > profiles/x.md
+    python -m cerebro_ds_kpgi_amd.tools.prof_summary gpurun_out/prof4 [--last-steps K] > profiles/x.md
 
 Groups kernels into the framework's op families (conv fwd/dgrad/wgrad, BN,
 pooling, optimizer, loss, data, torch glue) and reports time per step.
+``--last-steps K`` keeps only the dispatches of the last K training steps
+(step boundaries = the fused Adam kernel, one per step), i.e. the
+steady-state HIP-graph replays, excluding init, autotuning and warm-up.
 """
 
 import glob
@@ -13,9 +16,9 @@ import sqlite3
 import sys
 
 FAMILIES = [
-    ("conv/linear GEMM (MFMA, NT: fwd)", r"igemm_nt"),
-    ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad"),
-    ("conv/linear wgrad (MFMA, TN)", r"igemm_wgrad"),
+    ("conv/linear GEMM (MFMA, NT: fwd)", r"igemm_nt|pipe_nt"),
+    ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad|pipe_nn"),
+    ("conv/linear wgrad (MFMA, TN)", r"igemm_wgrad|pipe_wg"),
     ("weight transpose (dgrad)", r"transpose_w"),
     ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),
     ("pooling", r"maxpool|gavg"),
@@ -37,9 +40,28 @@ def find_db(path):
     return dbs[0]
 
 
-def summarize(path, steps=None, title=None):
+def _rows(con, last_steps):
+    """[(name, calls, total_us, avg_us)] aggregated over the chosen window."""
+    disp = list(con.execute("select name, start, end from kernels order by start"))
+    if last_steps:
+        ends = [e for n, _, e in disp if "adam_kernel" in n]
+        if len(ends) > last_steps:
+            t0 = ends[-last_steps - 1]
+            disp = [d for d in disp if d[1] >= t0 and d[2] <= ends[-1]]
+    agg = {}
+    for name, st, en in disp:
+        a = agg.setdefault(name, [0, 0.0])
+        a[0] += 1
+        a[1] += (en - st) / 1000.0
+    rows = [(n, c, d, d / c) for n, (c, d) in agg.items()]
+    return sorted(rows, key=lambda r: -r[2])
+
+
+def summarize(path, steps=None, title=None, last_steps=None):
     con = sqlite3.connect(find_db(path))
-    rows = list(con.execute("select name, total_calls, total_duration, average from top_kernels"))
+    rows = _rows(con, last_steps)
+    if last_steps:
+        steps = last_steps
     total = sum(r[2] for r in rows)
     fam = {}
     for name, calls, dur, avg in rows:
@@ -54,8 +76,10 @@ def summarize(path, steps=None, title=None):
     out = []
     out.append("# {}".format(title or "rocprofv3 kernel summary"))
     out.append("")
-    out.append("source: `{}`; total GPU kernel time {:.1f} ms{}".format(
-        os.path.relpath(find_db(path)), total / 1000.0,
+    out.append("source: `{}`; {}total GPU kernel time {:.1f} ms{}".format(
+        os.path.relpath(find_db(path)),
+        "steady state (last {} steps); ".format(last_steps) if last_steps else "",
+        total / 1000.0,
         "" if not steps else " over {} steps = {:.2f} ms/step".format(steps, total / 1000.0 / steps)))
     out.append("")
     out.append("| family | calls | time (ms) | share |")
@@ -68,7 +92,7 @@ def summarize(path, steps=None, title=None):
     out.append("")
     out.append("| kernel | calls | total (ms) | avg (us) | share |")
     out.append("|---|---:|---:|---:|---:|")
-    for name, calls, dur, avg in rows[:25]:
+    for name, calls, dur, avg in rows[:30]:
         short = name if len(name) < 90 else name[:87] + "..."
         out.append("| `{}` | {} | {:.2f} | {:.1f} | {:.1f}% |".format(
             short.replace("|", "\\|"), calls, dur / 1000.0, avg, 100.0 * dur / total))
@@ -76,6 +100,11 @@ def summarize(path, steps=None, title=None):
 
 
 if __name__ == "__main__":
-    steps = int(sys.argv[2]) if len(sys.argv) > 2 else None
-    title = sys.argv[3] if len(sys.argv) > 3 else None
-    sys.stdout.write(summarize(sys.argv[1], steps, title))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--last-steps", type=int, default=None)
+    ap.add_argument("--title", default=None)
+    a = ap.parse_args()
+    sys.stdout.write(summarize(a.path, a.steps, a.title, a.last_steps))

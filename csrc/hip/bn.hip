@@ -313,26 +313,54 @@ CER_API int64_t cer_bn_part_floats(int64_t M, int C) {
   return (int64_t)g.y * 2 * C;
 }
 
-CER_API int cer_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
+static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
                              int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
                              float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
-                             float* invstd_out, float* ws, float* part, int64_t M, int C,
-                             int Cper, float eps, float momentum, int act, hipStream_t stream) {
+                             float* invstd_out, float* ws, float* part, int nslab, int64_t M,
+                             int C, int Cper, float eps, float momentum, int act,
+                             hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 rg, ag;
   int rrows, arows;
-  make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
-                                          rrows, 0, mp);
-  bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, mean_out,
+  if (nslab <= 0) {  // statistics not produced upstream: reduce x here
+    make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
+    bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
+                                            rrows, 0, mp);
+    nslab = (int)rg.y;
+  }
+  bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
                                                           M, C, Cper, eps, momentum);
   bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                            Strided{gamma, gamma_stride},
                                            Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
   return (int)hipGetLastError();
+}
+
+CER_API int cer_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
+                             int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
+                             float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
+                             float* invstd_out, float* ws, float* part, int64_t M, int C,
+                             int Cper, float eps, float momentum, int act, hipStream_t stream) {
+  return bn_fwd_train_impl(x, res, y, gamma, gamma_stride, beta, beta_stride, rmean, rvar,
+                           rstat_stride, mean_out, invstd_out, ws, part, 0, M, C, Cper, eps,
+                           momentum, act, stream);
+}
+
+// same, with the per-slab (sum, sum^2) partials already produced by the
+// producing convolution's epilogue (cer_conv_fwd_stats)
+CER_API int cer_bn_fwd_train_part(const bf16_t* x, const bf16_t* res, bf16_t* y,
+                                  const bf16_t* gamma, int64_t gamma_stride, const bf16_t* beta,
+                                  int64_t beta_stride, float* rmean, float* rvar,
+                                  int64_t rstat_stride, float* mean_out, float* invstd_out,
+                                  float* ws, float* part, int nslab, int64_t M, int C, int Cper,
+                                  float eps, float momentum, int act, hipStream_t stream) {
+  if (nslab <= 0) return (int)hipErrorInvalidValue;
+  return bn_fwd_train_impl(x, res, y, gamma, gamma_stride, beta, beta_stride, rmean, rvar,
+                           rstat_stride, mean_out, invstd_out, ws, part, nslab, M, C, Cper, eps,
+                           momentum, act, stream);
 }
 
 CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,

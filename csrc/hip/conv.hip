@@ -84,6 +84,8 @@ struct NTParams {
   int64_t bias_gstride;
   int act;                // 0 none, 1 relu, 6 relu6
   int o_st, o_H, o_W;     // o_st > 1: GEMM row (b,y,x) stores to output pixel (b, y*o_st, x*o_st)
+  float* stats;           // optional BN partials part[slab][2][ldc] (sum, sum^2) of the
+                          // bf16 outputs; slab = 2 * M-tile + wave row (fused BN forward)
 };
 
 struct WGParams {
@@ -320,8 +322,8 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
 // in fp32, one rounding, one 8-B LDS write per fragment.
 template <int BM, int BN>
 __device__ __forceinline__ void stage_c(const NTParams& p, bf16_t* lds,
-                                        const f32x4 (&acc)[BM / 32][BN / 32], int cfg, int n0,
-                                        int wm, int wn, int lane) {
+                                        const f32x4 (&acc)[BM / 32][BN / 32], int cfg, int m0,
+                                        int n0, int wm, int wn, int lane) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16, LDE = BN + 8;
   const int fr = lane & 15, fc = lane >> 4;
   float bc[FN][4];
@@ -347,6 +349,36 @@ __device__ __forceinline__ void stage_c(const NTParams& p, bf16_t* lds,
       pk.y = pack_bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(lds + (wm * TM + 16 * i + fr) * LDE + wn * TN + 16 * j + 4 * fc) = pk;
     }
+  if (p.stats) {
+    // per-channel (sum, sum^2) of the ROUNDED outputs over this wave's TM
+    // rows: in-lane over i, then across the 16 lanes of equal fc.  Rows past
+    // M are zero (no bias on BN convs) and add nothing.  One writer per
+    // (slab, channel): deterministic, no atomics.
+    const int slab = 2 * (m0 / BM) + wm;
+    float* dst = p.stats + (int64_t)slab * 2 * p.ldc + (int64_t)cfg * p.N;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sm = 0.f, sq = 0.f;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const float r = bf2f(f2bf(acc[i][j][e]));
+          sm += r;
+          sq += r * r;
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sm += __shfl_xor(sm, o, 64);
+          sq += __shfl_xor(sq, o, 64);
+        }
+        const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+        if (fr == 0 && n < p.N) {
+          dst[n] = sm;
+          dst[p.ldc + n] = sq;
+        }
+      }
+  }
 }
 
 template <int BM, int BN, int GM>
@@ -461,7 +493,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
 
   // epilogue: stage the bf16 tile in LDS, then 16-B coalesced stores
   constexpr int LDE = BN + 8;
-  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
@@ -734,7 +766,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
     __syncthreads();
   }
   constexpr int LDE = BN + 8;
-  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
@@ -936,7 +968,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   });
 
   constexpr int LDE = BN + 8;
-  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
@@ -1006,7 +1038,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   });
 
   constexpr int LDE = BN + 8;
-  stage_c<BM, BN>(p, lds, acc, cfg, n0, wm, wn, lane);
+  stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
@@ -1182,11 +1214,16 @@ static bool nt_fast(const NTParams& p) {
          p.a.bytes != 0 && (uint64_t)p.N * p.K * 2 < (1ull << 31);
 }
 
-static int run_nt(const NTParams& p, int G, hipStream_t stream) {
+static int run_nt(const NTParams& p, int G, hipStream_t stream, int* nslab = nullptr) {
   const bool fast = nt_fast(p);
   const bool pipe_ok = fast && p.a.Cg % 64 == 0;
   const int v = fast ? choose(0, p.M, p.N, p.K, G, pipe_ok) : choose(0, p.M, p.N, p.K, G, false) % 3;
   const int kind = v / 3;
+  if (nslab) {
+    int bm, bn;
+    tile_dims(v, bm, bn);
+    *nslab = 2 * (int)((p.M + bm - 1) / bm);
+  }
   switch (v % 3) {
     case 0: launch_nt_t<64, 64>(p, G, kind, fast, stream); break;
     case 1: launch_nt_t<128, 128>(p, G, kind, fast, stream); break;
@@ -1195,10 +1232,39 @@ static int run_nt(const NTParams& p, int G, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+                         int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                         bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
+                         int act, float* stats, int* nslab, hipStream_t stream);
+
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
                          int act, hipStream_t stream) {
+  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
+                       bias_gstride, act, nullptr, nullptr, stream);
+}
+
+// forward + BN statistics partials (bias-free, no activation): part holds
+// cer_conv_stats_floats(M, C) floats; *nslab receives the slab count to hand
+// to the BN finalize
+CER_API int cer_conv_fwd_stats(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                               const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
+                               int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
+                               int* nslab, hipStream_t stream) {
+  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
+                       nullptr, 0, 0, part, nslab, stream);
+}
+
+// upper bound over tile choices: 2 slabs per 64-row M tile
+CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
+  return 2 * ((M + 63) / 64) * 2 * (int64_t)C;
+}
+
+static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+                         int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                         bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
+                         int act, float* stats, int* nslab, hipStream_t stream) {
   NTParams p;
   p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
   p.dgrad = 0;
@@ -1215,7 +1281,8 @@ CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
   p.o_st = 1;
   p.o_H = Ho;
   p.o_W = Wo;
-  return run_nt(p, G, stream);
+  p.stats = stats;
+  return run_nt(p, G, stream, nslab);
 }
 
 template <int BM, int BN>
@@ -1254,6 +1321,7 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
                            hipStream_t stream) {
   const int T = kh * kw;
   NTParams p;
+  p.stats = nullptr;
   p.bias = nullptr;
   p.bias_gstride = 0;
   p.act = 0;

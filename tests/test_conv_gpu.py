@@ -255,3 +255,49 @@ def test_conv_variant_matches_oracle(case, variant):
     finally:
         for op in range(3):
             _hip.conv_set_variant(op, -1)
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("case", [
+    (4, 14, 14, 64, 128, 3, 1, 1, 2, True, False),
+    (2, 28, 28, 64, 256, 1, 1, 0, 3, False, True),
+    (2, 56, 56, 3, 64, 7, 2, 3, 2, True, False),       # stem (unaligned conv path)
+    (3, 9, 9, 128, 64, 1, 2, 0, 2, 6, True),
+])
+def test_conv_bn_fused_matches_oracle(case, variant):
+    """Fused conv + BN(+res)(+act): BN statistics from the conv GEMM epilogue."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    B, H, W, cin, cout, k, s, p, G, act, res = case
+    specs = [ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin),
+             ParamSpec("g", (cout,), "gamma"), ParamSpec("b", (cout,), "beta"),
+             ParamSpec("rm", (cout,), "running_mean"), ParamSpec("rv", (cout,), "running_var")]
+    torch.manual_seed(7)
+    x = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+    Ho = (H + 2 * p - k) // s + 1
+    r = torch.randn(B, Ho, Ho, G * cout, device="cuda").to(torch.bfloat16) if res else None
+    outs = []
+    if variant >= 0:
+        _hip.conv_set_variant(0, variant)
+    try:
+        for force in ([], ["conv", "bn"]):
+            backend.force_torch_ops(force)
+            a, refs = _make(specs, G, seed=9)
+            xx = x.clone().requires_grad_(True)
+            rr = r.clone().requires_grad_(True) if res else None
+            y = P.conv_bn_act(xx, refs["w"], refs["g"], refs["b"], refs["rm"], refs["rv"], s, p,
+                              act, rr)
+            torch.manual_seed(3)
+            y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
+                         a.master.clone()))
+    finally:
+        backend.force_torch_ops([])
+        _hip.conv_set_variant(0, -1)
+    h, t = outs
+    assert _rel(h[0], t[0]) < 2e-2
+    assert _rel(h[1], t[1]) < 3e-2
+    if res:
+        assert _rel(h[2], t[2]) < 2e-2
+    assert _rel(h[3], t[3]) < 3e-2          # dW, dgamma, dbeta
+    assert _rel(h[4], t[4]) < 1e-3          # running stats (+ untouched weights)
