@@ -20,7 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libcerebro_hip.so")
 
 IMPLEMENTED = {"adam", "loss", "gather"}
-_RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats"}
+_RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -134,6 +134,12 @@ _SIGS.update({
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                            c_p, c_i, c_i, c_p, c_p, c_p],
     "cer_conv_stats_floats": [c_i64, c_i],
+    "cer_stem_ok": [c_i, c_i, c_i, c_i, c_i],
+    "cer_stem_wpk_elems": [c_i, c_i, c_i, c_i],
+    "cer_stem_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
+                     c_p, c_i, c_i, c_p, c_p, c_p],
+    "cer_stem_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
+                       c_i64, c_p],
     "cer_bn_fwd_train_part": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
                               c_p, c_p, c_i, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
     "cer_bn_fwd_train": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p,
@@ -265,6 +271,59 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
     launch()
     return z, part, nslab.value
+
+
+def stem_ok(x, wref, stride, pad):
+    """Narrow-input stem eligible for the pixel-pair path (cer_stem_fwd)."""
+    cout, kh, kw, cin = wref.spec.shape
+    return bool(lib().cer_stem_ok(cin, x.shape[2], kw, stride, pad))
+
+
+def stem_fwd_stats(x, wref, stride, pad):
+    """Stem conv via the repacked pixel-pair geometry, with BN partials.
+    Returns (z, part, nslab, x4) — x4 (the repacked input) feeds the wgrad."""
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    z = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
+    x4 = torch.empty((G, B, H, W, 4), dtype=torch.bfloat16, device=x.device)
+    L = lib()
+    wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.bfloat16,
+                      device=x.device)
+    part = torch.empty(int(L.cer_conv_stats_floats(B * Ho * Wo, G * cout)), dtype=torch.float32,
+                       device=x.device)
+    nslab = ctypes.c_int(0)
+    wp, ws = wref.work_ptr()
+
+    def launch():
+        rc = lib().cer_stem_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
+                                _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
+                                ctypes.byref(nslab), _stream())
+        _check(rc, "cer_stem_fwd")
+    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch)
+    launch()
+    return z, part, nslab.value, x4
+
+
+def stem_wgrad(x4, dy, wref, pad):
+    dy = _bf16(dy)
+    G, B, H, W, _ = x4.shape
+    _, Ho, Wo, _ = dy.shape
+    cout, kh, kw, cin = wref.spec.shape
+    L = lib()
+    dwp = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.float32,
+                      device=dy.device)
+    gp, gs = wref.grad_ptr()
+
+    def launch():
+        rc = lib().cer_stem_wgrad(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, pad,
+                                  _ptr(dwp), c_p(gp), gs, _stream())
+        _check(rc, "cer_stem_wgrad")
+    _select(2, ("stem", B, H, W, cin, cout, kh, kw, pad, G), launch)
+    launch()
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W):

@@ -204,9 +204,14 @@ class PackedConvBNAct(torch.autograd.Function):
         ctx.refs = (gref, bref)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.x4 = None
         if use_hip("conv", x) and use_hip("bn", x):
             h = _hip()
-            z, part, nslab = h.conv2d_fwd_stats(x, wref, stride, pad)
+            if not x.requires_grad and h.stem_ok(x, wref, stride, pad):
+                # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
+                z, part, nslab, ctx.x4 = h.stem_fwd_stats(x, wref, stride, pad)
+            else:
+                z, part, nslab = h.conv2d_fwd_stats(x, wref, stride, pad)
             y, mean, invstd = h.bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, relu,
                                                       momentum, eps, part, nslab)
         else:
@@ -222,7 +227,12 @@ class PackedConvBNAct(torch.autograd.Function):
         gref, bref = ctx.refs
         dy = dy.contiguous()
         dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
-        dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
+        if ctx.x4 is not None:
+            _hip().stem_wgrad(ctx.x4, dz, ctx.wref, ctx.pad)
+            ctx.x4 = None
+            dx = None
+        else:
+            dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
         return dx, dres, None, None, None, None, None, None, None, None, None, None, None
 
 

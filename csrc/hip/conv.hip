@@ -67,9 +67,11 @@ struct GatherGeom {
   int Cg;             // channels per config of the gathered tensor
   int Hs, Ws;         // gathered tensor spatial dims
   int Hm, Wm;         // GEMM row grid (pixels of the GEMM's M dimension)
-  int kh, kw, st, pad;
+  int kh, kw, st, pad;  // stride / padding along H (and W unless overridden below)
   uint32_t bytes;     // size of src in bytes (buffer-load range); 0 = too big for 32-bit offsets
   FastDiv dWm, dHm, dCg, dkw, dst;
+  int st_w, pad_w;    // stride / padding along W
+  int64_t cfg_off;    // elements between configs (Cg for the packed layout)
 };
 
 struct NTParams {
@@ -85,7 +87,7 @@ struct NTParams {
   int act;                // 0 none, 1 relu, 6 relu6
   int o_st, o_H, o_W;     // o_st > 1: GEMM row (b,y,x) stores to output pixel (b, y*o_st, x*o_st)
   float* stats;           // optional BN partials part[slab][2][ldc] (sum, sum^2) of the
-                          // bf16 outputs; slab = 2 * M-tile + wave row (fused BN forward)
+                          // bf16 outputs; slab = M tile (fused BN forward)
 };
 
 struct WGParams {
@@ -101,7 +103,7 @@ struct WGParams {
 
 static GatherGeom make_geom(const bf16_t* src, int B, int Ctot, int Cg, int Hs, int Ws, int Hm,
                             int Wm, int kh, int kw, int st, int pad) {
-  GatherGeom g{src, Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad, 0u, {}, {}, {}, {}, {}};
+  GatherGeom g{src, Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad, 0u, {}, {}, {}, {}, {}, st, pad, Cg};
   const uint64_t bytes = (uint64_t)B * Hs * Ws * Ctot * sizeof(bf16_t);
   g.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   g.dWm = make_div((uint32_t)Wm);
@@ -166,10 +168,10 @@ __device__ __forceinline__ RowA row_init(const GatherGeom& g, int m, int M) {
   RowA a;
   if (GM == GM_FWD) {
     a.hy = p.y * g.st - g.pad;
-    a.wx = p.x * g.st - g.pad;
+    a.wx = p.x * g.st_w - g.pad_w;
   } else {
     a.hy = p.y + g.pad;
-    a.wx = p.x + g.pad;
+    a.wx = p.x + g.pad_w;
   }
   a.pix = (GM == GM_DGS) ? p.b * g.Hs : (p.b * g.Hs + a.hy) * g.Ws + a.wx;
   if (!p.ok) a.hy = -(1 << 29);  // every tap out of range
@@ -208,9 +210,9 @@ __device__ __forceinline__ int64_t src_pixel(const GatherGeom& g, const RowPos& 
   int hi, wi;
   if (!dgrad) {
     hi = p.y * g.st - g.pad + r;
-    wi = p.x * g.st - g.pad + s;
+    wi = p.x * g.st_w - g.pad_w + s;
   } else {
-    int hn = p.y + g.pad - r, wn = p.x + g.pad - s;
+    int hn = p.y + g.pad - r, wn = p.x + g.pad_w - s;
     if (hn < 0 || wn < 0) return -1;
     if (g.st > 1) {
       if ((hn % g.st) | (wn % g.st)) return -1;
@@ -245,7 +247,7 @@ __device__ __forceinline__ uint4 gather_chunk_slow(const GatherGeom& g, int cfg,
       const int tap = (int)fdiv((uint32_t)k, g.dCg), c = k - tap * g.Cg;
       const int r = (int)fdiv((uint32_t)tap, g.dkw), s = tap - r * g.kw;
       const int64_t off = src_pixel(g, p, r, s, dgrad);
-      if (off >= 0) e[i] = g.src[off + (int64_t)cfg * g.Cg + c];
+      if (off >= 0) e[i] = g.src[off + (int64_t)cfg * g.cfg_off + c];
     }
   }
   return pack8(e);
@@ -316,6 +318,19 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
   }
 }
 
+// sum over each 16-lane row of the wave (DPP butterfly, no LDS traffic)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1,
+                                                             0xF, 0xF, false));  // quad [1,0,3,2]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E,
+                                                             0xF, 0xF, false));  // quad [2,3,0,1]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141,
+                                                             0xF, 0xF, false));  // row_half_mirror
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140,
+                                                             0xF, 0xF, false));  // row_mirror
+  return v;
+}
+
 // Epilogue staging for the NT / NN kernels.  Their MFMAs take the weight
 // fragment as the FIRST operand, so a lane's accumulator holds 4 consecutive
 // output channels of one output row, C[16i + fr][16j + 4fc + e]: bias + act
@@ -350,12 +365,12 @@ __device__ __forceinline__ void stage_c(const NTParams& p, bf16_t* lds,
       *reinterpret_cast<uint2*>(lds + (wm * TM + 16 * i + fr) * LDE + wn * TN + 16 * j + 4 * fc) = pk;
     }
   if (p.stats) {
-    // per-channel (sum, sum^2) of the ROUNDED outputs over this wave's TM
-    // rows: in-lane over i, then across the 16 lanes of equal fc.  Rows past
-    // M are zero (no bias on BN convs) and add nothing.  One writer per
-    // (slab, channel): deterministic, no atomics.
-    const int slab = 2 * (m0 / BM) + wm;
-    float* dst = p.stats + (int64_t)slab * 2 * p.ldc + (int64_t)cfg * p.N;
+    // per-channel (sum, sum^2) of the ROUNDED outputs: in-lane over the i
+    // fragments, DPP butterfly across the 16 lanes of equal fc, then the
+    // two M-direction waves meet in LDS (stats_finish) -> one deterministic
+    // partial per (M tile, channel).  Rows past M are zero (BN convs carry
+    // no bias) and add nothing.
+    float* xch = reinterpret_cast<float*>(lds + BM * LDE);  // [2 wm][2][BN]
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -367,17 +382,28 @@ __device__ __forceinline__ void stage_c(const NTParams& p, bf16_t* lds,
           sm += r;
           sq += r * r;
         }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          sm += __shfl_xor(sm, o, 64);
-          sq += __shfl_xor(sq, o, 64);
-        }
-        const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
-        if (fr == 0 && n < p.N) {
-          dst[n] = sm;
-          dst[p.ldc + n] = sq;
+        sm = row16_sum(sm);
+        sq = row16_sum(sq);
+        if (fr == 0) {
+          const int nl = wn * TN + 16 * j + 4 * fc + e;
+          xch[(wm * 2) * BN + nl] = sm;
+          xch[(wm * 2 + 1) * BN + nl] = sq;
         }
       }
+  }
+}
+
+// second half of the fused BN statistics (after the epilogue barrier)
+template <int BM, int BN>
+__device__ __forceinline__ void stats_finish(const NTParams& p, const bf16_t* lds, int cfg, int m0,
+                                             int n0, int tid) {
+  if (!p.stats) return;
+  constexpr int LDE = BN + 8;
+  const float* xch = reinterpret_cast<const float*>(lds + BM * LDE);
+  float* dst = p.stats + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  for (int t = tid; t < 2 * BN; t += NTHREADS) {
+    const int q = t / BN, nl = t - q * BN, n = n0 + nl;
+    if (n < p.N) dst[(int64_t)q * p.ldc + n] = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
   }
 }
 
@@ -387,7 +413,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   constexpr int CPR = BK / 8;                                  // 16-B chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int EPI_ELEMS = BM * (BN + 8);
+  constexpr int EPI_ELEMS = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = TILE_ELEMS > EPI_ELEMS ? TILE_ELEMS : EPI_ELEMS;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 #define SA(buf) (lds + (buf) * (BM * BK))
@@ -403,7 +429,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   const int wm = wid >> 1, wn = wid & 1;
   const int my_chunk = tid & (CPR - 1);                        // same for every i below
   const bf16_t* wbase = p.w + (int64_t)cfg * p.w_gstride;
-  const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.Cg;
+  const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.cfg_off;
 
   RowPos rows[A_CH];
   RowA rowa[A_CH];
@@ -495,6 +521,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
+  stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
@@ -555,7 +582,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
   if (b_kok) bk = kpos_init(p.x, kk0);
   uint4 ra[A_CH], rb[B_CH];
   const bf16_t* dyb = p.dy + (int64_t)cfg * p.N;
-  const bf16_t* xb = p.x.src + (int64_t)cfg * p.x.Cg;
+  const bf16_t* xb = p.x.src + (int64_t)cfg * p.x.cfg_off;
   __amdgpu_buffer_rsrc_t rDY, rX;
   if constexpr (GM != GM_SLOW) {
     rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 2u);
@@ -676,7 +703,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   constexpr int A_CH = BM * CPR / NTHREADS;
   constexpr int B_CPR = BN / 8, B_CH = BK * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int EPI_ELEMS = BM * (BN + 8);
+  constexpr int EPI_ELEMS = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = TILE_ELEMS > EPI_ELEMS ? TILE_ELEMS : EPI_ELEMS;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 
@@ -692,7 +719,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   const int Cout = p.a.Cg;          // reduction channels (k = tap*Cout + n)
   const int Cin = p.N;              // output channels
   const bf16_t* wbase = p.w + (int64_t)cfg * p.w_gstride;
-  const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.Cg;
+  const bf16_t* abase = p.a.src + (int64_t)cfg * p.a.cfg_off;
   const int b_col = 8 * (tid % B_CPR), b_row0 = tid / B_CPR;
   const __amdgpu_buffer_rsrc_t rA = make_rsrc(abase, p.a.bytes);
   const __amdgpu_buffer_rsrc_t rW = make_rsrc(wbase, (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 2u);
@@ -768,6 +795,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
+  stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
@@ -912,7 +940,7 @@ template <int BM, int BN, int S>
 __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int EPI = BM * (BN + 8);
+  constexpr int EPI = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 
@@ -925,7 +953,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
-  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.Cg, p.a.bytes);
+  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.cfg_off, p.a.bytes);
   const auto rB = make_rsrc(p.w + (int64_t)cfg * p.w_gstride, (uint32_t)p.N * (uint32_t)p.K * 2u);
 
   RowA arow[AJ];
@@ -970,6 +998,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
+  stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
@@ -978,7 +1007,7 @@ template <int BM, int BN, int S, int GM>
 __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int EPI = BM * (BN + 8);
+  constexpr int EPI = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
   constexpr int BROWS = 512 / BN, BC16 = BN / 8;   // rows / 16-B columns per B piece
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
@@ -993,7 +1022,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int Cout = p.a.Cg, Cin = p.N;
-  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.Cg, p.a.bytes);
+  const auto rA = make_rsrc(p.a.src + (int64_t)cfg * p.a.cfg_off, p.a.bytes);
   const auto rW = make_rsrc(p.w + (int64_t)cfg * p.w_gstride,
                             (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 2u);
 
@@ -1040,6 +1069,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
+  stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
   store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
@@ -1066,7 +1096,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_wg(WGParams p) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const auto rDY = make_rsrc(p.dy + (int64_t)cfg * p.N, (uint32_t)p.Mred * (uint32_t)p.ldy * 2u);
-  const auto rX = make_rsrc(p.x.src + (int64_t)cfg * p.x.Cg, p.x.bytes);
+  const auto rX = make_rsrc(p.x.src + (int64_t)cfg * p.x.cfg_off, p.x.bytes);
 
   int arow[AJ];
   uint32_t aoff[AJ];
@@ -1222,7 +1252,7 @@ static int run_nt(const NTParams& p, int G, hipStream_t stream, int* nslab = nul
   if (nslab) {
     int bm, bn;
     tile_dims(v, bm, bn);
-    *nslab = 2 * (int)((p.M + bm - 1) / bm);
+    *nslab = (int)((p.M + bm - 1) / bm);
   }
   switch (v % 3) {
     case 0: launch_nt_t<64, 64>(p, G, kind, fast, stream); break;
@@ -1256,9 +1286,9 @@ CER_API int cer_conv_fwd_stats(const bf16_t* x, int B, int H, int W, int Cin, in
                        nullptr, 0, 0, part, nslab, stream);
 }
 
-// upper bound over tile choices: 2 slabs per 64-row M tile
+// upper bound over tile choices: one slab per 64-row M tile
 CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
-  return 2 * ((M + 63) / 64) * 2 * (int64_t)C;
+  return ((M + 63) / 64) * 2 * (int64_t)C;
 }
 
 static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
@@ -1439,4 +1469,162 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
 // when channels are 8-aligned)
 CER_API int cer_wgrad_splits(int Mred, int N, int K, int G) {
   return wg_splits(Mred, N, K, G, wg_variant(N, K, G, true));
+}
+
+// ---------------------------------------------------------------------------
+// Narrow-input stem (Cin <= 4, stride 2, odd padding, even width: ResNet's
+// 7x7/2 and MobileNetV2's 3x3/2 first layers).  With 3 channels an im2col
+// row has no aligned 16-B chunks, so the generic path gathers element by
+// element.  Instead the image is repacked per config as [B][H][W][4]
+// (channel 3 = 0) and read as PIXEL PAIRS: [B][H][W/2][8].  The stride-2
+// conv over W becomes a stride-1 conv over pairs with kw' = kw/2 + 1 taps:
+// original tap s = 2*sp + px - 1 (px = pixel within the pair), so every
+// 16-B chunk is one (row tap, pair tap) and the aligned MFMA path applies.
+// Weights are re-laid [N][kh][kw'][8] per step (zeros on padded taps /
+// channels); the wgrad runs on the same geometry and is folded back.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void stem_repack_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ x4, int64_t P,
+                                                          int G, int C) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, config)
+  if (i >= P * G) return;
+  const int64_t p = i / G;
+  const int g = (int)(i - p * G);
+  const bf16_t* src = x + p * G * C + (int64_t)g * C;
+  uint16_t e[4] = {0, 0, 0, 0};
+  for (int c = 0; c < C; ++c) e[c] = src[c];
+  uint2 v;
+  v.x = e[0] | ((uint32_t)e[1] << 16);
+  v.y = e[2] | ((uint32_t)e[3] << 16);
+  *reinterpret_cast<uint2*>(x4 + ((int64_t)g * P + p) * 4) = v;
+}
+
+__global__ __launch_bounds__(256) void stem_pack_w_kernel(const bf16_t* __restrict__ w,
+                                                          int64_t w_gstride,
+                                                          bf16_t* __restrict__ wp, int N, int kh,
+                                                          int kw, int C, int kwp, int G) {
+  const int64_t per = (int64_t)N * kh * kwp * 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= per * G) return;
+  const int g = (int)(i / per);
+  int64_t t = i - g * per;
+  const int q = (int)(t % 8);
+  t /= 8;
+  const int sp = (int)(t % kwp);
+  t /= kwp;
+  const int r = (int)(t % kh);
+  const int n = (int)(t / kh);
+  const int px = q >> 2, c = q & 3, s = 2 * sp + px - 1;
+  bf16_t v = 0;
+  if (s >= 0 && s < kw && c < C) v = w[g * w_gstride + (((int64_t)n * kh + r) * kw + s) * C + c];
+  wp[i] = v;
+}
+
+__global__ __launch_bounds__(256) void stem_fold_grad_kernel(const float* __restrict__ dwp,
+                                                             float* __restrict__ dw,
+                                                             int64_t dw_gstride, int N, int kh,
+                                                             int kw, int C, int kwp, int G) {
+  const int64_t per = (int64_t)N * kh * kw * C;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= per * G) return;
+  const int g = (int)(i / per);
+  int64_t t = i - g * per;
+  const int c = (int)(t % C);
+  t /= C;
+  const int s = (int)(t % kw);
+  t /= kw;
+  const int r = (int)(t % kh);
+  const int n = (int)(t / kh);
+  const int sp = (s + 1) >> 1, px = (s + 1) & 1;
+  dw[g * dw_gstride + (((int64_t)n * kh + r) * kw + s) * C + c] =
+      dwp[((((int64_t)g * N + n) * kh + r) * kwp + sp) * 8 + px * 4 + c];
+}
+
+static int stem_kwp(int kw) { return kw / 2 + 1; }
+
+CER_API int cer_stem_ok(int Cin, int W, int kw, int st, int pad) {
+  return (Cin <= 4 && st == 2 && (pad & 1) && (W % 2) == 0 && kw >= 2) ? 1 : 0;
+}
+
+// scratch sizes (elements): x4 = B*H*W*4*G bf16, wpk = G*Cout*kh*kwp*8 bf16
+CER_API int64_t cer_stem_wpk_elems(int G, int Cout, int kh, int kw) {
+  return (int64_t)G * Cout * kh * stem_kwp(kw) * 8;
+}
+
+static GatherGeom stem_geom(const bf16_t* x4, int B, int H, int W, int Ho, int Wo, int kh,
+                            int kw, int pad) {
+  const int kwp = stem_kwp(kw);
+  GatherGeom g = make_geom(x4, B, 8, 8, H, W / 2, Ho, Wo, kh, kwp, 2, pad);
+  g.st_w = 1;
+  g.pad_w = (pad + 1) / 2;
+  g.cfg_off = (int64_t)B * H * (W / 2) * 8;
+  return g;
+}
+
+// repack + weight re-layout + forward conv (+ BN partials when part != null)
+CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+                         int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                         bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
+                         int* nslab, hipStream_t stream) {
+  if (!cer_stem_ok(Cin, W, kw, st, pad)) return (int)hipErrorInvalidValue;
+  const int64_t P = (int64_t)B * H * W;
+  stem_repack_kernel<<<cer_blocks(P * G, 256), 256, 0, stream>>>(x, x4, P, G, Cin);
+  const int kwp = stem_kwp(kw);
+  const int64_t nw = (int64_t)G * Cout * kh * kwp * 8;
+  stem_pack_w_kernel<<<cer_blocks(nw, 256), 256, 0, stream>>>(w, w_gstride, wpk, Cout, kh, kw,
+                                                              Cin, kwp, G);
+  NTParams p;
+  p.a = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
+  // the whole [G][B][H][W/2][8] buffer is the buffer-load range
+  const uint64_t bytes = (uint64_t)G * P * 4 * 2;
+  p.a.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
+  p.dgrad = 0;
+  p.w = wpk;
+  p.w_gstride = (int64_t)Cout * kh * kwp * 8;
+  p.out = y;
+  p.ldc = G * Cout;
+  p.M = B * Ho * Wo;
+  p.N = Cout;
+  p.K = kh * kwp * 8;
+  p.bias = nullptr;
+  p.bias_gstride = 0;
+  p.act = 0;
+  p.o_st = 1;
+  p.o_H = Ho;
+  p.o_W = Wo;
+  p.stats = part;
+  return run_nt(p, G, stream, nslab);
+}
+
+// dW of the stem from the repacked input; dwp: fp32 scratch of
+// cer_stem_wpk_elems floats (zeroed here when the reduction is split)
+CER_API int cer_stem_wgrad(const bf16_t* x4, int B, int H, int W, int Cin, int G,
+                           const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
+                           float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
+  const int kwp = stem_kwp(kw);
+  WGParams p;
+  p.x = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
+  const uint64_t bytes = (uint64_t)G * B * H * W * 4 * 2;
+  p.x.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
+  p.dy = dy;
+  p.ldy = G * Cout;
+  p.dw = dwp;
+  p.dw_gstride = (int64_t)Cout * kh * kwp * 8;
+  p.Mred = B * Ho * Wo;
+  p.N = Cout;
+  p.K = kh * kwp * 8;
+  const bool fast = wg_fast(8, Cout, p);
+  const int v = wg_variant(p.N, p.K, G, fast);
+  const int splits = wg_splits(p.Mred, p.N, p.K, G, v);
+  if (splits > 1) (void)hipMemsetAsync(dwp, 0, sizeof(float) * (size_t)G * p.dw_gstride, stream);
+  const int kind = v / 3;
+  switch (v % 3) {
+    case 0: launch_wg_t<64, 64>(p, G, kind, fast, splits, stream); break;
+    case 1: launch_wg_t<128, 128>(p, G, kind, fast, splits, stream); break;
+    default: launch_wg_t<128, 64>(p, G, kind, fast, splits, stream); break;
+  }
+  const int64_t n = (int64_t)G * Cout * kh * kw * Cin;
+  stem_fold_grad_kernel<<<cer_blocks(n, 256), 256, 0, stream>>>(dwp, dw, dw_gstride, Cout, kh, kw,
+                                                                Cin, kwp, G);
+  return (int)hipGetLastError();
 }

@@ -282,10 +282,11 @@ def test_conv_bn_fused_matches_oracle(case, variant):
         for force in ([], ["conv", "bn"]):
             backend.force_torch_ops(force)
             a, refs = _make(specs, G, seed=9)
-            xx = x.clone().requires_grad_(True)
+            # a 3-channel input (network input, no grad) takes the pixel-pair stem path
+            xx = x.clone().requires_grad_(cin > 4)
             rr = r.clone().requires_grad_(True) if res else None
             y = P.conv_bn_act(xx, refs["w"], refs["g"], refs["b"], refs["rm"], refs["rv"], s, p,
-                              act, rr)
+                              act, rr, anchor=torch.zeros((), device="cuda", requires_grad=True))
             torch.manual_seed(3)
             y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
             torch.cuda.synchronize()
@@ -296,7 +297,8 @@ def test_conv_bn_fused_matches_oracle(case, variant):
         _hip.conv_set_variant(0, -1)
     h, t = outs
     assert _rel(h[0], t[0]) < 2e-2
-    assert _rel(h[1], t[1]) < 3e-2
+    if cin > 4:
+        assert _rel(h[1], t[1]) < 3e-2
     if res:
         assert _rel(h[2], t[2]) < 2e-2
     assert _rel(h[3], t[3]) < 3e-2          # dW, dgamma, dbeta
