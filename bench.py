@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no_graphs", action="store_true")
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--configs", type=int, default=0,
+                    help="diagnostic: train only the first K configs (per-GPU work of N = 8/K "
+                         "GPUs); the headline number always uses all 8")
     args = ap.parse_args()
 
     import torch
@@ -60,6 +63,8 @@ def main():
     grid = dict(cat.param_grid_scalability)
     grid["model"] = [args.model]
     msts = get_msts(grid)
+    if args.configs:
+        msts = msts[:args.configs]
     S = len(msts)
     B = msts[0]["batch_size"]
     n_train = max(args.train_per_partition, B * args.steps_per_round)
@@ -89,7 +94,8 @@ def main():
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(N)
         out = {
-            "metric": "agg_train_images_per_sec_8cfg_resnet50_mop",
+            "metric": "agg_train_images_per_sec_8cfg_resnet50_mop" if S == 8 else
+                      "diag_train_images_per_sec_{}cfg_resnet50_mop".format(S),
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": N,

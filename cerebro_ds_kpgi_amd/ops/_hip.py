@@ -28,8 +28,8 @@ c_i = ctypes.c_int
 c_f = ctypes.c_float
 
 _SIGS = {
-    "cer_adam_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p,
-                      c_i, c_f, c_f, c_f, c_i, c_p],
+    "cer_adam_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p,
+                      c_p, c_i, c_f, c_f, c_f, c_i, c_p],
     "cer_softmax_ce": [c_p, c_i, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_gather_images": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p],
 }
@@ -70,7 +70,7 @@ def adam_step(arena, beta1, beta2, eps, l2):
     work = arena.work if arena.work is not arena.params else None
     rc = lib().cer_adam_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
-        _ptr(arena.grad), arena.grad.stride(0),
+        _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
         _ptr(work), work.stride(0) if work is not None else 0,
         _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)), _stream())
     _check(rc, "cer_adam_step")
@@ -183,7 +183,7 @@ def _tune_enabled():
     return os.environ.get("CER_CONV_TUNE", "1") != "0"
 
 
-def _select(op, key, launch):
+def _select(op, key, launch, after_tune=None):
     if op in _PINNED:
         lib().cer_conv_set_variant(op, _PINNED[op])
         return
@@ -191,12 +191,12 @@ def _select(op, key, launch):
     if v is None:
         v = -1
         if _tune_enabled() and not torch.cuda.is_current_stream_capturing():
-            v = _autotune(op, launch)
+            v = _autotune(op, launch, after=after_tune)
         _TUNED[(op, key)] = v
     lib().cer_conv_set_variant(op, v)
 
 
-def _autotune(op, launch, reps=3):
+def _autotune(op, launch, reps=3, after=None):
     L = lib()
     best, best_v = None, -1
     for v in range(NVARIANTS):
@@ -211,6 +211,8 @@ def _autotune(op, launch, reps=3):
         t = s.elapsed_time(e)
         if best is None or t < best:
             best, best_v = t, v
+    if after is not None:
+        after()
     return best_v
 
 
@@ -366,12 +368,15 @@ def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad
     def launch():
         L = lib()
         splits = L.cer_wgrad_splits(B * Ho * Wo, cout, kh * kw * cin, G)
-        if splits > 1:
+        if splits > 1 and not wref.arena.grad_clean:
             wref.grad().zero_()
         rc = L.cer_conv_wgrad(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride,
                               pad, c_p(gp), gs, splits, _stream())
         _check(rc, "cer_conv_wgrad")
-    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    # timing runs of split-K variants accumulate into the gradient: clear it
+    # before the real launch
+    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch,
+            after_tune=lambda: wref.grad().zero_())
     launch()
 
 

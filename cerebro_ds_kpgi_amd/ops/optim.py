@@ -36,3 +36,5 @@ def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
         p.sub_((arena.lr.unsqueeze(1) / bc1) * m / denom)
         if arena.work is not arena.params:
             arena.work.copy_(p)
+        if arena.grad_clean:
+            arena.grad.zero_()

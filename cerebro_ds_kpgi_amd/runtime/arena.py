@@ -143,6 +143,10 @@ class Arena(object):
             self.work = torch.zeros(G, L.n_train, dtype=compute_dtype, device=self.device)
         self.grad = (torch.zeros(G, L.n_train, dtype=torch.float32, device=self.device)
                      if trainable else None)
+        # True: the optimizer clears ``grad`` after consuming it, so every
+        # backward starts from zeros (split-K weight-gradient kernels then
+        # accumulate without a per-layer memset)
+        self.grad_clean = False
         self.lr = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.wd = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.model_ids = [None] * G

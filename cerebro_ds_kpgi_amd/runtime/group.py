@@ -100,6 +100,7 @@ class _Working(object):
         self.G = G
         g = group
         self.arena = Arena(g.layout, G, g.device, g.dtype, trainable=True)
+        self.arena.grad_clean = True      # adam_step clears the gradient it consumes
         self.net = create_model_from_mst({"model": g.arch})
         self.net.bind(self.arena)
         B = g.batch_size

@@ -8,6 +8,9 @@
 //   p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)
 // and the bf16 compute shadow of p is written in the same pass.
 // Bytes/param: read p,m,v,g (16) + write p,m,v (12) + bf16 shadow (2).
+// zero_grad: the consumed gradient is cleared in the same pass (+4 B), so the
+// next backward's split-K weight-gradient kernels can accumulate into it
+// without a memset per layer.
 #include "common.h"
 
 __global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G) {
@@ -18,7 +21,7 @@ __global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step
 template <bool WRITE_BF16>
 __global__ __launch_bounds__(256) void adam_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
-    int64_t off_v, int64_t off_step, const float* __restrict__ grad, int64_t grad_stride,
+    int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
     const float* __restrict__ wd, float b1, float b2, float eps, int l2) {
   const int g = blockIdx.y;
@@ -35,9 +38,13 @@ __global__ __launch_bounds__(256) void adam_kernel(
   float4* pp = reinterpret_cast<float4*>(row + i);
   float4* mp = reinterpret_cast<float4*>(row + off_m + i);
   float4* vp = reinterpret_cast<float4*>(row + off_v + i);
-  const float4* gp = reinterpret_cast<const float4*>(grad + g * grad_stride + i);
+  float4* gp = reinterpret_cast<float4*>(grad + g * grad_stride + i);
   float4 p[2] = {pp[0], pp[1]}, m[2] = {mp[0], mp[1]}, v[2] = {vp[0], vp[1]};
   const float4 gr[2] = {gp[0], gp[1]};
+  if (zero_grad) {
+    gp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   float* pf = reinterpret_cast<float*>(p);
   float* mf = reinterpret_cast<float*>(m);
   float* vf = reinterpret_cast<float*>(v);
@@ -64,20 +71,22 @@ __global__ __launch_bounds__(256) void adam_kernel(
 }
 
 CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
-                          int64_t off_v, int64_t off_step, const float* grad,
-                          int64_t grad_stride, bf16_t* work, int64_t work_stride,
-                          const float* lr, const float* wd, int G, float b1, float b2,
-                          float eps, int l2, hipStream_t stream) {
+                          int64_t off_v, int64_t off_step, float* grad, int64_t grad_stride,
+                          int zero_grad, bf16_t* work, int64_t work_stride, const float* lr,
+                          const float* wd, int G, float b1, float b2, float eps, int l2,
+                          hipStream_t stream) {
   if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
   if (work)
     adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
-                                                 off_step, grad, grad_stride, work, work_stride,
+                                                 off_step, grad, grad_stride, zero_grad, work,
+                                                 work_stride,
                                                  lr, wd, b1, b2, eps, l2);
   else
     adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
-                                                  off_step, grad, grad_stride, nullptr, 0, lr,
+                                                  off_step, grad, grad_stride, zero_grad, nullptr,
+                                                  0, lr,
                                                   wd, b1, b2, eps, l2);
   return (int)hipGetLastError();
 }
