@@ -49,6 +49,13 @@ class PartitionStore(object):
                 tx, ty = self._make(n_train, seed * 1000 + 2 * p)
                 vx, vy = self._make(n_valid, seed * 1000 + 2 * p + 1)
             parts.append(Partition(p, tx, ty, vx, vy))
+        if loader is not None and parts:
+            # loaded partitions: equal-size views (the engine steps all partitions together)
+            n_train = min(q.train_x.shape[0] for q in parts)
+            n_valid = min(q.valid_x.shape[0] for q in parts)
+            for q in parts:
+                q.train_x, q.train_y = q.train_x[:n_train], q.train_y[:n_train]
+                q.valid_x, q.valid_y = q.valid_x[:n_valid], q.valid_y[:n_valid]
         # stacked so a kernel can index [local_part, row]
         self.train_x = torch.stack([q.train_x for q in parts]) if parts else None
         self.train_y = torch.stack([q.train_y for q in parts]) if parts else None

@@ -428,7 +428,8 @@ def linear(x, wref, bref=None, relu=False, anchor=None):
 class PackedEmbeddingBag(torch.autograd.Function):
     """One-hot input with ``nnz`` active columns per row == sum of W columns.
 
-    idx [G, B, nnz] int32 (column ids into the K-wide input), W_g [N, K]:
+    idx [G, B, nnz] int32 (column ids into the K-wide input; -1 = padding for
+    rows with fewer active features), W_g [N, K]:
     y[b, g*N:(g+1)*N] = act(sum_j W_g[idx[g,b,j], :] + b_g).
     Weight layout is [K, N] (input-major), which is the Keras ``Dense``
     kernel layout, so the flat checkpoint blob matches a Dense(7306 -> N)
@@ -445,8 +446,9 @@ class PackedEmbeddingBag(torch.autograd.Function):
             y = _hip().embbag_fwd(idx, wref, bref, relu)
         else:
             w = wref.work().float()                                     # [G, K, N]
-            rows = torch.stack([w[g][idx[g].long()] for g in range(G)])  # [G, B, nnz, N]
-            z = rows.sum(2) + bref.work().float().unsqueeze(1)
+            valid = (idx >= 0).unsqueeze(-1).float()                    # -1 = padding
+            rows = torch.stack([w[g][idx[g].long().clamp(min=0)] for g in range(G)])
+            z = (rows * valid).sum(2) + bref.work().float().unsqueeze(1)
             if relu:
                 z = torch.relu(z)
             y = z.transpose(0, 1).reshape(B, G * N).to(wref.arena.compute_dtype)
@@ -472,7 +474,8 @@ class PackedEmbeddingBag(torch.autograd.Function):
         gw.zero_()
         for g in range(G):
             flat = idx[g].long().reshape(-1)
-            gw[g].index_add_(0, flat, dzg[g].repeat_interleave(idx.shape[2], 0))
+            keep = flat >= 0                                            # -1 = padding
+            gw[g].index_add_(0, flat[keep], dzg[g].repeat_interleave(idx.shape[2], 0)[keep])
         bref.grad().copy_(dzg.sum(1))
         return None, None, None, None, None
 

@@ -34,6 +34,12 @@ from ..utils.logging import GlobalLog, logs
 
 
 def _loader(args, device):
+    if getattr(args, "fs_root", ""):
+        from ..data import fs
+        if not fs.is_fs_root(args.fs_root):
+            raise SystemExit("--fs_root {} holds no train/ partitions".format(args.fs_root))
+        return fs.fs_partition_loader(args.fs_root, "criteo" if args.criteo else "imagenet",
+                                      device)
     if not getattr(args, "da", False):
         return None
     from ..data import da

@@ -129,6 +129,8 @@ class MOPEngine(object):
         self.store = PartitionStore(self.dataset, self.my_parts, self.n_train, self.n_valid,
                                     self.device, seed=opts.seed, loader=opts.store_loader)
         self.data_load_time = time.time() - t0
+        if opts.store_loader is not None:      # sizes come from the loaded partitions
+            self.n_train, self.n_valid = self.store.n_train, self.store.n_valid
         self.groups = {}
         self.group_of = {}
         self._build_groups(range(S))

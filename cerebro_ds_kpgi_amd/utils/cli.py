@@ -98,6 +98,9 @@ def get_main_parser():
                    help="write chrome-trace spans (logs_root/traces) and 1 Hz system telemetry")
     p.add_argument("--da", action="store_true", help="read partitions through the Direct-Access page reader")
     p.add_argument("--da_root", type=str, default="", help="root of GP-format segment files")
+    p.add_argument("--fs_root", type=str, default="",
+                   help="root of filesystem partitions ({train,valid}/{train,valid}_{i}.*; "
+                        "create with python -m cerebro_ds_kpgi_amd.tools.make_fs_data)")
     return p
 
 
