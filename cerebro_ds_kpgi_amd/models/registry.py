@@ -6,13 +6,16 @@ Configurations that share an architecture *and* a batch size can be packed
 into one horizontally-fused model on a GPU (``pack_key``).
 
 The reference's ``"inceptionresnetv2"`` name silently builds VGG19
-(``in_rdbms_helper.py:314-321``); that quirk is not reproduced.
+(``in_rdbms_helper.py:314-321``); it is kept as an alias of ``vgg19`` so
+grids naming it train what the reference actually trained.
+``nasnetmobile`` (B1) is not available yet.
 """
 
 from .mlp import PackedConfA, PackedSanity
 from .resnet import PackedResNet
 from .small import PackedMobileNetV2, PackedTinyCNN
-from .vgg import PackedVGG16
+from .vgg import PackedVGG16, PackedVGG19
+from .zoo import PackedDenseNet, PackedMobileNetV1, PackedResNeXt, PackedResNet50NoBN
 
 MODEL_FACTORIES = {
     "resnet18": lambda: PackedResNet(18),
@@ -20,7 +23,14 @@ MODEL_FACTORIES = {
     "resnet50": lambda: PackedResNet(50),
     "resnet101": lambda: PackedResNet(101),
     "resnet152": lambda: PackedResNet(152),
+    "resnet50_nobn": lambda: PackedResNet50NoBN(),
+    "resnext101": lambda: PackedResNeXt(101),
     "vgg16": lambda: PackedVGG16(),
+    "vgg19": lambda: PackedVGG19(),
+    "inceptionresnetv2": lambda: PackedVGG19(),
+    "densenet121": lambda: PackedDenseNet(121),
+    "densenet201": lambda: PackedDenseNet(201),
+    "mobilenetv1": lambda: PackedMobileNetV1(),
     "mobilenetv2": lambda: PackedMobileNetV2(),
     "confA": lambda: PackedConfA(),
     "sanity": lambda: PackedSanity(),

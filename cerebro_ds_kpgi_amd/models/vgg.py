@@ -1,4 +1,4 @@
-"""VGG-16 for ImageNet-112, packed over G configurations.
+"""VGG-16 / VGG-19 for ImageNet-112, packed over G configurations.
 
 ``keras.applications`` VGG16 as used by the reference
 (``cerebro_gpdb/vgg16tfk_default.py:49-263``; shapes SURVEY.md §2.8 K2):
@@ -13,12 +13,16 @@ from .common import Conv, Dense, PackedNet
 from ..ops import nn as P
 from ..runtime.arena import ParamSpec
 
-_CFG = [(64, 2), (128, 2), (256, 3), (512, 3), (512, 3)]
+_CFGS = {16: [(64, 2), (128, 2), (256, 3), (512, 3), (512, 3)],
+         19: [(64, 2), (128, 2), (256, 4), (512, 4), (512, 4)]}
 
 
 class PackedVGG16(PackedNet):
+    depth = 16
+
     def __init__(self, num_classes=1000, input_hw=112):
         super(PackedVGG16, self).__init__()
+        _CFG = _CFGS[self.depth]
         self.num_classes = num_classes
         self.input_hw = input_hw
         self.convs = []
@@ -56,3 +60,8 @@ class PackedVGG16(PackedNet):
         x = self.dense(x, self.fc1, relu=True)
         x = self.dense(x, self.fc2, relu=True)
         return self.dense(x, self.fc3)
+
+
+class PackedVGG19(PackedVGG16):
+    """VGG-19: blocks of 2, 2, 4, 4, 4 convs (``keras.applications.VGG19``)."""
+    depth = 19

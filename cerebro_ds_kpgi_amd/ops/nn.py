@@ -523,3 +523,63 @@ class PackedDWConv2d(torch.autograd.Function):
 
 def dwconv2d(x, wref, stride=1, pad=1, anchor=None):
     return PackedDWConv2d.apply(x, anchor, wref, stride, pad)
+
+
+# ---------------------------------------------------------------------------
+# grouped convolution inside each configuration (ResNeXt cardinality),
+# average pooling and per-config channel concat (DenseNet) — PyTorch path
+# ---------------------------------------------------------------------------
+
+class PackedGroupedConv2d(torch.autograd.Function):
+    """conv with ``groups`` channel groups per configuration.
+
+    W_g [cout, kh, kw, cin / groups]; all G configs run as one torch grouped
+    conv with G * groups groups.  No HIP kernel: the packed-G implicit GEMM
+    kernels assume dense per-config convs.
+    """
+
+    @staticmethod
+    def forward(ctx, x, anchor, wref, stride, pad, groups):
+        ctx.wref, ctx.stride, ctx.pad, ctx.groups = wref, stride, pad, groups
+        w = _torch_weight(wref)
+        y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * groups))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, = ctx.saved_tensors
+        wref, stride, pad, groups = ctx.wref, ctx.stride, ctx.pad, ctx.groups
+        G = wref.G
+        cout, kh, kw, cin_g = wref.spec.shape
+        w = _torch_weight(wref)
+        xn, dyn = _nchw(x), _nchw(dy.contiguous())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, G * groups))
+        dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, G * groups)
+        wref.grad().copy_(dw.view(G, cout, cin_g, kh, kw).permute(0, 1, 3, 4, 2))
+        return dx, None, None, None, None, None
+
+
+def grouped_conv2d(x, wref, stride=1, pad=0, groups=1, anchor=None):
+    if groups == 1:
+        return conv2d(x, wref, stride, pad, anchor)
+    return PackedGroupedConv2d.apply(x, anchor, wref, stride, pad, groups)
+
+
+def avgpool2d(x, k, s, p=0):
+    """Per-channel average pooling (count_include_pad=False, Keras 'valid')."""
+    return _nhwc(F.avg_pool2d(_nchw(x), k, s, p, count_include_pad=False))
+
+
+def cat_packed(xs, G):
+    """Channel concat per configuration of packed [B, H, W, G*C_i] tensors."""
+    B, H, W = xs[0].shape[:3]
+    parts = [t.reshape(B, H, W, G, t.shape[-1] // G) for t in xs]
+    return torch.cat(parts, dim=-1).reshape(B, H, W, -1)
+
+
+def relu_add(a, b):
+    """relu(a + b) in fp32 with one rounding (BN-free residual join)."""
+    return torch.relu(a.float() + b.float()).to(a.dtype)

@@ -104,6 +104,19 @@ def init_row(layout, master_row, seed):
     master_row.zero_()
     for s in layout.specs:
         view = master_row[s.offset:s.offset + s.numel]
+        if isinstance(s.init, str) and s.init.startswith("tn"):
+            # Keras TruncatedNormal(0, std): normal redrawn outside +-2 std
+            # (reference resnet50tfk.py KI, kernels AND biases)
+            std = float(s.init[2:])
+            t = torch.empty(s.numel, device=dev).normal_(0.0, 1.0, generator=g)
+            while True:
+                bad = t.abs() > 2.0
+                nb = int(bad.sum())
+                if not nb:
+                    break
+                t[bad] = torch.empty(nb, device=dev).normal_(0.0, 1.0, generator=g)
+            view.copy_(t * std)
+            continue
         if s.kind in ("weight",):
             fan_in = s.fan_in if s.fan_in else int(np.prod(s.shape[1:]))
             if s.init == "he":

@@ -1,0 +1,67 @@
+"""Model zoo: parameter counts vs the Keras / torchvision architectures the
+reference builds, packed forward/backward."""
+
+import os
+
+import pytest
+import torch
+
+os.environ.setdefault("CEREBRO_BACKEND", "torch")
+
+# (trainable, non-trainable) — keras.applications / classification_models /
+# torchvision counts for 1000 classes (input-size independent except VGG's
+# flatten: 3x3x512 at 112x112)
+COUNTS = {
+    "resnet50": (25557032, 53120),        # torchvision count (Keras minus conv biases)
+    "resnet18": (11689512, 9600),
+    "vgg16": (54471464, 0),               # 14 714 688 conv + 39 756 776 dense (flatten 4608)
+    "vgg19": (59781160, 0),
+    "inceptionresnetv2": (59781160, 0),   # the reference's name for VGG19
+    "mobilenetv1": (4231976, 21888),
+    "mobilenetv2": (3504872, 34112),
+    "densenet121": (7978856, 83648),
+    "densenet201": (20013928, 229056),
+    "resnext101": (44177704, 137856),     # ResNeXt-101 32x4d
+    "resnet50_nobn": (25530472, 0),       # Keras ResNet-50 minus BN (resnet50tfk.py)
+    "confA": (7306 * 1000 + 1000 + 1000 * 500 + 500 + 500 * 2 + 2, 0),
+}
+
+
+@pytest.mark.parametrize("name", sorted(COUNTS))
+def test_parameter_counts(name):
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    net = create_model_from_mst({"model": name})
+    tr = sum(s.numel for s in net.layout.train_specs)
+    nt = sum(s.numel for s in net.layout.buffer_specs)
+    want_tr, want_nt = COUNTS[name]
+    assert (tr, nt) == (want_tr, want_nt)
+
+
+@pytest.mark.parametrize("name", ["vgg19", "mobilenetv1", "densenet121", "resnext101",
+                                  "resnet50_nobn"])
+def test_packed_forward_backward(name):
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    from cerebro_ds_kpgi_amd.ops import set_backend
+    from cerebro_ds_kpgi_amd.runtime.arena import Arena
+    set_backend("torch")
+    net = create_model_from_mst({"model": name})
+    a = Arena(net.layout, 2, "cpu", torch.float32)
+    for g in range(2):
+        a.init_model(g, 10 + g)
+    net.bind(a)
+    x = torch.randn(1, 112, 112, 6)
+    y = net.forward(x, True)
+    assert tuple(y.shape) == (1, 2000)
+    y.sum().backward()
+    # every trainable tensor of both configs received a gradient row
+    assert float(a.grad[0].abs().sum()) > 0 and float(a.grad[1].abs().sum()) > 0
+    # configs are independent: config 1's logits do not depend on config 0's weights
+    with torch.no_grad():
+        a.params[0].mul_(0.5)
+        a.sync_work()
+        y2 = net.forward(x, False)
+        y1 = y2[:, 1000:].clone()
+        a.params[0].mul_(3.0)
+        a.sync_work()
+        y3 = net.forward(x, False)
+    assert torch.allclose(y1, y3[:, 1000:])
