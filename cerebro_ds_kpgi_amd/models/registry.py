@@ -47,7 +47,8 @@ def create_model_from_mst(mst):
 
 
 def pack_key(mst):
-    return (mst["model"], int(mst["batch_size"]))
+    """Configs sharing (architecture, batch size, optimizer) pack into one model."""
+    return (mst["model"], int(mst["batch_size"]), mst.get("optimizer", "adam"))
 
 
 def dataset_of(model_name):

@@ -30,6 +30,8 @@ c_f = ctypes.c_float
 _SIGS = {
     "cer_adam_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p,
                       c_p, c_i, c_f, c_f, c_f, c_i, c_p],
+    "cer_sgd_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p, c_p, c_i,
+                     c_f, c_i, c_p],
     "cer_softmax_ce": [c_p, c_i, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_gather_images": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p],
 }
@@ -74,6 +76,18 @@ def adam_step(arena, beta1, beta2, eps, l2):
         _ptr(work), work.stride(0) if work is not None else 0,
         _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)), _stream())
     _check(rc, "cer_adam_step")
+
+
+def sgd_step(arena, momentum, l2):
+    L = arena.layout
+    st = arena.state
+    work = arena.work if arena.work is not arena.params else None
+    rc = lib().cer_sgd_step(
+        _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_step,
+        _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
+        _ptr(work), work.stride(0) if work is not None else 0,
+        _ptr(arena.lr), _ptr(arena.wd), arena.G, float(momentum), int(bool(l2)), _stream())
+    _check(rc, "cer_sgd_step")
 
 
 def softmax_ce_fwd(logits, labels, acc, G, need_grad=True):

@@ -1,4 +1,4 @@
-"""Fused multi-config Adam over the flat arena.
+"""Fused multi-config Adam / SGD over the flat arena.
 
 One launch updates every parameter of all G packed configurations: per-row
 learning rate / lambda from device tensors, bias correction from the per-row
@@ -38,3 +38,37 @@ def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
             arena.work.copy_(p)
         if arena.grad_clean:
             arena.grad.zero_()
+
+
+SGD_MOMENTUM = 0.9
+
+
+def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
+    """``torch.optim.SGD(lr, momentum, weight_decay=lambda)``; the momentum
+    buffer lives in the arena's first-moment slot."""
+    if use_hip("adam", arena.state):
+        from . import _hip
+        _hip.sgd_step(arena, momentum, l2)
+        return
+    with torch.no_grad():
+        arena.step.add_(1.0)
+        p, g, m = arena.params, arena.grad, arena.m
+        if l2:
+            g = g + arena.wd.unsqueeze(1) * p
+        first = (arena.step <= 1.0).float()                               # [G, 1]
+        if momentum:
+            m.copy_(first * g + (1 - first) * (momentum * m + g))
+            upd = m
+        else:
+            upd = g
+        p.sub_(arena.lr.unsqueeze(1) * upd)
+        if arena.work is not arena.params:
+            arena.work.copy_(p)
+        if arena.grad_clean:
+            arena.grad.zero_()
+
+
+def optimizer_step(arena, name="adam", l2=True):
+    if name == "sgd":
+        return sgd_step(arena, l2=l2)
+    return adam_step(arena, l2=l2)

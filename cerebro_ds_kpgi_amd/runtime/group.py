@@ -23,7 +23,7 @@ import torch
 from ..data.store import gather_batch, input_buffers
 from ..models import create_model_from_mst
 from ..ops.loss import eval_metrics, softmax_ce
-from ..ops.optim import adam_step
+from ..ops.optim import optimizer_step
 from .arena import Arena
 
 
@@ -31,7 +31,8 @@ class PackGroup(object):
     def __init__(self, key, model_ids, msts, store, device, compute_dtype, seed_base,
                  use_graphs=True, l2=True, warmup_eager=3, init=True):
         self.key = key
-        self.arch, self.batch_size = key
+        self.arch, self.batch_size = key[0], key[1]
+        self.optimizer = key[2] if len(key) > 2 else "adam"
         self.model_ids = list(model_ids)
         self.home_row = {m: i for i, m in enumerate(self.model_ids)}
         self.msts = msts
@@ -100,7 +101,7 @@ class _Working(object):
         self.G = G
         g = group
         self.arena = Arena(g.layout, G, g.device, g.dtype, trainable=True)
-        self.arena.grad_clean = True      # adam_step clears the gradient it consumes
+        self.arena.grad_clean = True      # the optimizer clears the gradient it consumes
         self.net = create_model_from_mst({"model": g.arch})
         self.net.bind(self.arena)
         B = g.batch_size
@@ -149,7 +150,7 @@ class _Working(object):
         loss.sum().backward()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)
-        adam_step(self.arena, l2=g.l2)
+        optimizer_step(self.arena, g.optimizer, l2=g.l2)
         self.cursor.add_(1)
 
     def train_steps(self, nsteps):

@@ -76,6 +76,8 @@ def get_main_parser():
     p.add_argument("--l2_mode", choices=["adam_wd", "none"], default="adam_wd",
                    help="lambda as torch Adam weight_decay (reference DDP path) or a no-op (Keras path quirk)")
     p.add_argument("--compute_dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--optimizer", choices=["adam", "sgd"], default="adam",
+                   help="per-config optimizer (reference: Adam); sgd = momentum 0.9, coupled L2")
     p.add_argument("--data_dtype", choices=["uint8", "fp32"], default="uint8")
     p.add_argument("--train_per_partition", type=int, default=0,
                    help="train images per partition (0 = full ImageNet split: 1 281 280 / partitions)")
@@ -115,6 +117,9 @@ def main_prepare(argv=None, shuffle=True, to_set_seed=True, verbose=True):
     if to_set_seed:
         set_seed(SEED)
     msts = get_exp_specific_msts(args)
+    if args.optimizer != "adam":
+        for m in msts:
+            m["optimizer"] = args.optimizer
     if args.shuffle or shuffle:
         random.shuffle(msts)
     if verbose:

@@ -8,8 +8,11 @@
 
 
 def mst_2_str(mst):
-    return "learning_rate:{},lambda_value:{},batch_size:{},model:{}".format(
+    s = "learning_rate:{},lambda_value:{},batch_size:{},model:{}".format(
         mst["learning_rate"], mst["lambda_value"], mst["batch_size"], mst["model"])
+    if mst.get("optimizer", "adam") != "adam":     # extension: keeps Adam keys reference-exact
+        s += ",optimizer:{}".format(mst["optimizer"])
+    return s
 
 
 def mst2key(mst):

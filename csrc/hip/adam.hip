@@ -90,3 +90,69 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
                                                   wd, b1, b2, eps, l2);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// SGD with momentum, torch.optim.SGD semantics (dampening 0, no Nesterov):
+//   g += wd * p;  buf = mu * buf + g;  p -= lr * buf
+// (buf = the arena's first-moment slot; first step buf = g as in torch).
+// ---------------------------------------------------------------------------
+template <bool WRITE_BF16>
+__global__ __launch_bounds__(256) void sgd_kernel(
+    float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
+    int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
+    bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
+    const float* __restrict__ wd, float mu, int l2) {
+  const int g = blockIdx.y;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n_train) return;
+  float* row = state + g * row_stride;
+  const bool first = row[off_step] <= 1.0f;
+  const float rate = lr[g];
+  const float lam = l2 ? wd[g] : 0.f;
+  float4* pp = reinterpret_cast<float4*>(row + i);
+  float4* mp = reinterpret_cast<float4*>(row + off_m + i);
+  float4* gp = reinterpret_cast<float4*>(grad + g * grad_stride + i);
+  float4 p[2] = {pp[0], pp[1]}, m[2] = {mp[0], mp[1]};
+  const float4 gr[2] = {gp[0], gp[1]};
+  if (zero_grad) {
+    gp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float* pf = reinterpret_cast<float*>(p);
+  float* mf = reinterpret_cast<float*>(m);
+  const float* gf = reinterpret_cast<const float*>(gr);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float gk = gf[k] + lam * pf[k];
+    mf[k] = (mu == 0.f) ? gk : (first ? gk : mu * mf[k] + gk);
+    pf[k] -= rate * mf[k];
+  }
+  pp[0] = p[0]; pp[1] = p[1];
+  mp[0] = m[0]; mp[1] = m[1];
+  if (WRITE_BF16) {
+    uint4 o;
+    o.x = pack_bf2(pf[0], pf[1]);
+    o.y = pack_bf2(pf[2], pf[3]);
+    o.z = pack_bf2(pf[4], pf[5]);
+    o.w = pack_bf2(pf[6], pf[7]);
+    *reinterpret_cast<uint4*>(work + g * work_stride + i) = o;
+  }
+}
+
+CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
+                         int64_t off_step, float* grad, int64_t grad_stride, int zero_grad,
+                         bf16_t* work, int64_t work_stride, const float* lr, const float* wd,
+                         int G, float momentum, int l2, hipStream_t stream) {
+  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  dim3 grid(cer_blocks(n_train / 8, 256), G);
+  if (work)
+    sgd_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step, grad,
+                                               grad_stride, zero_grad, work, work_stride, lr, wd,
+                                               momentum, l2);
+  else
+    sgd_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step,
+                                                grad, grad_stride, zero_grad, nullptr, 0, lr, wd,
+                                                momentum, l2);
+  return (int)hipGetLastError();
+}

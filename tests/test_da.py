@@ -150,3 +150,18 @@ def test_dataset_writer_and_input_fn(tmp_path):
     from cerebro_ds_kpgi_amd.data import synthetic
     x_ref, y_ref = synthetic.image_partition(12, seed=2018 * 1000 + 2)
     assert (tx == x_ref).all() and (ty == y_ref).all()
+
+
+def test_da_export_to_filesystem(tmp_path):
+    """DA pages -> filesystem partitions (the reference's unload + ETL role)."""
+    import numpy as np
+    from cerebro_ds_kpgi_amd.data import da, fs
+    from cerebro_ds_kpgi_amd.tools import da_export
+    root = str(tmp_path / "da")
+    da.write_dataset(root, "imagenet", 2, 20, 6, buffer_size=8)
+    out = str(tmp_path / "fs")
+    counts = da_export.main(["--da_root", root, "--out", out])
+    assert counts == {"train": 40, "valid": 12}
+    tx, ty, vx, vy = fs.fs_partition_loader(out, "imagenet", "cpu")(1)
+    dx, dy, _, _ = da.da_partition_loader(root, "cpu")(1)
+    assert np.array_equal(tx.numpy(), dx.numpy()) and np.array_equal(ty.numpy(), dy.numpy())

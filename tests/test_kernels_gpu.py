@@ -45,6 +45,26 @@ def test_adam_matches_torch():
     torch.testing.assert_close(a.work.float(), b.work.float(), rtol=1e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("clean", [False, True])
+def test_sgd_matches_torch(clean):
+    from cerebro_ds_kpgi_amd.ops.optim import sgd_step
+    net, a = _arena()
+    net2, b = _arena()
+    a.grad_clean = b.grad_clean = clean
+    torch.manual_seed(0)
+    for it in range(3):
+        gr = torch.randn_like(a.grad)
+        a.grad.copy_(gr)
+        b.grad.copy_(gr)
+        sgd_step(a)                           # HIP
+        backend.force_torch_ops(["adam"])
+        sgd_step(b)                           # oracle
+        backend.force_torch_ops([])
+    torch.cuda.synchronize()
+    assert torch.allclose(a.state, b.state, rtol=1e-5, atol=1e-6)
+    assert bool((a.grad == 0).all()) == clean
+
+
 @pytest.mark.parametrize("N,G,B,dt", [(1000, 8, 32, torch.bfloat16), (1000, 8, 32, torch.float32),
                                       (2, 4, 64, torch.float32), (10, 3, 8, torch.bfloat16)])
 def test_softmax_ce_matches_torch(N, G, B, dt):

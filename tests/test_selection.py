@@ -100,3 +100,54 @@ def test_mst_eval_fn_hyperopt_contract():
     assert trials.trials[3]["loss"] == 0.73
     grid = hh.mst_eval_fn(2)
     assert sorted(grid(state)[0]) == list(range(8))
+
+
+def test_sgd_matches_torch_optim():
+    """Arena SGD (momentum, coupled L2) == torch.optim.SGD per configuration."""
+    import torch
+    from cerebro_ds_kpgi_amd.ops import set_backend
+    from cerebro_ds_kpgi_amd.ops.optim import sgd_step
+    from cerebro_ds_kpgi_amd.runtime.arena import Arena, ModelLayout, ParamSpec
+    set_backend("torch")
+    lay = ModelLayout([ParamSpec("w", (5, 3), "weight"), ParamSpec("b", (5,), "bias")])
+    a = Arena(lay, 2, "cpu", torch.float32)
+    for g in range(2):
+        a.init_model(g, g)
+        a.set_hparams(g, [0.1, 0.01][g], [1e-3, 0.0][g])
+    ref = [torch.nn.Parameter(a.params[g].clone()) for g in range(2)]
+    opts = [torch.optim.SGD([ref[g]], lr=[0.1, 0.01][g], momentum=0.9,
+                            weight_decay=[1e-3, 0.0][g]) for g in range(2)]
+    torch.manual_seed(0)
+    for _ in range(4):
+        gr = torch.randn_like(a.grad)
+        a.grad.copy_(gr)
+        sgd_step(a)
+        for g in range(2):
+            ref[g].grad = gr[g].clone()
+            opts[g].step()
+    for g in range(2):
+        assert torch.allclose(a.params[g], ref[g].detach(), atol=1e-6)
+
+
+def test_weight_blob_formats_roundtrip():
+    """MADlib-wrapper byte formats + arena row <-> nd weights."""
+    import numpy as np
+    import torch
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    from cerebro_ds_kpgi_amd.runtime import serialize as S
+    from cerebro_ds_kpgi_amd.runtime.arena import Arena
+    net = create_model_from_mst({"model": "tinycnn"})
+    a = Arena(net.layout, 2, "cpu", torch.float32)
+    a.init_model(0, 1)
+    a.init_model(1, 2)
+    w = S.arena_to_nd_weights(a, 1)
+    blob = S.serialize_nd_weights(w)
+    assert len(blob) == 4 * sum(x.size for x in w)
+    back = S.deserialize_as_nd_weights(blob, S.model_shapes(net.layout))
+    assert all(np.array_equal(x, y) for x, y in zip(w, back))
+    st = S.serialize_state_with_nd_weights(96.0, w)
+    cnt, flat = S.deserialize_as_image_1d_weights(st)
+    assert cnt == 96.0 and flat.tobytes() == blob
+    assert S.serialize_state_with_1d_weights(96.0, flat) == st
+    S.nd_weights_to_arena(a, 0, back)
+    assert torch.equal(a.state[0, :net.layout.n_master], a.state[1, :net.layout.n_master])
