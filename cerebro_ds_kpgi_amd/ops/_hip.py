@@ -171,6 +171,16 @@ _SIGS.update({
 })
 IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
 
+_SIGS2 = {
+    "cer_dwconv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_p, c_p],
+    "cer_dwconv_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i,
+                       c_p, c_p],
+    "cer_embbag_fwd": [c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p, c_p],
+    "cer_embbag_bwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
+}
+_SIGS.update(_SIGS2)
+IMPLEMENTED |= {"dwconv", "embbag"}
+
 
 def _act_code(a):
     if a == 6:
@@ -589,3 +599,64 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     wp, ws = wref.work_ptr()
     _conv_dgrad_launch(dz, B, 1, 1, N, G, wp, ws, K, 1, 1, 1, 0, dx, 1, 1)
     return dx
+
+
+
+# ---------------------------------------------------------------------------
+# depthwise conv (csrc/hip/dwconv.hip) and embedding bag (csrc/hip/embbag.hip)
+# ---------------------------------------------------------------------------
+def dwconv_fwd(x, wref, stride, pad):
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    C, kh, kw = wref.spec.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.empty((B, Ho, Wo, GC), dtype=torch.bfloat16, device=x.device)
+    wp, ws = wref.work_ptr()
+    rc = lib().cer_dwconv_fwd(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pad, _ptr(y),
+                              _stream())
+    _check(rc, "cer_dwconv_fwd")
+    return y
+
+
+def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
+    dy = _bf16(dy)
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    C, kh, kw = wref.spec.shape
+    if not wref.arena.grad_clean:
+        wref.grad().zero_()
+    dx = torch.empty_like(x) if need_dx else None
+    wp, ws = wref.work_ptr()
+    gp, gs = wref.grad_ptr()
+    rc = lib().cer_dwconv_bwd(_ptr(dy), _ptr(x), B, H, W, C, G, c_p(wp), ws, c_p(gp), gs, kh,
+                              stride, pad, _ptr(dx), _stream())
+    _check(rc, "cer_dwconv_bwd")
+    return dx
+
+
+def embbag_fwd(idx, wref, bref, relu):
+    G, B, nnz = idx.shape
+    K, N = wref.spec.shape
+    y = torch.empty((B, G * N), dtype=torch.bfloat16, device=idx.device)
+    wp, ws = wref.work_ptr()
+    bp, bs = bref.work_ptr()
+    rc = lib().cer_embbag_fwd(_ptr(idx.contiguous()), G, B, nnz, c_p(wp), ws, c_p(bp), bs, N,
+                              1 if relu else 0, _ptr(y), _stream())
+    _check(rc, "cer_embbag_fwd")
+    return y
+
+
+def embbag_bwd(dy, idx, y, wref, bref, relu):
+    G, B, nnz = idx.shape
+    K, N = wref.spec.shape
+    if not wref.arena.grad_clean:
+        wref.grad().zero_()
+        bref.grad().zero_()
+    gp, gs = wref.grad_ptr()
+    bp, bs = bref.grad_ptr()
+    rc = lib().cer_embbag_bwd(_ptr(_bf16(dy)), _ptr(y), _ptr(idx.contiguous()), G, B, nnz,
+                              c_p(gp), gs, c_p(bp), bs, N, 1 if relu else 0, _stream())
+    _check(rc, "cer_embbag_bwd")

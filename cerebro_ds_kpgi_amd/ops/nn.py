@@ -442,7 +442,9 @@ class PackedEmbeddingBag(torch.autograd.Function):
         G = wref.G
         K, N = wref.spec.shape
         Gi, B, nnz = idx.shape
-        if use_hip("embbag", idx):
+        ctx.hip = (use_hip("embbag", idx) and wref.arena.compute_dtype == torch.bfloat16
+                   and N % 8 == 0)
+        if ctx.hip:
             y = _hip().embbag_fwd(idx, wref, bref, relu)
         else:
             w = wref.work().float()                                     # [G, K, N]
@@ -460,7 +462,7 @@ class PackedEmbeddingBag(torch.autograd.Function):
         idx, y = ctx.saved_tensors
         wref, bref, relu = ctx.wref, ctx.bref, ctx.relu
         dy = dy.contiguous()
-        if use_hip("embbag", idx):
+        if ctx.hip:
             _hip().embbag_bwd(dy, idx, y, wref, bref, relu)
             return None, None, None, None, None
         G = wref.G
@@ -492,7 +494,9 @@ class PackedDWConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
-        if use_hip("dwconv", x):
+        C, kh, kw = wref.spec.shape
+        ctx.hip = use_hip("dwconv", x) and C % 8 == 0 and kh == kw and kh in (3, 5)
+        if ctx.hip:
             y = _hip().dwconv_fwd(x, wref, stride, pad)
         else:
             C, kh, kw = wref.spec.shape
@@ -506,7 +510,7 @@ class PackedDWConv2d(torch.autograd.Function):
         x, = ctx.saved_tensors
         wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
         dy = dy.contiguous()
-        if use_hip("dwconv", x):
+        if ctx.hip:
             dx = _hip().dwconv_bwd(dy, x, wref, stride, pad, ctx.needs_input_grad[0])
             return dx, None, None, None, None
         C, kh, kw = wref.spec.shape

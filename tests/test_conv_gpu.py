@@ -303,3 +303,50 @@ def test_conv_bn_fused_matches_oracle(case, variant):
         assert _rel(h[2], t[2]) < 2e-2
     assert _rel(h[3], t[3]) < 3e-2          # dW, dgamma, dbeta
     assert _rel(h[4], t[4]) < 1e-3          # running stats (+ untouched weights)
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 32, 1, 2), (2, 15, 13, 48, 2, 3), (3, 7, 7, 16, 1, 1)])
+def test_dwconv_matches_oracle(case):
+    B, H, W, C, s, G = case
+    spec = ParamSpec("dw", (C, 3, 3), "weight", fan_in=9)
+    torch.manual_seed(5)
+    x = torch.randn(B, H, W, G * C, device="cuda").to(torch.bfloat16)
+    outs = []
+    for force in ([], ["dwconv"]):
+        backend.force_torch_ops(force)
+        a, refs = _make([spec], G)
+        xx = x.clone().requires_grad_(True)
+        y = P.dwconv2d(xx, refs["dw"], s, 1)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xx.grad, a.grad.clone()))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert _rel(h[0], t[0]) < 1e-2
+    assert _rel(h[1], t[1]) < 1e-2
+    assert _rel(h[2], t[2]) < 1e-2
+
+
+@pytest.mark.parametrize("relu", [True, False])
+def test_embbag_matches_oracle(relu):
+    G, B, nnz, K, N = 3, 16, 39, 7306, 1000
+    specs = [ParamSpec("w", (K, N), "weight", init="glorot", fan_in=K),
+             ParamSpec("b", (N,), "bias")]
+    torch.manual_seed(6)
+    idx = torch.randint(0, K, (G, B, nnz), device="cuda", dtype=torch.int32)
+    idx[:, :, -3:] = -1                    # padded rows
+    outs = []
+    for force in ([], ["embbag"]):
+        backend.force_torch_ops(force)
+        a, refs = _make(specs, G)
+        anchor = torch.zeros((), device="cuda", requires_grad=True)
+        y = P.embedding_bag(idx, refs["w"], refs["b"], relu, anchor)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        torch.cuda.synchronize()
+        outs.append((y.detach(), a.grad.clone()))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert _rel(h[0], t[0]) < 1e-2
+    assert _rel(h[1], t[1]) < 1e-2

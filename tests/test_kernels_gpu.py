@@ -119,3 +119,21 @@ def test_engine_one_round_on_gpu():
         assert len(st["train_loss"]) == 2
         assert st["train_loss"][1] < st["train_loss"][0]
     eng.close()
+
+
+@pytest.mark.parametrize("model,bs", [("confA", 32), ("mobilenetv2", 8), ("mobilenetv1", 8),
+                                      ("vgg16", 8), ("densenet121", 8), ("resnext101", 4),
+                                      ("resnet50_nobn", 8), ("resnet18", 8)])
+def test_engine_trains_model_family(model, bs):
+    """Every model family steps through the HIP engine (graph capture included)."""
+    from cerebro_ds_kpgi_amd.parallel import init_distributed
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": bs, "model": model}
+            for lr in (1e-3, 1e-4)]
+    eng = MOPEngine(msts, init_distributed(), EngineOptions(
+        n_train=6 * bs, n_valid=2 * bs, slots_per_gpu=2, verbose=False, ckpt_every="none"))
+    eng.run(1)
+    for st in eng.mst_state.values():
+        assert len(st["train_loss"]) == 1 and st["train_loss"][0] == st["train_loss"][0]
+        assert 0.0 < st["train_loss"][0] < 50.0
+    eng.close()
