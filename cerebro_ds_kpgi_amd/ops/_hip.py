@@ -149,6 +149,13 @@ _SIGS.update({
                            c_p, c_i, c_i, c_p, c_p, c_p],
     "cer_conv_stats_floats": [c_i64, c_i],
     "cer_stem_ok": [c_i, c_i, c_i, c_i, c_i],
+    "cer_conv_fwd_bnstat": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
+                            c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f,
+                            c_p],
+    "cer_stem_fwd_bnstat": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
+                            c_p, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64,
+                            c_f, c_f, c_p],
+    "cer_bn_apply_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i64, c_i, c_i, c_i, c_p],
     "cer_stem_wpk_elems": [c_i, c_i, c_i, c_i],
     "cer_stem_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
                      c_p, c_i, c_i, c_p, c_p, c_p],
@@ -297,6 +304,106 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
     launch()
     return z, part, nslab.value
+
+
+_COUNTERS = {}
+_COUNTER_SLOTS = 1 << 16
+
+
+def _counters(device):
+    """Zeroed arrival counters shared by every fused conv+BN launch on a
+    device (each launch's last arriver re-zeroes its slots; allocated once so
+    captured HIP graphs keep a valid address)."""
+    key = str(device)
+    c = _COUNTERS.get(key)
+    if c is None:
+        c = torch.zeros(_COUNTER_SLOTS, dtype=torch.int32, device=device)
+        _COUNTERS[key] = c
+    return c
+
+
+# CER_BN_FUSED_FINALIZE=1: BN finalize by the last-arriving conv tile of each
+# channel column (one launch fewer per layer; slower on MI355X at ResNet-50
+# sizes because the arriving tile serialises the slab reduction) — default
+# off: conv epilogue partials + the parallel finalize kernel.
+_FUSED_FINALIZE = os.environ.get("CER_BN_FUSED_FINALIZE", "0") == "1"
+
+
+def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps):
+    y, mean, invstd = bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, act, momentum,
+                                            eps, part, nslab)
+    return y, z, mean, invstd
+
+
+def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
+                      stride, pad, stem=False):
+    """Fused training unit: conv (+ BN statistics + BN finalize in the GEMM
+    epilogue of the last tile of each channel column) then one BN-apply pass.
+    Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4 the
+    repacked stem input (stem path) or None."""
+    x = _bf16(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    C, M = G * cout, B * Ho * Wo
+    dev = x.device
+    L = lib()
+    z = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=dev)
+    part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dev)
+    mean = torch.empty(C, dtype=torch.float32, device=dev)
+    invstd = torch.empty(C, dtype=torch.float32, device=dev)
+    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    cnt = _counters(dev)
+    assert G * ((cout + 63) // 64) <= cnt.numel()
+    wp, wstr = wref.work_ptr()
+    rmp, rs = rmref.master_ptr()
+    rvp, _ = rvref.master_ptr()
+    nslab = ctypes.c_int(0)
+    x4 = wpk = None
+    if stem:
+        x4 = torch.empty((G, B, H, W, 4), dtype=torch.bfloat16, device=dev)
+        wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.bfloat16,
+                          device=dev)
+
+        def tune():        # statistics-only twin (no running-stat side effects)
+            _check(lib().cer_stem_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
+                                      stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
+                                      _ptr(part), ctypes.byref(nslab), _stream()), "cer_stem_fwd")
+        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), tune)
+        if not _FUSED_FINALIZE:
+            tune()
+            return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
+                                 momentum, eps) + (x4,)
+        rc = L.cer_stem_fwd_bnstat(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride,
+                                   pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
+                                   _ptr(cnt), _ptr(ws), _ptr(mean), _ptr(invstd), c_p(rmp),
+                                   c_p(rvp), rs, eps, momentum, _stream())
+        _check(rc, "cer_stem_fwd_bnstat")
+    else:
+        def tune():
+            _check(lib().cer_conv_fwd_stats(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
+                                            stride, pad, _ptr(z), Ho, Wo, _ptr(part),
+                                            ctypes.byref(nslab), _stream()), "cer_conv_fwd_stats")
+        _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), tune)
+        if not _FUSED_FINALIZE:
+            tune()
+            return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
+                                 momentum, eps) + (None,)
+        rc = L.cer_conv_fwd_bnstat(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride,
+                                   pad, _ptr(z), Ho, Wo, _ptr(part), _ptr(cnt), _ptr(ws),
+                                   _ptr(mean), _ptr(invstd), c_p(rmp), c_p(rvp), rs, eps,
+                                   momentum, _stream())
+        _check(rc, "cer_conv_fwd_bnstat")
+    y = torch.empty_like(z)
+    gp, gs = gref.work_ptr()
+    bp, bs = bref.work_ptr()
+    res = _bf16(residual) if residual is not None else None
+    rc = L.cer_bn_apply_fwd(_ptr(z), _ptr(res), _ptr(y), _ptr(ws), c_p(gp), gs, c_p(bp), bs, M,
+                            C, cout, _act_code(act), _stream())
+    _check(rc, "cer_bn_apply_fwd")
+    return y, z, mean, invstd, x4
 
 
 def stem_ok(x, wref, stride, pad):

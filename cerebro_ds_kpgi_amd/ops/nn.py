@@ -205,15 +205,13 @@ class PackedConvBNAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.x4 = None
-        if use_hip("conv", x) and use_hip("bn", x):
+        if use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0:
             h = _hip()
-            if not x.requires_grad and h.stem_ok(x, wref, stride, pad):
-                # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
-                z, part, nslab, ctx.x4 = h.stem_fwd_stats(x, wref, stride, pad)
-            else:
-                z, part, nslab = h.conv2d_fwd_stats(x, wref, stride, pad)
-            y, mean, invstd = h.bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, relu,
-                                                      momentum, eps, part, nslab)
+            # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
+            stem = not x.requires_grad and h.stem_ok(x, wref, stride, pad)
+            y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
+                x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride, pad,
+                stem=stem)
         else:
             z = _conv_forward(x, wref, stride, pad)
             y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,

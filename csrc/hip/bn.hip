@@ -146,8 +146,9 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
 // ---------------------------------------------------------------------------
 // stage 2: finalize
 // ---------------------------------------------------------------------------
-// one block = 32 channels x 8 slab lanes; lanes strided over slabs, LDS tree
-constexpr int FIN_C = 32, FIN_L = 8;
+// one block = 16 channels x 16 slab lanes; lanes strided over slabs (4
+// independent accumulators keep loads in flight), LDS tree
+constexpr int FIN_C = 16, FIN_L = 16;
 
 __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int slabs, int C,
                                           float* a_out, float* b_out) {
@@ -155,11 +156,23 @@ __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int sl
   const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
   const int c = blockIdx.x * FIN_C + cl;
   float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int k = ln; k < slabs; k += FIN_L) {
-      a += part[(int64_t)k * 2 * C + c];
-      b += part[(int64_t)k * 2 * C + C + c];
+  if (c < C) {
+    float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
+    int k = ln;
+    for (; k + 3 * FIN_L < slabs; k += 4 * FIN_L) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a4[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + c];
+        b4[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + C + c];
+      }
     }
+    for (; k < slabs; k += FIN_L) {
+      a4[0] += part[(int64_t)k * 2 * C + c];
+      b4[0] += part[(int64_t)k * 2 * C + C + c];
+    }
+    a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    b = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+  }
   sa[ln][cl] = a;
   sb[ln][cl] = b;
   __syncthreads();
@@ -361,6 +374,23 @@ CER_API int cer_bn_fwd_train_part(const bf16_t* x, const bf16_t* res, bf16_t* y,
   return bn_fwd_train_impl(x, res, y, gamma, gamma_stride, beta, beta_stride, rmean, rvar,
                            rstat_stride, mean_out, invstd_out, ws, part, nslab, M, C, Cper, eps,
                            momentum, act, stream);
+}
+
+// apply only: y = act(xhat * gamma + beta (+ res)) with ws = (mean, invstd)
+// already produced (conv-fused statistics, cer_conv_fwd_bnstat)
+CER_API int cer_bn_apply_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ws,
+                             const bf16_t* gamma, int64_t gamma_stride, const bf16_t* beta,
+                             int64_t beta_stride, int64_t M, int C, int Cper, int act,
+                             hipStream_t stream) {
+  if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
+  const Map mp = make_map(C);
+  dim3 ag;
+  int arows;
+  make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
+  bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                           Strided{gamma, gamma_stride},
+                                           Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
+  return (int)hipGetLastError();
 }
 
 CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,

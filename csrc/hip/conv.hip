@@ -36,6 +36,10 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int BK = 64;
 constexpr int NTHREADS = 256;
+// bf16 elements after the staged C tile for the BN-statistics exchange
+// ([2 waves][2][BN] floats, reused as [2][NTHREADS] floats by the fused
+// finalize) and the last-arriver flag
+constexpr int STAT_XCH = 2 * (2 * NTHREADS) + 8;
 
 // ---------------------------------------------------------------------------
 // n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery)
@@ -74,6 +78,19 @@ struct GatherGeom {
   int64_t cfg_off;    // elements between configs (Cg for the packed layout)
 };
 
+// BN statistics finalize fused into the producing conv (the arithmetic of
+// bn_finalize_fwd in bn.hip); cnt == nullptr: off
+struct BNFinal {
+  unsigned* cnt;          // [G * tiles_n] arrival counters (zero; the last arriver re-zeroes)
+  float* ws;              // [2][C]: mean, invstd (consumed by the BN apply)
+  float* mean_out;        // [C] saved for backward
+  float* invstd_out;      // [C]
+  float* rmean;           // running stats, config stride rstride
+  float* rvar;
+  int64_t rstride;
+  float eps, momentum;
+};
+
 struct NTParams {
   GatherGeom a;
   int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
@@ -88,7 +105,9 @@ struct NTParams {
   int o_st, o_H, o_W;     // o_st > 1: GEMM row (b,y,x) stores to output pixel (b, y*o_st, x*o_st)
   float* stats;           // optional BN partials part[slab][2][ldc] (sum, sum^2) of the
                           // bf16 outputs; slab = M tile (fused BN forward)
+  BNFinal fin;            // optional: the last M tile of each N-tile column finalizes BN
 };
+
 
 struct WGParams {
   GatherGeom x;           // im2col source (Hm, Wm = output grid Ho, Wo)
@@ -318,6 +337,37 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
   }
 }
 
+// In-launch hand-off (agent-scope release/acquire, cdna_hip_programming.md
+// Guideline 16 recipe): every block of a group publishes its slab, then
+// takes a ticket; returns true in the block that arrives last, after which
+// all its threads may read the other blocks' slabs.  The last arriver
+// re-zeroes the counter, so a persistent counter serves every replay.
+// The published slabs are written with sc1 (write-through) stores and read
+// back with sc1 loads, so no agent-scope release fence (= an L2 writeback,
+// buffer_wbl2) is needed: every wave drains its stores, then one relaxed
+// agent-scope ticket.
+__device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == expected - 1;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // sum over each 16-lane row of the wave (DPP butterfly, no LDS traffic)
 __device__ __forceinline__ float row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1,
@@ -403,7 +453,55 @@ __device__ __forceinline__ void stats_finish(const NTParams& p, const bf16_t* ld
   float* dst = p.stats + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
-    if (n < p.N) dst[(int64_t)q * p.ldc + n] = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
+    if (n < p.N) {
+      const float v = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
+      if (p.fin.cnt)
+        st_sc1(dst + (int64_t)q * p.ldc + n, v);   // read by another CU's finalize
+      else
+        dst[(int64_t)q * p.ldc + n] = v;
+    }
+  }
+  if (!p.fin.cnt) return;
+  // ---- fused finalize: the last M tile of this (config, N tile) column ----
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  int* flag = reinterpret_cast<int*>(const_cast<float*>(xch) + 2 * NTHREADS);
+  if (!last_arriver(p.fin.cnt + cfg * tiles_n + n0 / BN, (unsigned)tiles_m, flag)) return;
+  // 256 threads = BN channels x (256 / BN) slab lanes, LDS combine
+  constexpr int LANES = NTHREADS / BN;
+  float* red = const_cast<float*>(xch);   // reuse: [2][LANES][BN]
+  const int nl = tid % BN, ln = tid / BN, n = n0 + nl;
+  float sa = 0.f, sb = 0.f;
+  if (n < p.N) {
+    const float* col = p.stats + (int64_t)cfg * p.N + n;
+    for (int sl = ln; sl < tiles_m; sl += LANES) {
+      sa += ld_sc1(col + (int64_t)sl * 2 * p.ldc);
+      sb += ld_sc1(col + (int64_t)sl * 2 * p.ldc + p.ldc);
+    }
+  }
+  __syncthreads();
+  red[ln * BN + nl] = sa;
+  red[(LANES + ln) * BN + nl] = sb;
+  __syncthreads();
+  if (ln == 0 && n < p.N) {
+    for (int k = 1; k < LANES; ++k) {
+      sa += red[k * BN + nl];
+      sb += red[(LANES + k) * BN + nl];
+    }
+    const BNFinal& f = p.fin;
+    const float inv_m = 1.f / (float)p.M;
+    const float mu = sa * inv_m;
+    const float var = fmaxf(sb * inv_m - mu * mu, 0.f);
+    const float is = rsqrtf(var + f.eps);
+    const int c = cfg * p.N + n;
+    f.ws[c] = mu;
+    f.ws[p.ldc + c] = is;
+    f.mean_out[c] = mu;
+    f.invstd_out[c] = is;
+    float* rm = f.rmean + cfg * f.rstride + n;
+    float* rv = f.rvar + cfg * f.rstride + n;
+    const float unb = p.M > 1 ? var * (float)p.M / (float)(p.M - 1) : var;
+    *rm = (1.f - f.momentum) * *rm + f.momentum * mu;
+    *rv = (1.f - f.momentum) * *rv + f.momentum * unb;
   }
 }
 
@@ -413,7 +511,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
   constexpr int CPR = BK / 8;                                  // 16-B chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int EPI_ELEMS = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
+  constexpr int EPI_ELEMS = BM * (BN + 8) + STAT_XCH;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = TILE_ELEMS > EPI_ELEMS ? TILE_ELEMS : EPI_ELEMS;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 #define SA(buf) (lds + (buf) * (BM * BK))
@@ -703,7 +801,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   constexpr int A_CH = BM * CPR / NTHREADS;
   constexpr int B_CPR = BN / 8, B_CH = BK * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int EPI_ELEMS = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
+  constexpr int EPI_ELEMS = BM * (BN + 8) + STAT_XCH;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = TILE_ELEMS > EPI_ELEMS ? TILE_ELEMS : EPI_ELEMS;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 
@@ -940,7 +1038,7 @@ template <int BM, int BN, int S>
 __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int EPI = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
+  constexpr int EPI = BM * (BN + 8) + STAT_XCH;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
 
@@ -1007,7 +1105,7 @@ template <int BM, int BN, int S, int GM>
 __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int EPI = BM * (BN + 8) + 8 * BN;   // C tile + BN-stat exchange
+  constexpr int EPI = BM * (BN + 8) + STAT_XCH;   // C tile + BN-stat exchange
   constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
   constexpr int BROWS = 512 / BN, BC16 = BN / 8;   // rows / 16-B columns per B piece
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
@@ -1265,14 +1363,15 @@ static int run_nt(const NTParams& p, int G, hipStream_t stream, int* nslab = nul
 static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, hipStream_t stream);
+                         int act, float* stats, int* nslab, const BNFinal* fin,
+                         hipStream_t stream);
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
                          int act, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
-                       bias_gstride, act, nullptr, nullptr, stream);
+                       bias_gstride, act, nullptr, nullptr, nullptr, stream);
 }
 
 // forward + BN statistics partials (bias-free, no activation): part holds
@@ -1283,7 +1382,20 @@ CER_API int cer_conv_fwd_stats(const bf16_t* x, int B, int H, int W, int Cin, in
                                int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
                                int* nslab, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nslab, stream);
+                       nullptr, 0, 0, part, nslab, nullptr, stream);
+}
+
+// forward + BN statistics + BN finalize (mean / invstd / running stats) in
+// one launch; cnt: G * ceil(Cout / 64) zeroed unsigned counters, persistent
+CER_API int cer_conv_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
+                                int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
+                                unsigned* cnt, float* ws, float* mean_out, float* invstd_out,
+                                float* rmean, float* rvar, int64_t rstride, float eps,
+                                float momentum, hipStream_t stream) {
+  BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
+  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
+                       nullptr, 0, 0, part, nullptr, &f, stream);
 }
 
 // upper bound over tile choices: one slab per 64-row M tile
@@ -1294,8 +1406,10 @@ CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
 static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, hipStream_t stream) {
+                         int act, float* stats, int* nslab, const BNFinal* fin,
+                         hipStream_t stream) {
   NTParams p;
+  p.fin = fin ? *fin : BNFinal{};
   p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
   p.dgrad = 0;
   p.w = w;
@@ -1352,6 +1466,7 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   const int T = kh * kw;
   NTParams p;
   p.stats = nullptr;
+  p.fin = BNFinal{};
   p.bias = nullptr;
   p.bias_gstride = 0;
   p.act = 0;
@@ -1561,11 +1676,10 @@ static GatherGeom stem_geom(const bf16_t* x4, int B, int H, int W, int Ho, int W
   return g;
 }
 
-// repack + weight re-layout + forward conv (+ BN partials when part != null)
-CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+static int stem_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
-                         int* nslab, hipStream_t stream) {
+                         int* nslab, const BNFinal* fin, hipStream_t stream) {
   if (!cer_stem_ok(Cin, W, kw, st, pad)) return (int)hipErrorInvalidValue;
   const int64_t P = (int64_t)B * H * W;
   stem_repack_kernel<<<cer_blocks(P * G, 256), 256, 0, stream>>>(x, x4, P, G, Cin);
@@ -1593,7 +1707,29 @@ CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
   p.o_H = Ho;
   p.o_W = Wo;
   p.stats = part;
+  p.fin = fin ? *fin : BNFinal{};
   return run_nt(p, G, stream, nslab);
+}
+
+// repack + weight re-layout + forward conv (+ BN partials when part != null)
+CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+                         int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                         bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
+                         int* nslab, hipStream_t stream) {
+  return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
+                       Wo, part, nslab, nullptr, stream);
+}
+
+// same with the BN finalize fused (see cer_conv_fwd_bnstat)
+CER_API int cer_stem_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
+                                int st, int pad, bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho,
+                                int Wo, float* part, unsigned* cnt, float* ws, float* mean_out,
+                                float* invstd_out, float* rmean, float* rvar, int64_t rstride,
+                                float eps, float momentum, hipStream_t stream) {
+  BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
+  return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
+                       Wo, part, nullptr, &f, stream);
 }
 
 // dW of the stem from the repacked input; dwp: fp32 scratch of

@@ -350,3 +350,16 @@ def test_embbag_matches_oracle(relu):
     h, t = outs
     assert _rel(h[0], t[0]) < 1e-2
     assert _rel(h[1], t[1]) < 1e-2
+
+
+@pytest.mark.parametrize("case", [
+    (4, 14, 14, 64, 128, 3, 1, 1, 2, True, False),
+    (2, 56, 56, 3, 64, 7, 2, 3, 2, True, False),
+    (3, 9, 9, 128, 64, 1, 2, 0, 2, 6, True),
+])
+def test_conv_bn_fused_finalize_matches_oracle(case, monkeypatch):
+    """BN finalize by the last-arriving conv tile (CER_BN_FUSED_FINALIZE path)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    monkeypatch.setattr(_hip, "_FUSED_FINALIZE", True)
+    test_conv_bn_fused_matches_oracle(case, -1)
+    test_conv_bn_fused_matches_oracle(case, 4)
