@@ -8,10 +8,11 @@ into one horizontally-fused model on a GPU (``pack_key``).
 The reference's ``"inceptionresnetv2"`` name silently builds VGG19
 (``in_rdbms_helper.py:314-321``); it is kept as an alias of ``vgg19`` so
 grids naming it train what the reference actually trained.
-``nasnetmobile`` (B1) is not available yet.
+``nasnetmobile`` = ``keras.applications.NASNetMobile`` (``models/nasnet.py``).
 """
 
 from .mlp import PackedConfA, PackedSanity
+from .nasnet import PackedNASNetMobile
 from .resnet import PackedResNet
 from .small import PackedMobileNetV2, PackedTinyCNN
 from .vgg import PackedVGG16, PackedVGG19
@@ -32,6 +33,7 @@ MODEL_FACTORIES = {
     "densenet201": lambda: PackedDenseNet(201),
     "mobilenetv1": lambda: PackedMobileNetV1(),
     "mobilenetv2": lambda: PackedMobileNetV2(),
+    "nasnetmobile": lambda: PackedNASNetMobile(),
     "confA": lambda: PackedConfA(),
     "sanity": lambda: PackedSanity(),
     "tinycnn": lambda: PackedTinyCNN(),

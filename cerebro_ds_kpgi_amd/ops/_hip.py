@@ -179,9 +179,12 @@ _SIGS.update({
 IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
 
 _SIGS2 = {
-    "cer_dwconv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_p, c_p],
-    "cer_dwconv_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i,
+    "cer_dwconv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_i,
                        c_p, c_p],
+    "cer_dwconv_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i,
+                       c_i, c_i, c_i, c_p, c_p],
+    "cer_avgpool_fwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "cer_avgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_embbag_fwd": [c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p, c_p],
     "cer_embbag_bwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
 }
@@ -712,17 +715,29 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
 # ---------------------------------------------------------------------------
 # depthwise conv (csrc/hip/dwconv.hip) and embedding bag (csrc/hip/embbag.hip)
 # ---------------------------------------------------------------------------
+def _pad4(pad):
+    """int (symmetric) or (top, bottom, left, right)."""
+    if isinstance(pad, int):
+        return pad, pad, pad, pad
+    return tuple(int(p) for p in pad)
+
+
+def dw_out_hw(H, W, k, stride, pad):
+    pt, pb, pl, pr = _pad4(pad)
+    return (H + pt + pb - k) // stride + 1, (W + pl + pr - k) // stride + 1
+
+
 def dwconv_fwd(x, wref, stride, pad):
     x = _bf16(x)
     B, H, W, GC = x.shape
     G = wref.G
     C, kh, kw = wref.spec.shape
-    Ho = (H + 2 * pad - kh) // stride + 1
-    Wo = (W + 2 * pad - kw) // stride + 1
+    Ho, Wo = dw_out_hw(H, W, kh, stride, pad)
+    pt, _, pl, _ = _pad4(pad)
     y = torch.empty((B, Ho, Wo, GC), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
-    rc = lib().cer_dwconv_fwd(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pad, _ptr(y),
-                              _stream())
+    rc = lib().cer_dwconv_fwd(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pt, pl, Ho, Wo,
+                              _ptr(y), _stream())
     _check(rc, "cer_dwconv_fwd")
     return y
 
@@ -731,16 +746,44 @@ def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
     dy = _bf16(dy)
     x = _bf16(x)
     B, H, W, GC = x.shape
+    _, Ho, Wo, _ = dy.shape
     G = wref.G
     C, kh, kw = wref.spec.shape
+    pt, _, pl, _ = _pad4(pad)
     if not wref.arena.grad_clean:
         wref.grad().zero_()
     dx = torch.empty_like(x) if need_dx else None
     wp, ws = wref.work_ptr()
     gp, gs = wref.grad_ptr()
     rc = lib().cer_dwconv_bwd(_ptr(dy), _ptr(x), B, H, W, C, G, c_p(wp), ws, c_p(gp), gs, kh,
-                              stride, pad, _ptr(dx), _stream())
+                              stride, pt, pl, Ho, Wo, _ptr(dx), _stream())
     _check(rc, "cer_dwconv_bwd")
+    return dx
+
+
+def avgpool_fwd(x, k, s, pad, count_pad):
+    """k x k / s average pool; pad = int or (top, bottom, left, right) zero
+    padding; count_pad: divide by k*k, else by the in-bounds tap count."""
+    x = _bf16(x)
+    B, H, W, C = x.shape
+    Ho, Wo = dw_out_hw(H, W, k, s, pad)
+    pt, _, pl, _ = _pad4(pad)
+    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    rc = lib().cer_avgpool_fwd(_ptr(x), _ptr(y), B, H, W, C, Ho, Wo, k, s, pt, pl,
+                               int(bool(count_pad)), _stream())
+    _check(rc, "cer_avgpool_fwd")
+    return y
+
+
+def avgpool_bwd(dy, xshape, k, s, pad, count_pad):
+    dy = _bf16(dy)
+    B, H, W, C = xshape
+    _, Ho, Wo, _ = dy.shape
+    pt, _, pl, _ = _pad4(pad)
+    dx = torch.empty(xshape, dtype=torch.bfloat16, device=dy.device)
+    rc = lib().cer_avgpool_bwd(_ptr(dy), _ptr(dx), B, H, W, C, Ho, Wo, k, s, pt, pl,
+                               int(bool(count_pad)), _stream())
+    _check(rc, "cer_avgpool_bwd")
     return dx
 
 

@@ -53,6 +53,37 @@ def use_hip(op, *tensors):
     return True
 
 
+# Ops that ran their PyTorch path on a GPU tensor while the HIP backend is
+# active (a shape no HIP kernel covers, or an op without one).  The runtime
+# captures a training step in a HIP graph only if the step made none: the
+# MIOpen-backed torch convolutions / pools are not stream-capture safe on this
+# stack (replays diverge from eager; scripts/debug/nasnet_capture.py), while
+# elementwise torch glue is.
+_FALLBACKS = set()
+
+
+def hip_gate(op, shape_ok, *tensors):
+    """use_hip(op) and the HIP kernel covers this shape; records a fallback
+    when the HIP backend is active but the shape is not covered."""
+    if not use_hip(op, *tensors):
+        return False
+    if not shape_ok:
+        _FALLBACKS.add(op)
+        return False
+    return True
+
+
+def note_fallback(op):
+    _FALLBACKS.add(op)
+
+
+def take_fallbacks():
+    """Fallbacks recorded since the last call (and reset)."""
+    out = set(_FALLBACKS)
+    _FALLBACKS.clear()
+    return out
+
+
 def force_torch_ops(ops):
     _FORCED_TORCH.clear()
     _FORCED_TORCH.update(ops)

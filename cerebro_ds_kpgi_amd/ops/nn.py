@@ -20,7 +20,7 @@ implementation in this file (``ops.backend``).
 import torch
 import torch.nn.functional as F
 
-from .backend import use_hip
+from .backend import hip_gate, note_fallback, use_hip
 
 
 def _hip():
@@ -141,13 +141,18 @@ def conv2d_bias_act(x, wref, bref, stride=1, pad=0, act=1, anchor=None):
 # batch norm (+ residual add) (+ ReLU)
 # ---------------------------------------------------------------------------
 
+def _bn_hip(x, gref):
+    """HIP BN kernels move 8 channels per thread: per-config channels % 8 == 0."""
+    return hip_gate("bn", gref.spec.shape[0] % 8 == 0, x)
+
+
 def _flat_param(ref):
     return ref.work().reshape(-1).float() if ref.spec.kind in ("gamma", "beta") else ref.master().reshape(-1)
 
 
 def _bn_forward_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
     C = x.shape[-1]
-    if use_hip("bn", x):
+    if _bn_hip(x, gref):
         return _hip().bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps)
     x2 = x.reshape(-1, C).float()
     n = x2.shape[0]
@@ -205,7 +210,8 @@ class PackedConvBNAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.x4 = None
-        if use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0:
+        if use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0 \
+                and gref.spec.shape[0] % 8 == 0:
             h = _hip()
             # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
             stem = not x.requires_grad and h.stem_ok(x, wref, stride, pad)
@@ -235,7 +241,7 @@ class PackedConvBNAct(torch.autograd.Function):
 
 
 def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
-    if use_hip("bn", x):
+    if _bn_hip(x, gref):
         return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res)
     C = x.shape[-1]
     dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
@@ -260,7 +266,7 @@ def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, r
 
 def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):
     C = x.shape[-1]
-    if use_hip("bn", x):
+    if _bn_hip(x, gref):
         return _hip().bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, relu, eps)
     rm = rmref.master().reshape(-1)
     rv = rvref.master().reshape(-1)
@@ -339,12 +345,12 @@ class MaxPoolHip(torch.autograd.Function):
 
 
 def maxpool2d(x, k, s, p=0):
-    if use_hip("pool", x):
+    if hip_gate("pool", x.shape[-1] % 8 == 0, x):
         return MaxPoolHip.apply(x, k, s, p)
     return _nhwc(F.max_pool2d(_nchw(x), k, s, p))
 
 
-class AvgPoolHip(torch.autograd.Function):
+class GlobalAvgPoolHip(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         ctx.xshape = x.shape
@@ -357,8 +363,8 @@ class AvgPoolHip(torch.autograd.Function):
 
 def global_avgpool(x):
     """[B, H, W, C] -> [B, C]."""
-    if use_hip("pool", x):
-        return AvgPoolHip.apply(x)
+    if hip_gate("pool", x.shape[-1] % 8 == 0, x):
+        return GlobalAvgPoolHip.apply(x)
     return x.float().mean(dim=(1, 2)).to(x.dtype)
 
 
@@ -440,8 +446,8 @@ class PackedEmbeddingBag(torch.autograd.Function):
         G = wref.G
         K, N = wref.spec.shape
         Gi, B, nnz = idx.shape
-        ctx.hip = (use_hip("embbag", idx) and wref.arena.compute_dtype == torch.bfloat16
-                   and N % 8 == 0)
+        ctx.hip = hip_gate("embbag", wref.arena.compute_dtype == torch.bfloat16 and N % 8 == 0,
+                           idx)
         if ctx.hip:
             y = _hip().embbag_fwd(idx, wref, bref, relu)
         else:
@@ -488,18 +494,34 @@ def embedding_bag(idx, wref, bref, relu=True, anchor=None):
 # depthwise conv (MobileNetV2) — packed channels, one filter per channel
 # ---------------------------------------------------------------------------
 
+def _pad4(pad):
+    if isinstance(pad, int):
+        return pad, pad, pad, pad
+    return tuple(int(p) for p in pad)
+
+
+def _zero_pad(x, pad):
+    """Explicit zero padding of packed NHWC; pad = (top, bottom, left, right)."""
+    pt, pb, pl, pr = pad
+    return F.pad(x, (0, 0, pl, pr, pt, pb))
+
+
 class PackedDWConv2d(torch.autograd.Function):
+    """Depthwise k x k conv (k in {3, 5, 7}), stride 1/2; ``pad`` is an int or
+    (top, bottom, left, right) — Keras stride-2 ``correct_pad`` is asymmetric."""
+
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         C, kh, kw = wref.spec.shape
-        ctx.hip = use_hip("dwconv", x) and C % 8 == 0 and kh == kw and kh in (3, 5)
+        ctx.hip = hip_gate("dwconv", C % 8 == 0 and kh == kw and kh in (3, 5, 7)
+                           and stride in (1, 2) and max(_pad4(pad)) < kh, x)
         if ctx.hip:
             y = _hip().dwconv_fwd(x, wref, stride, pad)
         else:
-            C, kh, kw = wref.spec.shape
             w = wref.work().reshape(wref.G * C, 1, kh, kw)
-            y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * C))
+            y = _nhwc(F.conv2d(_nchw(_zero_pad(x, _pad4(pad))), w, None, stride, 0, 1,
+                               wref.G * C))
         ctx.save_for_backward(x)
         return y
 
@@ -514,11 +536,14 @@ class PackedDWConv2d(torch.autograd.Function):
         C, kh, kw = wref.spec.shape
         GC = wref.G * C
         w = wref.work().reshape(GC, 1, kh, kw)
-        xn, dyn = _nchw(x), _nchw(dy)
+        pt, pb, pl, pr = _pad4(pad)
+        xp = _nchw(_zero_pad(x, (pt, pb, pl, pr)))
+        dyn = _nchw(dy)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, GC))
-        dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, GC)
+            dxp = torch.nn.grad.conv2d_input(xp.shape, w, dyn, stride, 0, 1, GC)
+            dx = _nhwc(dxp[:, :, pt:pt + x.shape[1], pl:pl + x.shape[2]])
+        dw = torch.nn.grad.conv2d_weight(xp, w.shape, dyn, stride, 0, 1, GC)
         wref.grad().copy_(dw.view(wref.G, C, kh, kw))
         return dx, None, None, None, None
 
@@ -543,6 +568,8 @@ class PackedGroupedConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad, groups):
         ctx.wref, ctx.stride, ctx.pad, ctx.groups = wref, stride, pad, groups
+        if use_hip("conv", x):
+            note_fallback("grouped_conv")
         w = _torch_weight(wref)
         y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * groups))
         ctx.save_for_backward(x)
@@ -570,9 +597,29 @@ def grouped_conv2d(x, wref, stride=1, pad=0, groups=1, anchor=None):
     return PackedGroupedConv2d.apply(x, anchor, wref, stride, pad, groups)
 
 
-def avgpool2d(x, k, s, p=0):
-    """Per-channel average pooling (count_include_pad=False, Keras 'valid')."""
-    return _nhwc(F.avg_pool2d(_nchw(x), k, s, p, count_include_pad=False))
+class AvgPoolHip(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p, count_pad):
+        ctx.geom = (x.shape, k, s, p, count_pad)
+        return _hip().avgpool_fwd(x, k, s, p, count_pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xshape, k, s, p, count_pad = ctx.geom
+        dx = _hip().avgpool_bwd(dy.contiguous(), xshape, k, s, p, count_pad)
+        return dx, None, None, None, None
+
+
+def avgpool2d(x, k, s, p=0, count_include_pad=False):
+    """Per-channel k x k / s average pooling with symmetric zero padding ``p``;
+    count_include_pad=False divides by the in-bounds taps (Keras/TF 'same')."""
+    if hip_gate("pool", x.shape[-1] % 8 == 0 and p < k, x):
+        return AvgPoolHip.apply(x, k, s, p, count_include_pad)
+    # contiguous NCHW: PyTorch-ROCm's avg_pool2d backward on a channels-last
+    # view with padding and count_include_pad=False returns wrong gradients
+    # (rel. error ~1.0; scripts/debug/avgpool_check.py)
+    return _nhwc(F.avg_pool2d(_nchw(x).contiguous(), k, s, p,
+                              count_include_pad=count_include_pad))
 
 
 def cat_packed(xs, G):

@@ -614,5 +614,13 @@ class MOPEngine(object):
 
     def close(self):
         self.writer.close()
+        # release captured HIP graphs deterministically (device drained first)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        for grp in self.groups.values():
+            for w in grp._work.values():
+                if w.graph is not None:
+                    w.graph.reset()
+                    w.graph = None
         if self.o.trace and self.o.logs_root:
             self.tracer.dump(os.path.join(self.o.logs_root, "traces"))

@@ -23,7 +23,9 @@ import torch
 from ..data.store import gather_batch, input_buffers
 from ..models import create_model_from_mst
 from ..ops.loss import eval_metrics, softmax_ce
+from ..ops.backend import take_fallbacks
 from ..ops.optim import optimizer_step
+from ..utils.logging import log_once
 from .arena import Arena
 
 
@@ -113,6 +115,7 @@ class _Working(object):
         self.vcursor = torch.zeros(1, dtype=torch.int32, device=g.device)
         self.vacc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
         self.graph = None
+        self.eager_only = False
         self.eager_steps = 0
         self.jobs = []
         # called between backward and the optimizer (DDP gradient all-reduce)
@@ -155,7 +158,7 @@ class _Working(object):
 
     def train_steps(self, nsteps):
         done = 0
-        if not self.group.use_graphs:
+        if not self.group.use_graphs or self.eager_only:
             for _ in range(nsteps):
                 self._step()
             return nsteps
@@ -163,12 +166,25 @@ class _Working(object):
             # eager warm-up on a side stream (real steps), then capture once
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
+            take_fallbacks()
             with torch.cuda.stream(s):
                 while self.eager_steps < self.group.warmup_eager and done < nsteps:
                     self._step()
                     self.eager_steps += 1
                     done += 1
             torch.cuda.current_stream().wait_stream(s)
+            fb = take_fallbacks()
+            if fb:
+                # a step with PyTorch-path convs / pools is not capture safe:
+                # this working set stays eager (ops.backend.hip_gate)
+                self.eager_only = True
+                log_once("{} G={}: ops {} have no HIP kernel for these shapes; "
+                         "running eagerly (no HIP graph)".format(self.group.arch, self.G,
+                                                                 sorted(fb)))
+                while done < nsteps:
+                    self._step()
+                    done += 1
+                return done
             if done >= nsteps:
                 return done
             self.graph = torch.cuda.CUDAGraph()

@@ -119,3 +119,14 @@ class GlobalLog(object):
         self._write("{}, TOTAL EXECUTION TIME OVER ALL MST {}".format(
             self.exp_name, int(round(seconds))))
         return seconds
+
+
+_ONCE = set()
+
+
+def log_once(message):
+    """``logs`` a message the first time it is seen in this process."""
+    if message in _ONCE:
+        return None
+    _ONCE.add(message)
+    return logs(message)

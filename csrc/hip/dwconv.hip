@@ -1,15 +1,24 @@
-// Depthwise k x k convolution over packed NHWC channels (MobileNet V1/V2;
-// SURVEY.md §2.2 B1).  Channel (g, c) of the packed tensor has its own k x k
-// filter at w + g*w_gstride + c*k*k (Keras depthwise_kernel, per-config).
-// Purely bandwidth-bound, so every kernel moves 8 channels (16 B) per
-// thread; the weights for those 8 channels stay in registers.
+// Depthwise k x k convolution over packed NHWC channels (MobileNet V1/V2,
+// NASNet-Mobile separable convs).  Channel (g, c) of the
+// packed tensor has its own k x k filter at w + g*w_gstride + c*k*k (Keras
+// depthwise_kernel, per-config).  k in {3, 5, 7}, stride 1 or 2; padding may
+// be asymmetric (Keras stride-2 "correct_pad": top/left = k/2 - 1 on even
+// inputs): the caller passes the top/left pad and the output size, and the
+// bottom/right pad is implied by the bounds checks.
 //
-//  fwd   : one thread = 8 channels x 4 consecutive output columns
+// Bandwidth-bound, so every kernel moves 8 channels (16 B) per thread; only
+// one filter row (k x 8 fp32) is register-resident at a time, so k = 7 does
+// not spill.
+//
+//  fwd   : one thread = 8 channels x 4 consecutive output columns; per filter
+//          row the (4-1)*stride + k input pixels are loaded once (sliding
+//          window) instead of 4k times
 //  dgrad : one thread = 8 channels x 1 input pixel (gathers the dy taps that
 //          reach it; stride 2 handled by divisibility)
-//  wgrad : block = 8 channels x 256 row lanes; each lane accumulates the
-//          k*k*8 products over its pixels, LDS tree, fp32 atomics into the
-//          gradient arena (which the optimizer keeps zeroed)
+//  wgrad : block = 8 channels x 256 row lanes x a band of filter rows; each
+//          lane accumulates the band's taps over its pixels, wave reduction,
+//          LDS across waves, fp32 atomics into the gradient arena (which the
+//          optimizer keeps zeroed)
 #include "common.h"
 
 namespace {
@@ -37,25 +46,27 @@ __device__ __forceinline__ void st8(bf16_t* p, const float* v) {
 }
 
 struct DWGeom {
-  int B, H, W, C, G, Ho, Wo, k, st, pad;
+  int B, H, W, C, G, Ho, Wo, pt, pl;
   int64_t w_gstride;
 };
 
+// filter row r of the 8 channels starting at packed channel gc0
 template <int K>
-__device__ __forceinline__ void load_w(const bf16_t* w, const DWGeom& d, int gc0,
-                                       float (&wr)[K * K][DW_V]) {
+__device__ __forceinline__ void load_wrow(const bf16_t* w, const DWGeom& d, int gc0, int r,
+                                          float (&wr)[K][DW_V]) {
   const int g = gc0 / d.C, c0 = gc0 - g * d.C;
-  const bf16_t* base = w + g * d.w_gstride + (int64_t)c0 * K * K;
+  const bf16_t* base = w + g * d.w_gstride + (int64_t)c0 * K * K + r * K;
 #pragma unroll
   for (int i = 0; i < DW_V; ++i)
 #pragma unroll
-    for (int t = 0; t < K * K; ++t) wr[t][i] = bf2f(base[i * K * K + t]);
+    for (int s = 0; s < K; ++s) wr[s][i] = bf2f(base[i * K * K + s]);
 }
 
-template <int K>
+template <int K, int ST>
 __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16_t* __restrict__ x,
                                                      const bf16_t* __restrict__ w,
                                                      bf16_t* __restrict__ y, DWGeom d) {
+  constexpr int NWIN = (DW_X - 1) * ST + K;
   const int GC = d.G * d.C, CV = GC / DW_V;
   const int xgroups = (d.Wo + DW_X - 1) / DW_X;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -68,31 +79,45 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16_t* __restrict__ 
   const int ho = (int)(t % d.Ho);
   const int b = (int)(t / d.Ho);
   const int gc0 = cv * DW_V;
-  float wr[K * K][DW_V];
-  load_w<K>(w, d, gc0, wr);
-  for (int xi = 0; xi < DW_X; ++xi) {
-    const int wo = xg * DW_X + xi;
-    if (wo >= d.Wo) break;
-    float acc[DW_V] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int wo0 = xg * DW_X;
+  const int wi0 = wo0 * ST - d.pl;
+  float acc[DW_X][DW_V];
 #pragma unroll
-    for (int r = 0; r < K; ++r) {
-      const int hi = ho * d.st - d.pad + r;
-      if (hi < 0 || hi >= d.H) continue;
+  for (int xi = 0; xi < DW_X; ++xi)
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const int wi = wo * d.st - d.pad + s;
-        if (wi < 0 || wi >= d.W) continue;
-        float v[DW_V];
-        ld8(x + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, v);
+    for (int i = 0; i < DW_V; ++i) acc[xi][i] = 0.f;
+  for (int r = 0; r < K; ++r) {
+    const int hi = ho * ST - d.pt + r;
+    if (hi < 0 || hi >= d.H) continue;
+    float wr[K][DW_V];
+    load_wrow<K>(w, d, gc0, r, wr);
+    const bf16_t* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
+    float win[NWIN][DW_V];
 #pragma unroll
-        for (int i = 0; i < DW_V; ++i) acc[i] += v[i] * wr[r * K + s][i];
+    for (int j = 0; j < NWIN; ++j) {
+      const int wi = wi0 + j;
+      if (wi >= 0 && wi < d.W) {
+        ld8(xrow + (int64_t)wi * GC, win[j]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < DW_V; ++i) win[j][i] = 0.f;
       }
     }
-    st8(y + (((int64_t)b * d.Ho + ho) * d.Wo + wo) * GC + gc0, acc);
+#pragma unroll
+    for (int xi = 0; xi < DW_X; ++xi)
+#pragma unroll
+      for (int s = 0; s < K; ++s)
+#pragma unroll
+        for (int i = 0; i < DW_V; ++i) acc[xi][i] += win[xi * ST + s][i] * wr[s][i];
+  }
+#pragma unroll
+  for (int xi = 0; xi < DW_X; ++xi) {
+    const int wo = wo0 + xi;
+    if (wo < d.Wo) st8(y + (((int64_t)b * d.Ho + ho) * d.Wo + wo) * GC + gc0, acc[xi]);
   }
 }
 
-template <int K>
+template <int K, int ST>
 __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16_t* __restrict__ dy,
                                                        const bf16_t* __restrict__ w,
                                                        bf16_t* __restrict__ dx, DWGeom d) {
@@ -107,47 +132,48 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16_t* __restrict_
   const int hi = (int)(t % d.H);
   const int b = (int)(t / d.H);
   const int gc0 = cv * DW_V;
-  float wr[K * K][DW_V];
-  load_w<K>(w, d, gc0, wr);
   float acc[DW_V] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
   for (int r = 0; r < K; ++r) {
-    const int hn = hi + d.pad - r;
-    if (hn < 0 || hn % d.st) continue;
-    const int ho = hn / d.st;
+    const int hn = hi + d.pt - r;
+    if (hn < 0 || hn % ST) continue;
+    const int ho = hn / ST;
     if (ho >= d.Ho) continue;
+    float wr[K][DW_V];
+    load_wrow<K>(w, d, gc0, r, wr);
 #pragma unroll
     for (int s = 0; s < K; ++s) {
-      const int wn = wi + d.pad - s;
-      if (wn < 0 || wn % d.st) continue;
-      const int wo = wn / d.st;
+      const int wn = wi + d.pl - s;
+      if (wn < 0 || wn % ST) continue;
+      const int wo = wn / ST;
       if (wo >= d.Wo) continue;
       float v[DW_V];
       ld8(dy + (((int64_t)b * d.Ho + ho) * d.Wo + wo) * GC + gc0, v);
 #pragma unroll
-      for (int i = 0; i < DW_V; ++i) acc[i] += v[i] * wr[r * K + s][i];
+      for (int i = 0; i < DW_V; ++i) acc[i] += v[i] * wr[s][i];
     }
   }
   st8(dx + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, acc);
 }
 
-// grid (GC / 8, row slabs); 256 lanes stride over the slab's output pixels
-template <int K>
+// grid (GC / 8, row slabs, K / RB filter-row bands); 256 lanes stride over the
+// slab's output pixels, each accumulating RB x K taps x 8 channels
+template <int K, int RB>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict__ x,
                                                        const bf16_t* __restrict__ dy,
                                                        float* __restrict__ dw,
-                                                       int64_t dw_gstride, DWGeom d,
+                                                       int64_t dw_gstride, DWGeom d, int st,
                                                        int64_t pix_per_slab) {
-  __shared__ float red[K * K * DW_V][4];
+  constexpr int NT = RB * K;
+  __shared__ float red[NT * DW_V][4];
   const int GC = d.G * d.C;
   const int gc0 = blockIdx.x * DW_V;
-  constexpr int kk = K * K;
+  const int r0 = blockIdx.z * RB;
   const int64_t P = (int64_t)d.B * d.Ho * d.Wo;
   const int64_t p0 = (int64_t)blockIdx.y * pix_per_slab;
   const int64_t p1 = min(P, p0 + pix_per_slab);
-  float acc[kk][DW_V];
+  float acc[NT][DW_V];
 #pragma unroll
-  for (int t = 0; t < kk; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < DW_V; ++i) acc[t][i] = 0.f;
   for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
@@ -158,92 +184,123 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict_
     float g[DW_V];
     ld8(dy + p * GC + gc0, g);
 #pragma unroll
-    for (int r = 0; r < K; ++r) {
-      const int hi = ho * d.st - d.pad + r;
+    for (int rr = 0; rr < RB; ++rr) {
+      const int hi = ho * st - d.pt + r0 + rr;
       if (hi < 0 || hi >= d.H) continue;
 #pragma unroll
       for (int s = 0; s < K; ++s) {
-        const int wi = wo * d.st - d.pad + s;
+        const int wi = wo * st - d.pl + s;
         if (wi < 0 || wi >= d.W) continue;
         float v[DW_V];
         ld8(x + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, v);
 #pragma unroll
-        for (int i = 0; i < DW_V; ++i) acc[r * K + s][i] += v[i] * g[i];
+        for (int i = 0; i < DW_V; ++i) acc[rr * K + s][i] += v[i] * g[i];
       }
     }
   }
   // wave reduction, then 4 waves -> LDS -> one atomic per (tap, channel)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int t = 0; t < kk; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < DW_V; ++i) {
       const float v = warp_sum(acc[t][i]);
       if (lane == 0) red[t * DW_V + i][wid] = v;
     }
   __syncthreads();
-  for (int e = threadIdx.x; e < kk * DW_V; e += 256) {
+  for (int e = threadIdx.x; e < NT * DW_V; e += 256) {
     const float v = red[e][0] + red[e][1] + red[e][2] + red[e][3];
     const int t = e / DW_V, i = e - t * DW_V;
     const int gc = gc0 + i, g = gc / d.C, c = gc - g * d.C;
-    atomicAdd(dw + g * dw_gstride + (int64_t)c * kk + t, v);
+    atomicAdd(dw + g * dw_gstride + (int64_t)c * K * K + r0 * K + t, v);
   }
 }
 
-DWGeom make_dw(int B, int H, int W, int C, int G, int k, int st, int pad, int64_t ws) {
+DWGeom make_dw(int B, int H, int W, int C, int G, int pt, int pl, int Ho, int Wo, int64_t ws) {
   DWGeom d;
   d.B = B;
   d.H = H;
   d.W = W;
   d.C = C;
   d.G = G;
-  d.k = k;  // dispatch picks the K template
-  d.st = st;
-  d.pad = pad;
-  d.Ho = (H + 2 * pad - k) / st + 1;
-  d.Wo = (W + 2 * pad - k) / st + 1;
+  d.pt = pt;
+  d.pl = pl;
+  d.Ho = Ho;
+  d.Wo = Wo;
   d.w_gstride = ws;
   return d;
 }
 
+bool dw_shape_ok(int C, int k, int st, int pt, int pl, int Ho, int Wo) {
+  return C % DW_V == 0 && (k == 3 || k == 5 || k == 7) && (st == 1 || st == 2) && pt >= 0 &&
+         pl >= 0 && pt < k && pl < k && Ho > 0 && Wo > 0;
+}
+
+template <int K>
+void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const DWGeom& d, int st,
+                hipStream_t stream) {
+  const int64_t n = (int64_t)d.B * d.Ho * ((d.Wo + DW_X - 1) / DW_X) * (d.G * d.C / DW_V);
+  if (st == 1)
+    dw_fwd_kernel<K, 1><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+  else
+    dw_fwd_kernel<K, 2><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+}
+
+template <int K>
+void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DWGeom& d, int st,
+                  hipStream_t stream) {
+  const int64_t n = (int64_t)d.B * d.H * d.W * (d.G * d.C / DW_V);
+  if (st == 1)
+    dw_dgrad_kernel<K, 1><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+  else
+    dw_dgrad_kernel<K, 2><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+}
+
 }  // namespace
 
+// pt / pl: top / left zero padding; Ho / Wo: output size (fixes bottom/right)
 CER_API int cer_dwconv_fwd(const bf16_t* x, int B, int H, int W, int C, int G, const bf16_t* w,
-                           int64_t w_gstride, int k, int st, int pad, bf16_t* y,
-                           hipStream_t stream) {
-  if (C % DW_V || (k != 3 && k != 5)) return (int)hipErrorInvalidValue;
-  const DWGeom d = make_dw(B, H, W, C, G, k, st, pad, w_gstride);
-  const int64_t n = (int64_t)B * d.Ho * ((d.Wo + DW_X - 1) / DW_X) * (G * C / DW_V);
+                           int64_t w_gstride, int k, int st, int pt, int pl, int Ho, int Wo,
+                           bf16_t* y, hipStream_t stream) {
+  if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo)) return (int)hipErrorInvalidValue;
+  const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
   if (k == 3)
-    dw_fwd_kernel<3><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+    launch_fwd<3>(x, w, y, d, st, stream);
+  else if (k == 5)
+    launch_fwd<5>(x, w, y, d, st, stream);
   else
-    dw_fwd_kernel<5><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+    launch_fwd<7>(x, w, y, d, st, stream);
   return (int)hipGetLastError();
 }
 
 // dw must be zero on entry (accumulated with atomics); dx may be null
 CER_API int cer_dwconv_bwd(const bf16_t* dy, const bf16_t* x, int B, int H, int W, int C, int G,
                            const bf16_t* w, int64_t w_gstride, float* dw, int64_t dw_gstride,
-                           int k, int st, int pad, bf16_t* dx, hipStream_t stream) {
-  if (C % DW_V || (k != 3 && k != 5)) return (int)hipErrorInvalidValue;
-  const DWGeom d = make_dw(B, H, W, C, G, k, st, pad, w_gstride);
+                           int k, int st, int pt, int pl, int Ho, int Wo, bf16_t* dx,
+                           hipStream_t stream) {
+  if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo)) return (int)hipErrorInvalidValue;
+  const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
   if (dx) {
-    const int64_t n = (int64_t)B * H * W * (G * C / DW_V);
     if (k == 3)
-      dw_dgrad_kernel<3><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+      launch_dgrad<3>(dy, w, dx, d, st, stream);
+    else if (k == 5)
+      launch_dgrad<5>(dy, w, dx, d, st, stream);
     else
-      dw_dgrad_kernel<5><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+      launch_dgrad<7>(dy, w, dx, d, st, stream);
   }
-  const int64_t P = (int64_t)B * d.Ho * d.Wo;
+  const int64_t P = (int64_t)B * Ho * Wo;
   const int cblocks = G * C / DW_V;
-  int64_t slabs = (2048 + cblocks - 1) / cblocks;
+  const int bands = (k == 7) ? 7 : 1;      // k = 7: one filter row per block (56 accumulators)
+  int64_t slabs = (2048 + (int64_t)cblocks * bands - 1) / ((int64_t)cblocks * bands);
   int64_t per = (P + slabs - 1) / slabs;
   if (per < 256) per = 256;
   slabs = (P + per - 1) / per;
-  dim3 grid(cblocks, (unsigned)slabs);
+  dim3 grid(cblocks, (unsigned)slabs, bands);
   if (k == 3)
-    dw_wgrad_kernel<3><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, per);
+    dw_wgrad_kernel<3, 3><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+  else if (k == 5)
+    dw_wgrad_kernel<5, 5><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
   else
-    dw_wgrad_kernel<5><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, per);
+    dw_wgrad_kernel<7, 1><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
   return (int)hipGetLastError();
 }

@@ -312,3 +312,107 @@ CER_API int cer_bias_act_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, floa
   bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// k x k average pooling, stride s, top/left zero padding (pt, pl); the output
+// size fixes the bottom/right padding.  count_pad: divide by k*k, else by the
+// number of in-bounds taps (TF/Keras 'same', torch count_include_pad=False).
+// DenseNet transitions (2x2/2) and NASNet cells (3x3/1 same, 3x3/2 valid).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float avg_div(int ho, int wo, int H, int W, int k, int s, int pt,
+                                         int pl, int count_pad) {
+  if (count_pad) return 1.f / (float)(k * k);
+  const int h0 = max(ho * s - pt, 0), h1 = min(ho * s - pt + k, H);
+  const int w0 = max(wo * s - pl, 0), w1 = min(wo * s - pl + k, W);
+  const int n = max(h1 - h0, 0) * max(w1 - w0, 0);
+  return n > 0 ? 1.f / (float)n : 0.f;
+}
+
+__global__ __launch_bounds__(PT) void avgpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                         bf16_t* __restrict__ y, int B, int H,
+                                                         int W, int C, int Ho, int Wo, int k,
+                                                         int s, int pt, int pl, int count_pad) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * Ho * Wo * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int wo = (int)(pix % Wo);
+  pix /= Wo;
+  const int ho = (int)(pix % Ho);
+  const int b = (int)(pix / Ho);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < k; ++r) {
+    const int h = ho * s - pt + r;
+    if (h < 0 || h >= H) continue;
+    for (int q = 0; q < k; ++q) {
+      const int w = wo * s - pl + q;
+      if (w < 0 || w >= W) continue;
+      float v[8];
+      ld8(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[i];
+    }
+  }
+  const float inv = avg_div(ho, wo, H, W, k, s, pt, pl, count_pad);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] *= inv;
+  st8(y + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, acc);
+}
+
+// deterministic gather: each input pixel sums dy / divisor over the windows covering it
+__global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                         bf16_t* __restrict__ dx, int B, int H,
+                                                         int W, int C, int Ho, int Wo, int k,
+                                                         int s, int pt, int pl, int count_pad) {
+  const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)B * H * W * cv;
+  if (t >= total) return;
+  const int c0 = (int)(t % cv) * 8;
+  int64_t pix = t / cv;
+  const int w = (int)(pix % W);
+  pix /= W;
+  const int h = (int)(pix % H);
+  const int b = (int)(pix / H);
+  // windows containing h: ho*s - pt <= h <= ho*s - pt + k - 1
+  const int hl = h + pt - k + 1, wl = w + pl - k + 1;
+  const int ho0 = hl <= 0 ? 0 : (hl + s - 1) / s;
+  const int wo0 = wl <= 0 ? 0 : (wl + s - 1) / s;
+  const int ho1 = min(Ho - 1, (h + pt) / s);
+  const int wo1 = min(Wo - 1, (w + pl) / s);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int ho = ho0; ho <= ho1; ++ho) {
+    for (int wo = wo0; wo <= wo1; ++wo) {
+      float g[8];
+      ld8(dy + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, g);
+      const float inv = avg_div(ho, wo, H, W, k, s, pt, pl, count_pad);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += g[i] * inv;
+    }
+  }
+  st8(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
+}
+
+CER_API int cer_avgpool_fwd(const bf16_t* x, bf16_t* y, int B, int H, int W, int C, int Ho,
+                            int Wo, int k, int s, int pt, int pl, int count_pad,
+                            hipStream_t stream) {
+  if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
+    return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * Ho * Wo * (C / 8);
+  avgpool_fwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, B, H, W, C, Ho, Wo, k, s,
+                                                               pt, pl, count_pad);
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_avgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int H, int W, int C, int Ho,
+                            int Wo, int k, int s, int pt, int pl, int count_pad,
+                            hipStream_t stream) {
+  if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
+    return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)B * H * W * (C / 8);
+  avgpool_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, H, W, C, Ho, Wo, k, s,
+                                                               pt, pl, count_pad);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,14 @@
+#!/bin/bash
+# bench + 1-config bench + profile, then a verbose model-family test run (HIP error log on).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-s3}
+timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench_$TAG.log; exit 1; }
+tail -1 gpurun_out/bench_$TAG.log
+timeout -k 10 300 python bench.py --configs 1 > gpurun_out/bench_${TAG}_c1.log 2>&1 || { echo "bench c1 failed"; tail -30 gpurun_out/bench_${TAG}_c1.log; exit 1; }
+tail -1 gpurun_out/bench_${TAG}_c1.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_c1 -o prof -- python3 bench.py --configs 1 --steps 20 --warmup 10 --steps_per_round 10 > gpurun_out/prof_${TAG}_c1.log 2>&1
+echo "rocprof rc=$?"
+AMD_LOG_LEVEL=1 timeout -k 10 400 python -u -X faulthandler -m pytest tests/test_kernels_gpu.py -k model_family -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_family_$TAG.log 2>&1
+echo "family rc=$?"; tail -5 gpurun_out/pytest_family_$TAG.log

@@ -22,3 +22,19 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_teardown(request):
+    """After every GPU test: drain the device, then collect the test's garbage
+    (engines, captured HIP graphs, arenas) at a known point instead of at a
+    random later allocation."""
+    yield
+    if "gpu" not in request.keywords:
+        return
+    import gc
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.synchronize()

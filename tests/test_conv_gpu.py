@@ -305,10 +305,15 @@ def test_conv_bn_fused_matches_oracle(case, variant):
     assert _rel(h[4], t[4]) < 1e-3          # running stats (+ untouched weights)
 
 
-@pytest.mark.parametrize("case", [(2, 14, 14, 32, 1, 2), (2, 15, 13, 48, 2, 3), (3, 7, 7, 16, 1, 1)])
+@pytest.mark.parametrize("case", [
+    (2, 14, 14, 32, 1, 2, 3, 1), (2, 15, 13, 48, 2, 3, 3, 1), (3, 7, 7, 16, 1, 1, 3, 1),
+    (2, 14, 14, 16, 1, 2, 5, 2), (2, 14, 14, 24, 2, 2, 5, (1, 2, 1, 2)),     # NASNet 5x5
+    (2, 28, 28, 16, 2, 2, 7, (2, 3, 2, 3)), (2, 7, 7, 8, 1, 3, 7, 3),          # NASNet 7x7
+    (2, 15, 15, 8, 2, 2, 7, (3, 3, 3, 3)), (1, 9, 10, 8, 2, 2, 3, (0, 1, 0, 1))])
 def test_dwconv_matches_oracle(case):
-    B, H, W, C, s, G = case
-    spec = ParamSpec("dw", (C, 3, 3), "weight", fan_in=9)
+    """Depthwise k in {3,5,7}, stride 1/2, symmetric and Keras-asymmetric padding."""
+    B, H, W, C, s, G, k, pad = case
+    spec = ParamSpec("dw", (C, k, k), "weight", fan_in=k * k)
     torch.manual_seed(5)
     x = torch.randn(B, H, W, G * C, device="cuda").to(torch.bfloat16)
     outs = []
@@ -316,16 +321,41 @@ def test_dwconv_matches_oracle(case):
         backend.force_torch_ops(force)
         a, refs = _make([spec], G)
         xx = x.clone().requires_grad_(True)
-        y = P.dwconv2d(xx, refs["dw"], s, 1)
+        y = P.dwconv2d(xx, refs["dw"], s, pad)
         torch.manual_seed(3)
         y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
         torch.cuda.synchronize()
         outs.append((y.detach(), xx.grad, a.grad.clone()))
     backend.force_torch_ops([])
     h, t = outs
+    assert h[0].shape == t[0].shape
     assert _rel(h[0], t[0]) < 1e-2
     assert _rel(h[1], t[1]) < 1e-2
     assert _rel(h[2], t[2]) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 16, 3, 1, 1, False), (2, 14, 14, 16, 2, 2, 0, False),
+                                  (2, 9, 9, 24, 3, 2, 0, True), (2, 7, 7, 8, 3, 1, 1, True),
+                                  (3, 15, 15, 8, 3, 2, 1, False)])
+def test_avgpool_matches_oracle(case):
+    """k x k / s average pool (DenseNet transitions, NASNet 'same' and 'valid' pools)."""
+    B, H, W, C, k, s, p, cip = case
+    torch.manual_seed(8)
+    x = torch.randn(B, H, W, C, device="cuda").to(torch.bfloat16)
+    outs = []
+    for force in ([], ["pool"]):
+        backend.force_torch_ops(force)
+        xx = x.clone().requires_grad_(True)
+        y = P.avgpool2d(xx, k, s, p, count_include_pad=cip)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xx.grad))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert h[0].shape == t[0].shape
+    assert _rel(h[0], t[0]) < 1e-2
+    assert _rel(h[1], t[1]) < 1e-2
 
 
 @pytest.mark.parametrize("relu", [True, False])

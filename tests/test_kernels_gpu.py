@@ -125,7 +125,8 @@ def test_engine_one_round_on_gpu():
 
 @pytest.mark.parametrize("model,bs", [("confA", 32), ("mobilenetv2", 8), ("mobilenetv1", 8),
                                       ("vgg16", 8), ("densenet121", 8), ("resnext101", 4),
-                                      ("resnet50_nobn", 8), ("resnet18", 8)])
+                                      ("resnet50_nobn", 8), ("resnet18", 8),
+                                      ("nasnetmobile", 4)])
 def test_engine_trains_model_family(model, bs):
     """Every model family steps through the HIP engine (graph capture included)."""
     from cerebro_ds_kpgi_amd.parallel import init_distributed
@@ -139,3 +140,24 @@ def test_engine_trains_model_family(model, bs):
         loss = st["train_loss"][0]
         assert len(st["train_loss"]) == 1 and math.isfinite(loss) and loss > 0.0
     eng.close()
+
+
+@pytest.mark.parametrize("model,bs", [("resnet18", 8), ("mobilenetv2", 8), ("nasnetmobile", 4)])
+def test_graph_replay_matches_eager(model, bs):
+    """HIP-graph replayed training (the default) follows the eager trajectory;
+    a model whose step needs a PyTorch-path conv/pool stays eager instead."""
+    from cerebro_ds_kpgi_amd.parallel import init_distributed
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": bs, "model": model}
+            for lr in (1e-4, 1e-5)]
+    losses = []
+    for graphs in (False, True):
+        eng = MOPEngine(msts, init_distributed(), EngineOptions(
+            n_train=8 * bs, n_valid=2 * bs, slots_per_gpu=2, verbose=False, ckpt_every="none",
+            use_graphs=graphs))
+        eng.run(2)
+        losses.append([st["train_loss"] for st in eng.mst_state.values()])
+        eng.close()
+    for eager, graph in zip(*losses):
+        for a, b in zip(eager, graph):
+            assert math.isfinite(b) and abs(a - b) <= 2e-2 * abs(a), (eager, graph)

@@ -19,6 +19,7 @@ COUNTS = {
     "inceptionresnetv2": (59781160, 0),   # the reference's name for VGG19
     "mobilenetv1": (4231976, 21888),
     "mobilenetv2": (3504872, 34112),
+    "nasnetmobile": (5289978, 36738),     # Keras NASNetMobile summary: 5 326 716 total
     "densenet121": (7978856, 83648),
     "densenet201": (20013928, 229056),
     "resnext101": (44177704, 137856),     # ResNeXt-101 32x4d
@@ -38,7 +39,7 @@ def test_parameter_counts(name):
 
 
 @pytest.mark.parametrize("name", ["vgg19", "mobilenetv1", "densenet121", "resnext101",
-                                  "resnet50_nobn"])
+                                  "resnet50_nobn", "nasnetmobile"])
 def test_packed_forward_backward(name):
     from cerebro_ds_kpgi_amd.models import create_model_from_mst
     from cerebro_ds_kpgi_amd.ops import set_backend
@@ -65,3 +66,38 @@ def test_packed_forward_backward(name):
         a.sync_work()
         y3 = net.forward(x, False)
     assert torch.allclose(y1, y3[:, 1000:])
+
+
+def test_nasnet_correct_pad_and_shapes():
+    """Keras correct_pad (stride 2) and the 112 -> 55 -> 28 -> 14 -> 7 -> 4 cell plan."""
+    from cerebro_ds_kpgi_amd.models.nasnet import PackedNASNetMobile, correct_pad
+    assert correct_pad(28, 3) == (0, 1) and correct_pad(55, 7) == (3, 3)
+    assert correct_pad(14, 5) == (1, 2) and correct_pad(7, 3) == (1, 1)
+    net = PackedNASNetMobile()
+    hw = [c.hout for c in net.cells]
+    assert hw == [28, 14, 14, 14, 14, 14, 7, 7, 7, 7, 7, 4, 4, 4, 4, 4]
+    assert [c.cout for c in net.cells][-1] == 1056
+    kinds = [c.adj.kind for c in net.cells]
+    assert kinds[:3] == [None, "reduce", "reduce"]
+
+
+def test_dwconv_asymmetric_pad_matches_explicit_pad():
+    """Asymmetric depthwise padding (torch oracle path) == explicit zero pad + valid conv."""
+    import torch.nn.functional as F
+    from cerebro_ds_kpgi_amd.ops import nn as P, set_backend
+    from cerebro_ds_kpgi_amd.runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
+    set_backend("torch")
+    spec = ParamSpec("dw", (4, 7, 7), "weight", fan_in=49)
+    a = Arena(ModelLayout([spec]), 2, "cpu", torch.float32)
+    for g in range(2):
+        a.init_model(g, 3 + g)
+    ref = ParamRef(a, spec)
+    x = torch.randn(2, 14, 14, 8, requires_grad=True)
+    y = P.dwconv2d(x, ref, 2, (2, 3, 2, 3))
+    w = a.work.view(2, -1)[:, :4 * 49].reshape(8, 1, 7, 7)
+    xp = F.pad(x.detach().permute(0, 3, 1, 2), (2, 3, 2, 3))
+    want = F.conv2d(xp, w, None, 2, 0, 1, 8).permute(0, 2, 3, 1)
+    assert y.shape == (2, 7, 7, 8)
+    assert torch.allclose(y, want, atol=1e-5)
+    y.sum().backward()
+    assert x.grad.shape == x.shape
