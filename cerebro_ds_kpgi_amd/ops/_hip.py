@@ -15,6 +15,8 @@ import os
 
 import torch
 
+from . import streams
+
 _LIB = None
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libcerebro_hip.so")
@@ -144,6 +146,7 @@ _SIGS.update({
                        c_p, c_i64, c_i, c_p],
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
+    "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                            c_p, c_i, c_i, c_p, c_p, c_p],
@@ -204,17 +207,37 @@ def _bf16(t):
 
 
 # Kernel-variant autotuning (the MIOpen "find" step, done by the framework):
-# every conv problem is timed once under each of the 6 kernel variants
-# (register-staged / LDS-DMA ring x 64x64 / 128x128 / 128x64 tiles) on its
-# first eager call and the fastest is pinned for all later calls, including
-# HIP-graph capture.  CER_CONV_TUNE=0 keeps the built-in heuristic.
-NVARIANTS = 6
+# every conv problem is timed once under each of the 12 kernel variants
+# ({register-staged, LDS-DMA ring} x {one block per tile, split-K} x
+# {64x64, 128x128, 128x64} tiles; split-K applies to fwd / dgrad GEMMs whose
+# tile count cannot fill the chip) on its first eager call and the fastest is
+# pinned for all later calls, including HIP-graph capture.  CER_CONV_TUNE=0
+# keeps the built-in heuristic.
+NVARIANTS = 12
+SPLITK_FLOATS = 1 << 24      # 64 MB of fp32 split-K partial slots per device
+_SPLITK = {}
 _TUNED = {}
 _PINNED = {}
 
 
 def _tune_enabled():
     return os.environ.get("CER_CONV_TUNE", "1") != "0"
+
+
+def _splitk_ready(device):
+    """Register this device's persistent split-K workspace with the library
+    (once per device switch; the pointers are baked into captured graphs)."""
+    key = str(device)
+    cur = _SPLITK.get("_current")
+    if cur == key:
+        return
+    ws = _SPLITK.get(key)
+    if ws is None:
+        ws = (torch.empty(SPLITK_FLOATS, dtype=torch.float32, device=device),
+              torch.zeros(1 << 16, dtype=torch.int32, device=device))
+        _SPLITK[key] = ws
+    lib().cer_conv_set_splitk(_ptr(ws[0]), ws[0].numel(), _ptr(ws[1]), ws[1].numel())
+    _SPLITK["_current"] = key
 
 
 def _select(op, key, launch, after_tune=None):
@@ -257,6 +280,7 @@ def tuned_variants():
 
 def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,
                      act):
+    _splitk_ready(x.device)
     def launch():
         rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
                                 _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
@@ -298,6 +322,7 @@ def conv2d_fwd_stats(x, wref, stride, pad):
                        device=x.device)
     nslab = ctypes.c_int(0)
     wp, ws = wref.work_ptr()
+    _splitk_ready(x.device)
 
     def launch():
         rc = lib().cer_conv_fwd_stats(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride,
@@ -353,6 +378,7 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     C, M = G * cout, B * Ho * Wo
     dev = x.device
     L = lib()
+    _splitk_ready(dev)
     z = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=dev)
     part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dev)
     mean = torch.empty(C, dtype=torch.float32, device=dev)
@@ -463,6 +489,7 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W):
+    _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
     wt = torch.empty(n_wt, dtype=torch.bfloat16, device=dy.device)
@@ -702,7 +729,9 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     N, K = wref.spec.shape
     B = x.shape[0]
     dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _bf16(dy)
-    _conv_wgrad_launch(_bf16(x), B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref)
+    xb = _bf16(x)
+    streams.run_side(lambda: _conv_wgrad_launch(xb, B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref),
+                     xb, dz)
     if not need_dx:
         return None
     dx = torch.empty((B, G * K), dtype=torch.bfloat16, device=dy.device)

@@ -20,6 +20,7 @@ implementation in this file (``ops.backend``).
 import torch
 import torch.nn.functional as F
 
+from . import streams
 from .backend import hip_gate, note_fallback, use_hip
 
 
@@ -91,7 +92,8 @@ class PackedConv2d(torch.autograd.Function):
             h = _hip()
             if need_dx:
                 dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad)
-            h.conv2d_wgrad(x, dy, wref, stride, pad)
+            # off the critical path: overlaps the dgrad chain below (ops.streams)
+            streams.run_side(lambda: h.conv2d_wgrad(x, dy, wref, stride, pad), x, dy)
         else:
             G = wref.G
             cout, kh, kw, cin = wref.spec.shape
@@ -232,7 +234,8 @@ class PackedConvBNAct(torch.autograd.Function):
         dy = dy.contiguous()
         dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
         if ctx.x4 is not None:
-            _hip().stem_wgrad(ctx.x4, dz, ctx.wref, ctx.pad)
+            x4, wref, pad = ctx.x4, ctx.wref, ctx.pad
+            streams.run_side(lambda: _hip().stem_wgrad(x4, dz, wref, pad), x4, dz)
             ctx.x4 = None
             dx = None
         else:

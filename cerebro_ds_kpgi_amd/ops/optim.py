@@ -12,12 +12,14 @@ PyTorch trainer, ``cerebro_gpdb/run_pytorchddp.py:288-292``): coupled L2,
 
 import torch
 
+from . import streams
 from .backend import use_hip
 
 BETA1, BETA2, EPS = 0.9, 0.999, 1e-8
 
 
 def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
+    streams.join()
     if use_hip("adam", arena.state):
         from . import _hip
         _hip.adam_step(arena, beta1, beta2, eps, l2)
@@ -46,6 +48,7 @@ SGD_MOMENTUM = 0.9
 def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
     """``torch.optim.SGD(lr, momentum, weight_decay=lambda)``; the momentum
     buffer lives in the arena's first-moment slot."""
+    streams.join()
     if use_hip("adam", arena.state):
         from . import _hip
         _hip.sgd_step(arena, momentum, l2)
@@ -69,6 +72,7 @@ def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
 
 
 def optimizer_step(arena, name="adam", l2=True):
+    streams.join()          # side-stream weight gradients (ops.streams) land first
     if name == "sgd":
         return sgd_step(arena, l2=l2)
     return adam_step(arena, l2=l2)

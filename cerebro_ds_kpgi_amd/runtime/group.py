@@ -23,6 +23,7 @@ import torch
 from ..data.store import gather_batch, input_buffers
 from ..models import create_model_from_mst
 from ..ops.loss import eval_metrics, softmax_ce
+from ..ops import streams
 from ..ops.backend import take_fallbacks
 from ..ops.optim import optimizer_step
 from ..utils.logging import log_once
@@ -151,6 +152,7 @@ class _Working(object):
         logits = self.net.forward(self.x, True)
         loss = softmax_ce(logits, self.y, self.acc, self.G)
         loss.sum().backward()
+        streams.join()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)
         optimizer_step(self.arena, g.optimizer, l2=g.l2)
@@ -158,6 +160,7 @@ class _Working(object):
 
     def train_steps(self, nsteps):
         done = 0
+        streams.join()
         if not self.group.use_graphs or self.eager_only:
             for _ in range(nsteps):
                 self._step()
@@ -187,6 +190,7 @@ class _Working(object):
                 return done
             if done >= nsteps:
                 return done
+            streams.join()
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._step()

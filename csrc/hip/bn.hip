@@ -98,25 +98,41 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
   }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
+  // PU rows in flight per thread: loads of all rows issue before any use
+  // (narrow layers / small batches leave few waves per CU to hide latency)
+  constexpr int PU = 4;
   if (cok) {
-    for (int64_t r = r0 + tr; r < r1; r += mp.tr_n) {
-      float v[VEC];
-      load8(x + r * C + c0, v);
-      if (MODE == 0) {
+    for (int64_t r = r0 + tr; r < r1; r += PU * mp.tr_n) {
+      float v[PU][VEC], d[PU][VEC], yv[PU][VEC];
+      bool ok[PU];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          s[i] += v[i];
-          q[i] += v[i] * v[i];
+      for (int u = 0; u < PU; ++u) {
+        const int64_t rr = r + (int64_t)u * mp.tr_n;
+        ok[u] = rr < r1;
+        if (ok[u]) {
+          load8(x + rr * C + c0, v[u]);
+          if (MODE == 1) {
+            load8(dy + rr * C + c0, d[u]);
+            load8(y + rr * C + c0, yv[u]);
+          }
         }
-      } else {
-        float d[VEC], yv[VEC];
-        load8(dy + r * C + c0, d);
-        load8(y + r * C + c0, yv);
+      }
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          const float dz = act_bwd(d[i], yv[i], act);
-          s[i] += dz;
-          q[i] += dz * (v[i] - mu[i]) * is[i];
+      for (int u = 0; u < PU; ++u) {
+        if (!ok[u]) continue;
+        if (MODE == 0) {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            s[i] += v[u][i];
+            q[i] += v[u][i] * v[u][i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            const float dz = act_bwd(d[u][i], yv[u][i], act);
+            s[i] += dz;
+            q[i] += dz * (v[u][i] - mu[i]) * is[i];
+          }
         }
       }
     }
@@ -146,9 +162,10 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
 // ---------------------------------------------------------------------------
 // stage 2: finalize
 // ---------------------------------------------------------------------------
-// one block = 16 channels x 16 slab lanes; lanes strided over slabs (4
-// independent accumulators keep loads in flight), LDS tree
-constexpr int FIN_C = 16, FIN_L = 16;
+// one block = 8 channels x 32 slab lanes; each lane keeps 8 slab loads in
+// flight (the partials were just written by other CUs: every round trip is an
+// L2/MALL miss, so the reduction is latency-bound), LDS tree
+constexpr int FIN_C = 8, FIN_L = 32, FIN_U = 8;
 
 __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int slabs, int C,
                                           float* a_out, float* b_out) {
@@ -157,21 +174,30 @@ __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int sl
   const int c = blockIdx.x * FIN_C + cl;
   float a = 0.f, b = 0.f;
   if (c < C) {
-    float a4[4] = {0.f, 0.f, 0.f, 0.f}, b4[4] = {0.f, 0.f, 0.f, 0.f};
-    int k = ln;
-    for (; k + 3 * FIN_L < slabs; k += 4 * FIN_L) {
+    float au[FIN_U], bu[FIN_U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a4[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + c];
-        b4[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + C + c];
+    for (int u = 0; u < FIN_U; ++u) au[u] = bu[u] = 0.f;
+    int k = ln;
+    for (; k + (FIN_U - 1) * FIN_L < slabs; k += FIN_U * FIN_L) {
+#pragma unroll
+      for (int u = 0; u < FIN_U; ++u) {
+        au[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + c];
+        bu[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + C + c];
       }
     }
-    for (; k < slabs; k += FIN_L) {
-      a4[0] += part[(int64_t)k * 2 * C + c];
-      b4[0] += part[(int64_t)k * 2 * C + C + c];
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      const int kk = k + u * FIN_L;
+      if (kk < slabs) {
+        au[u] += part[(int64_t)kk * 2 * C + c];
+        bu[u] += part[(int64_t)kk * 2 * C + C + c];
+      }
     }
-    a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-    b = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+#pragma unroll
+    for (int u = 0; u < FIN_U; ++u) {
+      a += au[u];
+      b += bu[u];
+    }
   }
   sa[ln][cl] = a;
   sb[ln][cl] = b;
@@ -257,19 +283,27 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
   }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
-  for (int64_t r = r0 + tr; r < r1; r += mp.tr_n) {
-    float v[VEC], o[VEC];
-    load8(x + r * C + c0, v);
-    if (res) {
-      float rr[VEC];
-      load8(res + r * C + c0, rr);
+  constexpr int AU = 2;     // rows in flight per thread
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float v[AU][VEC], rv[AU][VEC];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) o[i] = act_fwd(v[i] * sc[i] + sh[i] + rr[i], act);
-    } else {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) o[i] = act_fwd(v[i] * sc[i] + sh[i], act);
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        load8(x + rr * C + c0, v[u]);
+        if (res) load8(res + rr * C + c0, rv[u]);
+      }
     }
-    store8(y + r * C + c0, o);
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr >= r1) continue;
+      float o[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i)
+        o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
+      store8(y + rr * C + c0, o);
+    }
   }
 }
 
@@ -295,19 +329,32 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
   }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
-  for (int64_t r = r0 + tr; r < r1; r += mp.tr_n) {
-    float d[VEC], xv[VEC], yv[VEC], o[VEC], dz[VEC];
-    load8(dy + r * C + c0, d);
-    load8(x + r * C + c0, xv);
-    load8(y + r * C + c0, yv);
+  constexpr int AU = 2;     // rows in flight per thread
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      dz[i] = act_bwd(d[i], yv[i], act);
-      const float xh = (xv[i] - mu[i]) * is[i];
-      o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        load8(dy + rr * C + c0, d[u]);
+        load8(x + rr * C + c0, xv[u]);
+        load8(y + rr * C + c0, yv[u]);
+      }
     }
-    store8(dx + r * C + c0, o);
-    if (dres) store8(dres + r * C + c0, dz);
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr >= r1) continue;
+      float o[VEC], dz[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        dz[i] = act_bwd(d[u][i], yv[u][i], act);
+        const float xh = (xv[u][i] - mu[i]) * is[i];
+        o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
+      }
+      store8(dx + rr * C + c0, o);
+      if (dres) store8(dres + rr * C + c0, dz);
+    }
   }
 }
 

@@ -106,6 +106,9 @@ struct NTParams {
   float* stats;           // optional BN partials part[slab][2][ldc] (sum, sum^2) of the
                           // bf16 outputs; slab = M tile (fused BN forward)
   BNFinal fin;            // optional: the last M tile of each N-tile column finalizes BN
+  int splits = 1;         // split-K: K-tile ranges per output tile (fwd / dgrad, small grids)
+  float* skws = nullptr;  // split-K fp32 partial slots [tile][split][acc regs x threads]
+  unsigned* skcnt = nullptr;  // split-K per-tile arrival counters (zero; last arriver re-zeroes)
 };
 
 
@@ -368,6 +371,54 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// K-tile range [kt0, kt1) of this block's split
+struct KRange {
+  int kt0, kt1;
+};
+
+__device__ __forceinline__ KRange split_range(const NTParams& p, int split) {
+  const int KT = (p.K + BK - 1) / BK;
+  const int per = (KT + p.splits - 1) / p.splits;
+  const int kt0 = split * per;
+  return KRange{kt0, min(KT, kt0 + per)};
+}
+
+// Split-K seam (fwd / dgrad GEMMs whose tile count cannot fill 256 CUs, e.g.
+// the 4x4 / 7x7 stages of a one-config step): every split publishes its fp32
+// accumulators to its own slot with write-through stores (thread-private
+// layout, coalesced across the block); the last-arriving split of the tile
+// re-reads all slots in split order (deterministic sum) and runs the normal
+// epilogue.  Returns false in the blocks that must exit.
+template <int BM, int BN>
+__device__ __forceinline__ bool splitk_reduce(const NTParams& p, f32x4 (&acc)[BM / 32][BN / 32],
+                                              int tile_id, int split, int tid) {
+  constexpr int FI = BM / 32, FJ = BN / 32, NA = FI * FJ * 4;
+  __shared__ int sk_flag;
+  float* base = p.skws + (int64_t)tile_id * p.splits * (NA * NTHREADS);
+  float* mine = base + (int64_t)split * (NA * NTHREADS);
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st_sc1(mine + ((i * FJ + j) * 4 + e) * NTHREADS + tid, acc[i][j][e]);
+  if (!last_arriver(p.skcnt + tile_id, (unsigned)p.splits, &sk_flag)) return false;
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < p.splits; ++sp) {
+    const float* src = base + (int64_t)sp * (NA * NTHREADS);
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] += ld_sc1(src + ((i * FJ + j) * 4 + e) * NTHREADS + tid);
+  }
+  return true;
+}
+
 // sum over each 16-lane row of the wave (DPP butterfly, no LDS traffic)
 __device__ __forceinline__ float row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1,
@@ -519,8 +570,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;       // splits of one tile: adjacent ids, one XCD
+  work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range(p, split);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -541,7 +595,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
-  KPos kp = kpos_init(p.a, 8 * my_chunk);
+  KPos kp = kpos_init(p.a, kr.kt0 * BK + 8 * my_chunk);
   uint4 ra[A_CH], rb[B_CH];
 
   auto load_tiles = [&](int kt) {
@@ -588,14 +642,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = (p.K + BK - 1) / BK;
-  load_tiles(0);
+  load_tiles(kr.kt0);
   store_tiles(0);
   __syncthreads();
   const int fr = lane & 15, fc = lane >> 4;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_tiles(kt + 1);
+  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
+    const int cur = (kt - kr.kt0) & 1;
+    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[FM], bfr[FN];
@@ -611,11 +664,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt(NTParams p) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < KT) store_tiles(cur ^ 1);
+    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
     __syncthreads();
   }
 
   // epilogue: stage the bf16 tile in LDS, then 16-B coalesced stores
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
@@ -807,8 +861,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;       // splits of one tile: adjacent ids, one XCD
+  work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range(p, split);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -825,7 +882,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   RowA rowa[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
-  KPos kp = kpos_init(p.a, 8 * my_chunk);
+  KPos kp = kpos_init(p.a, kr.kt0 * BK + 8 * my_chunk);
   uint4 ra[A_CH], rb[B_CH];
 
   auto load_tiles = [&](int kt) {
@@ -863,14 +920,13 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = (p.K + BK - 1) / BK;
-  load_tiles(0);
+  load_tiles(kr.kt0);
   store_tiles(0);
   __syncthreads();
   const int fr = lane & 15, fc = lane >> 4;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_tiles(kt + 1);
+  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
+    const int cur = (kt - kr.kt0) & 1;
+    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
     const bf16_t* sa = lds + cur * (BM * BK);
     const bf16_t* sb = lds + 2 * BM * BK + cur * (BK * BN);
 #pragma unroll
@@ -887,9 +943,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < KT) store_tiles(cur ^ 1);
+    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
     __syncthreads();
   }
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
@@ -1044,8 +1101,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;       // splits of one tile: adjacent ids, one XCD
+  work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range(p, split);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1069,7 +1129,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
     const int n = n0 + row;
     boff[j] = n < p.N ? (uint32_t)(n * p.K + 8 * ((lane & 7) ^ ((row >> 1) & 7))) * 2u : OOB;
   }
-  int tr = 0, ts = 0, tc = 0;  // tap / channel of the next K tile to issue (uniform)
+  // tap / channel of the next K tile to issue (uniform; Cg % 64 == 0: a K tile
+  // never straddles taps)
+  int tc = (kr.kt0 * BK) % p.a.Cg, tr = (kr.kt0 * BK) / p.a.Cg;
+  int ts = tr % p.a.kw;
+  tr /= p.a.kw;
   auto issue = [&](int kt, int st) {
     bf16_t* sa = lds + st * STAGE;
     bf16_t* sb = sa + BM * BK;
@@ -1089,10 +1153,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt(NTParams p) {
   };
   f32x4 acc[BM / 32][BN / 32];
   zero_acc<BM, BN>(acc);
-  ring_loop<S, LPW>(p.K / BK, issue, [&](int st) {
+  ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
     mma_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
   });
 
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
@@ -1112,8 +1177,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;       // splits of one tile: adjacent ids, one XCD
+  work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range(p, split);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1139,7 +1207,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
     const int c = n0 + 8 * tn_col16<BN>(row, lane % BC16);
     boff[j] = c < Cin ? (uint32_t)(row * T * Cin + c) * 2u : OOB;
   }
-  int tr = 0, ts = 0, tc = 0;
+  int tc = (kr.kt0 * BK) % Cout, tr = (kr.kt0 * BK) / Cout;
+  int ts = tr % p.a.kw;
+  tr /= p.a.kw;
   auto issue = [&](int kt, int st) {
     bf16_t* sa = lds + st * STAGE;
     bf16_t* sb = sa + BM * BK;
@@ -1160,10 +1230,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   };
   f32x4 acc[BM / 32][BN / 32];
   zero_acc<BM, BN>(acc);
-  ring_loop<S, LPW>(p.K / BK, issue, [&](int st) {
+  ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
     mma_nn<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
   });
 
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   constexpr int LDE = BN + 8;
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
@@ -1296,14 +1367,34 @@ CER_API void cer_conv_set_variant(int op, int v) {
   if (op >= 0 && op < 3) g_variant[op] = v;
 }
 
+// split-K workspace (persistent; registered by the host before launches)
+struct SplitKWs {
+  float* ws = nullptr;
+  int64_t floats = 0;
+  unsigned* cnt = nullptr;
+  int ncnt = 0;
+};
+static SplitKWs g_sk;
+
+CER_API void cer_conv_set_splitk(float* ws, int64_t floats, unsigned* cnt, int ncnt) {
+  g_sk.ws = ws;
+  g_sk.floats = floats;
+  g_sk.cnt = cnt;
+  g_sk.ncnt = ncnt;
+}
+
 static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); }
 
 // built-in choice (from the per-shape sweep of tools/bench_conv --sweep)
 static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
   if (g_variant[op] >= 0) {
-    const int v = g_variant[op];
-    return (v >= 3 && !pipe_ok) ? v - 3 : v;
+    int v = g_variant[op];
+    if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
+    if (((v / 3) & 1) && !pipe_ok) v -= 3;
+    return v;
   }
+  if (op != 2 && ntiles(M, N, 64, 64) * G < 128 && K / BK >= 16)
+    return 6;                                       // too few tiles to fill the chip
   int tile;
   if (op == 2) {
     tile = ntiles(N, K, 128, 128) * G >= 256 ? 1 : 0;
@@ -1321,9 +1412,32 @@ static void tile_dims(int v, int& bm, int& bn) {
   bn = t == 1 ? 128 : 64;
 }
 
+// split count for a fwd / dgrad GEMM: enough blocks for ~1.5 waves of 256 CUs,
+// >= 4 K tiles per split, within the registered workspace
+static int nt_splits(const NTParams& p, int G, int bm, int bn) {
+  const long tiles = ntiles(p.M, p.N, bm, bn) * G;
+  const int KT = (p.K + BK - 1) / BK;
+  int s = (int)((384 + tiles - 1) / tiles);
+  if (s > 8) s = 8;
+  if (s > KT / 4) s = KT / 4;
+  if (s < 2 || !g_sk.ws || tiles > g_sk.ncnt) return 1;
+  const int per = (KT + s - 1) / s;
+  s = (KT + per - 1) / per;
+  if ((int64_t)tiles * s * bm * bn > g_sk.floats) return 1;
+  return s;
+}
+
+static void set_splits(NTParams& p, int G, int v) {
+  int bm, bn;
+  tile_dims(v, bm, bn);
+  p.splits = (v / 3) >= 2 ? nt_splits(p, G, bm, bn) : 1;
+  p.skws = g_sk.ws;
+  p.skcnt = g_sk.cnt;
+}
+
 template <int BM, int BN>
 static void launch_nt_t(const NTParams& p, int G, int kind, bool fast, hipStream_t stream) {
-  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G));
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if (kind == 1) {
     if (p.K / BK >= 3)
       pipe_nt<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(p);
@@ -1342,11 +1456,13 @@ static bool nt_fast(const NTParams& p) {
          p.a.bytes != 0 && (uint64_t)p.N * p.K * 2 < (1ull << 31);
 }
 
-static int run_nt(const NTParams& p, int G, hipStream_t stream, int* nslab = nullptr) {
+static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   const bool fast = nt_fast(p);
   const bool pipe_ok = fast && p.a.Cg % 64 == 0;
-  const int v = fast ? choose(0, p.M, p.N, p.K, G, pipe_ok) : choose(0, p.M, p.N, p.K, G, false) % 3;
-  const int kind = v / 3;
+  int v = choose(0, p.M, p.N, p.K, G, pipe_ok);
+  if (!fast) v = (v >= 6 ? 6 : 0) + v % 3;         // generic gather: register-staged only
+  set_splits(p, G, v);
+  const int kind = (v / 3) & 1;
   if (nslab) {
     int bm, bn;
     tile_dims(v, bm, bn);
@@ -1432,7 +1548,7 @@ static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, c
 template <int BM, int BN>
 static void launch_nn_t(const NTParams& p, int G, int T, int kind, bool strided,
                         hipStream_t stream) {
-  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G));
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if (kind == 1) {
     const bool s3 = p.K / BK >= 3;
     if (strided) {
@@ -1498,7 +1614,8 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
       strided = st > 1;
     }
     const int v = choose(1, p.M, p.N, p.K, G, Cout % 64 == 0);
-    const int kind = v / 3;
+    set_splits(p, G, v);
+    const int kind = (v / 3) & 1;
     switch (v % 3) {
       case 0: launch_nn_t<64, 64>(p, G, T, kind, strided, stream); break;
       case 1: launch_nn_t<128, 128>(p, G, T, kind, strided, stream); break;
