@@ -147,6 +147,7 @@ _SIGS.update({
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
+    "cer_bn_set_coop": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                            c_p, c_i, c_i, c_p, c_p, c_p],

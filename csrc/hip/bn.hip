@@ -15,6 +15,8 @@
 // dres = dz.
 #include "common.h"
 
+#include <stdlib.h>
+
 constexpr int BN_T = 256;
 constexpr int VEC = 8;  // channels per thread
 
@@ -76,16 +78,80 @@ static void make_grid(int64_t M, int C, const Map& mp, int target, int min_rows,
 }
 
 // ---------------------------------------------------------------------------
+// cross-block hand-off for the cooperative kernels
+// ---------------------------------------------------------------------------
+// A value written by one block and read by a block on another XCD (whose L2
+// is not coherent with ours) inside the same kernel moves by agent-scope
+// atomic stores / loads; SC selects those in the tile functions below.
+template <bool SC>
+__device__ __forceinline__ float ldf(const float* p) {
+  if (SC) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
+template <bool SC>
+__device__ __forceinline__ void stf(float* p, float v) {
+  if (SC)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
+// Grid-wide barrier for a co-resident grid (the host caps the grid at the
+// occupancy-derived resident-block count).  Same-address atomics from every
+// block serialise at the coherence point (~20 ns each: a 512-block counter
+// barrier costs ~10 us), so arrival is a plain flag store per block instead:
+// block b writes the barrier's epoch into flags[b]; block 0 polls all flags
+// (one per thread, in parallel) and then publishes the epoch in bar[0]; the
+// other blocks spin on bar[0].  The epoch is the bar[0] value every block read
+// at kernel start (before any block can arrive) plus the barrier's ordinal,
+// so barriers never need re-arming.
+struct GridBar {
+  unsigned* rel;     // bar[0]: last published epoch
+  unsigned* flags;   // one arrival word per block
+  unsigned base;     // bar[0] at kernel start
+};
+
+__device__ __forceinline__ GridBar grid_bar_open(unsigned* bar) {
+  __shared__ unsigned base_s;
+  if (threadIdx.x == 0)
+    base_s = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return GridBar{bar, bar + 64, base_s};
+}
+
+__device__ __forceinline__ void grid_sync(const GridBar& gb, unsigned ordinal) {
+  const unsigned epoch = gb.base + ordinal;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(gb.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0) {
+    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+      while (__hip_atomic_load(gb.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(gb.rel, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (threadIdx.x == 0) {
+    while (__hip_atomic_load(gb.rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+      __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // stage 1: per-slab partial sums -> part[slab][2][C]
 // ---------------------------------------------------------------------------
-template <int MODE>  // 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
-__global__ __launch_bounds__(BN_T) void bn_partials(
+// one (channel block cbk, row slab) tile; `red` = 2*BN_T*VEC floats of LDS
+template <int MODE, bool SC>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
+__device__ __forceinline__ void partials_tile(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
-    int64_t M, int C, int rows_per_slab, int act, Map mp) {
-  __shared__ float red[2 * BN_T * VEC];
+    int64_t M, int C, int rows_per_slab, int act, const Map& mp, int cbk, int slab, float* red) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  const int c0 = cbk * mp.cb + tc * VEC;
   const bool cok = c0 < C;
   float s[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, q[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[VEC], is[VEC];
@@ -96,7 +162,7 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
       is[i] = invstd[c0 + i];
     }
   }
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   // PU rows in flight per thread: loads of all rows issue before any use
   // (narrow layers / small batches leave few waves per CU to hide latency)
@@ -146,32 +212,44 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
   }
   __syncthreads();
   for (int cl = threadIdx.x; cl < mp.cb; cl += BN_T) {
-    const int c = blockIdx.x * mp.cb + cl;
+    const int c = cbk * mp.cb + cl;
     if (c >= C) continue;
     float a = 0.f, b = 0.f;
     for (int k = 0; k < mp.tr_n; ++k) {
       a += rs[k * mp.cb + cl];
       b += rq[k * mp.cb + cl];
     }
-    float* dst = part + (int64_t)blockIdx.y * 2 * C;
-    dst[c] = a;
-    dst[C + c] = b;
+    float* dst = part + (int64_t)slab * 2 * C;
+    stf<SC>(dst + c, a);
+    stf<SC>(dst + C + c, b);
   }
+  __syncthreads();  // `red` is reused by the next tile of a cooperative block
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BN_T) void bn_partials(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
+    int64_t M, int C, int rows_per_slab, int act, Map mp) {
+  __shared__ float red[2 * BN_T * VEC];
+  partials_tile<MODE, false>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+                             blockIdx.x, blockIdx.y, red);
 }
 
 // ---------------------------------------------------------------------------
 // stage 2: finalize
 // ---------------------------------------------------------------------------
-// one block = 8 channels x 32 slab lanes; each lane keeps 8 slab loads in
+// one task = 8 channels x 32 slab lanes; each lane keeps 8 slab loads in
 // flight (the partials were just written by other CUs: every round trip is an
 // L2/MALL miss, so the reduction is latency-bound), LDS tree
 constexpr int FIN_C = 8, FIN_L = 32, FIN_U = 8;
 
+template <bool SC>
 __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int slabs, int C,
-                                          float* a_out, float* b_out) {
+                                          int task, float* a_out, float* b_out) {
   __shared__ float sa[FIN_L][FIN_C], sb[FIN_L][FIN_C];
   const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
-  const int c = blockIdx.x * FIN_C + cl;
+  const int c = task * FIN_C + cl;
   float a = 0.f, b = 0.f;
   if (c < C) {
     float au[FIN_U], bu[FIN_U];
@@ -181,16 +259,16 @@ __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int sl
     for (; k + (FIN_U - 1) * FIN_L < slabs; k += FIN_U * FIN_L) {
 #pragma unroll
       for (int u = 0; u < FIN_U; ++u) {
-        au[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + c];
-        bu[u] += part[(int64_t)(k + u * FIN_L) * 2 * C + C + c];
+        au[u] += ldf<SC>(part + (int64_t)(k + u * FIN_L) * 2 * C + c);
+        bu[u] += ldf<SC>(part + (int64_t)(k + u * FIN_L) * 2 * C + C + c);
       }
     }
 #pragma unroll
     for (int u = 0; u < FIN_U; ++u) {
       const int kk = k + u * FIN_L;
       if (kk < slabs) {
-        au[u] += part[(int64_t)kk * 2 * C + c];
-        bu[u] += part[(int64_t)kk * 2 * C + C + c];
+        au[u] += ldf<SC>(part + (int64_t)kk * 2 * C + c);
+        bu[u] += ldf<SC>(part + (int64_t)kk * 2 * C + C + c);
       }
     }
 #pragma unroll
@@ -209,24 +287,28 @@ __device__ __forceinline__ void sum_slabs(const float* __restrict__ part, int sl
       b += sb[k][cl];
     }
   }
+  __syncthreads();  // sa/sb are reused by the next task of a cooperative block
   *a_out = a;
   *b_out = b;
 }
 
-__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_fwd(
+// partials from an earlier kernel (plain loads); ws written for the apply
+// stage (SC: read by other blocks of the same kernel)
+template <bool SC>
+__device__ __forceinline__ void finalize_fwd_task(
     const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
     float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, int64_t M, int C,
-    int Cper, float eps, float momentum) {
+    int Cper, float eps, float momentum, int task) {
   float a, b;
-  sum_slabs(part, slabs, C, &a, &b);
-  const int c = blockIdx.x * FIN_C + threadIdx.x;
+  sum_slabs<false>(part, slabs, C, task, &a, &b);
+  const int c = task * FIN_C + threadIdx.x;
   if (threadIdx.x >= FIN_C || c >= C) return;
   const float inv_m = 1.f / (float)M;
   const float mu = a * inv_m;
   const float var = fmaxf(b * inv_m - mu * mu, 0.f);
   const float is = rsqrtf(var + eps);
-  ws[c] = mu;
-  ws[C + c] = is;
+  stf<SC>(ws + c, mu);
+  stf<SC>(ws + C + c, is);
   mean_out[c] = mu;
   invstd_out[c] = is;
   const int g = c / Cper, cc = c - g * Cper;
@@ -237,32 +319,49 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_fwd(
   *rv = (1.f - momentum) * *rv + momentum * unb;
 }
 
-__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
-    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* dgamma,
-    float* dbeta, int64_t gstride, int C, int Cper) {
+template <bool SC>
+__device__ __forceinline__ void finalize_bwd_task(const float* __restrict__ part, int slabs,
+                                                  float* __restrict__ ws, float* dgamma,
+                                                  float* dbeta, int64_t gstride, int C, int Cper,
+                                                  int task) {
   float a, b;
-  sum_slabs(part, slabs, C, &a, &b);
-  const int c = blockIdx.x * FIN_C + threadIdx.x;
+  sum_slabs<SC>(part, slabs, C, task, &a, &b);
+  const int c = task * FIN_C + threadIdx.x;
   if (threadIdx.x >= FIN_C || c >= C) return;
-  ws[c] = a;
-  ws[C + c] = b;
+  stf<SC>(ws + c, a);
+  stf<SC>(ws + C + c, b);
   const int g = c / Cper, cc = c - g * Cper;
   dgamma[g * gstride + cc] = b;
   dbeta[g * gstride + cc] = a;
+}
+
+__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_fwd(
+    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
+    float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, int64_t M, int C,
+    int Cper, float eps, float momentum) {
+  finalize_fwd_task<false>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
+                           C, Cper, eps, momentum, blockIdx.x);
+}
+
+__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
+    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* dgamma,
+    float* dbeta, int64_t gstride, int C, int Cper) {
+  finalize_bwd_task<false>(part, slabs, ws, dgamma, dbeta, gstride, C, Cper, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
 // stage 3: elementwise apply (scale/shift per channel computed once per thread)
 // ---------------------------------------------------------------------------
 // MODE 0: train fwd, ws = (mean, invstd); MODE 1: eval fwd from running stats
-template <int MODE>
-__global__ __launch_bounds__(BN_T) void bn_apply_fwd(
+template <int MODE, bool SC>
+__device__ __forceinline__ void apply_fwd_tile(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
-    const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
-    Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+    const float* __restrict__ rvar, int64_t rstat_stride, float eps, const Strided& gamma,
+    const Strided& beta, int64_t M, int C, int Cper, int rows_per_slab, int act, const Map& mp,
+    int cbk, int slab) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   float ga[VEC], be[VEC], sc[VEC], sh[VEC];
@@ -272,8 +371,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
   for (int i = 0; i < VEC; ++i) {
     float mu, is;
     if (MODE == 0) {
-      mu = ws[c0 + i];
-      is = ws[C + c0 + i];
+      mu = ldf<SC>(ws + c0 + i);
+      is = ldf<SC>(ws + C + c0 + i);
     } else {
       mu = rmean[g * rstat_stride + cc + i];
       is = rsqrtf(rvar[g * rstat_stride + cc + i] + eps);
@@ -281,7 +380,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
     sc[i] = is * ga[i];
     sh[i] = be[i] - mu * sc[i];
   }
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;     // rows in flight per thread
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -307,13 +406,24 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
   }
 }
 
-__global__ __launch_bounds__(BN_T) void bn_apply_bwd(
+template <int MODE>
+__global__ __launch_bounds__(BN_T) void bn_apply_fwd(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    const float* __restrict__ ws, const float* __restrict__ rmean,
+    const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
+    Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+  apply_fwd_tile<MODE, false>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
+                              Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
+}
+
+template <bool SC>
+__device__ __forceinline__ void apply_bwd_tile(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
-    Strided gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
-    int Cper, int rows_per_slab, int act, Map mp) {
+    const Strided& gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
+    int Cper, int rows_per_slab, int act, const Map& mp, int cbk, int slab) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC];
@@ -324,10 +434,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
     mu[i] = mean[c0 + i];
     is[i] = invstd[c0 + i];
     k1[i] = ga[i] * is[i];
-    k2[i] = ws[C + c0 + i] * inv_m;
-    sdz[i] = ws[c0 + i] * inv_m;
+    k2[i] = ldf<SC>(ws + C + c0 + i) * inv_m;
+    sdz[i] = ldf<SC>(ws + c0 + i) * inv_m;
   }
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;     // rows in flight per thread
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -358,11 +468,130 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
   }
 }
 
+__global__ __launch_bounds__(BN_T) void bn_apply_bwd(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
+    Strided gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
+    int Cper, int rows_per_slab, int act, Map mp) {
+  apply_bwd_tile<false>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
+                        act, mp, blockIdx.x, blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------
+// cooperative single-launch BN (one kernel per layer and direction)
+// ---------------------------------------------------------------------------
+// A one-config ResNet-50 step is launch-bound: ~470 kernels at 5-20 us each,
+// a third of them BN stages over a few hundred KB.  These kernels run the
+// stages of one layer in ONE launch on a co-resident grid, separated by
+// grid_sync: forward = finalize -> apply (2 launches -> 1), backward =
+// partials -> finalize -> apply (3 -> 1).  Blocks grid-stride over the same
+// (channel block, row slab) tiles in every stage, so the backward apply
+// re-reads the rows its own block reduced (L2-warm).
+__global__ __launch_bounds__(BN_T) void bn_fwd_coop(
+    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
+    float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, float eps,
+    float momentum, const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+    bf16_t* __restrict__ y, Strided gamma, Strided beta, int64_t M, int C, int Cper,
+    int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
+  const GridBar gb = grid_bar_open(bar);
+  const int fin_tasks = (C + FIN_C - 1) / FIN_C;
+  for (int t = blockIdx.x; t < fin_tasks; t += gridDim.x)
+    finalize_fwd_task<true>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
+                            C, Cper, eps, momentum, t);
+  grid_sync(gb, 1);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
+    apply_fwd_tile<0, true>(x, res, y, ws, nullptr, nullptr, 0, 0.f, gamma, beta, M, C, Cper,
+                            rows_per_slab, act, mp, t % cblocks, t / cblocks);
+}
+
+__global__ __launch_bounds__(BN_T) void bn_bwd_coop(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
+    float* dgamma, float* dbeta, int64_t gstride, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dres, float* __restrict__ ws, float* __restrict__ part, int64_t M, int C,
+    int Cper, int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
+  __shared__ float red[2 * BN_T * VEC];
+  const GridBar gb = grid_bar_open(bar);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
+    partials_tile<1, true>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+                           t % cblocks, t / cblocks, red);
+  grid_sync(gb, 1);
+  const int fin_tasks = (C + FIN_C - 1) / FIN_C;
+  const int slabs = (ntiles + cblocks - 1) / cblocks;
+  for (int t = blockIdx.x; t < fin_tasks; t += gridDim.x)
+    finalize_bwd_task<true>(part, slabs, ws, dgamma, dbeta, gstride, C, Cper, t);
+  grid_sync(gb, 2);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
+    apply_bwd_tile<true>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
+                         act, mp, t % cblocks, t / cblocks);
+}
+
 // ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
 constexpr int RED_TARGET = 512, RED_MIN_ROWS = 64;
 constexpr int APPLY_TARGET = 2048, APPLY_MIN_ROWS = 16;
+
+// cooperative path (bn_fwd_coop / bn_bwd_coop): off unless CER_BN_COOP=1 /
+// cer_bn_set_coop(1); the grid never exceeds the blocks the device can hold
+// at once (occupancy x CUs), which is what makes grid_sync safe.  Measured on
+// MI355X (profiles/r1_ab_bn_coop.md) it is SLOWER than the staged kernels:
+// the cross-XCD barrier round trips (~5 us) cost more than the launches they
+// remove, and a co-resident grid hides less latency than a 2048-block apply.
+static int g_coop = -1;
+constexpr int COOP_SLOTS = 16;               // barrier slots, rotated per launch
+constexpr int COOP_MAX_GRID = 1024;          // arrival flags per slot
+constexpr int COOP_SLOT_WORDS = 64 + COOP_MAX_GRID;
+__device__ unsigned g_coop_bar[COOP_SLOTS * COOP_SLOT_WORDS];
+
+CER_API void cer_bn_set_coop(int on) { g_coop = on; }
+
+static bool coop_on() {
+  if (g_coop < 0) {
+    const char* e = getenv("CER_BN_COOP");
+    g_coop = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_coop == 1;
+}
+
+// resident-block capacity of `kern` on the current device (cached per device)
+template <typename K>
+static int coop_capacity(K kern, int* cache) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BN_T, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      per_cu = cus = 0;
+    cache[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
+  }
+  return cache[dev] > 0 ? cache[dev] : 0;
+}
+
+static unsigned* coop_bar() {
+  static int slot = 0;
+  unsigned* base = nullptr;
+  if (hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_coop_bar)) != hipSuccess) return nullptr;
+  slot = (slot + 1) % COOP_SLOTS;
+  return base + slot * COOP_SLOT_WORDS;
+}
+
+// grid of a cooperative launch: one block per tile up to 4 per CU, never
+// more than the device can keep resident
+static int coop_grid(int ntiles, int capacity, int cus_x2) {
+  int g = ntiles < cus_x2 ? ntiles : cus_x2;
+  if (g > COOP_MAX_GRID) g = COOP_MAX_GRID;
+  return g <= capacity ? g : capacity;
+}
+
+static int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cache[dev]) hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev);
+  return cache[dev];
+}
 
 // floats of scratch the partials need (part[slabs][2][C])
 CER_API int64_t cer_bn_part_floats(int64_t M, int C) {
@@ -389,6 +618,24 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
                                             rrows, 0, mp);
     nslab = (int)rg.y;
+  }
+  if (coop_on()) {
+    static int cap_cache[64] = {0};
+    const int cap = coop_capacity(bn_fwd_coop, cap_cache);
+    unsigned* bar = coop_bar();
+    dim3 cg;
+    int crows;
+    make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &cg, &crows);
+    const int ntiles = (int)(cg.x * cg.y);
+    const int grid = coop_grid(ntiles, cap, 4 * device_cus());
+    if (grid > 0 && bar) {
+      bn_fwd_coop<<<grid, BN_T, 0, stream>>>(part, nslab, ws, mean_out, invstd_out, rmean, rvar,
+                                             rstat_stride, eps, momentum, x, res, y,
+                                             Strided{gamma, gamma_stride},
+                                             Strided{beta, beta_stride}, M, C, Cper, crows,
+                                             (int)cg.x, ntiles, act, mp, bar);
+      return (int)hipGetLastError();
+    }
   }
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
@@ -466,6 +713,20 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   int rrows, arows;
   make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
+  if (coop_on()) {
+    // same (channel block, slab) tiling as bn_partials: part has room for it
+    static int cap_cache[64] = {0};
+    const int cap = coop_capacity(bn_bwd_coop, cap_cache);
+    unsigned* bar = coop_bar();
+    const int ntiles = (int)(rg.x * rg.y);
+    const int grid = coop_grid(ntiles, cap, 4 * device_cus());
+    if (grid > 0 && bar) {
+      bn_bwd_coop<<<grid, BN_T, 0, stream>>>(dy, x, y, mean, invstd, Strided{gamma, gamma_stride},
+                                             dgamma, dbeta, grad_stride, dx, dres, ws, part, M, C,
+                                             Cper, rrows, (int)rg.x, ntiles, act, mp, bar);
+      return (int)hipGetLastError();
+    }
+  }
   bn_partials<1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows, act, mp);
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);

@@ -393,3 +393,37 @@ def test_conv_bn_fused_finalize_matches_oracle(case, monkeypatch):
     monkeypatch.setattr(_hip, "_FUSED_FINALIZE", True)
     test_conv_bn_fused_matches_oracle(case, -1)
     test_conv_bn_fused_matches_oracle(case, 4)
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (True, True), (6, False)])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64), (2, 7, 7, 3 * 256), (32, 28, 28, 256),
+                                   (32, 4, 4, 8 * 2048), (3, 5, 7, 48)])
+def test_bn_coop_bitwise_equals_staged(act, res, shape):
+    """Cooperative one-launch BN (grid_sync between stages) == the staged
+    partials / finalize / apply kernels, bit for bit (same reduction tiling)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    G = 1 if shape[-1] % 2 else 2
+    C = shape[-1] // G
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    torch.manual_seed(7)
+    x = (2 * torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16)
+    r = torch.randn(shape, device="cuda").to(torch.bfloat16) if res else None
+    gy = torch.randn(shape, device="cuda").to(torch.bfloat16)
+    outs = []
+    try:
+        for coop in (1, 0):
+            _hip.lib().cer_bn_set_coop(coop)
+            a, refs = _make(specs, G, seed=5)
+            xx = x.clone().requires_grad_(True)
+            rr = r.clone().requires_grad_(True) if res else None
+            y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
+                         a.master.clone()))
+    finally:
+        _hip.lib().cer_bn_set_coop(0)
+    for u, v in zip(*outs):
+        if u is not None:
+            assert torch.equal(u, v)
