@@ -8,13 +8,15 @@ into one horizontally-fused model on a GPU (``pack_key``).
 The reference's ``"inceptionresnetv2"`` name silently builds VGG19
 (``in_rdbms_helper.py:314-321``); it is kept as an alias of ``vgg19`` so
 grids naming it train what the reference actually trained.
-``nasnetmobile`` = ``keras.applications.NASNetMobile`` (``models/nasnet.py``).
+``nasnetmobile`` = ``keras.applications.NASNetMobile`` (``models/nasnet.py``);
+``squeezenet`` / ``densenet_tf1`` = the raw-TF1 zoo (``models/tf1zoo.py``).
 """
 
 from .mlp import PackedConfA, PackedSanity
 from .nasnet import PackedNASNetMobile
 from .resnet import PackedResNet
 from .small import PackedMobileNetV2, PackedTinyCNN
+from .tf1zoo import PackedDenseNetTF1, PackedSqueezeNet
 from .vgg import PackedVGG16, PackedVGG19
 from .zoo import PackedDenseNet, PackedMobileNetV1, PackedResNeXt, PackedResNet50NoBN
 
@@ -34,6 +36,8 @@ MODEL_FACTORIES = {
     "mobilenetv1": lambda: PackedMobileNetV1(),
     "mobilenetv2": lambda: PackedMobileNetV2(),
     "nasnetmobile": lambda: PackedNASNetMobile(),
+    "squeezenet": lambda: PackedSqueezeNet(),
+    "densenet_tf1": lambda: PackedDenseNetTF1(),
     "confA": lambda: PackedConfA(),
     "sanity": lambda: PackedSanity(),
     "tinycnn": lambda: PackedTinyCNN(),

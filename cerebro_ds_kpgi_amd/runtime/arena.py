@@ -117,6 +117,9 @@ def init_row(layout, master_row, seed):
                 t[bad] = torch.empty(nb, device=dev).normal_(0.0, 1.0, generator=g)
             view.copy_(t * std)
             continue
+        if isinstance(s.init, str) and s.init.startswith("const"):
+            view.fill_(float(s.init[5:]))      # e.g. TF constant_initializer(0.1) biases
+            continue
         if s.kind in ("weight",):
             fan_in = s.fan_in if s.fan_in else int(np.prod(s.shape[1:]))
             if s.init == "he":

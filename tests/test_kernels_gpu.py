@@ -126,7 +126,8 @@ def test_engine_one_round_on_gpu():
 @pytest.mark.parametrize("model,bs", [("confA", 32), ("mobilenetv2", 8), ("mobilenetv1", 8),
                                       ("vgg16", 8), ("densenet121", 8), ("resnext101", 4),
                                       ("resnet50_nobn", 8), ("resnet18", 8),
-                                      ("nasnetmobile", 4)])
+                                      ("nasnetmobile", 4), ("squeezenet", 8),
+                                      ("densenet_tf1", 4)])
 def test_engine_trains_model_family(model, bs):
     """Every model family steps through the HIP engine (graph capture included)."""
     from cerebro_ds_kpgi_amd.parallel import init_distributed

@@ -24,6 +24,8 @@ COUNTS = {
     "densenet201": (20013928, 229056),
     "resnext101": (44177704, 137856),     # ResNeXt-101 32x4d
     "resnet50_nobn": (25530472, 0),       # Keras ResNet-50 minus BN (resnet50tfk.py)
+    "squeezenet": (1235496, 0),           # SqueezeNet 1.1 layout of models/cnn/tf/squeezenet.py
+    "densenet_tf1": (7040440, 0),         # models/cnn/tf/densenet.py (k=24, no BN, no conv bias)
     "confA": (7306 * 1000 + 1000 + 1000 * 500 + 500 + 500 * 2 + 2, 0),
 }
 
@@ -39,7 +41,8 @@ def test_parameter_counts(name):
 
 
 @pytest.mark.parametrize("name", ["vgg19", "mobilenetv1", "densenet121", "resnext101",
-                                  "resnet50_nobn", "nasnetmobile"])
+                                  "resnet50_nobn", "nasnetmobile", "squeezenet",
+                                  "densenet_tf1"])
 def test_packed_forward_backward(name):
     from cerebro_ds_kpgi_amd.models import create_model_from_mst
     from cerebro_ds_kpgi_amd.ops import set_backend
