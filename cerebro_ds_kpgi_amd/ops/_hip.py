@@ -148,6 +148,7 @@ _SIGS.update({
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_bn_set_coop": [c_i],
+    "cer_bn_set_zmask": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                            c_p, c_i, c_i, c_p, c_p, c_p],
@@ -171,7 +172,8 @@ _SIGS.update({
                          c_p, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
     "cer_bn_fwd_eval": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i, c_i,
                         c_f, c_i, c_p],
-    "cer_bn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p, c_p,
+    "cer_bn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
+                   c_p, c_p,
                    c_i64, c_i, c_i, c_i, c_p],
     "cer_maxpool_fwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_maxpool_bwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
@@ -632,10 +634,11 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res):
     ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
     part = _bn_part(M, C, x.device)
     gp, gs = gref.work_ptr()
+    bp, bs = bref.work_ptr()
     dgp, dgs = gref.grad_ptr()
     dbp, _ = bref.grad_ptr()
     rc = lib().cer_bn_bwd(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
-                          c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
+                          c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
                           M, C, Cper, _act_code(act), _stream())
     _check(rc, "cer_bn_bwd")
     return dx, dres

@@ -12,7 +12,12 @@
 // finalize (mean, invstd, running stats) -> apply y = act(xhat*g + b + res).
 // Backward: partials (sum dz, sum dz*xhat) -> finalize (dgamma, dbeta into the
 // fp32 gradient arena) -> apply dx = g*invstd*(dz - mean dz - xhat mean(dz xhat)),
-// dres = dz.
+// dres = dz.  dz = act'(.) * dy takes the activation mask from (YM):
+//   YM_NONE  no activation: y is never read,
+//   YM_Y     y (ReLU6, or a residual join: y = act(xhat*g + b + res)),
+//   YM_Z     a plain ReLU without residual: mask = (x*sc + sh > 0), recomputed
+//            from the BN input with the forward's exact scale/shift, so the
+//            backward reads two tensors per pass (dy, x) instead of three.
 #include "common.h"
 
 #include <stdlib.h>
@@ -144,22 +149,52 @@ __device__ __forceinline__ void grid_sync(const GridBar& gb, unsigned ordinal) {
 // ---------------------------------------------------------------------------
 // stage 1: per-slab partial sums -> part[slab][2][C]
 // ---------------------------------------------------------------------------
+constexpr int YM_NONE = 0, YM_Y = 1, YM_Z = 2;
+
+// forward scale / shift of 8 channels (bitwise the apply_fwd_tile values)
+__device__ __forceinline__ void bn_scale_shift(const Strided& gamma, const Strided& beta, int g,
+                                               int cc, const float* mu, const float* is,
+                                               float* sc, float* sh) {
+  float ga[VEC], be[VEC];
+  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
+  load8((const bf16_t*)beta.p + g * beta.stride + cc, be);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    sc[i] = is[i] * ga[i];
+    sh[i] = be[i] - mu[i] * sc[i];
+  }
+}
+
+// activation gradient of one element under mask mode YM
+template <int YM>
+__device__ __forceinline__ float dz_of(float d, float yv, float xv, float sc, float sh, int act) {
+  if (YM == YM_NONE) return d;
+  if (YM == YM_Z) return (xv * sc + sh + 0.f) > 0.f ? d : 0.f;
+  return act_bwd(d, yv, act);
+}
+
 // one (channel block cbk, row slab) tile; `red` = 2*BN_T*VEC floats of LDS
-template <int MODE, bool SC>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
+template <int MODE, bool SC, int YM = YM_Y>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
 __device__ __forceinline__ void partials_tile(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
-    int64_t M, int C, int rows_per_slab, int act, const Map& mp, int cbk, int slab, float* red) {
+    int64_t M, int C, int rows_per_slab, int act, const Map& mp, int cbk, int slab, float* red,
+    const Strided& gamma = Strided{nullptr, 0}, const Strided& beta = Strided{nullptr, 0},
+    int Cper = 1) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   const bool cok = c0 < C;
   float s[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, q[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float mu[VEC], is[VEC];
+  float mu[VEC], is[VEC], sc[VEC], sh[VEC];
   if (MODE == 1 && cok) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       mu[i] = mean[c0 + i];
       is[i] = invstd[c0 + i];
+    }
+    if (YM == YM_Z) {
+      const int g = c0 / Cper;
+      bn_scale_shift(gamma, beta, g, c0 - g * Cper, mu, is, sc, sh);
     }
   }
   const int64_t r0 = (int64_t)slab * rows_per_slab;
@@ -179,7 +214,7 @@ __device__ __forceinline__ void partials_tile(
           load8(x + rr * C + c0, v[u]);
           if (MODE == 1) {
             load8(dy + rr * C + c0, d[u]);
-            load8(y + rr * C + c0, yv[u]);
+            if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
           }
         }
       }
@@ -195,7 +230,7 @@ __device__ __forceinline__ void partials_tile(
         } else {
 #pragma unroll
           for (int i = 0; i < VEC; ++i) {
-            const float dz = act_bwd(d[u][i], yv[u][i], act);
+            const float dz = dz_of<YM>(d[u][i], yv[u][i], v[u][i], sc[i], sh[i], act);
             s[i] += dz;
             q[i] += dz * (v[u][i] - mu[i]) * is[i];
           }
@@ -226,14 +261,15 @@ __device__ __forceinline__ void partials_tile(
   __syncthreads();  // `red` is reused by the next tile of a cooperative block
 }
 
-template <int MODE>
+template <int MODE, int YM = YM_Y>
 __global__ __launch_bounds__(BN_T) void bn_partials(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
-    int64_t M, int C, int rows_per_slab, int act, Map mp) {
+    int64_t M, int C, int rows_per_slab, int act, Map mp, Strided gamma = Strided{nullptr, 0},
+    Strided beta = Strided{nullptr, 0}, int Cper = 1) {
   __shared__ float red[2 * BN_T * VEC];
-  partials_tile<MODE, false>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
-                             blockIdx.x, blockIdx.y, red);
+  partials_tile<MODE, false, YM>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+                                 blockIdx.x, blockIdx.y, red, gamma, beta, Cper);
 }
 
 // ---------------------------------------------------------------------------
@@ -364,22 +400,18 @@ __device__ __forceinline__ void apply_fwd_tile(
   const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
-  float ga[VEC], be[VEC], sc[VEC], sh[VEC];
-  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
-  load8((const bf16_t*)beta.p + g * beta.stride + cc, be);
+  float mu[VEC], is[VEC], sc[VEC], sh[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
-    float mu, is;
     if (MODE == 0) {
-      mu = ldf<SC>(ws + c0 + i);
-      is = ldf<SC>(ws + C + c0 + i);
+      mu[i] = ldf<SC>(ws + c0 + i);
+      is[i] = ldf<SC>(ws + C + c0 + i);
     } else {
-      mu = rmean[g * rstat_stride + cc + i];
-      is = rsqrtf(rvar[g * rstat_stride + cc + i] + eps);
+      mu[i] = rmean[g * rstat_stride + cc + i];
+      is[i] = rsqrtf(rvar[g * rstat_stride + cc + i] + eps);
     }
-    sc[i] = is * ga[i];
-    sh[i] = be[i] - mu * sc[i];
   }
+  bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;     // rows in flight per thread
@@ -416,17 +448,18 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
                               Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
 }
 
-template <bool SC>
+template <bool SC, int YM = YM_Y>
 __device__ __forceinline__ void apply_bwd_tile(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
     const Strided& gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
-    int Cper, int rows_per_slab, int act, const Map& mp, int cbk, int slab) {
+    int Cper, int rows_per_slab, int act, const Map& mp, int cbk, int slab,
+    const Strided& beta = Strided{nullptr, 0}) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
-  float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC];
+  float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
   load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
   const float inv_m = 1.f / (float)M;
 #pragma unroll
@@ -437,6 +470,7 @@ __device__ __forceinline__ void apply_bwd_tile(
     k2[i] = ldf<SC>(ws + C + c0 + i) * inv_m;
     sdz[i] = ldf<SC>(ws + c0 + i) * inv_m;
   }
+  if (YM == YM_Z) bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;     // rows in flight per thread
@@ -448,7 +482,7 @@ __device__ __forceinline__ void apply_bwd_tile(
       if (rr < r1) {
         load8(dy + rr * C + c0, d[u]);
         load8(x + rr * C + c0, xv[u]);
-        load8(y + rr * C + c0, yv[u]);
+        if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
       }
     }
 #pragma unroll
@@ -458,7 +492,7 @@ __device__ __forceinline__ void apply_bwd_tile(
       float o[VEC], dz[VEC];
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        dz[i] = act_bwd(d[u][i], yv[u][i], act);
+        dz[i] = dz_of<YM>(d[u][i], yv[u][i], xv[u][i], sc[i], sh[i], act);
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
@@ -468,13 +502,14 @@ __device__ __forceinline__ void apply_bwd_tile(
   }
 }
 
+template <int YM>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
     Strided gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
-    int Cper, int rows_per_slab, int act, Map mp) {
-  apply_bwd_tile<false>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
-                        act, mp, blockIdx.x, blockIdx.y);
+    int Cper, int rows_per_slab, int act, Map mp, Strided beta) {
+  apply_bwd_tile<false, YM>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
+                            rows_per_slab, act, mp, blockIdx.x, blockIdx.y, beta);
 }
 
 // ---------------------------------------------------------------------------
@@ -545,6 +580,10 @@ constexpr int COOP_SLOT_WORDS = 64 + COOP_MAX_GRID;
 __device__ unsigned g_coop_bar[COOP_SLOTS * COOP_SLOT_WORDS];
 
 CER_API void cer_bn_set_coop(int on) { g_coop = on; }
+
+// ReLU mask recomputed from the BN input in backward (YM_Z); 0 = always read y
+static int g_zmask = 1;
+CER_API void cer_bn_set_zmask(int on) { g_zmask = on; }
 
 static bool coop_on() {
   if (g_coop < 0) {
@@ -704,9 +743,9 @@ CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
 
 CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
                        const float* invstd, const bf16_t* gamma, int64_t gamma_stride,
-                       float* dgamma, float* dbeta, int64_t grad_stride, bf16_t* dx,
-                       bf16_t* dres, float* ws, float* part, int64_t M, int C, int Cper, int act,
-                       hipStream_t stream) {
+                       const bf16_t* beta, int64_t beta_stride, float* dgamma, float* dbeta,
+                       int64_t grad_stride, bf16_t* dx, bf16_t* dres, float* ws, float* part,
+                       int64_t M, int C, int Cper, int act, hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 rg, ag;
@@ -727,11 +766,29 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
       return (int)hipGetLastError();
     }
   }
-  bn_partials<1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows, act, mp);
+  // mask source: none / y / recomputed from x (see the header); a residual
+  // join's mask depends on the residual, so it needs y
+  const int ym = act == 0 ? YM_NONE : (act == 1 && !dres && g_zmask) ? YM_Z : YM_Y;
+  const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
+  if (ym == YM_NONE)
+    bn_partials<1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                     act, mp, gs, bs, Cper);
+  else if (ym == YM_Z)
+    bn_partials<1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                  act, mp, gs, bs, Cper);
+  else
+    bn_partials<1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                  act, mp, gs, bs, Cper);
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
-  bn_apply_bwd<<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws,
-                                        Strided{gamma, gamma_stride}, dx, dres, M, C, Cper, arows,
-                                        act, mp);
+  if (ym == YM_NONE)
+    bn_apply_bwd<YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+                                                   C, Cper, arows, act, mp, bs);
+  else if (ym == YM_Z)
+    bn_apply_bwd<YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                Cper, arows, act, mp, bs);
+  else
+    bn_apply_bwd<YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                Cper, arows, act, mp, bs);
   return (int)hipGetLastError();
 }

@@ -427,3 +427,35 @@ def test_bn_coop_bitwise_equals_staged(act, res, shape):
     for u, v in zip(*outs):
         if u is not None:
             assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("shape", [(4, 14, 14, 64), (32, 28, 28, 256), (2, 7, 7, 3 * 256)])
+def test_bn_bwd_mask_from_input_equals_mask_from_output(act, res, shape):
+    """Backward with the ReLU mask recomputed from the BN input (no y read)
+    == the y-masked backward, bit for bit."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    G = 3 if shape[-1] == 768 else 2
+    C = shape[-1] // G
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    torch.manual_seed(9)
+    x = (2 * torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16)
+    r = torch.randn(shape, device="cuda").to(torch.bfloat16) if res else None
+    gy = torch.randn(shape, device="cuda").to(torch.bfloat16)
+    outs = []
+    try:
+        for zm in (1, 0):
+            _hip.lib().cer_bn_set_zmask(zm)
+            a, refs = _make(specs, G, seed=5)
+            xx = x.clone().requires_grad_(True)
+            rr = r.clone().requires_grad_(True) if res else None
+            y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append((xx.grad, rr.grad if res else None, a.grad.clone()))
+    finally:
+        _hip.lib().cer_bn_set_zmask(1)
+    for u, v in zip(*outs):
+        if u is not None:
+            assert torch.equal(u, v)
