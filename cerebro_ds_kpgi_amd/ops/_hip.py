@@ -148,6 +148,10 @@ _SIGS.update({
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_bn_set_coop": [c_i],
+    "cer_wgrad_batch_add": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                            c_p, c_i64],
+    "cer_wgrad_batch_flush": [c_i, c_i, c_p],
+    "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
@@ -528,6 +532,14 @@ def conv_set_variant(op, v):
 
 def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref):
     gp, gs = wref.grad_ptr()
+    if streams.batching():
+        splits = lib().cer_wgrad_batch_add(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh,
+                                           kw, stride, pad, c_p(gp), gs)
+        if splits > 0:
+            if splits > 1 and not wref.arena.grad_clean:
+                wref.grad().zero_()
+            streams.hold(x, dy)
+            return
 
     def launch():
         L = lib()

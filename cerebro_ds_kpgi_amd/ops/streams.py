@@ -1,4 +1,13 @@
-"""Weight-gradient overlap: wgrad kernels on a side HIP stream.
+"""Weight-gradient scheduling: batched (deferred) wgrads, optional side stream.
+
+Batched wgrads (default on, ``CER_WGRAD_BATCH=0`` disables): inside
+``deferred_wgrad()`` (the engine's training step) a layer's weight-gradient
+GEMM is only queued (``cer_wgrad_batch_add``); ``join`` — at the end of the
+context and before the optimizer — launches the queue as a few multi-layer
+kernels (``wgrad_batch`` in csrc/hip/conv.hip).  The operands stay referenced
+here until the flush.  Measured effect in profiles/.
+
+Side stream (``CER_WGRAD_STREAM=1``, default off):
 
 In backward, a layer's input gradient (dgrad) is on the critical path — the
 next layer down needs it — while its weight gradient (wgrad) is only needed
@@ -16,6 +25,7 @@ allocator does not hand their memory to the main stream while the wgrad may
 still read it.  ``CER_WGRAD_STREAM=0`` keeps everything on one stream.
 """
 
+import contextlib
 import os
 
 import torch
@@ -23,6 +33,50 @@ import torch
 _ON = os.environ.get("CER_WGRAD_STREAM", "0") == "1"
 _SIDE = {}
 _PENDING = set()
+
+_BATCH = os.environ.get("CER_WGRAD_BATCH", "1") != "0"
+_BATCH_VARIANT = int(os.environ.get("CER_WGB_VARIANT", "1"))   # reg 128x128 (A/B in profiles/)
+_DEFER = 0
+_HELD = []          # operands of queued wgrads (alive until the flush)
+
+
+def batching():
+    """True while wgrads are being queued (inside ``deferred_wgrad``)."""
+    return _DEFER > 0
+
+
+def hold(*tensors):
+    _HELD.extend(t for t in tensors if t is not None)
+
+
+def set_batch_variant(v):
+    global _BATCH_VARIANT
+    _BATCH_VARIANT = int(v)
+
+
+@contextlib.contextmanager
+def deferred_wgrad(enabled=True):
+    """Queue HIP weight gradients issued inside the block; flush them on exit."""
+    global _DEFER
+    on = enabled and _BATCH
+    if on:
+        _DEFER += 1
+    try:
+        yield
+    finally:
+        if on:
+            _DEFER -= 1
+            if _DEFER == 0:
+                flush_wgrad()
+
+
+def flush_wgrad(discard=False):
+    if not _HELD:
+        return
+    from . import _hip
+    rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 1 if discard else 0, _hip._stream())
+    del _HELD[:]
+    _hip._check(rc, "cer_wgrad_batch_flush")
 
 
 def enabled():
@@ -62,7 +116,9 @@ def run_side(fn, *tensors):
 
 
 def join():
-    """Current stream waits for every side-stream launch issued so far."""
+    """Launch queued wgrads; current stream waits for every side-stream launch."""
+    if _HELD and not _DEFER:
+        flush_wgrad()
     if not _PENDING:
         return
     cur = torch.cuda.current_stream()

@@ -149,9 +149,12 @@ class _Working(object):
     def _step(self):
         g = self.group
         gather_batch(g.store, True, self.part_of_row, self.cursor, g.batch_size, self.x, self.y)
-        logits = self.net.forward(self.x, True)
-        loss = softmax_ce(logits, self.y, self.acc, self.G)
-        loss.sum().backward()
+        # weight gradients are queued during backward and launched as a few
+        # multi-layer kernels when the block exits (ops.streams)
+        with streams.deferred_wgrad(self.x.device.type == "cuda"):
+            logits = self.net.forward(self.x, True)
+            loss = softmax_ce(logits, self.y, self.acc, self.G)
+            loss.sum().backward()
         streams.join()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)

@@ -28,6 +28,8 @@
 //    row decode uses magic-number division.
 #include "common.h"
 
+#include <stdlib.h>
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -703,17 +705,17 @@ __device__ __forceinline__ bf16x8 tn_frag(const bf16_t* tile, int row0, int col_
   return __builtin_bit_cast(bf16x8, t);
 }
 
+// register-staged wgrad tile body; `work` = this block's (config, split, tile)
+// index, `lds` = 2 * (BM + BN) * BK bf16
 template <int BM, int BN, int GM>
-__global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
+__device__ __forceinline__ void wgrad_reg_body(const WGParams& p, int work, bf16_t* lds) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;           // 16-B chunks per tile row
   constexpr int A_CH = BK * A_CPR / NTHREADS, B_CH = BK * B_CPR / NTHREADS;
   constexpr int A_RSTEP = NTHREADS / A_CPR, B_RSTEP = NTHREADS / B_CPR;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
 
   const int tiles_k = (p.K + BN - 1) / BN;
   const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
   const int cfg = work / (tiles * p.splits);
   const int rem = work - cfg * tiles * p.splits;
   const int split = rem / tiles, tile = rem - split * tiles;
@@ -838,6 +840,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
             *d = acc[i][j][e];
         }
       }
+}
+
+template <int BM, int BN, int GM>
+__global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad(WGParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
+  wgrad_reg_body<BM, BN, GM>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
 }
 
 
@@ -1243,16 +1251,15 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
 }
 
 // wgrad: dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]; requires Cin % 8 == 0, Cout % 8 == 0
+// LDS-DMA ring wgrad tile body; `lds` = S * (BM + BN) * BK bf16
 template <int BM, int BN, int S>
-__global__ __launch_bounds__(NTHREADS, 2) void pipe_wg(WGParams p) {
+__device__ __forceinline__ void wgrad_pipe_body(const WGParams& p, int work, bf16_t* lds) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;
   constexpr int AROWS = 512 / BM, AC16 = BM / 8, BROWS = 512 / BN, BC16 = BN / 8;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[S * STAGE];
 
   const int tiles_k = (p.K + BN - 1) / BN;
   const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
   const int cfg = work / (tiles * p.splits);
   const int rem = work - cfg * tiles * p.splits;
   const int split = rem / tiles, tile = rem - split * tiles;
@@ -1325,6 +1332,44 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_wg(WGParams p) {
             *d = acc[i][j][e];
         }
       }
+}
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(NTHREADS, 2) void pipe_wg(WGParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * (BM + BN) * BK];
+  wgrad_pipe_body<BM, BN, S>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
+}
+
+// ---------------------------------------------------------------------------
+// Batched weight gradients: the wgrads of up to WGB_MAX conv layers in ONE
+// launch.  Each layer's wgrad only feeds the optimizer, so the engine defers
+// them during backward (ops.streams) and flushes them together: one launch
+// instead of one per layer, and the small late-stage layers of a one-config
+// step (a few dozen tiles each) share the chip instead of running alone.
+// Block b (XCD-remapped) belongs to the layer whose [start, start + blocks)
+// range holds it; every layer splits its reduction into chunks of at most
+// `rows` GEMM rows so all blocks carry similar work.
+// ---------------------------------------------------------------------------
+constexpr int WGB_MAX = 20;
+struct WGBatch {
+  int n;
+  int start[WGB_MAX + 1];
+  WGParams p[WGB_MAX];
+};
+static_assert(sizeof(WGBatch) <= 4096, "WGBatch must fit the 4 KB kernel-argument segment");
+
+template <int BM, int BN, int KIND>  // KIND 0: register-staged, 1: LDS-DMA ring (2 stages)
+__global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch(WGBatch b) {
+  constexpr int LDSE = 2 * (BM + BN) * BK;   // both bodies use two stages
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDSE];
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int i = 0;
+  while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
+  const WGParams p = b.p[i];
+  if (KIND == 0)
+    wgrad_reg_body<BM, BN, GM_FWD>(p, work - b.start[i], lds);
+  else
+    wgrad_pipe_body<BM, BN, 2>(p, work - b.start[i], lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1695,6 +1740,86 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
   }
   return (int)hipGetLastError();
 }
+
+// ---- batched (deferred) weight gradients ----------------------------------
+static WGParams g_wgq[4096];
+static int g_wgq_G[4096];
+static int g_wgq_n = 0;
+static int g_wgb_rows = 0;
+
+static int wgb_rows() {
+  if (!g_wgb_rows) {
+    const char* e = getenv("CER_WGB_ROWS");
+    g_wgb_rows = e ? atoi(e) : 1024;
+    if (g_wgb_rows < BK) g_wgb_rows = BK;
+    g_wgb_rows = g_wgb_rows / BK * BK;
+  }
+  return g_wgb_rows;
+}
+
+// Queue one layer's wgrad for cer_wgrad_batch_flush.  Returns the split count
+// the batch will use (> 1: dw must be zero before the flush) or 0 when the
+// layer is not eligible (unaligned channels / >2 GB operands / queue full):
+// the caller then launches it on its own (cer_conv_wgrad).
+CER_API int cer_wgrad_batch_add(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw,
+                                int st, int pad, float* dw, int64_t dw_gstride) {
+  if (g_wgq_n >= 4096) return 0;
+  WGParams p;
+  p.x = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
+  p.dy = dy;
+  p.ldy = G * Cout;
+  p.dw = dw;
+  p.dw_gstride = dw_gstride;
+  p.Mred = B * Ho * Wo;
+  p.N = Cout;
+  p.K = kh * kw * Cin;
+  if (!wg_fast(Cin, Cout, p)) return 0;
+  const int rows = wgb_rows();
+  p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
+  p.splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
+  g_wgq_G[g_wgq_n] = G;     // folded into the block count at flush time
+  g_wgq[g_wgq_n++] = p;
+  return p.splits;
+}
+
+template <int BM, int BN, int KIND>
+static int wgb_launch(hipStream_t stream) {
+  for (int b0 = 0; b0 < g_wgq_n; b0 += WGB_MAX) {
+    WGBatch bt;
+    bt.n = g_wgq_n - b0 < WGB_MAX ? g_wgq_n - b0 : WGB_MAX;
+    int tot = 0;
+    for (int i = 0; i < bt.n; ++i) {
+      bt.p[i] = g_wgq[b0 + i];
+      bt.start[i] = tot;
+      tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq_G[b0 + i]);
+    }
+    bt.start[bt.n] = tot;
+    if (tot > 0) wgrad_batch<BM, BN, KIND><<<tot, NTHREADS, 0, stream>>>(bt);
+  }
+  return (int)hipGetLastError();
+}
+
+// Launch every queued wgrad (WGB_MAX layers per launch) with tile variant v
+// (0 reg 64x64, 1 reg 128x128, 2 reg 128x64, 3-5 the LDS-DMA ring twins) and
+// clear the queue.  `discard` != 0 only clears it.
+CER_API int cer_wgrad_batch_flush(int v, int discard, hipStream_t stream) {
+  int rc = 0;
+  if (!discard && g_wgq_n > 0) {
+    switch (v) {
+      case 1: rc = wgb_launch<128, 128, 0>(stream); break;
+      case 2: rc = wgb_launch<128, 64, 0>(stream); break;
+      case 3: rc = wgb_launch<64, 64, 1>(stream); break;
+      case 4: rc = wgb_launch<128, 128, 1>(stream); break;
+      case 5: rc = wgb_launch<128, 64, 1>(stream); break;
+      default: rc = wgb_launch<64, 64, 0>(stream); break;
+    }
+  }
+  g_wgq_n = 0;
+  return rc;
+}
+
+CER_API int cer_wgrad_batch_pending() { return g_wgq_n; }
 
 // the split count the host should use (and whether dw needs zeroing); the
 // variant is re-derived exactly as cer_conv_wgrad will (fast path assumed

@@ -459,3 +459,36 @@ def test_bn_bwd_mask_from_input_equals_mask_from_output(act, res, shape):
     for u, v in zip(*outs):
         if u is not None:
             assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_batched_wgrad_matches_per_layer(variant):
+    """Deferred multi-layer wgrad launch (wgrad_batch) == per-layer wgrads."""
+    from cerebro_ds_kpgi_amd.ops import streams
+    cases = [(2, 28, 28, 64, 64, 3, 1, 1), (2, 28, 28, 64, 256, 1, 1, 0),
+             (2, 14, 14, 256, 128, 1, 2, 0), (4, 7, 7, 256, 256, 3, 1, 1),
+             (4, 4, 4, 512, 512, 3, 1, 1), (2, 9, 11, 24, 40, 3, 2, 1)]
+    G = 2
+    specs = [ParamSpec("w{}".format(i), (co, k, k, ci), "weight", fan_in=k * k * ci)
+             for i, (_, _, _, ci, co, k, _, _) in enumerate(cases)]
+    torch.manual_seed(11)
+    xs = [torch.randn(B, H, W, G * ci, device="cuda").to(torch.bfloat16)
+          for (B, H, W, ci, _, _, _, _) in cases]
+    grads = []
+    old = streams._BATCH_VARIANT
+    try:
+        streams.set_batch_variant(variant)
+        for defer in (True, False):
+            a, refs = _make(specs, G)
+            a.grad.zero_()
+            with streams.deferred_wgrad(defer):
+                for i, (B, H, W, ci, co, k, s, p) in enumerate(cases):
+                    y = P.conv2d(xs[i].clone().requires_grad_(True), refs["w{}".format(i)], s, p)
+                    torch.manual_seed(20 + i)
+                    y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+            streams.join()
+            torch.cuda.synchronize()
+            grads.append(a.grad.clone())
+    finally:
+        streams.set_batch_variant(old)
+    assert _rel(grads[0], grads[1]) < 1e-3
