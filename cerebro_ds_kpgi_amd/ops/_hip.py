@@ -153,6 +153,7 @@ _SIGS.update({
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
+    "cer_bn_set_fold": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                            c_p, c_i, c_i, c_p, c_p, c_p],

@@ -513,6 +513,186 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
 }
 
 // ---------------------------------------------------------------------------
+// finalize folded into the apply (few slabs)
+// ---------------------------------------------------------------------------
+// When a layer has at most g_fold_max row slabs of partials (the small late
+// stages of a one-config step), every apply block reduces the partials of its
+// own channel block itself instead of waiting for a separate finalize launch:
+// one launch per layer and direction fewer, at the price of re-reading
+// nslab x 2 x (channels of the block) floats per block from L2.  All blocks
+// sum in the same order, so they agree bit for bit (the order differs from
+// bn_finalize_*; results match it to fp32 rounding).  Returns the block's
+// (a, b) sums for this thread's 8 channels.
+__device__ __forceinline__ void fold_partials(const float* __restrict__ part, int nslab, int C,
+                                              const Map& mp, int cbk, float* red, float* a8,
+                                              float* b8) {
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = cbk * mp.cb + tc * VEC;
+  float a[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, b[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c0 < C) {
+    for (int sl = tr; sl < nslab; sl += mp.tr_n) {
+      const float4* pa = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + c0);
+      const float4* pb = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + C + c0);
+      const float4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+      a[0] += a0.x; a[1] += a0.y; a[2] += a0.z; a[3] += a0.w;
+      a[4] += a1.x; a[5] += a1.y; a[6] += a1.z; a[7] += a1.w;
+      b[0] += b0.x; b[1] += b0.y; b[2] += b0.z; b[3] += b0.w;
+      b[4] += b1.x; b[5] += b1.y; b[6] += b1.z; b[7] += b1.w;
+    }
+  }
+  float* rs = red;
+  float* rq = red + BN_T * VEC;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    rs[tr * mp.cb + tc * VEC + i] = a[i];
+    rq[tr * mp.cb + tc * VEC + i] = b[i];
+  }
+  __syncthreads();
+  float* fin = red + 2 * BN_T * VEC;          // [2][cb]
+  for (int cl = threadIdx.x; cl < mp.cb; cl += BN_T) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k < mp.tr_n; ++k) {
+      sa += rs[k * mp.cb + cl];
+      sb += rq[k * mp.cb + cl];
+    }
+    fin[cl] = sa;
+    fin[mp.cb + cl] = sb;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    a8[i] = fin[tc * VEC + i];
+    b8[i] = fin[mp.cb + tc * VEC + i];
+  }
+}
+
+constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
+
+__global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
+    const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
+    float* rvar, int64_t rstat_stride, float eps, float momentum, const bf16_t* __restrict__ x,
+    const bf16_t* __restrict__ res, bf16_t* __restrict__ y, Strided gamma, Strided beta,
+    int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+  __shared__ float red[FOLD_LDS];
+  float a[VEC], b[VEC];
+  fold_partials(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  if (c0 >= C) return;
+  const float inv_m = 1.f / (float)M;
+  float mu[VEC], is[VEC], var[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    mu[i] = a[i] * inv_m;
+    var[i] = fmaxf(b[i] * inv_m - mu[i] * mu[i], 0.f);
+    is[i] = rsqrtf(var[i] + eps);
+  }
+  const int g = c0 / Cper, cc = c0 - g * Cper;
+  if (blockIdx.y == 0 && tr == 0) {          // one writer per channel
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mean_out[c0 + i] = mu[i];
+      invstd_out[c0 + i] = is[i];
+      float* rm = rmean + g * rstat_stride + cc + i;
+      float* rv = rvar + g * rstat_stride + cc + i;
+      const float unb = M > 1 ? var[i] * (float)M / (float)(M - 1) : var[i];
+      *rm = (1.f - momentum) * *rm + momentum * mu[i];
+      *rv = (1.f - momentum) * *rv + momentum * unb;
+    }
+  }
+  float sc[VEC], sh[VEC];
+  bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float v[AU][VEC], rv[AU][VEC];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        load8(x + rr * C + c0, v[u]);
+        if (res) load8(res + rr * C + c0, rv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr >= r1) continue;
+      float o[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i)
+        o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
+      store8(y + rr * C + c0, o);
+    }
+  }
+}
+
+template <int YM>
+__global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
+    const float* __restrict__ part, int nslab, float* dgamma, float* dbeta, int64_t gstride,
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
+    Strided beta, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C, int Cper,
+    int rows_per_slab, int act, Map mp) {
+  __shared__ float red[FOLD_LDS];
+  float a[VEC], b[VEC];
+  fold_partials(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  if (c0 >= C) return;
+  const int g = c0 / Cper, cc = c0 - g * Cper;
+  if (blockIdx.y == 0 && tr == 0) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      dgamma[g * gstride + cc + i] = b[i];
+      dbeta[g * gstride + cc + i] = a[i];
+    }
+  }
+  float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
+  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
+  const float inv_m = 1.f / (float)M;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    mu[i] = mean[c0 + i];
+    is[i] = invstd[c0 + i];
+    k1[i] = ga[i] * is[i];
+    k2[i] = b[i] * inv_m;
+    sdz[i] = a[i] * inv_m;
+  }
+  if (YM == YM_Z) bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        load8(dy + rr * C + c0, d[u]);
+        load8(x + rr * C + c0, xv[u]);
+        if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr >= r1) continue;
+      float o[VEC], dz[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        dz[i] = dz_of<YM>(d[u][i], yv[u][i], xv[u][i], sc[i], sh[i], act);
+        const float xh = (xv[u][i] - mu[i]) * is[i];
+        o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
+      }
+      store8(dx + rr * C + c0, o);
+      if (dres) store8(dres + rr * C + c0, dz);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // cooperative single-launch BN (one kernel per layer and direction)
 // ---------------------------------------------------------------------------
 // A one-config ResNet-50 step is launch-bound: ~470 kernels at 5-20 us each,
@@ -580,6 +760,18 @@ constexpr int COOP_SLOT_WORDS = 64 + COOP_MAX_GRID;
 __device__ unsigned g_coop_bar[COOP_SLOTS * COOP_SLOT_WORDS];
 
 CER_API void cer_bn_set_coop(int on) { g_coop = on; }
+
+// finalize folded into the apply when a layer has at most this many slabs
+// (CER_BN_FOLD, default 64; 0 = always launch the finalize kernel)
+static int g_fold_max = -1;
+static int fold_max() {
+  if (g_fold_max < 0) {
+    const char* e = getenv("CER_BN_FOLD");
+    g_fold_max = e ? atoi(e) : 64;
+  }
+  return g_fold_max;
+}
+CER_API void cer_bn_set_fold(int max_slabs) { g_fold_max = max_slabs; }
 
 // ReLU mask recomputed from the BN input in backward (YM_Z); 0 = always read y
 static int g_zmask = 1;
@@ -657,6 +849,14 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
                                             rrows, 0, mp);
     nslab = (int)rg.y;
+  }
+  if (nslab <= fold_max()) {
+    bn_apply_fwd_fold<<<ag, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
+                                               rstat_stride, eps, momentum, x, res, y,
+                                               Strided{gamma, gamma_stride},
+                                               Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                               mp);
+    return (int)hipGetLastError();
   }
   if (coop_on()) {
     static int cap_cache[64] = {0};
@@ -779,6 +979,22 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   else
     bn_partials<1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                   act, mp, gs, bs, Cper);
+  if ((int)rg.y <= fold_max()) {
+    if (ym == YM_NONE)
+      bn_apply_bwd_fold<YM_NONE><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+                                                          grad_stride, dy, x, y, mean, invstd, gs,
+                                                          bs, dx, dres, M, C, Cper, arows, act,
+                                                          mp);
+    else if (ym == YM_Z)
+      bn_apply_bwd_fold<YM_Z><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, arows, act, mp);
+    else
+      bn_apply_bwd_fold<YM_Y><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, arows, act, mp);
+    return (int)hipGetLastError();
+  }
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
   if (ym == YM_NONE)

@@ -492,3 +492,38 @@ def test_batched_wgrad_matches_per_layer(variant):
     finally:
         streams.set_batch_variant(old)
     assert _rel(grads[0], grads[1]) < 1e-3
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (False, False), (True, True), (6, False)])
+@pytest.mark.parametrize("shape", [(4, 7, 7, 512), (32, 4, 4, 2048), (2, 7, 7, 3 * 256)])
+def test_bn_folded_finalize_matches_staged(act, res, shape):
+    """Finalize folded into the apply (few slabs) == separate finalize kernel,
+    to fp32 rounding (the slab sums are added in a different order)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    G = 3 if shape[-1] == 768 else 2
+    C = shape[-1] // G
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    torch.manual_seed(13)
+    x = (2 * torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16)
+    r = torch.randn(shape, device="cuda").to(torch.bfloat16) if res else None
+    gy = torch.randn(shape, device="cuda").to(torch.bfloat16)
+    outs = []
+    try:
+        for fold in (1 << 20, 0):
+            _hip.lib().cer_bn_set_fold(fold)
+            a, refs = _make(specs, G, seed=5)
+            xx = x.clone().requires_grad_(True)
+            rr = r.clone().requires_grad_(True) if res else None
+            y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
+                         a.master.clone()))
+    finally:
+        _hip.lib().cer_bn_set_fold(64)
+    for u, v in zip(*outs):
+        if u is not None:
+            assert _rel(u, v) < 1e-2
+    assert _rel(outs[0][3], outs[1][3]) < 1e-4      # dgamma / dbeta
+    assert _rel(outs[0][4], outs[1][4]) < 1e-5      # running statistics
