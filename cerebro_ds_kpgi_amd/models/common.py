@@ -76,14 +76,17 @@ class PackedNet(object):
         return P.bn_act(x, self.ref(b.g), self.ref(b.b), self.ref(b.rm), self.ref(b.rv),
                         training, relu, residual, self.bn_momentum, self.bn_eps)
 
-    def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False):
+    def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False, join=None,
+                res_join=None):
         """act(BN(conv(x)) + residual); in training the conv epilogue feeds BN
-        its batch statistics (ops.nn.PackedConvBNAct)."""
+        its batch statistics (ops.nn.PackedConvBNAct).  ``join`` / ``res_join``:
+        a ``P.GradJoin`` shared with the other consumer of ``x`` / ``residual``
+        (the two input gradients are summed in a dgrad epilogue)."""
         if not training:
             return self.bn(self.conv(x, c, anchor), b, training, relu, residual)
         return P.conv_bn_act(x, self.ref(c.w), self.ref(b.g), self.ref(b.b), self.ref(b.rm),
                              self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
-                             self.bn_eps, self.anchor if anchor else None)
+                             self.bn_eps, self.anchor if anchor else None, join, res_join)
 
     def dense(self, x, d, relu=False, anchor=False):
         return P.linear(x, self.ref(d.w), self.ref(d.b), relu, self.anchor if anchor else None)

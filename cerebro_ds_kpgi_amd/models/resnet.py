@@ -73,16 +73,22 @@ class PackedResNet(PackedNet):
         x = self.conv_bn(x, self.conv1, self.bn1, training, anchor=True)
         x = P.maxpool2d(x, 3, 2, 1)  # ZeroPad(1) + MaxPool 3x3/2 valid (inputs >= 0 post-ReLU)
         for blk in self.blocks:
+            # x has two consumers (c1 and the shortcut): their input gradients
+            # meet in a GradJoin instead of an autograd add kernel
+            j = P.GradJoin() if training else None
             if "cs" in blk:
-                sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False)
+                sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j)
+                rj = None
             else:
-                sc = x
-            h = self.conv_bn(x, blk["c1"], blk["b1"], training)
+                sc, rj = x, j
+            h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j)
             if self.bottleneck:
                 h = self.conv_bn(h, blk["c2"], blk["b2"], training)
-                h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc)
+                h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc,
+                                 res_join=rj)
             else:
-                h = self.conv_bn(h, blk["c2"], blk["b2"], training, relu=True, residual=sc)
+                h = self.conv_bn(h, blk["c2"], blk["b2"], training, relu=True, residual=sc,
+                                 res_join=rj)
             x = h
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

@@ -141,7 +141,7 @@ _SIGS.update({
     "cer_conv_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p,
                      c_i, c_i, c_p, c_i64, c_i, c_p],
     "cer_conv_dgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_i, c_i, c_i, c_i,
-                       c_p, c_i, c_i, c_p],
+                       c_p, c_i, c_i, c_p, c_p],
     "cer_conv_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                        c_p, c_i64, c_i, c_p],
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
@@ -496,7 +496,8 @@ def stem_wgrad(x4, dy, wref, pad):
     launch()
 
 
-def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W):
+def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
+                       addend=None):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -504,13 +505,15 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
 
     def launch():
         rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
-                                  kw, stride, pad, _ptr(dx), H, W, _stream())
+                                  kw, stride, pad, _ptr(dx), H, W, _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W), launch)
     launch()
 
 
-def conv2d_dgrad(dy, wref, xshape, stride, pad):
+def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None):
+    """dx of the conv; ``addend`` (same shape as dx, bf16) is added in the
+    GEMM epilogue (the other consumer's gradient of a shared input)."""
     dy = _bf16(dy)
     B, Ho, Wo, _ = dy.shape
     _, H, W, _ = xshape
@@ -518,7 +521,11 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad):
     cout, kh, kw, cin = wref.spec.shape
     dx = torch.empty((B, H, W, G * cin), dtype=torch.bfloat16, device=dy.device)
     wp, ws = wref.work_ptr()
-    _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W)
+    if addend is not None:
+        addend = _bf16(addend).contiguous()
+        assert addend.shape == dx.shape
+    _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
+                       addend)
     return dx
 
 

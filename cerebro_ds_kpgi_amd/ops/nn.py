@@ -71,10 +71,40 @@ def _conv_forward(x, wref, stride, pad):
     return _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G))
 
 
+class GradJoin(object):
+    """A tensor read by exactly two of our autograd Functions (a ResNet block
+    input: the first conv and the shortcut).  Autograd would add the two input
+    gradients in a separate elementwise kernel; instead the consumer whose
+    backward runs first parks its gradient here (and returns None to
+    autograd), and the second adds it — inside its dgrad GEMM epilogue when it
+    is a HIP conv (``conv2d_dgrad(addend=...)``).  Correct in either order."""
+    __slots__ = ("pending",)
+
+    def __init__(self):
+        self.pending = None
+
+    def join(self, g):
+        """First arrival: park g, return None.  Second: return the other one."""
+        if self.pending is None:
+            self.pending = g
+            return None
+        other, self.pending = self.pending, None
+        return other
+
+
+def _join_after(join, g):
+    """Join a gradient computed without the fused add (torch paths)."""
+    if join is None or g is None:
+        return g
+    other = join.join(g)
+    return None if other is None else g + other
+
+
 class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        ctx.join = None
         y = _conv_forward(x, wref, stride, pad)
         ctx.save_for_backward(x)
         return y
@@ -87,11 +117,19 @@ class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def backward_core(ctx, x, dy, need_dx):
         wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
+        join = getattr(ctx, "join", None) if need_dx else None
         dx = None
         if use_hip("conv", x):
             h = _hip()
             if need_dx:
-                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad)
+                # the other consumer's gradient, if it already ran, joins in the epilogue
+                addend = join.pending if join is not None else None
+                if addend is not None:
+                    join.pending = None
+                    join = None
+                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend)
+                if join is not None:       # first of the two: park dx for the other one
+                    dx = join.join(dx)
             # off the critical path: overlaps the dgrad chain below (ops.streams)
             streams.run_side(lambda: h.conv2d_wgrad(x, dy, wref, stride, pad), x, dy)
         else:
@@ -101,6 +139,7 @@ class PackedConv2d(torch.autograd.Function):
             xn, dyn = _nchw(x), _nchw(dy)
             if need_dx:
                 dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, G))
+                dx = _join_after(join, dx)
             dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, G)
             wref.grad().copy_(dw.view(G, cout, cin, kh, kw).permute(0, 1, 3, 4, 2))
         return dx, None, None, None, None
@@ -206,8 +245,9 @@ class PackedConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
-                momentum, eps):
+                momentum, eps, join=None, res_join=None):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        ctx.join, ctx.res_join = join, res_join
         ctx.refs = (gref, bref)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -233,6 +273,8 @@ class PackedConvBNAct(torch.autograd.Function):
         gref, bref = ctx.refs
         dy = dy.contiguous()
         dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
+        if ctx.res_join is not None and ctx.needs_input_grad[1]:
+            dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
             x4, wref, pad = ctx.x4, ctx.wref, ctx.pad
             streams.run_side(lambda: _hip().stem_wgrad(x4, dz, wref, pad), x4, dz)
@@ -240,7 +282,8 @@ class PackedConvBNAct(torch.autograd.Function):
             dx = None
         else:
             dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
-        return dx, dres, None, None, None, None, None, None, None, None, None, None, None
+        return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
+                None)
 
 
 def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
@@ -262,9 +305,11 @@ def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
 
 
 def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
-                momentum=0.1, eps=1e-5, anchor=None):
+                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None):
+    """``join``: GradJoin shared with the other consumer of ``x``;
+    ``res_join``: GradJoin shared with the other consumer of ``residual``."""
     return PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
-                                 relu, momentum, eps)
+                                 relu, momentum, eps, join, res_join)
 
 
 def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):

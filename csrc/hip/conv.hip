@@ -111,6 +111,9 @@ struct NTParams {
   int splits = 1;         // split-K: K-tile ranges per output tile (fwd / dgrad, small grids)
   float* skws = nullptr;  // split-K fp32 partial slots [tile][split][acc regs x threads]
   unsigned* skcnt = nullptr;  // split-K per-tile arrival counters (zero; last arriver re-zeroes)
+  const bf16_t* addend = nullptr;  // optional: out += addend (same layout as out), rounded once
+                                   // (dgrad of a tensor with two consumers: the other one's
+                                   // input gradient joins here instead of in an add kernel)
 };
 
 
@@ -334,7 +337,26 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
     }
     bf16_t* dst = obase + orow * p.ldc + n;
     const bf16_t* src = lds + r * LDE + 8 * cc;
-    if (vec_ok && n + 8 <= p.N) {
+    if (p.addend) {
+      // bf16(acc) + addend in fp32, one rounding: the same value an add kernel
+      // over the two bf16 tensors would produce
+      const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
+      if (vec_ok && n + 8 <= p.N) {
+        const uint4 u = *reinterpret_cast<const uint4*>(src);
+        const uint4 w = *reinterpret_cast<const uint4*>(ad);
+        const uint32_t us[4] = {u.x, u.y, u.z, u.w}, ws[4] = {w.x, w.y, w.z, w.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float lo = __uint_as_float(us[q] << 16) + __uint_as_float(ws[q] << 16);
+          const float hi = __uint_as_float(us[q] & 0xffff0000u) + __uint_as_float(ws[q] & 0xffff0000u);
+          o[q] = pack_bf2(lo, hi);
+        }
+        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+      } else {
+        for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = f2bf(bf2f(src[e]) + bf2f(ad[e]));
+      }
+    } else if (vec_ok && n + 8 <= p.N) {
       *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     } else {
       for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = src[e];
@@ -1623,9 +1645,10 @@ static void launch_nn_t(const NTParams& p, int G, int T, int kind, bool strided,
 CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, int G,
                            const bf16_t* w, int64_t w_gstride, bf16_t* wt, int Cin, int kh,
                            int kw, int st, int pad, bf16_t* dx, int H, int W,
-                           hipStream_t stream) {
+                           const bf16_t* addend, hipStream_t stream) {
   const int T = kh * kw;
   NTParams p;
+  p.addend = addend;           // dx = dgrad + addend (nullptr: dx = dgrad)
   p.stats = nullptr;
   p.fin = BNFinal{};
   p.bias = nullptr;
@@ -1647,7 +1670,12 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
     bool strided = false;
     if (kh == 1 && kw == 1 && pad == 0 && st > 1) {
       // rows (b, ho, wo) of dy map to dx pixels (b, ho*st, wo*st); others get 0
-      (void)hipMemsetAsync(dx, 0, sizeof(bf16_t) * (size_t)B * H * W * G * Cin, stream);
+      // (or the addend, which the kernel adds on the written pixels)
+      const size_t bytes = sizeof(bf16_t) * (size_t)B * H * W * G * Cin;
+      if (addend)
+        (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, stream);
+      else
+        (void)hipMemsetAsync(dx, 0, bytes, stream);
       p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0);
       p.dgrad = 0;
       p.M = B * Ho * Wo;

@@ -527,3 +527,44 @@ def test_bn_folded_finalize_matches_staged(act, res, shape):
             assert _rel(u, v) < 1e-2
     assert _rel(outs[0][3], outs[1][3]) < 1e-4      # dgamma / dbeta
     assert _rel(outs[0][4], outs[1][4]) < 1e-5      # running statistics
+
+
+@pytest.mark.parametrize("case", [(2, 14, 14, 256, 64, 1, 1, 0, 2), (2, 14, 14, 256, 128, 1, 2, 0, 2),
+                                  (4, 7, 7, 64, 64, 3, 1, 1, 2), (2, 9, 11, 24, 40, 3, 2, 1, 2)])
+def test_dgrad_addend_equals_dgrad_plus_add(case):
+    """dx = dgrad(dy) + addend in the GEMM epilogue == dgrad then a bf16 add."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    B, H, W, cin, cout, k, s, p, G = case
+    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+    a, refs = _make([spec], G)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    torch.manual_seed(5)
+    dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(torch.bfloat16)
+    add = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+    xshape = (B, H, W, G * cin)
+    fused = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add)
+    plain = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p) + add
+    torch.cuda.synchronize()
+    assert torch.equal(fused, plain)
+
+
+def test_resnet50_gradjoin_on_gpu(monkeypatch):
+    """HIP ResNet-50 step: block-input gradients joined in dgrad epilogues ==
+    autograd accumulation (same bf16 rounding: bit-identical)."""
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    grads = []
+    for joined in (True, False):
+        if not joined:
+            monkeypatch.setattr(P, "GradJoin", lambda: None)
+        net = create_model_from_mst({"model": "resnet50"})
+        a = Arena(net.layout, 2, "cuda", torch.bfloat16)
+        for g in range(2):
+            a.init_model(g, 3 + g)
+        a.sync_work()
+        net.bind(a)
+        torch.manual_seed(0)
+        x = torch.randn(4, 64, 64, 6, device="cuda").to(torch.bfloat16)
+        net.forward(x, True).float().square().sum().backward()
+        torch.cuda.synchronize()
+        grads.append(a.grad.clone())
+    assert _rel(grads[0], grads[1]) < 1e-3

@@ -104,3 +104,28 @@ def test_dwconv_asymmetric_pad_matches_explicit_pad():
     assert torch.allclose(y, want, atol=1e-5)
     y.sum().backward()
     assert x.grad.shape == x.shape
+
+
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_resnet_gradjoin_equals_autograd_sum(name, monkeypatch):
+    """Block-input gradients joined through GradJoin (first consumer parks,
+    second adds) == autograd's own accumulation."""
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    from cerebro_ds_kpgi_amd.ops import nn as P
+    from cerebro_ds_kpgi_amd.ops import set_backend
+    from cerebro_ds_kpgi_amd.runtime.arena import Arena
+    set_backend("torch")
+    grads = []
+    for joined in (True, False):
+        if not joined:
+            monkeypatch.setattr(P, "GradJoin", lambda: None)
+        net = create_model_from_mst({"model": name})
+        a = Arena(net.layout, 1, "cpu", torch.float32)
+        a.init_model(0, 3)
+        net.bind(a)
+        torch.manual_seed(0)
+        x = torch.randn(2, 64, 64, 3, requires_grad=True)
+        net.forward(x, True).square().sum().backward()
+        grads.append((a.grad.clone(), x.grad.clone()))
+    torch.testing.assert_close(grads[0][0], grads[1][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-5, atol=1e-6)
