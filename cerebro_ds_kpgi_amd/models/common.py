@@ -7,6 +7,8 @@ runs forward on packed NHWC activations ``[B, H, W, G*C]`` through
 straight into the arena.
 """
 
+import os
+
 import torch
 
 from ..ops import nn as P
@@ -48,6 +50,8 @@ class PackedNet(object):
         self.arena = None
         self.bn_momentum = 0.1
         self.bn_eps = 1e-5
+        # BN backward partials in consumer dgrad epilogues (ops.nn.BNLink)
+        self.bn_links = os.environ.get("CER_BN_LINKS", "1") != "0"
 
     def spec(self, s):
         self._specs.append(s)
@@ -77,7 +81,7 @@ class PackedNet(object):
                         training, relu, residual, self.bn_momentum, self.bn_eps)
 
     def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False, join=None,
-                res_join=None):
+                res_join=None, link_out=False):
         """act(BN(conv(x)) + residual); in training the conv epilogue feeds BN
         its batch statistics (ops.nn.PackedConvBNAct).  ``join`` / ``res_join``:
         a ``P.GradJoin`` shared with the other consumer of ``x`` / ``residual``
@@ -86,7 +90,8 @@ class PackedNet(object):
             return self.bn(self.conv(x, c, anchor), b, training, relu, residual)
         return P.conv_bn_act(x, self.ref(c.w), self.ref(b.g), self.ref(b.b), self.ref(b.rm),
                              self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
-                             self.bn_eps, self.anchor if anchor else None, join, res_join)
+                             self.bn_eps, self.anchor if anchor else None, join, res_join,
+                             link_out and self.bn_links)
 
     def dense(self, x, d, relu=False, anchor=False):
         return P.linear(x, self.ref(d.w), self.ref(d.b), relu, self.anchor if anchor else None)

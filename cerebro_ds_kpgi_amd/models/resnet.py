@@ -72,7 +72,8 @@ class PackedResNet(PackedNet):
     def forward(self, x, training):
         x = self.conv_bn(x, self.conv1, self.bn1, training, anchor=True)
         x = P.maxpool2d(x, 3, 2, 1)  # ZeroPad(1) + MaxPool 3x3/2 valid (inputs >= 0 post-ReLU)
-        for blk in self.blocks:
+        nb = len(self.blocks)
+        for bi, blk in enumerate(self.blocks):
             # x has two consumers (c1 and the shortcut): their input gradients
             # meet in a GradJoin instead of an autograd add kernel
             j = P.GradJoin() if training else None
@@ -81,14 +82,18 @@ class PackedResNet(PackedNet):
                 rj = None
             else:
                 sc, rj = x, j
-            h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j)
+            # every BN output inside the block has one conv consumer, and the
+            # block output's two consumers are joined: all link (BNLink), except
+            # the last block's output (global average pool)
+            link_blk = j is not None and bi + 1 < nb
+            h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j, link_out=True)
             if self.bottleneck:
-                h = self.conv_bn(h, blk["c2"], blk["b2"], training)
+                h = self.conv_bn(h, blk["c2"], blk["b2"], training, link_out=True)
                 h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc,
-                                 res_join=rj)
+                                 res_join=rj, link_out=link_blk)
             else:
                 h = self.conv_bn(h, blk["c2"], blk["b2"], training, relu=True, residual=sc,
-                                 res_join=rj)
+                                 res_join=rj, link_out=link_blk)
             x = h
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

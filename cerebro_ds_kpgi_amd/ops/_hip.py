@@ -148,6 +148,9 @@ _SIGS.update({
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_bn_set_coop": [c_i],
+    "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
+    "cer_bn_bwd_part": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p,
+                        c_p, c_p, c_p, c_i, c_i64, c_i, c_i, c_i, c_p],
     "cer_wgrad_batch_add": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                             c_p, c_i64],
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
@@ -306,6 +309,10 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     assert GC == G * cin, (x.shape, wref.spec.shape, G)
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
+    if bref is None and act == 0 and stem_ok(x, wref, stride, pad):
+        # narrow-input stem (e.g. ResNet's 7x7/2 on RGB in validation): the
+        # pixel-pair MFMA path instead of the element-gather fallback
+        return stem_fwd_stats(x, wref, stride, pad)[0]
     y = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
@@ -497,7 +504,7 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend=None):
+                       addend=None, bnstats=False):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -507,13 +514,17 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
         rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
                                   kw, stride, pad, _ptr(dx), H, W, _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
-    _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W), launch)
+    _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
+            launch)
     launch()
 
 
-def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None):
+def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     """dx of the conv; ``addend`` (same shape as dx, bf16) is added in the
-    GEMM epilogue (the other consumer's gradient of a shared input)."""
+    GEMM epilogue (the other consumer's gradient of a shared input).
+    ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
+    output y this conv consumed — the epilogue also computes that BN's
+    backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink)."""
     dy = _bf16(dy)
     B, Ho, Wo, _ = dy.shape
     _, H, W, _ = xshape
@@ -524,8 +535,27 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None):
     if addend is not None:
         addend = _bf16(addend).contiguous()
         assert addend.shape == dx.shape
-    _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend)
+    if bnlink is None:
+        _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
+                           addend)
+        return dx
+    link, ybn = bnlink
+    L = lib()
+    M, C = B * H * W, G * cin
+    part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dy.device)
+    nslab = ctypes.c_int(0)
+    gp, gs = link.gref.work_ptr()
+    bp, bs = link.bref.work_ptr()
+    L.cer_conv_dgrad_bnbwd(_ptr(part), _ptr(link.z), _ptr(_bf16(ybn)), _ptr(link.mean),
+                           _ptr(link.invstd), c_p(gp), gs, c_p(bp), bs, _act_code(link.act),
+                           1 if link.has_res else 0, ctypes.byref(nslab))
+    try:
+        _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
+                           addend, bnstats=True)
+    finally:
+        L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
+    if nslab.value > 0:
+        link.part, link.nslab = part, nslab.value
     return dx
 
 
@@ -644,7 +674,9 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
     return y
 
 
-def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res):
+def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0):
+    """BN backward; ``part`` / ``nslab``: the (sum dz, sum dz*xhat) partials
+    already computed by the dgrad epilogue that produced dy."""
     dy = _bf16(dy)
     C = x.shape[-1]
     M = x.numel() // C
@@ -652,11 +684,18 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res):
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if has_res else None
     ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-    part = _bn_part(M, C, x.device)
     gp, gs = gref.work_ptr()
     bp, bs = bref.work_ptr()
     dgp, dgs = gref.grad_ptr()
     dbp, _ = bref.grad_ptr()
+    if part is not None and nslab > 0:
+        rc = lib().cer_bn_bwd_part(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
+                                   gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx),
+                                   _ptr(dres), _ptr(ws), _ptr(part), int(nslab), M, C, Cper,
+                                   _act_code(act), _stream())
+        _check(rc, "cer_bn_bwd_part")
+        return dx, dres
+    part = _bn_part(M, C, x.device)
     rc = lib().cer_bn_bwd(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
                           c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
                           M, C, Cper, _act_code(act), _stream())

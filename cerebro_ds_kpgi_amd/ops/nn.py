@@ -100,11 +100,37 @@ def _join_after(join, g):
     return None if other is None else g + other
 
 
+class BNLink(object):
+    """Forward-time handle from a BatchNorm output to the conv that consumes
+    it (``y._cer_bnlink``).  In backward, the consumer's dgrad output IS the
+    BN's input gradient dy, so its GEMM epilogue also computes the BN's
+    backward partials (``conv2d_dgrad(bnlink=...)``) and the BN backward skips
+    its own pass over (dy, z[, y]).  Only set by models on outputs whose whole
+    gradient comes out of one dgrad — a sole conv consumer, or two consumers
+    joined by a GradJoin (the second arrival holds the full gradient)."""
+    __slots__ = ("z", "mean", "invstd", "gref", "bref", "act", "has_res", "part", "nslab")
+
+    def __init__(self):
+        self.z = self.mean = self.invstd = self.gref = self.bref = None
+        self.act, self.has_res, self.part, self.nslab = 0, False, None, 0
+
+
+def _bnlink_for(ctx, x, join, addend):
+    """(link, y) when this conv's dx will be the full input gradient of a linked BN."""
+    link = getattr(ctx, "bnlink", None)
+    if link is None or link.z is None or link.part is not None:
+        return None
+    if join is not None and addend is None:    # first of two consumers: partial gradient
+        return None
+    return link, x
+
+
 class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join = None
+        ctx.bnlink = getattr(x, "_cer_bnlink", None)
         y = _conv_forward(x, wref, stride, pad)
         ctx.save_for_backward(x)
         return y
@@ -124,10 +150,11 @@ class PackedConv2d(torch.autograd.Function):
             if need_dx:
                 # the other consumer's gradient, if it already ran, joins in the epilogue
                 addend = join.pending if join is not None else None
+                bnl = _bnlink_for(ctx, x, join, addend)
                 if addend is not None:
                     join.pending = None
                     join = None
-                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend)
+                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl)
                 if join is not None:       # first of the two: park dx for the other one
                     dx = join.join(dx)
             # off the critical path: overlaps the dgrad chain below (ops.streams)
@@ -245,9 +272,11 @@ class PackedConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
-                momentum, eps, join=None, res_join=None):
+                momentum, eps, join=None, res_join=None, link=None):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join, ctx.res_join = join, res_join
+        ctx.bnlink = getattr(x, "_cer_bnlink", None)     # x is a linked BN's output
+        ctx.link = link                                  # this unit's own BN output
         ctx.refs = (gref, bref)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -264,6 +293,9 @@ class PackedConvBNAct(torch.autograd.Function):
             z = _conv_forward(x, wref, stride, pad)
             y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,
                                                 momentum, eps)
+        if link is not None and _bn_hip(z, gref):
+            link.z, link.mean, link.invstd = z, mean, invstd
+            link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
         ctx.save_for_backward(x, z, y, mean, invstd)
         return y
 
@@ -272,7 +304,16 @@ class PackedConvBNAct(torch.autograd.Function):
         x, z, y, mean, invstd = ctx.saved_tensors
         gref, bref = ctx.refs
         dy = dy.contiguous()
-        dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
+        link = ctx.link
+        if link is not None and link.part is not None:
+            # partials from the consumer's dgrad epilogue
+            dz, dres = _hip().bn_act_bwd(dy, z, y, mean, invstd, gref, bref, ctx.relu,
+                                         ctx.has_res, part=link.part, nslab=link.nslab)
+            link.part = None
+        else:
+            dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
+        if link is not None:
+            link.z = link.mean = link.invstd = None
         if ctx.res_join is not None and ctx.needs_input_grad[1]:
             dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
@@ -283,7 +324,7 @@ class PackedConvBNAct(torch.autograd.Function):
         else:
             dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
-                None)
+                None, None)
 
 
 def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
@@ -305,11 +346,17 @@ def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
 
 
 def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
-                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None):
+                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False):
     """``join``: GradJoin shared with the other consumer of ``x``;
-    ``res_join``: GradJoin shared with the other consumer of ``residual``."""
-    return PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
-                                 relu, momentum, eps, join, res_join)
+    ``res_join``: GradJoin shared with the other consumer of ``residual``;
+    ``link_out``: the output's whole gradient comes out of one consumer dgrad
+    (see BNLink) — its BN backward partials are computed there."""
+    link = BNLink() if link_out else None
+    y = PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
+                              relu, momentum, eps, join, res_join, link)
+    if link is not None:
+        y._cer_bnlink = link
+    return y
 
 
 def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):

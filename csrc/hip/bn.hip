@@ -777,6 +777,11 @@ CER_API void cer_bn_set_fold(int max_slabs) { g_fold_max = max_slabs; }
 static int g_zmask = 1;
 CER_API void cer_bn_set_zmask(int on) { g_zmask = on; }
 
+// mask source of a BN backward (also used by the dgrad-epilogue statistics)
+int bn_mask_mode(int act, int has_res) {
+  return act == 0 ? YM_NONE : (act == 1 && !has_res && g_zmask) ? YM_Z : YM_Y;
+}
+
 static bool coop_on() {
   if (g_coop < 0) {
     const char* e = getenv("CER_BN_COOP");
@@ -941,18 +946,20 @@ CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
+// pre_nslab > 0: part already holds pre_nslab partials (computed in the
+// epilogue of the dgrad that produced dy): skip the partials pass
+static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
                        const float* invstd, const bf16_t* gamma, int64_t gamma_stride,
                        const bf16_t* beta, int64_t beta_stride, float* dgamma, float* dbeta,
                        int64_t grad_stride, bf16_t* dx, bf16_t* dres, float* ws, float* part,
-                       int64_t M, int C, int Cper, int act, hipStream_t stream) {
+                       int pre_nslab, int64_t M, int C, int Cper, int act, hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 rg, ag;
   int rrows, arows;
   make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  if (coop_on()) {
+  if (pre_nslab <= 0 && coop_on()) {
     // same (channel block, slab) tiling as bn_partials: part has room for it
     static int cap_cache[64] = {0};
     const int cap = coop_capacity(bn_bwd_coop, cap_cache);
@@ -968,34 +975,37 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   }
   // mask source: none / y / recomputed from x (see the header); a residual
   // join's mask depends on the residual, so it needs y
-  const int ym = act == 0 ? YM_NONE : (act == 1 && !dres && g_zmask) ? YM_Z : YM_Y;
+  const int ym = bn_mask_mode(act, dres != nullptr);
   const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
-  if (ym == YM_NONE)
-    bn_partials<1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                     act, mp, gs, bs, Cper);
-  else if (ym == YM_Z)
-    bn_partials<1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                  act, mp, gs, bs, Cper);
-  else
-    bn_partials<1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                  act, mp, gs, bs, Cper);
-  if ((int)rg.y <= fold_max()) {
+  const int nslab = pre_nslab > 0 ? pre_nslab : (int)rg.y;
+  if (pre_nslab <= 0) {
     if (ym == YM_NONE)
-      bn_apply_bwd_fold<YM_NONE><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+      bn_partials<1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
+                                                       rrows, act, mp, gs, bs, Cper);
+    else if (ym == YM_Z)
+      bn_partials<1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                    act, mp, gs, bs, Cper);
+    else
+      bn_partials<1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                    act, mp, gs, bs, Cper);
+  }
+  if (nslab <= fold_max()) {
+    if (ym == YM_NONE)
+      bn_apply_bwd_fold<YM_NONE><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                           grad_stride, dy, x, y, mean, invstd, gs,
                                                           bs, dx, dres, M, C, Cper, arows, act,
                                                           mp);
     else if (ym == YM_Z)
-      bn_apply_bwd_fold<YM_Z><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+      bn_apply_bwd_fold<YM_Z><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
                                                        dx, dres, M, C, Cper, arows, act, mp);
     else
-      bn_apply_bwd_fold<YM_Y><<<ag, BN_T, 0, stream>>>(part, (int)rg.y, dgamma, dbeta,
+      bn_apply_bwd_fold<YM_Y><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
                                                        dx, dres, M, C, Cper, arows, act, mp);
     return (int)hipGetLastError();
   }
-  bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma, dbeta,
+  bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
   if (ym == YM_NONE)
     bn_apply_bwd<YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
@@ -1007,4 +1017,26 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
     bn_apply_bwd<YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                 Cper, arows, act, mp, bs);
   return (int)hipGetLastError();
+}
+
+CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
+                       const float* invstd, const bf16_t* gamma, int64_t gamma_stride,
+                       const bf16_t* beta, int64_t beta_stride, float* dgamma, float* dbeta,
+                       int64_t grad_stride, bf16_t* dx, bf16_t* dres, float* ws, float* part,
+                       int64_t M, int C, int Cper, int act, hipStream_t stream) {
+  return bn_bwd_impl(dy, x, y, mean, invstd, gamma, gamma_stride, beta, beta_stride, dgamma,
+                     dbeta, grad_stride, dx, dres, ws, part, 0, M, C, Cper, act, stream);
+}
+
+// same, with the nslab (sum dz, sum dz*xhat) partials already in `part`
+// (cer_conv_dgrad_bnbwd)
+CER_API int cer_bn_bwd_part(const bf16_t* dy, const bf16_t* x, const bf16_t* y,
+                            const float* mean, const float* invstd, const bf16_t* gamma,
+                            int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
+                            float* dgamma, float* dbeta, int64_t grad_stride, bf16_t* dx,
+                            bf16_t* dres, float* ws, float* part, int nslab, int64_t M, int C,
+                            int Cper, int act, hipStream_t stream) {
+  if (nslab <= 0) return (int)hipErrorInvalidValue;
+  return bn_bwd_impl(dy, x, y, mean, invstd, gamma, gamma_stride, beta, beta_stride, dgamma,
+                     dbeta, grad_stride, dx, dres, ws, part, nslab, M, C, Cper, act, stream);
 }

@@ -40,8 +40,10 @@ constexpr int BK = 64;
 constexpr int NTHREADS = 256;
 // bf16 elements after the staged C tile for the BN-statistics exchange
 // ([2 waves][2][BN] floats, reused as [2][NTHREADS] floats by the fused
-// finalize) and the last-arriver flag
-constexpr int STAT_XCH = 2 * (2 * NTHREADS) + 8;
+// finalize, and as [2][lanes][BN] = 4096 floats by the BN-backward
+// statistics of a dgrad epilogue) and the last-arriver flag.  Every kernel's
+// operand staging area is at least this big, so it costs no LDS.
+constexpr int STAT_XCH = 2 * 4096 + 8;
 
 // ---------------------------------------------------------------------------
 // n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery)
@@ -93,6 +95,25 @@ struct BNFinal {
   float eps, momentum;
 };
 
+// BN-backward statistics in a dgrad epilogue: the dgrad output is the input
+// gradient dy of a BatchNorm layer (whose output the conv consumed), so the
+// epilogue also produces that BN's per-(M tile, channel) partials
+// (sum dz, sum dz * xhat), dz = act'(.) dy, exactly what bn_partials<1>
+// would compute from the stored bf16 dy -> the BN backward skips its
+// partials pass over (dy, x[, y]).  part == nullptr: off.
+struct BNBwdEpi {
+  float* part;                  // [M tiles][2][ldc]
+  const bf16_t* z;              // BN input, [M][ldc]
+  const bf16_t* y;              // BN output (mask mode YM_Y)
+  const float* mean;            // [ldc]
+  const float* invstd;
+  const bf16_t* gamma;          // per-config parameters (mask mode YM_Z)
+  int64_t gstride;
+  const bf16_t* beta;
+  int64_t bstride;
+  int ym, act;                  // mask mode (bn.hip YM_*) and activation code
+};
+
 struct NTParams {
   GatherGeom a;
   int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
@@ -114,6 +135,8 @@ struct NTParams {
   const bf16_t* addend = nullptr;  // optional: out += addend (same layout as out), rounded once
                                    // (dgrad of a tensor with two consumers: the other one's
                                    // input gradient joins here instead of in an add kernel)
+  BNBwdEpi bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
+                         0, 0};
 };
 
 
@@ -324,11 +347,34 @@ template <int BM, int BN>
 __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds, int LDE, int cfg,
                                            int m0, int n0, int tid) {
   constexpr int OCPR = BN / 8;
+  constexpr int LANES = NTHREADS / OCPR;    // rows in flight; a thread keeps one column chunk
+  static_assert(NTHREADS % OCPR == 0, "store_tile: column chunk must be thread-invariant");
   bf16_t* obase = p.out + (int64_t)cfg * p.N;
   const bool vec_ok = ((p.N | p.ldc) & 7) == 0;
+  const BNBwdEpi& bb = p.bb;
+  const bool bstat = bb.part != nullptr;    // host guarantees vec_ok
+  const int cc = tid % OCPR, lane = tid / OCPR;
+  const int ncol = n0 + 8 * cc;
+  float s8[8], q8[8], mu8[8], is8[8], sc8[8], sh8[8];
+  if (bstat) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s8[e] = q8[e] = 0.f;
+      const int n = min(ncol + e, p.N - 1);
+      const int64_t c = (int64_t)cfg * p.N + n;
+      mu8[e] = bb.mean[c];
+      is8[e] = bb.invstd[c];
+      if (bb.ym == 2) {                     // YM_Z: the forward's scale / shift
+        const float ga = bf2f(bb.gamma[cfg * bb.gstride + n]);
+        const float be = bf2f(bb.beta[cfg * bb.bstride + n]);
+        sc8[e] = is8[e] * ga;
+        sh8[e] = be - mu8[e] * sc8[e];
+      }
+    }
+  }
   for (int idx = tid; idx < BM * OCPR; idx += NTHREADS) {
-    const int r = idx / OCPR, cc = idx - r * OCPR;
-    const int m = m0 + r, n = n0 + 8 * cc;
+    const int r = idx / OCPR;
+    const int m = m0 + r, n = ncol;
     if (m >= p.M || n >= p.N) continue;
     int64_t orow = m;
     if (p.o_st > 1) {
@@ -337,30 +383,72 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
     }
     bf16_t* dst = obase + orow * p.ldc + n;
     const bf16_t* src = lds + r * LDE + 8 * cc;
-    if (p.addend) {
-      // bf16(acc) + addend in fp32, one rounding: the same value an add kernel
-      // over the two bf16 tensors would produce
-      const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
-      if (vec_ok && n + 8 <= p.N) {
-        const uint4 u = *reinterpret_cast<const uint4*>(src);
+    if (vec_ok && n + 8 <= p.N) {
+      uint4 u = *reinterpret_cast<const uint4*>(src);
+      if (p.addend) {
+        // bf16(acc) + addend in fp32, one rounding: the same value an add
+        // kernel over the two bf16 tensors would produce
+        const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
         const uint4 w = *reinterpret_cast<const uint4*>(ad);
         const uint32_t us[4] = {u.x, u.y, u.z, u.w}, ws[4] = {w.x, w.y, w.z, w.w};
         uint32_t o[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float lo = __uint_as_float(us[q] << 16) + __uint_as_float(ws[q] << 16);
-          const float hi = __uint_as_float(us[q] & 0xffff0000u) + __uint_as_float(ws[q] & 0xffff0000u);
-          o[q] = pack_bf2(lo, hi);
+        for (int k = 0; k < 4; ++k) {
+          const float lo = __uint_as_float(us[k] << 16) + __uint_as_float(ws[k] << 16);
+          const float hi =
+              __uint_as_float(us[k] & 0xffff0000u) + __uint_as_float(ws[k] & 0xffff0000u);
+          o[k] = pack_bf2(lo, hi);
         }
-        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-      } else {
-        for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = f2bf(bf2f(src[e]) + bf2f(ad[e]));
+        u = make_uint4(o[0], o[1], o[2], o[3]);
       }
-    } else if (vec_ok && n + 8 <= p.N) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      *reinterpret_cast<uint4*>(dst) = u;
+      if (bstat) {
+        const int64_t zo = (int64_t)cfg * p.N + orow * p.ldc + n;
+        const uint4 zu = *reinterpret_cast<const uint4*>(bb.z + zo);
+        uint4 yu = make_uint4(0, 0, 0, 0);
+        if (bb.ym == 1) yu = *reinterpret_cast<const uint4*>(bb.y + zo);
+        const uint32_t dw[4] = {u.x, u.y, u.z, u.w}, zw[4] = {zu.x, zu.y, zu.z, zu.w},
+                       yw[4] = {yu.x, yu.y, yu.z, yu.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t sh = (e & 1) ? 0u : 16u, mk = 0xffff0000u;
+          const float d = __uint_as_float((dw[e >> 1] << sh) & mk);
+          const float zv = __uint_as_float((zw[e >> 1] << sh) & mk);
+          float dz = d;
+          if (bb.ym == 2) {
+            dz = (zv * sc8[e] + sh8[e] + 0.f) > 0.f ? d : 0.f;
+          } else if (bb.ym == 1) {
+            const float yv = __uint_as_float((yw[e >> 1] << sh) & mk);
+            dz = bb.act == 6 ? ((yv > 0.f && yv < 6.f) ? d : 0.f) : (yv > 0.f ? d : 0.f);
+          }
+          s8[e] += dz;
+          q8[e] += dz * (zv - mu8[e]) * is8[e];
+        }
+      }
+    } else if (p.addend) {
+      const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
+      for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = f2bf(bf2f(src[e]) + bf2f(ad[e]));
     } else {
       for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = src[e];
     }
+  }
+  if (!bstat) return;
+  // rows of the tile -> one deterministic partial per (M tile, channel)
+  float* xs = reinterpret_cast<float*>(const_cast<bf16_t*>(lds) + BM * LDE);  // [2][LANES][BN]
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    xs[lane * BN + 8 * cc + e] = s8[e];
+    xs[(LANES + lane) * BN + 8 * cc + e] = q8[e];
+  }
+  __syncthreads();
+  float* dstp = bb.part + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  for (int t = tid; t < 2 * BN; t += NTHREADS) {
+    const int q = t / BN, nl = t - q * BN, n = n0 + nl;
+    if (n >= p.N) continue;
+    float v = 0.f;
+    for (int l = 0; l < LANES; ++l) v += xs[(q * LANES + l) * BN + nl];
+    dstp[(int64_t)q * p.ldc + n] = v;
   }
 }
 
@@ -1642,6 +1730,23 @@ static void launch_nn_t(const NTParams& p, int G, int T, int kind, bool strided,
 // transpose); a strided 1x1 conv only computes the B*Ho*Wo rows that receive
 // gradient (the rest of dx is zero-filled).  Otherwise the transpose + NT path.
 // wt: scratch of G * Cout*kh*kw*Cin elements (used by the fallback only)
+// BN-backward statistics for the NEXT cer_conv_dgrad calls (until cleared
+// with part == nullptr): see BNBwdEpi.  *nslab_out receives the partial count
+// (M tiles of the variant that ran).  bn_mask_mode is bn.hip's YM rule.
+int bn_mask_mode(int act, int has_res);
+static BNBwdEpi g_bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr,
+                                0, 0, 0};
+static int* g_bb_nslab = nullptr;
+
+CER_API void cer_conv_dgrad_bnbwd(float* part, const bf16_t* z, const bf16_t* y,
+                                  const float* mean, const float* invstd, const bf16_t* gamma,
+                                  int64_t gstride, const bf16_t* beta, int64_t bstride, int act,
+                                  int has_res, int* nslab_out) {
+  g_bb = BNBwdEpi{part, z, y, mean, invstd, gamma, gstride, beta, bstride,
+                  bn_mask_mode(act, has_res), act};
+  g_bb_nslab = part ? nslab_out : nullptr;
+}
+
 CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, int G,
                            const bf16_t* w, int64_t w_gstride, bf16_t* wt, int Cin, int kh,
                            int kw, int st, int pad, bf16_t* dx, int H, int W,
@@ -1689,6 +1794,16 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
     const int v = choose(1, p.M, p.N, p.K, G, Cout % 64 == 0);
     set_splits(p, G, v);
     const int kind = (v / 3) & 1;
+    // BN-backward statistics: every dx pixel must come out of the epilogue
+    // (a strided 1x1 dgrad leaves pixels at zero: fine without an addend)
+    if (g_bb.part && (p.o_st == 1 || !addend)) {
+      p.bb = g_bb;
+      int bm, bn;
+      tile_dims(v, bm, bn);
+      if (g_bb_nslab) *g_bb_nslab = (p.M + bm - 1) / bm;
+    } else if (g_bb_nslab) {
+      *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
+    }
     switch (v % 3) {
       case 0: launch_nn_t<64, 64>(p, G, T, kind, strided, stream); break;
       case 1: launch_nn_t<128, 128>(p, G, T, kind, strided, stream); break;
@@ -1696,6 +1811,7 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
     }
     return (int)hipGetLastError();
   }
+  if (g_bb_nslab) *g_bb_nslab = 0;       // fallback path: no BN statistics
   dim3 tg(((Cout + 31) / 32) * ((Cin + 31) / 32), T, G);
   transpose_w_kernel<<<tg, 256, 0, stream>>>(w, w_gstride, wt, Cout, T, Cin);
   p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);

@@ -557,6 +557,7 @@ def test_resnet50_gradjoin_on_gpu(monkeypatch):
         if not joined:
             monkeypatch.setattr(P, "GradJoin", lambda: None)
         net = create_model_from_mst({"model": "resnet50"})
+        net.bn_links = False    # isolate the join (BN-link partials change summation order)
         a = Arena(net.layout, 2, "cuda", torch.bfloat16)
         for g in range(2):
             a.init_model(g, 3 + g)
@@ -568,3 +569,56 @@ def test_resnet50_gradjoin_on_gpu(monkeypatch):
         torch.cuda.synchronize()
         grads.append(a.grad.clone())
     assert _rel(grads[0], grads[1]) < 1e-3
+
+
+@pytest.mark.parametrize("act,res,k2,s2", [(True, False, 3, 1), (False, False, 1, 1),
+                                          (True, True, 1, 1), (True, False, 1, 2),
+                                          (6, False, 1, 1)])
+def test_bn_partials_in_dgrad_epilogue(act, res, k2, s2):
+    """conv_bn(link_out) -> conv: the BN's backward partials computed in the
+    consumer conv's dgrad epilogue == the BN's own partials pass (fp32
+    summation order only)."""
+    G, B, H, cin, cmid, cout = 2, 4, 14, 64, 128, 64
+    specs = [ParamSpec("w1", (cmid, 1, 1, cin), "weight", fan_in=cin),
+             ParamSpec("w2", (cout, k2, k2, cmid), "weight", fan_in=k2 * k2 * cmid),
+             ParamSpec("g", (cmid,), "gamma"), ParamSpec("b", (cmid,), "beta"),
+             ParamSpec("rm", (cmid,), "running_mean"), ParamSpec("rv", (cmid,), "running_var")]
+    torch.manual_seed(3)
+    x = torch.randn(B, H, H, G * cin, device="cuda").to(torch.bfloat16)
+    r = torch.randn(B, H, H, G * cmid, device="cuda").to(torch.bfloat16) if res else None
+    outs = []
+    for link in (True, False):
+        a, refs = _make(specs, G, seed=4)
+        xx = x.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True) if res else None
+        h = P.conv_bn_act(xx, refs["w1"], refs["g"], refs["b"], refs["rm"], refs["rv"], 1, 0,
+                          act, rr, link_out=link)
+        y = P.conv2d(h, refs["w2"], s2, k2 // 2)
+        torch.manual_seed(9)
+        y.backward(torch.randn_like(y.float()).to(torch.bfloat16))
+        torch.cuda.synchronize()
+        outs.append((xx.grad.float(), a.grad.clone()))
+    assert _rel(outs[0][0], outs[1][0]) < 1e-2
+    assert _rel(outs[0][1], outs[1][1]) < 1e-2
+
+
+def test_resnet50_bn_links_train_finite():
+    """Whole ResNet-50 step with BN links: finite, same loss, gradients within
+    the chaotic-init spread of the unlinked path."""
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    grads = []
+    for links in (True, False):
+        net = create_model_from_mst({"model": "resnet50"})
+        net.bn_links = links
+        a = Arena(net.layout, 2, "cuda", torch.bfloat16)
+        for g in range(2):
+            a.init_model(g, 3 + g)
+        a.sync_work()
+        net.bind(a)
+        torch.manual_seed(0)
+        x = torch.randn(8, 64, 64, 6, device="cuda").to(torch.bfloat16)
+        net.forward(x, True).float().square().sum().backward()
+        torch.cuda.synchronize()
+        grads.append(a.grad.clone())
+    assert torch.isfinite(grads[0]).all()
+    assert _rel(grads[0], grads[1]) < 0.1
