@@ -18,10 +18,11 @@ import sys
 FAMILIES = [
     ("conv/linear GEMM (MFMA, NT: fwd)", r"igemm_nt|pipe_nt"),
     ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad|pipe_nn"),
-    ("conv/linear wgrad (MFMA, TN)", r"igemm_wgrad|pipe_wg"),
+    ("conv/linear wgrad (MFMA, TN; batched)", r"igemm_wgrad|pipe_wg|wgrad_batch"),
     ("weight transpose (dgrad)", r"transpose_w"),
     ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),
-    ("pooling", r"maxpool|gavg"),
+    ("pooling", r"maxpool|gavg|avgpool"),
+    ("stem repack / fold", r"stem_"),
     ("bias/act", r"bias_act|bias_grad"),
     ("adam (fused, flat arena)", r"adam"),
     ("softmax-CE + metrics", r"softmax_ce"),

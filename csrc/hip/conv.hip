@@ -343,18 +343,46 @@ __device__ __forceinline__ int nt_off(int row, int chunk) {
 }
 
 // epilogue store of a staged [BM][BN] bf16 tile (shared by the NT and NN kernels)
-template <int BM, int BN>
+// EXT (the NN dgrad kernels): addend + BN-backward statistics, loads of
+// PF rows issued together; otherwise (NT kernels) a plain store loop that
+// still honours an addend (the unaligned dgrad fallback runs on NT).
+template <int BM, int BN, bool EXT = false>
 __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds, int LDE, int cfg,
                                            int m0, int n0, int tid) {
   constexpr int OCPR = BN / 8;
   constexpr int LANES = NTHREADS / OCPR;    // rows in flight; a thread keeps one column chunk
-  static_assert(NTHREADS % OCPR == 0, "store_tile: column chunk must be thread-invariant");
+  constexpr int NIT = BM * OCPR / NTHREADS;
+  constexpr int PF = NIT > 4 ? 4 : NIT;     // rows per prefetch group (bounds the VGPRs)
+  static_assert(NTHREADS % OCPR == 0 && NIT * NTHREADS == BM * OCPR && NIT % PF == 0,
+                "store_tile mapping");
   bf16_t* obase = p.out + (int64_t)cfg * p.N;
   const bool vec_ok = ((p.N | p.ldc) & 7) == 0;
-  const BNBwdEpi& bb = p.bb;
-  const bool bstat = bb.part != nullptr;    // host guarantees vec_ok
   const int cc = tid % OCPR, lane = tid / OCPR;
   const int ncol = n0 + 8 * cc;
+  if (!EXT || !vec_ok) {  // (BN statistics need aligned channels: host-gated)
+    for (int it = 0; it < NIT; ++it) {
+      const int r = lane + it * LANES, m = m0 + r;
+      if (m >= p.M || ncol >= p.N) continue;
+      int64_t orow = m;
+      if (p.o_st > 1) {
+        const RowPos q = decode_row(m, p.M, p.a);
+        orow = ((int64_t)q.b * p.o_H + (int64_t)q.y * p.o_st) * p.o_W + (int64_t)q.x * p.o_st;
+      }
+      bf16_t* dst = obase + orow * p.ldc + ncol;
+      const bf16_t* src = lds + r * LDE + 8 * cc;
+      if (vec_ok && !p.addend) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        continue;
+      }
+      for (int e = 0; e < 8 && ncol + e < p.N; ++e)
+        dst[e] = p.addend ? f2bf(bf2f(src[e]) + bf2f(p.addend[(int64_t)cfg * p.N + orow * p.ldc +
+                                                             ncol + e]))
+                          : src[e];
+    }
+    return;
+  }
+  const BNBwdEpi& bb = p.bb;
+  const bool bstat = bb.part != nullptr;
   float s8[8], q8[8], mu8[8], is8[8], sc8[8], sh8[8];
   if (bstat) {
 #pragma unroll
@@ -372,65 +400,74 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
       }
     }
   }
-  for (int idx = tid; idx < BM * OCPR; idx += NTHREADS) {
-    const int r = idx / OCPR;
-    const int m = m0 + r, n = ncol;
-    if (m >= p.M || n >= p.N) continue;
-    int64_t orow = m;
-    if (p.o_st > 1) {
+  // per group of PF rows: issue the group's global loads (addend, BN input /
+  // output) together, then store and accumulate
+#pragma unroll
+  for (int g0 = 0; g0 < NIT; g0 += PF) {
+  int64_t orow[PF];
+  bool ok[PF];
+  uint4 ad[PF], zu[PF], yu[PF];
+#pragma unroll
+  for (int it = 0; it < PF; ++it) {
+    const int m = m0 + lane + (g0 + it) * LANES;
+    ok[it] = m < p.M && ncol < p.N;
+    orow[it] = m;
+    if (ok[it] && p.o_st > 1) {
       const RowPos q = decode_row(m, p.M, p.a);
-      orow = ((int64_t)q.b * p.o_H + (int64_t)q.y * p.o_st) * p.o_W + (int64_t)q.x * p.o_st;
+      orow[it] = ((int64_t)q.b * p.o_H + (int64_t)q.y * p.o_st) * p.o_W + (int64_t)q.x * p.o_st;
     }
-    bf16_t* dst = obase + orow * p.ldc + n;
-    const bf16_t* src = lds + r * LDE + 8 * cc;
-    if (vec_ok && n + 8 <= p.N) {
-      uint4 u = *reinterpret_cast<const uint4*>(src);
-      if (p.addend) {
-        // bf16(acc) + addend in fp32, one rounding: the same value an add
-        // kernel over the two bf16 tensors would produce
-        const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
-        const uint4 w = *reinterpret_cast<const uint4*>(ad);
-        const uint32_t us[4] = {u.x, u.y, u.z, u.w}, ws[4] = {w.x, w.y, w.z, w.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float lo = __uint_as_float(us[k] << 16) + __uint_as_float(ws[k] << 16);
-          const float hi =
-              __uint_as_float(us[k] & 0xffff0000u) + __uint_as_float(ws[k] & 0xffff0000u);
-          o[k] = pack_bf2(lo, hi);
-        }
-        u = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-      *reinterpret_cast<uint4*>(dst) = u;
-      if (bstat) {
-        const int64_t zo = (int64_t)cfg * p.N + orow * p.ldc + n;
-        const uint4 zu = *reinterpret_cast<const uint4*>(bb.z + zo);
-        uint4 yu = make_uint4(0, 0, 0, 0);
-        if (bb.ym == 1) yu = *reinterpret_cast<const uint4*>(bb.y + zo);
-        const uint32_t dw[4] = {u.x, u.y, u.z, u.w}, zw[4] = {zu.x, zu.y, zu.z, zu.w},
-                       yw[4] = {yu.x, yu.y, yu.z, yu.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t sh = (e & 1) ? 0u : 16u, mk = 0xffff0000u;
-          const float d = __uint_as_float((dw[e >> 1] << sh) & mk);
-          const float zv = __uint_as_float((zw[e >> 1] << sh) & mk);
-          float dz = d;
-          if (bb.ym == 2) {
-            dz = (zv * sc8[e] + sh8[e] + 0.f) > 0.f ? d : 0.f;
-          } else if (bb.ym == 1) {
-            const float yv = __uint_as_float((yw[e >> 1] << sh) & mk);
-            dz = bb.act == 6 ? ((yv > 0.f && yv < 6.f) ? d : 0.f) : (yv > 0.f ? d : 0.f);
-          }
-          s8[e] += dz;
-          q8[e] += dz * (zv - mu8[e]) * is8[e];
-        }
-      }
-    } else if (p.addend) {
-      const bf16_t* ad = p.addend + (int64_t)cfg * p.N + orow * p.ldc + n;
-      for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = f2bf(bf2f(src[e]) + bf2f(ad[e]));
-    } else {
-      for (int e = 0; e < 8 && n + e < p.N; ++e) dst[e] = src[e];
+    const int64_t go = (int64_t)cfg * p.N + orow[it] * p.ldc + ncol;
+    if (ok[it] && p.addend) ad[it] = *reinterpret_cast<const uint4*>(p.addend + go);
+    if (ok[it] && bstat) {
+      zu[it] = *reinterpret_cast<const uint4*>(bb.z + go);
+      if (bb.ym == 1) yu[it] = *reinterpret_cast<const uint4*>(bb.y + go);
     }
+  }
+#pragma unroll
+  for (int it = 0; it < PF; ++it) {
+    if (!ok[it]) continue;
+    const int r = lane + (g0 + it) * LANES;
+    uint4 u = *reinterpret_cast<const uint4*>(lds + r * LDE + 8 * cc);
+    if (p.addend) {
+      // bf16(acc) + addend in fp32, one rounding: the same value an add
+      // kernel over the two bf16 tensors would produce
+      const uint32_t us[4] = {u.x, u.y, u.z, u.w},
+                     ws[4] = {ad[it].x, ad[it].y, ad[it].z, ad[it].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float lo = __uint_as_float(us[k] << 16) + __uint_as_float(ws[k] << 16);
+        const float hi =
+            __uint_as_float(us[k] & 0xffff0000u) + __uint_as_float(ws[k] & 0xffff0000u);
+        o[k] = pack_bf2(lo, hi);
+      }
+      u = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    *reinterpret_cast<uint4*>(obase + orow[it] * p.ldc + ncol) = u;
+    if (bstat) {
+      const uint32_t dw[4] = {u.x, u.y, u.z, u.w},
+                     zw[4] = {zu[it].x, zu[it].y, zu[it].z, zu[it].w};
+      uint32_t yw[4] = {0u, 0u, 0u, 0u};
+      if (bb.ym == 1) {
+        yw[0] = yu[it].x; yw[1] = yu[it].y; yw[2] = yu[it].z; yw[3] = yu[it].w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t shf = (e & 1) ? 0u : 16u, mk = 0xffff0000u;
+        const float d = __uint_as_float((dw[e >> 1] << shf) & mk);
+        const float zv = __uint_as_float((zw[e >> 1] << shf) & mk);
+        float dz = d;
+        if (bb.ym == 2) {
+          dz = (zv * sc8[e] + sh8[e] + 0.f) > 0.f ? d : 0.f;
+        } else if (bb.ym == 1) {
+          const float yv = __uint_as_float((yw[e >> 1] << shf) & mk);
+          dz = bb.act == 6 ? ((yv > 0.f && yv < 6.f) ? d : 0.f) : (yv > 0.f ? d : 0.f);
+        }
+        s8[e] += dz;
+        q8[e] += dz * (zv - mu8[e]) * is8[e];
+      }
+    }
+  }
   }
   if (!bstat) return;
   // rows of the tile -> one deterministic partial per (M tile, channel)
@@ -1069,7 +1106,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn_dgrad(NTParams p, int T,
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
-  store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
+  store_tile<BM, BN, true>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
 #undef SA
@@ -1357,7 +1394,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nn(NTParams p, int T) {
   stage_c<BM, BN>(p, lds, acc, cfg, m0, n0, wm, wn, lane);
   __syncthreads();
   stats_finish<BM, BN>(p, lds, cfg, m0, n0, tid);
-  store_tile<BM, BN>(p, lds, LDE, cfg, m0, n0, tid);
+  store_tile<BM, BN, true>(p, lds, LDE, cfg, m0, n0, tid);
 }
 
 // wgrad: dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]; requires Cin % 8 == 0, Cout % 8 == 0
