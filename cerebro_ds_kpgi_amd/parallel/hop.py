@@ -48,12 +48,57 @@ def validate_plan(moves, world):
     return True
 
 
-def execute_moves(moves, rank, send_buf, recv_buf, group=None):
+class HopChecksumError(RuntimeError):
+    pass
+
+
+def checksum(t):
+    """Position-sensitive fp64 digest of a state buffer (debug hop check):
+    total sum, stride-7 subsample sum, first-half sum."""
+    v = t.reshape(-1)
+    n = v.numel()
+    return torch.stack([v.sum(dtype=torch.float64), v[::7].sum(dtype=torch.float64),
+                        v[:n // 2].sum(dtype=torch.float64)])
+
+
+def execute_moves(moves, rank, send_buf, recv_buf, group=None, check=False):
     """Post this rank's part of the plan; returns after all transfers land.
 
     ``send_buf(model) -> tensor`` and ``recv_buf(model) -> tensor`` give the
     contiguous buffers.  Model id doubles as the tag (gloo matching).
+
+    ``check`` (debug, ``CER_HOP_CHECK=1``; SURVEY.md §5.2 stream-ordering
+    checks): after the transfers every sender ships the digest of what it
+    sent, every receiver compares it with the digest of what landed, after a
+    device synchronisation — a hop racing a kernel that still writes the
+    buffer, or a mis-paired send/recv, raises ``HopChecksumError``.
     """
+    n = _post(moves, rank, send_buf, recv_buf, group)
+    if not check or not n:
+        return n
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    ops, mine = [], {}
+    for mv in moves:
+        if mv.src == rank:
+            ops.append(dist.P2POp(dist.isend, checksum(send_buf(mv.model)), mv.dst, group,
+                                  tag=100000 + mv.model))
+        elif mv.dst == rank:
+            buf = recv_buf(mv.model)
+            mine[mv.model] = (checksum(buf), torch.empty(3, dtype=torch.float64,
+                                                         device=buf.device))
+            ops.append(dist.P2POp(dist.irecv, mine[mv.model][1], mv.src, group,
+                                  tag=100000 + mv.model))
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+    for m, (got, sent) in mine.items():
+        if not torch.equal(got, sent):
+            raise HopChecksumError("model {} arrived corrupted on rank {}: digest {} != sent {}"
+                                   .format(m, rank, got.tolist(), sent.tolist()))
+    return n
+
+
+def _post(moves, rank, send_buf, recv_buf, group):
     ops = []
     for mv in moves:
         if mv.src == rank:

@@ -78,6 +78,8 @@ class EngineOptions(object):
         self.store_loader = kw.get("store_loader", None)
         self.partitions = kw.get("partitions", 0)
         self.trace = kw.get("trace", False)
+        # debug: verify every hop with sender/receiver digests (parallel.hop)
+        self.hop_check = kw.get("hop_check", os.environ.get("CER_HOP_CHECK", "0") == "1")
         self.max_retries = kw.get("max_retries", 2)
         self.resume = kw.get("resume", False)
         self.heartbeat = kw.get("heartbeat", 0)     # watchdog timeout (s); 0 = off
@@ -220,7 +222,7 @@ class MOPEngine(object):
             def recv_buf(m):
                 w, row = row_of[m]
                 return w.recv_buffer(row, hopt)
-            n = execute_moves(moves, rank, send_buf, recv_buf)
+            n = execute_moves(moves, rank, send_buf, recv_buf, check=self.o.hop_check)
             if n:
                 for mv in moves:
                     if mv.src == rank:

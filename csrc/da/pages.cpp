@@ -113,12 +113,19 @@ bool parse_datum(const uint8_t* p, const uint8_t* end, Datum* d, int64_t* consum
     d->ptr.extsize = rdi32(p + 8);
     d->ptr.valueid = rd32(p + 12);
     d->ptr.toastrelid = rd32(p + 16);
+    // sizes straight from the file: reject what no writer produces (a 1 GB
+    // datum limit, as in PostgreSQL) before anything is allocated from them
+    if (d->ptr.rawsize < 4 || d->ptr.extsize <= 0 || d->ptr.extsize > (1 << 30) ||
+        d->ptr.rawsize > (1 << 30) + 4)
+      return set_err("bad TOAST pointer sizes");
     *consumed = kExtPtr;
     return true;
   }
   if ((p[0] & 0xC0) == 0x40) {  // inline 4B compressed
+    if (p + 8 > end) return set_err("truncated inline datum header");
     uint32_t vs = varsize_4b(p);
-    if (p + vs > end) return set_err("truncated inline datum");
+    if (vs < 8 || p + vs > end) return set_err("truncated inline datum");
+    if (rd32(p + 4) > (1u << 30)) return set_err("bad inline raw size");
     d->external = false;
     d->inl = p;
     *consumed = vs;
@@ -181,7 +188,8 @@ static bool index_toast(DAReader* r) {
     const uint8_t* page = r->toast.data() + pg * kBlck;
     PageHdr h = page_header(page);
     if (h.special != kBlck) return set_err("THERE SHALL NOT BE INDICES (special space on TOAST page)");
-    if ((h.lower - kPageHeader) % kItemId) return set_err("bad TOAST line pointer area");
+    if (h.lower < kPageHeader || h.lower > kBlck || (h.lower - kPageHeader) % kItemId)
+      return set_err("bad TOAST line pointer area");
     const int n = (h.lower - kPageHeader) / kItemId;
     int64_t off = h.upper;
     for (int i = 0; i < n; ++i) {
@@ -189,11 +197,13 @@ static bool index_toast(DAReader* r) {
       if (off + kTupleHeader > kBlck) return set_err("TOAST item beyond page");
       const uint8_t* item = page + off;
       const uint8_t t_hoff = item[22];
+      if (off + t_hoff + 12 > kBlck) return set_err("TOAST chunk header beyond page");
       const uint8_t* tup = item + t_hoff;
       const uint32_t chunk_id = rd32(tup), chunk_seq = rd32(tup + 4);
       const uint8_t* cv = tup + 8;
       const uint32_t csize = varsize_4b(cv);
       if (cv[0] & 0xC0) return set_err("TOAST chunk must be a plain 4B varlena");
+      if (csize < 4) return set_err("TOAST chunk shorter than its header");
       if (off + t_hoff + 8 + csize > (uint32_t)kBlck) return set_err("TOAST chunk beyond page");
       if (want.count(chunk_id))
         r->chunks[chunk_id].push_back(Chunk{(int32_t)chunk_seq, cv + 4, csize - 4});
@@ -237,6 +247,7 @@ static bool detoast(const DAReader* r, const Datum& d, uint8_t* out, int64_t out
     std::memcpy(out, scratch->data(), (size_t)ext);
     return true;
   }
+  if (ext < 4) return set_err("external compressed datum shorter than its header");
   const uint32_t raw = rd32(scratch->data());
   if ((int64_t)raw != out_size) return set_err("external raw size does not match");
   if (cer_pglz_decompress(scratch->data() + 4, ext - 4, out, raw) < 0)

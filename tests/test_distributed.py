@@ -7,6 +7,7 @@ Model hopping must be transparent: final weights, optimizer state and the
 per-epoch metrics must agree.
 """
 
+import collections
 import json
 import os
 import socket
@@ -117,23 +118,38 @@ def _hop_worker(rank, world, port, outdir):
     g = torch.Generator().manual_seed(7)
     rows = {m: torch.randn(1000, generator=g) for m in range(6)}
     recv = {m: torch.full((1000,), float("nan")) for m in range(6)}
-    execute_moves(moves, rank, lambda m: rows[m], lambda m: recv[m])
+    execute_moves(moves, rank, lambda m: rows[m], lambda m: recv[m], check=True)
     got = {m: recv[m] for m in range(6) if dest[m] == rank and holder[m] != rank}
     ok = all(torch.equal(got[m], rows[m]) for m in got)
+    # debug hop check: a send buffer that changes while "in flight" (here: a
+    # different tensor the second time it is asked for) must be caught
+    from cerebro_ds_kpgi_amd.parallel.hop import HopChecksumError
+    asked = collections.Counter()
+
+    def racy(m):
+        asked[m] += 1
+        return rows[m] if asked[m] == 1 or rank != 0 else rows[m] + 1.0
+    caught = 0
+    try:
+        execute_moves(moves, rank, racy, lambda m: recv[m], check=True)
+    except HopChecksumError:
+        caught = 1
     with open(os.path.join(outdir, "hop_{}.txt".format(rank)), "w") as f:
-        f.write("{} {}".format(int(ok), len(got)))
+        f.write("{} {} {}".format(int(ok), len(got), caught))
     shutdown(ctx)
 
 
 def test_hop_bitwise(tmp_path):
     world = 3
     mp.spawn(_hop_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    total = 0
+    total = caught = 0
     for r in range(world):
-        ok, n = open(tmp_path / "hop_{}.txt".format(r)).read().split()
+        ok, n, c = open(tmp_path / "hop_{}.txt".format(r)).read().split()
         assert ok == "1"
         total += int(n)
+        caught += int(c)
     assert total == 4   # models 0, 1, 2, 4 change rank; 3 and 5 stay
+    assert caught >= 1  # rank 0's racing sends are detected by their receivers
 
 
 def test_checkpoint_layout_and_resume(tmp_path):
