@@ -44,6 +44,9 @@ class PackedNet(object):
     num_classes = 1000
     input_hw = 112
     input_c = 3
+    # False: the engine runs this architecture's step eagerly instead of
+    # replaying a captured HIP graph (runtime.group)
+    graph_safe = True
 
     def __init__(self):
         self._specs = []

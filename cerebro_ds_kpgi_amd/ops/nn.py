@@ -724,6 +724,23 @@ def cat_packed(xs, G):
     return torch.cat(parts, dim=-1).reshape(B, H, W, -1)
 
 
+class ReluAdd(torch.autograd.Function):
+    """y = relu(a + b) in fp32 with one rounding; backward da = db = dy * (y > 0)
+    (one saved tensor, no fp32 temporaries kept for autograd)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        y = torch.relu(a.float() + b.float()).to(a.dtype)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, = ctx.saved_tensors
+        g = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+        return g, g.clone()
+
+
 def relu_add(a, b):
     """relu(a + b) in fp32 with one rounding (BN-free residual join)."""
-    return torch.relu(a.float() + b.float()).to(a.dtype)
+    return ReluAdd.apply(a, b)

@@ -624,5 +624,8 @@ class MOPEngine(object):
                 if w.graph is not None:
                     w.graph.reset()
                     w.graph = None
+                if w.vgraph is not None:
+                    w.vgraph.reset()
+                    w.vgraph = None
         if self.o.trace and self.o.logs_root:
             self.tracer.dump(os.path.join(self.o.logs_root, "traces"))

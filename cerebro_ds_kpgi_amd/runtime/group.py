@@ -16,6 +16,7 @@ captured once in a HIP graph and replayed for the rest of the run.
 jobs, ``run_cerebro_standalone_helper.py:270-289``, ``ctq.py:110-121``.)
 """
 
+import os
 import time
 
 import torch
@@ -116,7 +117,9 @@ class _Working(object):
         self.vcursor = torch.zeros(1, dtype=torch.int32, device=g.device)
         self.vacc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
         self.graph = None
-        self.eager_only = False
+        self.vgraph = None        # validation step graph
+        self.veager = False       # validation step not capture safe
+        self.eager_only = not getattr(self.net, "graph_safe", True)
         self.eager_steps = 0
         self.jobs = []
         # called between backward and the optimizer (DDP gradient all-reduce)
@@ -202,16 +205,45 @@ class _Working(object):
             done += 1
         return done
 
-    def validate(self, nsteps):
+    def _vstep(self):
         g = self.group
+        gather_batch(g.store, False, self.part_of_row, self.vcursor, g.batch_size,
+                     self.vx, self.vy)
+        logits = self.net.forward(self.vx, False)
+        eval_metrics(logits, self.vy, self.vacc, self.G)
+        self.vcursor.add_(1)
+
+    def validate(self, nsteps):
+        """Forward-only passes over this round's validation rows.  Like the
+        training step, the validation step is captured once in a HIP graph
+        (after one eager step: kernel-variant tuning for the eval-path shapes)
+        and replayed; the device-side cursor advances inside the graph."""
         self.vcursor.zero_()
+        done = 0
         with torch.no_grad():
-            for _ in range(nsteps):
-                gather_batch(g.store, False, self.part_of_row, self.vcursor, g.batch_size,
-                             self.vx, self.vy)
-                logits = self.net.forward(self.vx, False)
-                eval_metrics(logits, self.vy, self.vacc, self.G)
-                self.vcursor.add_(1)
+            if not self.group.use_graphs or self.eager_only or not _VALID_GRAPH:
+                for _ in range(nsteps):
+                    self._vstep()
+                return
+            if self.vgraph is None and nsteps > 0:
+                take_fallbacks()
+                self._vstep()
+                done += 1
+                if take_fallbacks():
+                    self.veager = True
+                if done < nsteps and not self.veager:
+                    self.vgraph = torch.cuda.CUDAGraph()
+                    # share the training graph's memory pool (the two never run
+                    # concurrently)
+                    pool = self.graph.pool() if self.graph is not None else None
+                    with torch.cuda.graph(self.vgraph, pool=pool):
+                        self._vstep()
+            while done < nsteps:
+                if self.vgraph is not None and not self.veager:
+                    self.vgraph.replay()
+                else:
+                    self._vstep()
+                done += 1
 
     def read_metrics(self):
         """(train, valid) per row: dict(loss, top1, top5, n) — one host sync."""
@@ -225,6 +257,9 @@ class _Working(object):
                              "top5": float(a[2]) / n, "n": int(a[3])}
             out.append(rec)
         return out
+
+
+_VALID_GRAPH = os.environ.get("CER_VALID_GRAPH", "1") != "0"
 
 
 def now():
