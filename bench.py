@@ -75,9 +75,13 @@ def main():
     eng = MOPEngine(msts, ctx, opts)
     sync = (torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None))
 
-    # warm-up (includes HIP-graph capture), untimed
+    # warm-up (includes HIP-graph capture), untimed; then open every RCCL
+    # peer connection a hop may use, so no connection setup lands in the
+    # first timed hop
     if args.warmup > 0:
         eng.run_steps(args.warmup, args.steps_per_round)
+    from cerebro_ds_kpgi_amd.parallel.hop import warm_p2p
+    warm_p2p(ctx.world, ctx.rank, ctx.device)
     sync()
     ctx.barrier()
     sync()

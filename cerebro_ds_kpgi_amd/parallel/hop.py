@@ -111,3 +111,29 @@ def _post(moves, rank, send_buf, recv_buf, group):
     for r in reqs:
         r.wait()
     return len(ops)
+
+
+def warm_p2p(world, rank, device, group=None):
+    """Open every point-to-point connection this rank may use for a hop
+    (RCCL sets peer connections up lazily, on the first send/recv to a peer:
+    that setup must not land in the first real hop).  One tiny send/recv
+    with every other rank, as one batched group."""
+    if world <= 1:
+        return 0
+    ops = []
+    bufs = []
+    for peer in range(world):
+        if peer == rank:
+            continue
+        s = torch.full((16,), float(rank), device=device)
+        r = torch.empty(16, device=device)
+        bufs.append((s, r, peer))
+        ops.append(dist.P2POp(dist.isend, s, peer, group, tag=900000 + rank))
+        ops.append(dist.P2POp(dist.irecv, r, peer, group, tag=900000 + peer))
+    for q in dist.batch_isend_irecv(ops):
+        q.wait()
+    for s, r, peer in bufs:
+        if float(r[0]) != float(peer):
+            raise RuntimeError("p2p warm-up: rank {} got {} from {}".format(rank, float(r[0]), peer))
+    return len(bufs)
+

@@ -108,8 +108,10 @@ def _hop_worker(rank, world, port, outdir):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
-    from cerebro_ds_kpgi_amd.parallel.hop import execute_moves, plan_moves, validate_plan
+    from cerebro_ds_kpgi_amd.parallel.hop import (execute_moves, plan_moves, validate_plan,
+                                                  warm_p2p)
     ctx = init_distributed(device_type="cpu")
+    assert warm_p2p(world, rank, "cpu") == world - 1
     # 6 models on 3 ranks, arbitrary permutation incl. 2-cycles and a 3-cycle
     holder = {m: m % world for m in range(6)}
     dest = {0: 1, 1: 0, 2: 0, 3: 2, 4: 1, 5: 2}
