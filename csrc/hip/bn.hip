@@ -389,7 +389,7 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
 // stage 3: elementwise apply (scale/shift per channel computed once per thread)
 // ---------------------------------------------------------------------------
 // MODE 0: train fwd, ws = (mean, invstd); MODE 1: eval fwd from running stats
-template <int MODE, bool SC>
+template <int MODE, bool SC, int AU = 2>   // AU: rows in flight per thread
 __device__ __forceinline__ void apply_fwd_tile(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
@@ -414,7 +414,6 @@ __device__ __forceinline__ void apply_fwd_tile(
   bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
-  constexpr int AU = 2;     // rows in flight per thread
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
     float v[AU][VEC], rv[AU][VEC];
 #pragma unroll
@@ -438,17 +437,17 @@ __device__ __forceinline__ void apply_fwd_tile(
   }
 }
 
-template <int MODE>
+template <int MODE, int AU = 2>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
     Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
-  apply_fwd_tile<MODE, false>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
+  apply_fwd_tile<MODE, false, AU>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
                               Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
 }
 
-template <bool SC, int YM = YM_Y>
+template <bool SC, int YM = YM_Y, int AU = 2>
 __device__ __forceinline__ void apply_bwd_tile(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
@@ -473,7 +472,6 @@ __device__ __forceinline__ void apply_bwd_tile(
   if (YM == YM_Z) bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
-  constexpr int AU = 2;     // rows in flight per thread
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
     float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
 #pragma unroll
@@ -502,13 +500,13 @@ __device__ __forceinline__ void apply_bwd_tile(
   }
 }
 
-template <int YM>
+template <int YM, int AU = 2>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
     Strided gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
     int Cper, int rows_per_slab, int act, Map mp, Strided beta) {
-  apply_bwd_tile<false, YM>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
+  apply_bwd_tile<false, YM, AU>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
                             rows_per_slab, act, mp, blockIdx.x, blockIdx.y, beta);
 }
 
@@ -773,6 +771,16 @@ static int fold_max() {
 }
 CER_API void cer_bn_set_fold(int max_slabs) { g_fold_max = max_slabs; }
 
+// rows in flight per thread of the streaming apply kernels (CER_BN_AU: 2 or 4)
+static int g_apply_au = 0;
+static int apply_au() {
+  if (!g_apply_au) {
+    const char* e = getenv("CER_BN_AU");
+    g_apply_au = (e && atoi(e) == 4) ? 4 : 2;
+  }
+  return g_apply_au;
+}
+
 // ReLU mask recomputed from the BN input in backward (YM_Z); 0 = always read y
 static int g_zmask = 1;
 CER_API void cer_bn_set_zmask(int on) { g_zmask = on; }
@@ -884,9 +892,16 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
                                                           M, C, Cper, eps, momentum);
-  bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                           Strided{gamma, gamma_stride},
-                                           Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
+  if (apply_au() == 4)
+    bn_apply_fwd<0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                                Strided{gamma, gamma_stride},
+                                                Strided{beta, beta_stride}, M, C, Cper, arows,
+                                                act, mp);
+  else
+    bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                             Strided{gamma, gamma_stride},
+                                             Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                             mp);
   return (int)hipGetLastError();
 }
 
@@ -925,9 +940,16 @@ CER_API int cer_bn_apply_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   dim3 ag;
   int arows;
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                           Strided{gamma, gamma_stride},
-                                           Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
+  if (apply_au() == 4)
+    bn_apply_fwd<0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                                Strided{gamma, gamma_stride},
+                                                Strided{beta, beta_stride}, M, C, Cper, arows,
+                                                act, mp);
+  else
+    bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                             Strided{gamma, gamma_stride},
+                                             Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                             mp);
   return (int)hipGetLastError();
 }
 
@@ -1007,15 +1029,28 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   }
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
-  if (ym == YM_NONE)
-    bn_apply_bwd<YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
-                                                   C, Cper, arows, act, mp, bs);
-  else if (ym == YM_Z)
-    bn_apply_bwd<YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                Cper, arows, act, mp, bs);
-  else
-    bn_apply_bwd<YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                Cper, arows, act, mp, bs);
+  if (ym == YM_NONE) {
+    if (apply_au() == 4)
+      bn_apply_bwd<YM_NONE, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+                                                     C, Cper, arows, act, mp, bs);
+    else
+      bn_apply_bwd<YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+                                                     C, Cper, arows, act, mp, bs);
+  } else if (ym == YM_Z) {
+    if (apply_au() == 4)
+      bn_apply_bwd<YM_Z, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                  Cper, arows, act, mp, bs);
+    else
+      bn_apply_bwd<YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                  Cper, arows, act, mp, bs);
+  } else {
+    if (apply_au() == 4)
+      bn_apply_bwd<YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                  Cper, arows, act, mp, bs);
+    else
+      bn_apply_bwd<YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                  Cper, arows, act, mp, bs);
+  }
   return (int)hipGetLastError();
 }
 
