@@ -528,14 +528,29 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   const int c0 = cbk * mp.cb + tc * VEC;
   float a[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, b[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (c0 < C) {
-    for (int sl = tr; sl < nslab; sl += mp.tr_n) {
-      const float4* pa = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + c0);
-      const float4* pb = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + C + c0);
-      const float4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-      a[0] += a0.x; a[1] += a0.y; a[2] += a0.z; a[3] += a0.w;
-      a[4] += a1.x; a[5] += a1.y; a[6] += a1.z; a[7] += a1.w;
-      b[0] += b0.x; b[1] += b0.y; b[2] += b0.z; b[3] += b0.w;
-      b[4] += b1.x; b[5] += b1.y; b[6] += b1.z; b[7] += b1.w;
+    // FU slabs' loads issued before any add (the partials were just written
+    // by other CUs: each load is an L2/MALL round trip)
+    constexpr int FU = 4;
+    for (int sl0 = tr; sl0 < nslab; sl0 += FU * mp.tr_n) {
+      float4 a0[FU], a1[FU], b0[FU], b1[FU];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        const int sl = sl0 + u * mp.tr_n;
+        if (sl < nslab) {
+          const float4* pa = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + c0);
+          const float4* pb = reinterpret_cast<const float4*>(part + (int64_t)sl * 2 * C + C + c0);
+          a0[u] = pa[0]; a1[u] = pa[1]; b0[u] = pb[0]; b1[u] = pb[1];
+        } else {
+          a0[u] = a1[u] = b0[u] = b1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < FU; ++u) {
+        a[0] += a0[u].x; a[1] += a0[u].y; a[2] += a0[u].z; a[3] += a0[u].w;
+        a[4] += a1[u].x; a[5] += a1[u].y; a[6] += a1[u].z; a[7] += a1[u].w;
+        b[0] += b0[u].x; b[1] += b0[u].y; b[2] += b0[u].z; b[3] += b0[u].w;
+        b[4] += b1[u].x; b[5] += b1[u].y; b[6] += b1[u].z; b[7] += b1[u].w;
+      }
     }
   }
   float* rs = red;
