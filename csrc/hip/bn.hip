@@ -786,6 +786,19 @@ static int fold_max() {
 }
 CER_API void cer_bn_set_fold(int max_slabs) { g_fold_max = max_slabs; }
 
+// minimum rows per block of a folded apply: every block re-reads the layer's
+// partials, so fewer, fatter blocks cut the redundant L2 traffic
+// (CER_BN_FOLD_ROWS, default 16 = the plain apply grid)
+static int g_fold_rows = 0;
+static int fold_rows() {
+  if (!g_fold_rows) {
+    const char* e = getenv("CER_BN_FOLD_ROWS");
+    g_fold_rows = e ? atoi(e) : 16;
+    if (g_fold_rows < 1) g_fold_rows = 16;
+  }
+  return g_fold_rows;
+}
+
 // rows in flight per thread of the streaming apply kernels (CER_BN_AU: 2 or 4)
 static int g_apply_au = 0;
 static int apply_au() {
@@ -879,10 +892,13 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     nslab = (int)rg.y;
   }
   if (nslab <= fold_max()) {
-    bn_apply_fwd_fold<<<ag, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
+    dim3 fg;
+    int frows;
+    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
+    bn_apply_fwd_fold<<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
                                                rstat_stride, eps, momentum, x, res, y,
                                                Strided{gamma, gamma_stride},
-                                               Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                               Strided{beta, beta_stride}, M, C, Cper, frows, act,
                                                mp);
     return (int)hipGetLastError();
   }
@@ -1027,19 +1043,22 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
                                                     act, mp, gs, bs, Cper);
   }
   if (nslab <= fold_max()) {
+    dim3 fg;
+    int frows;
+    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
     if (ym == YM_NONE)
-      bn_apply_bwd_fold<YM_NONE><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                           grad_stride, dy, x, y, mean, invstd, gs,
-                                                          bs, dx, dres, M, C, Cper, arows, act,
+                                                          bs, dx, dres, M, C, Cper, frows, act,
                                                           mp);
     else if (ym == YM_Z)
-      bn_apply_bwd_fold<YM_Z><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
-                                                       dx, dres, M, C, Cper, arows, act, mp);
+                                                       dx, dres, M, C, Cper, frows, act, mp);
     else
-      bn_apply_bwd_fold<YM_Y><<<ag, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<YM_Y><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
-                                                       dx, dres, M, C, Cper, arows, act, mp);
+                                                       dx, dres, M, C, Cper, frows, act, mp);
     return (int)hipGetLastError();
   }
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
