@@ -21,7 +21,7 @@ def fwd(self, x, training):
     if variant != "nopool":
         x = P.maxpool2d(x, 3, 2, 1)
     for i, blk in enumerate(self.blocks):
-        if variant == "noblocks" and i > 0:
+        if variant in ("noblocks", "pad3", "pad2", "pad1") and i > 0:
             break
         sc = self._cba(x, blk["cs"], 0) if "cs" in blk else x
         h = self._cba(x, blk["c1"], 1)
@@ -36,11 +36,20 @@ def fwd(self, x, training):
     if variant == "noblocks":
         x = self._cba(x, self.blocks[-1]["c3"], 0) if False else x
     x = P.global_avgpool(x)
-    if variant == "noblocks":
+    if variant in ("noblocks", "pad3", "pad2", "pad1"):
         x = torch.nn.functional.pad(x, (0, self.G * 2048 - x.shape[1])) if x.shape[1] != self.G * 2048 else x
     return self.dense(x, self.fc)
 
 
+if variant.startswith("pad"):
+    _orig_init = zoo.PackedResNet50NoBN.__init__
+
+    def _init(self, *a, **k):
+        _orig_init(self, *a, **k)
+        self.conv1.pad = int(variant[3:])
+    zoo.PackedResNet50NoBN.__init__ = _init
+    zoo.PackedResNet50NoBN.forward = fwd
+    variant_fwd = "noblocks"
 if variant == "heinit":
     zoo.PackedResNet50NoBN.KI = "he"
 elif variant == "anchorless":
