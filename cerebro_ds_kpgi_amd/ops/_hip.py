@@ -264,21 +264,28 @@ def _select(op, key, launch, after_tune=None):
     lib().cer_conv_set_variant(op, v)
 
 
-def _autotune(op, launch, reps=3, after=None):
+def _autotune(op, launch, reps=3, passes=None, after=None):
+    """Time every variant (``reps`` back-to-back launches after a warm one)
+    over ``passes`` interleaved passes and keep each variant's best pass:
+    one noisy measurement no longer pins a slow kernel for the whole run."""
     L = lib()
-    best, best_v = None, -1
-    for v in range(NVARIANTS):
-        L.cer_conv_set_variant(op, v)
-        launch()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(reps):
+    if passes is None:
+        passes = int(os.environ.get("CER_TUNE_PASSES", "2"))
+    best_t = [None] * NVARIANTS
+    for _ in range(max(1, passes)):
+        for v in range(NVARIANTS):
+            L.cer_conv_set_variant(op, v)
             launch()
-        e.record()
-        e.synchronize()
-        t = s.elapsed_time(e)
-        if best is None or t < best:
-            best, best_v = t, v
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                launch()
+            e.record()
+            e.synchronize()
+            t = s.elapsed_time(e)
+            if best_t[v] is None or t < best_t[v]:
+                best_t[v] = t
+    best_v = min(range(NVARIANTS), key=lambda v: best_t[v])
     if after is not None:
         after()
     return best_v
