@@ -45,6 +45,10 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no_graphs", action="store_true")
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--workload", default="headline", choices=["headline", "criteo16", "hetero8"],
+                    help="headline = BASELINE.json's metric; criteo16 / hetero8 = the other "
+                         "BASELINE configs (16-config Criteo confA grid; {ResNet-50, VGG-16} x "
+                         "{lr, batch}), reported as diag_* metrics")
     ap.add_argument("--configs", type=int, default=0,
                     help="diagnostic: train only the first K configs (per-GPU work of N = 8/K "
                          "GPUs); the headline number always uses all 8")
@@ -60,13 +64,18 @@ def main():
     ctx = init_distributed()
     N = ctx.world
     backend = set_backend(args.backend)
-    grid = dict(cat.param_grid_scalability)
-    grid["model"] = [args.model]
+    if args.workload == "criteo16":
+        grid = dict(cat.param_grid_criteo)            # 2 lr x 2 lambda x 4 batch = 16
+    elif args.workload == "hetero8":
+        grid = dict(cat.param_grid_hetero_rv)         # 2 lr x 2 batch x {resnet50, vgg16}
+    else:
+        grid = dict(cat.param_grid_scalability)
+        grid["model"] = [args.model]
     msts = get_msts(grid)
     if args.configs:
         msts = msts[:args.configs]
     S = len(msts)
-    B = msts[0]["batch_size"]
+    B = max(m["batch_size"] for m in msts)
     n_train = max(args.train_per_partition, B * args.steps_per_round)
     n_valid = max(B, int(round(n_train * cat.IMAGENET_VALID_TOTAL / cat.IMAGENET_TRAIN_TOTAL)))
     opts = EngineOptions(slots_per_gpu=max(1, S // N), scheduler="rotation", n_train=n_train,
@@ -98,25 +107,37 @@ def main():
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(N)
         out = {
-            "metric": "agg_train_images_per_sec_8cfg_resnet50_mop" if S == 8 else
-                      "diag_train_images_per_sec_{}cfg_resnet50_mop".format(S),
+            "metric": ("agg_train_images_per_sec_8cfg_resnet50_mop"
+                       if S == 8 and args.workload == "headline" else
+                       "diag_train_{}_per_sec_{}cfg_{}_mop".format(
+                           "samples" if args.workload == "criteo16" else "images", S,
+                           {"headline": "resnet50", "criteo16": "criteo_confA",
+                            "hetero8": "resnet50_vgg16"}[args.workload])),
             "value": round(value, 2),
-            "unit": "images/s",
+            "unit": "samples/s" if args.workload == "criteo16" else "images/s",
             "n_gpus": N,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": round(value / base, 3) if base else None,
+            "vs_baseline": (round(value / base, 3) if base and args.workload == "headline"
+                            else None),
             "dtype": args.dtype,
             "data": "synthetic",
-            "config": {"model": args.model, "global_batch": S * B, "seq_len": None,
+            "config": {"model": {"headline": args.model, "criteo16": "confA",
+                                 "hetero8": "resnet50+vgg16"}[args.workload],
+                       "global_batch": sum(m["batch_size"] for m in msts), "seq_len": None,
                        "parallelism": "mop{}x{}".format(N, max(1, S // N)),
-                       "configs": S, "batch_per_config": B, "input": "112x112x3",
+                       "configs": S,
+                       "batch_per_config": sorted({m["batch_size"] for m in msts}),
+                       "input": "7306-d sparse (39 ids)" if args.workload == "criteo16"
+                       else "112x112x3",
                        "partitions": eng.P},
-            "projected_makespan_s": round(S * TRAIN_IMAGES_PER_EPOCH / value, 1),
-            "baseline_makespan_s": {1: 35440, 2: 17754, 4: 10229, 8: 5715}.get(N),
+            "projected_makespan_s": round(S * (cat.CRITEO_TOTAL if args.workload == "criteo16"
+                                               else TRAIN_IMAGES_PER_EPOCH) / value, 1),
+            "baseline_makespan_s": ({1: 35440, 2: 17754, 4: 10229, 8: 5715}.get(N)
+                                    if args.workload == "headline" else None),
             "backend": backend,
             "hop_bytes_rank0": eng.hop_bytes,
         }
