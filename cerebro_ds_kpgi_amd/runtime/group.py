@@ -173,7 +173,8 @@ class _Working(object):
             return nsteps
         if self.graph is None:
             # eager warm-up on a side stream (real steps), then capture once
-            s = torch.cuda.Stream()
+            s = (torch.cuda.Stream() if os.environ.get("CER_WARM_SIDE", "1") == "1"
+                 else torch.cuda.current_stream())
             s.wait_stream(torch.cuda.current_stream())
             take_fallbacks()
             with torch.cuda.stream(s):

@@ -76,5 +76,7 @@ msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": 8, "model": "r
         for lr in (1e-4, 1e-5)]
 eng = MOPEngine(msts, init_distributed(), EngineOptions(
     n_train=48, n_valid=16, slots_per_gpu=2, verbose=False, ckpt_every="none"))
+for grp in eng.groups.values():
+    grp.warmup_eager = int(os.environ.get("DBG_WARM", grp.warmup_eager))
 eng.run(1)
 print("variant", variant, "first non-finite step", state["first_bad"], "of", state["step"])
