@@ -13,12 +13,35 @@
 // without a memset per layer.
 #include "common.h"
 
+#include <stdlib.h>
+
+// streamed-once operands: non-temporal loads / stores (NT) keep them from
+// evicting the L2 / MALL lines the next forward reads (CER_ADAM_NT)
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float4* p) {
+  if (NT) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float4* p, float4 v) {
+  if (NT) {
+    const f4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 __global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < G) state[g * row_stride + off_step] += 1.0f;
 }
 
-template <bool WRITE_BF16>
+template <bool WRITE_BF16, bool NT = false>
 __global__ __launch_bounds__(256) void adam_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
@@ -39,11 +62,12 @@ __global__ __launch_bounds__(256) void adam_kernel(
   float4* mp = reinterpret_cast<float4*>(row + off_m + i);
   float4* vp = reinterpret_cast<float4*>(row + off_v + i);
   float4* gp = reinterpret_cast<float4*>(grad + g * grad_stride + i);
-  float4 p[2] = {pp[0], pp[1]}, m[2] = {mp[0], mp[1]}, v[2] = {vp[0], vp[1]};
-  const float4 gr[2] = {gp[0], gp[1]};
+  float4 p[2] = {ld4<NT>(pp), ld4<NT>(pp + 1)}, m[2] = {ld4<NT>(mp), ld4<NT>(mp + 1)},
+         v[2] = {ld4<NT>(vp), ld4<NT>(vp + 1)};
+  const float4 gr[2] = {ld4<NT>(gp), ld4<NT>(gp + 1)};
   if (zero_grad) {
-    gp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-    gp[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    st4<NT>(gp, make_float4(0.f, 0.f, 0.f, 0.f));
+    st4<NT>(gp + 1, make_float4(0.f, 0.f, 0.f, 0.f));
   }
   float* pf = reinterpret_cast<float*>(p);
   float* mf = reinterpret_cast<float*>(m);
@@ -57,9 +81,9 @@ __global__ __launch_bounds__(256) void adam_kernel(
     float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
     pf[k] -= step_size * mf[k] / denom;
   }
-  pp[0] = p[0]; pp[1] = p[1];
-  mp[0] = m[0]; mp[1] = m[1];
-  vp[0] = v[0]; vp[1] = v[1];
+  st4<NT>(pp, p[0]); st4<NT>(pp + 1, p[1]);
+  st4<NT>(mp, m[0]); st4<NT>(mp + 1, m[1]);
+  st4<NT>(vp, v[0]); st4<NT>(vp + 1, v[1]);
   if (WRITE_BF16) {
     uint4 o;
     o.x = pack_bf2(pf[0], pf[1]);
@@ -78,7 +102,17 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
   if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
-  if (work)
+  static int nt = -1;
+  if (nt < 0) {
+    const char* e = getenv("CER_ADAM_NT");
+    nt = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (work && nt)
+    adam_kernel<true, true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
+                                                       off_step, grad, grad_stride, zero_grad,
+                                                       work, work_stride, lr, wd, b1, b2, eps,
+                                                       l2);
+  else if (work)
     adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
                                                  off_step, grad, grad_stride, zero_grad, work,
                                                  work_stride,
