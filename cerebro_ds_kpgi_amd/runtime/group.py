@@ -25,7 +25,7 @@ from ..data.store import gather_batch, input_buffers
 from ..models import create_model_from_mst
 from ..ops.loss import eval_metrics, softmax_ce
 from ..ops import streams
-from ..ops.backend import take_fallbacks
+from ..ops.backend import get_backend, take_fallbacks
 from ..ops.optim import optimizer_step
 from ..utils.logging import log_once
 from .arena import Arena
@@ -43,7 +43,13 @@ class PackGroup(object):
         self.store = store
         self.device = torch.device(device)
         self.dtype = compute_dtype
-        self.use_graphs = use_graphs and self.device.type == "cuda"
+        # HIP graphs only over our HIP kernels: with the PyTorch oracle backend
+        # (MIOpen convolutions) the second replay of a captured step already
+        # gives non-finite weights for every architecture
+        # (scripts/debug/nobn_bisect.py, CEREBRO_BACKEND=torch), so the oracle
+        # path always runs eagerly
+        self.use_graphs = (use_graphs and self.device.type == "cuda" and
+                           get_backend() == "hip")
         self.l2 = l2
         self.warmup_eager = warmup_eager
         proto = create_model_from_mst({"model": self.arch})

@@ -23,6 +23,8 @@ def fwd(self, x, training):
     for i, blk in enumerate(self.blocks):
         if variant in ("noblocks", "pad3", "pad2", "pad1") and i > 0:
             break
+        if variant.startswith("nb") and i >= int(variant[2:]):
+            break
         sc = self._cba(x, blk["cs"], 0) if "cs" in blk else x
         h = self._cba(x, blk["c1"], 1)
         h = self._cba(h, blk["c2"], 1)
@@ -36,7 +38,7 @@ def fwd(self, x, training):
     if variant == "noblocks":
         x = self._cba(x, self.blocks[-1]["c3"], 0) if False else x
     x = P.global_avgpool(x)
-    if variant in ("noblocks", "pad3", "pad2", "pad1"):
+    if variant in ("noblocks", "pad3", "pad2", "pad1") or variant.startswith("nb"):
         x = torch.nn.functional.pad(x, (0, self.G * 2048 - x.shape[1])) if x.shape[1] != self.G * 2048 else x
     return self.dense(x, self.fc)
 
@@ -56,6 +58,13 @@ elif variant == "anchorless":
     pass
 elif variant != "orig":
     zoo.PackedResNet50NoBN.forward = fwd
+if variant.startswith("nb"):
+    zoo.PackedResNet50NoBN.forward = fwd
+if os.environ.get("DBG_PIN"):
+    from cerebro_ds_kpgi_amd.ops import _hip
+    for kv in os.environ["DBG_PIN"].split(","):
+        op, v = kv.split(":")
+        _hip.conv_set_variant(int(op), int(v))
 orig_t = G._Working.train_steps
 state = {"first_bad": None, "step": 0}
 
@@ -72,7 +81,8 @@ def t(self, n):
 
 
 G._Working.train_steps = t
-msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": 8, "model": "resnet50_nobn"}
+msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": 8,
+         "model": os.environ.get("DBG_MODEL", "resnet50_nobn")}
         for lr in (1e-4, 1e-5)]
 eng = MOPEngine(msts, init_distributed(), EngineOptions(
     n_train=48, n_valid=16, slots_per_gpu=2, verbose=False, ckpt_every="none"))
