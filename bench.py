@@ -42,7 +42,9 @@ def main():
     ap.add_argument("--steps_per_round", type=int, default=20)
     ap.add_argument("--train_per_partition", type=int, default=8192)
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="fp32", choices=["bf16", "fp32"],
+                    help="fp32 = the reference's training precision (headline); bf16 is "
+                         "reported as a diag_ metric")
     ap.add_argument("--no_graphs", action="store_true")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--workload", default="headline", choices=["headline", "criteo16", "hetero8"],

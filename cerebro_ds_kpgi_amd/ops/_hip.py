@@ -8,6 +8,11 @@ silent fallback on a GPU.
 
 ``IMPLEMENTED`` lists the ops with a native path; ``ops.backend.use_hip``
 routes only those here.
+
+Every activation op exists in two storage dtypes: the bf16 compute mode and
+the reference-precision fp32 mode (entry point suffix ``_f32``; convolutions
+run as 3-pass split-bf16 MFMA GEMMs with fp32 accumulation, csrc/hip/conv.hip).
+``_fn(name, t)`` picks the entry point matching tensor ``t``'s dtype.
 """
 
 import ctypes
@@ -47,11 +52,22 @@ def lib():
                                .format(LIB_PATH))
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         for name, args in _SIGS.items():
-            fn = getattr(L, name)
-            fn.argtypes = args
-            fn.restype = c_i64 if name in _RET_I64 else c_i
+            for nm in (name, name + "_f32"):
+                if nm != name and not hasattr(L, nm):
+                    continue
+                fn = getattr(L, nm)
+                fn.argtypes = args
+                fn.restype = c_i64 if name in _RET_I64 else c_i
         _LIB = L
     return _LIB
+
+
+def _fn(name, t):
+    """Entry point ``name`` for the storage dtype of tensor ``t``."""
+    if t.dtype == torch.float32:
+        return getattr(lib(), name + "_f32")
+    assert t.dtype == torch.bfloat16, t.dtype
+    return getattr(lib(), name)
 
 
 def _stream():
@@ -97,6 +113,13 @@ def softmax_ce_fwd(logits, labels, acc, G, need_grad=True):
     B, GN = logits.shape
     N = GN // G
     loss = torch.empty(G, dtype=torch.float32, device=logits.device)
+    if logits.dtype == torch.float32:
+        # reference-precision mode: fp32 dlogits
+        d = torch.empty((B, GN), dtype=torch.float32, device=logits.device) if need_grad else None
+        rc = lib().cer_softmax_ce_f32(_ptr(logits), _ptr(labels.contiguous()), _ptr(acc),
+                                      _ptr(loss), _ptr(d), B, G, N, _stream())
+        _check(rc, "cer_softmax_ce_f32")
+        return loss, d
     d = torch.empty((B, GN), dtype=torch.bfloat16, device=logits.device) if need_grad else None
     is_bf16 = 1 if logits.dtype == torch.bfloat16 else 0
     if not is_bf16 and logits.dtype != torch.float32:
@@ -122,13 +145,13 @@ def _norm(device):
 
 
 def gather_images(X, Y, perm, part_of_row, cursor, B, x_out, y_out):
-    assert x_out.dtype == torch.bfloat16 and x_out.is_contiguous()
+    assert x_out.dtype in (torch.bfloat16, torch.float32) and x_out.is_contiguous()
     P, n, H, W, C = X.shape
     assert C == 3 and perm.shape == (P, n)
     G = part_of_row.shape[0]
     assert x_out.shape == (B, H, W, G * 3)
     mean, inv = _norm(X.device)
-    rc = lib().cer_gather_images(_ptr(X), _ptr(Y), _ptr(perm), _ptr(part_of_row), _ptr(cursor),
+    rc = _fn("cer_gather_images", x_out)(_ptr(X), _ptr(Y), _ptr(perm), _ptr(part_of_row), _ptr(cursor),
                                  _ptr(x_out), _ptr(y_out), n, H * W, G, B,
                                  ctypes.cast(mean, c_p), ctypes.cast(inv, c_p), _stream())
     _check(rc, "cer_gather_images")
@@ -189,7 +212,10 @@ _SIGS.update({
     "cer_gavgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_bias_act_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_bias_act_bwd": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
+    "cer_softmax_ce_f32": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
+    "cer_conv_dgrad_bnbwd_f32": None,
 })
+_SIGS.pop("cer_conv_dgrad_bnbwd_f32")
 IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
 
 _SIGS2 = {
@@ -212,8 +238,15 @@ def _act_code(a):
     return 1 if a else 0
 
 
-def _bf16(t):
-    assert t.dtype == torch.bfloat16, t.dtype
+def _act(t):
+    """Activation operand: bf16 (compute mode) or fp32 (reference precision)."""
+    assert t.dtype in (torch.bfloat16, torch.float32), t.dtype
+    return t.contiguous()
+
+
+def _same(t, ref):
+    """Operand that must share ``ref``'s storage dtype."""
+    assert t.dtype == ref.dtype, (t.dtype, ref.dtype)
     return t.contiguous()
 
 
@@ -251,29 +284,39 @@ def _splitk_ready(device):
     _SPLITK["_current"] = key
 
 
-def _select(op, key, launch, after_tune=None):
+# fp32 mode: register-staged 3-pass kernels only (an LDS-DMA id maps to its
+# register-staged twin in conv.hip), so only these ids are distinct
+FP32_VARIANTS = (0, 1, 2, 6, 7, 8)
+
+
+def _select(op, key, launch, dtype, after_tune=None):
+    """Pin the kernel variant of conv problem ``key`` (tuned once per problem
+    and storage dtype)."""
     if op in _PINNED:
         lib().cer_conv_set_variant(op, _PINNED[op])
         return
+    key = (str(dtype),) + tuple(key)
     v = _TUNED.get((op, key))
     if v is None:
         v = -1
         if _tune_enabled() and not torch.cuda.is_current_stream_capturing():
-            v = _autotune(op, launch, after=after_tune)
+            cands = FP32_VARIANTS if dtype == torch.float32 else range(NVARIANTS)
+            v = _autotune(op, launch, after=after_tune, variants=cands)
         _TUNED[(op, key)] = v
     lib().cer_conv_set_variant(op, v)
 
 
-def _autotune(op, launch, reps=3, passes=None, after=None):
+def _autotune(op, launch, reps=3, passes=None, after=None, variants=None):
     """Time every variant (``reps`` back-to-back launches after a warm one)
     over ``passes`` interleaved passes and keep each variant's best pass:
     one noisy measurement no longer pins a slow kernel for the whole run."""
     L = lib()
     if passes is None:
         passes = int(os.environ.get("CER_TUNE_PASSES", "2"))
+    variants = list(range(NVARIANTS) if variants is None else variants)
     best_t = [None] * NVARIANTS
     for _ in range(max(1, passes)):
-        for v in range(NVARIANTS):
+        for v in variants:
             L.cer_conv_set_variant(op, v)
             launch()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -285,7 +328,7 @@ def _autotune(op, launch, reps=3, passes=None, after=None):
             t = s.elapsed_time(e)
             if best_t[v] is None or t < best_t[v]:
                 best_t[v] = t
-    best_v = min(range(NVARIANTS), key=lambda v: best_t[v])
+    best_v = min(variants, key=lambda v: best_t[v])
     if after is not None:
         after()
     return best_v
@@ -300,16 +343,16 @@ def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, H
                      act):
     _splitk_ready(x.device)
     def launch():
-        rc = lib().cer_conv_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
+        rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
                                 _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
         _check(rc, "cer_conv_fwd")
-    _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
 
 
 def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     """y = act(conv(x, W) + b): bias and activation fused in the GEMM epilogue."""
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
@@ -320,7 +363,7 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
         # narrow-input stem (e.g. ResNet's 7x7/2 on RGB in validation): the
         # pixel-pair MFMA path instead of the element-gather fallback
         return stem_fwd_stats(x, wref, stride, pad)[0]
-    y = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
     _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs, act)
@@ -330,14 +373,14 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
 def conv2d_fwd_stats(x, wref, stride, pad):
     """z = conv(x, W) plus the BN (sum, sum^2) per-slab partials of z, computed
     in the GEMM epilogue.  Returns (z, part, nslab)."""
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
     assert GC == G * cin, (x.shape, wref.spec.shape, G)
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
-    z = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
+    z = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
     C = G * cout
     M = B * Ho * Wo
     part = torch.empty(int(lib().cer_conv_stats_floats(M, C)), dtype=torch.float32,
@@ -347,11 +390,11 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _splitk_ready(x.device)
 
     def launch():
-        rc = lib().cer_conv_fwd_stats(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride,
+        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride,
                                       pad, _ptr(z), Ho, Wo, _ptr(part), ctypes.byref(nslab),
                                       _stream())
         _check(rc, "cer_conv_fwd_stats")
-    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch)
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
     return z, part, nslab.value
 
@@ -391,7 +434,7 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     epilogue of the last tile of each channel column) then one BN-apply pass.
     Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4 the
     repacked stem input (stem path) or None."""
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
@@ -401,7 +444,7 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     dev = x.device
     L = lib()
     _splitk_ready(dev)
-    z = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=dev)
+    z = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=dev)
     part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dev)
     mean = torch.empty(C, dtype=torch.float32, device=dev)
     invstd = torch.empty(C, dtype=torch.float32, device=dev)
@@ -413,17 +456,18 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     rvp, _ = rvref.master_ptr()
     nslab = ctypes.c_int(0)
     x4 = wpk = None
+    fused_fin = _FUSED_FINALIZE and x.dtype == torch.bfloat16   # bf16 kernels only
     if stem:
-        x4 = torch.empty((G, B, H, W, 4), dtype=torch.bfloat16, device=dev)
-        wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.bfloat16,
+        x4 = torch.empty((G, B, H, W, 4), dtype=x.dtype, device=dev)
+        wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
                           device=dev)
 
         def tune():        # statistics-only twin (no running-stat side effects)
-            _check(lib().cer_stem_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
+            _check(_fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                       stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
                                       _ptr(part), ctypes.byref(nslab), _stream()), "cer_stem_fwd")
-        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), tune)
-        if not _FUSED_FINALIZE:
+        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), tune, x.dtype)
+        if not fused_fin:
             tune()
             return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                                  momentum, eps) + (x4,)
@@ -434,11 +478,11 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
         _check(rc, "cer_stem_fwd_bnstat")
     else:
         def tune():
-            _check(lib().cer_conv_fwd_stats(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
+            _check(_fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                             stride, pad, _ptr(z), Ho, Wo, _ptr(part),
                                             ctypes.byref(nslab), _stream()), "cer_conv_fwd_stats")
-        _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), tune)
-        if not _FUSED_FINALIZE:
+        _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), tune, x.dtype)
+        if not fused_fin:
             tune()
             return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                                  momentum, eps) + (None,)
@@ -450,8 +494,8 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     y = torch.empty_like(z)
     gp, gs = gref.work_ptr()
     bp, bs = bref.work_ptr()
-    res = _bf16(residual) if residual is not None else None
-    rc = L.cer_bn_apply_fwd(_ptr(z), _ptr(res), _ptr(y), _ptr(ws), c_p(gp), gs, c_p(bp), bs, M,
+    res = _same(residual, x) if residual is not None else None
+    rc = _fn("cer_bn_apply_fwd", z)(_ptr(z), _ptr(res), _ptr(y), _ptr(ws), c_p(gp), gs, c_p(bp), bs, M,
                             C, cout, _act_code(act), _stream())
     _check(rc, "cer_bn_apply_fwd")
     return y, z, mean, invstd, x4
@@ -466,16 +510,16 @@ def stem_ok(x, wref, stride, pad):
 def stem_fwd_stats(x, wref, stride, pad):
     """Stem conv via the repacked pixel-pair geometry, with BN partials.
     Returns (z, part, nslab, x4) — x4 (the repacked input) feeds the wgrad."""
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
-    z = torch.empty((B, Ho, Wo, G * cout), dtype=torch.bfloat16, device=x.device)
-    x4 = torch.empty((G, B, H, W, 4), dtype=torch.bfloat16, device=x.device)
+    z = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
+    x4 = torch.empty((G, B, H, W, 4), dtype=x.dtype, device=x.device)
     L = lib()
-    wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.bfloat16,
+    wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
                       device=x.device)
     part = torch.empty(int(L.cer_conv_stats_floats(B * Ho * Wo, G * cout)), dtype=torch.float32,
                        device=x.device)
@@ -483,17 +527,17 @@ def stem_fwd_stats(x, wref, stride, pad):
     wp, ws = wref.work_ptr()
 
     def launch():
-        rc = lib().cer_stem_fwd(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
+        rc = _fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
                                 _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
                                 ctypes.byref(nslab), _stream())
         _check(rc, "cer_stem_fwd")
-    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch)
+    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype)
     launch()
     return z, part, nslab.value, x4
 
 
 def stem_wgrad(x4, dy, wref, pad):
-    dy = _bf16(dy)
+    dy = _same(dy, x4)
     G, B, H, W, _ = x4.shape
     _, Ho, Wo, _ = dy.shape
     cout, kh, kw, cin = wref.spec.shape
@@ -503,10 +547,10 @@ def stem_wgrad(x4, dy, wref, pad):
     gp, gs = wref.grad_ptr()
 
     def launch():
-        rc = lib().cer_stem_wgrad(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, pad,
+        rc = _fn("cer_stem_wgrad", x4)(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, pad,
                                   _ptr(dwp), c_p(gp), gs, _stream())
         _check(rc, "cer_stem_wgrad")
-    _select(2, ("stem", B, H, W, cin, cout, kh, kw, pad, G), launch)
+    _select(2, ("stem", B, H, W, cin, cout, kh, kw, pad, G), launch, dy.dtype)
     launch()
 
 
@@ -515,32 +559,32 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
-    wt = torch.empty(n_wt, dtype=torch.bfloat16, device=dy.device)
+    wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
 
     def launch():
-        rc = lib().cer_conv_dgrad(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
+        rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
                                   kw, stride, pad, _ptr(dx), H, W, _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
-            launch)
+            launch, dy.dtype)
     launch()
 
 
 def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
-    """dx of the conv; ``addend`` (same shape as dx, bf16) is added in the
+    """dx of the conv; ``addend`` (same shape and dtype as dx) is added in the
     GEMM epilogue (the other consumer's gradient of a shared input).
     ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
     output y this conv consumed — the epilogue also computes that BN's
     backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink)."""
-    dy = _bf16(dy)
+    dy = _act(dy)
     B, Ho, Wo, _ = dy.shape
     _, H, W, _ = xshape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
-    dx = torch.empty((B, H, W, G * cin), dtype=torch.bfloat16, device=dy.device)
+    dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
     wp, ws = wref.work_ptr()
     if addend is not None:
-        addend = _bf16(addend).contiguous()
+        addend = _same(addend, dy)
         assert addend.shape == dx.shape
     if bnlink is None:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
@@ -553,7 +597,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     nslab = ctypes.c_int(0)
     gp, gs = link.gref.work_ptr()
     bp, bs = link.bref.work_ptr()
-    L.cer_conv_dgrad_bnbwd(_ptr(part), _ptr(link.z), _ptr(_bf16(ybn)), _ptr(link.mean),
+    L.cer_conv_dgrad_bnbwd(_ptr(part), _ptr(link.z), _ptr(_same(ybn, dy)), _ptr(link.mean),
                            _ptr(link.invstd), c_p(gp), gs, c_p(bp), bs, _act_code(link.act),
                            1 if link.has_res else 0, ctypes.byref(nslab))
     try:
@@ -578,7 +622,7 @@ def conv_set_variant(op, v):
 def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref):
     gp, gs = wref.grad_ptr()
     if streams.batching():
-        splits = lib().cer_wgrad_batch_add(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh,
+        splits = _fn("cer_wgrad_batch_add", x)(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh,
                                            kw, stride, pad, c_p(gp), gs)
         if splits > 0:
             if splits > 1 and not wref.arena.grad_clean:
@@ -591,19 +635,19 @@ def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad
         splits = L.cer_wgrad_splits(B * Ho * Wo, cout, kh * kw * cin, G)
         if splits > 1 and not wref.arena.grad_clean:
             wref.grad().zero_()
-        rc = L.cer_conv_wgrad(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride,
+        rc = _fn("cer_conv_wgrad", x)(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, stride,
                               pad, c_p(gp), gs, splits, _stream())
         _check(rc, "cer_conv_wgrad")
     # timing runs of split-K variants accumulate into the gradient: clear it
     # before the real launch
-    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch,
+    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
             after_tune=lambda: wref.grad().zero_())
     launch()
 
 
 def conv2d_wgrad(x, dy, wref, stride, pad):
-    x = _bf16(x)
-    dy = _bf16(dy)
+    x = _act(x)
+    dy = _act(dy)
     B, H, W, _ = x.shape
     _, Ho, Wo, _ = dy.shape
     G = wref.G
@@ -619,7 +663,7 @@ def _bn_part(M, C, device):
 
 
 def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
-    x = _bf16(x)
+    x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
     Cper = gref.spec.shape[0]
@@ -632,8 +676,8 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
     bp, bs = bref.work_ptr()
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
-    res = _bf16(residual) if residual is not None else None
-    rc = lib().cer_bn_fwd_train(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
+    res = _same(residual, x) if residual is not None else None
+    rc = _fn("cer_bn_fwd_train", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
                                 c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
                                 _ptr(part), M, C, Cper, eps, momentum, _act_code(act), _stream())
     _check(rc, "cer_bn_fwd_train")
@@ -643,7 +687,7 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
 def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, eps, part,
                           nslab):
     """BN forward from conv-epilogue partials (cer_conv_fwd_stats)."""
-    x = _bf16(x)
+    x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
     Cper = gref.spec.shape[0]
@@ -655,8 +699,8 @@ def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, 
     bp, bs = bref.work_ptr()
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
-    res = _bf16(residual) if residual is not None else None
-    rc = lib().cer_bn_fwd_train_part(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
+    res = _same(residual, x) if residual is not None else None
+    rc = _fn("cer_bn_fwd_train_part", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
                                      c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
                                      _ptr(part), int(nslab), M, C, Cper, eps, momentum,
                                      _act_code(act), _stream())
@@ -665,7 +709,7 @@ def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, 
 
 
 def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
-    x = _bf16(x)
+    x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
     Cper = gref.spec.shape[0]
@@ -674,8 +718,8 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
     bp, bs = bref.work_ptr()
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
-    res = _bf16(residual) if residual is not None else None
-    rc = lib().cer_bn_fwd_eval(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs, c_p(rmp),
+    res = _same(residual, x) if residual is not None else None
+    rc = _fn("cer_bn_fwd_eval", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs, c_p(rmp),
                                c_p(rvp), rs, M, C, Cper, eps, _act_code(act), _stream())
     _check(rc, "cer_bn_fwd_eval")
     return y
@@ -684,7 +728,7 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
 def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0):
     """BN backward; ``part`` / ``nslab``: the (sum dz, sum dz*xhat) partials
     already computed by the dgrad epilogue that produced dy."""
-    dy = _bf16(dy)
+    dy = _act(dy)
     C = x.shape[-1]
     M = x.numel() // C
     Cper = gref.spec.shape[0]
@@ -696,14 +740,14 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
     dgp, dgs = gref.grad_ptr()
     dbp, _ = bref.grad_ptr()
     if part is not None and nslab > 0:
-        rc = lib().cer_bn_bwd_part(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
+        rc = _fn("cer_bn_bwd_part", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
                                    gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx),
                                    _ptr(dres), _ptr(ws), _ptr(part), int(nslab), M, C, Cper,
                                    _act_code(act), _stream())
         _check(rc, "cer_bn_bwd_part")
         return dx, dres
     part = _bn_part(M, C, x.device)
-    rc = lib().cer_bn_bwd(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
+    rc = _fn("cer_bn_bwd", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
                           c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
                           M, C, Cper, _act_code(act), _stream())
     _check(rc, "cer_bn_bwd")
@@ -714,13 +758,13 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
 # pooling / bias+act (csrc/hip/pool.hip)
 # ---------------------------------------------------------------------------
 def maxpool_fwd(x, k, s, p):
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, C = x.shape
     Ho = (H + 2 * p - k) // s + 1
     Wo = (W + 2 * p - k) // s + 1
-    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
     arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
-    rc = lib().cer_maxpool_fwd(_ptr(x), _ptr(y), _ptr(arg), B, H, W, C, Ho, Wo, k, s, p,
+    rc = _fn("cer_maxpool_fwd", x)(_ptr(x), _ptr(y), _ptr(arg), B, H, W, C, Ho, Wo, k, s, p,
                                _stream())
     _check(rc, "cer_maxpool_fwd")
     return y, (arg, k, s, p)
@@ -730,50 +774,50 @@ def maxpool_bwd(dy, saved, xshape):
     arg, k, s, p = saved
     B, H, W, C = xshape
     _, Ho, Wo, _ = dy.shape
-    dx = torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dy.device)
-    rc = lib().cer_maxpool_bwd(_ptr(_bf16(dy)), _ptr(arg), _ptr(dx), B, H, W, C, Ho, Wo, k, s, p,
+    dx = torch.empty((B, H, W, C), dtype=dy.dtype, device=dy.device)
+    rc = _fn("cer_maxpool_bwd", dy)(_ptr(_act(dy)), _ptr(arg), _ptr(dx), B, H, W, C, Ho, Wo, k, s, p,
                                _stream())
     _check(rc, "cer_maxpool_bwd")
     return dx
 
 
 def gavgpool_fwd(x):
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, C = x.shape
-    y = torch.empty((B, C), dtype=torch.bfloat16, device=x.device)
-    rc = lib().cer_gavgpool_fwd(_ptr(x), _ptr(y), B, H * W, C, _stream())
+    y = torch.empty((B, C), dtype=x.dtype, device=x.device)
+    rc = _fn("cer_gavgpool_fwd", x)(_ptr(x), _ptr(y), B, H * W, C, _stream())
     _check(rc, "cer_gavgpool_fwd")
     return y
 
 
 def gavgpool_bwd(dy, xshape):
     B, H, W, C = xshape
-    dx = torch.empty(xshape, dtype=torch.bfloat16, device=dy.device)
-    rc = lib().cer_gavgpool_bwd(_ptr(_bf16(dy)), _ptr(dx), B, H * W, C, _stream())
+    dx = torch.empty(xshape, dtype=dy.dtype, device=dy.device)
+    rc = _fn("cer_gavgpool_bwd", dy)(_ptr(_act(dy)), _ptr(dx), B, H * W, C, _stream())
     _check(rc, "cer_gavgpool_bwd")
     return (dx,)
 
 
 def bias_act_fwd(x, bref, act, out=None):
-    x = _bf16(x)
+    x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
     y = torch.empty_like(x) if out is None else out
     bp, bs = bref.work_ptr()
-    rc = lib().cer_bias_act_fwd(_ptr(x), c_p(bp), bs, _ptr(y), M, C, bref.spec.shape[0],
+    rc = _fn("cer_bias_act_fwd", x)(_ptr(x), c_p(bp), bs, _ptr(y), M, C, bref.spec.shape[0],
                                 _act_code(act), _stream())
     _check(rc, "cer_bias_act_fwd")
     return y
 
 
 def bias_act_bwd(dy, y, bref, act):
-    dy = _bf16(dy)
+    dy = _act(dy)
     C = y.shape[-1]
     M = y.numel() // C
     dx = torch.empty_like(dy)
     ws = torch.empty(C, dtype=torch.float32, device=dy.device)
     gp, gs = bref.grad_ptr()
-    rc = lib().cer_bias_act_bwd(_ptr(dy), _ptr(y), _ptr(dx), c_p(gp), gs, _ptr(ws), M, C,
+    rc = _fn("cer_bias_act_bwd", dy)(_ptr(dy), _ptr(y), _ptr(dx), c_p(gp), gs, _ptr(ws), M, C,
                                 bref.spec.shape[0], _act_code(act), _stream())
     _check(rc, "cer_bias_act_bwd")
     return dx
@@ -783,11 +827,11 @@ def bias_act_bwd(dy, y, bref, act):
 # grouped linear = 1x1 conv on a 1x1 image (+ bias/act kernel)
 # ---------------------------------------------------------------------------
 def linear_fwd(x, wref, bref, act):
-    x = _bf16(x)
+    x = _act(x)
     B = x.shape[0]
     G = wref.G
     N, K = wref.spec.shape
-    y = torch.empty((B, G * N), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty((B, G * N), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
     _conv_fwd_launch(x, B, 1, 1, K, G, wp, ws, N, 1, 1, 1, 0, y, 1, 1, bp, bs, act)
@@ -798,13 +842,13 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     G = wref.G
     N, K = wref.spec.shape
     B = x.shape[0]
-    dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _bf16(dy)
-    xb = _bf16(x)
+    dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _act(dy)
+    xb = _act(x)
     streams.run_side(lambda: _conv_wgrad_launch(xb, B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref),
                      xb, dz)
     if not need_dx:
         return None
-    dx = torch.empty((B, G * K), dtype=torch.bfloat16, device=dy.device)
+    dx = torch.empty((B, G * K), dtype=dy.dtype, device=dy.device)
     wp, ws = wref.work_ptr()
     _conv_dgrad_launch(dz, B, 1, 1, N, G, wp, ws, K, 1, 1, 1, 0, dx, 1, 1)
     return dx
@@ -827,23 +871,23 @@ def dw_out_hw(H, W, k, stride, pad):
 
 
 def dwconv_fwd(x, wref, stride, pad):
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
     C, kh, kw = wref.spec.shape
     Ho, Wo = dw_out_hw(H, W, kh, stride, pad)
     pt, _, pl, _ = _pad4(pad)
-    y = torch.empty((B, Ho, Wo, GC), dtype=torch.bfloat16, device=x.device)
+    y = torch.empty((B, Ho, Wo, GC), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
-    rc = lib().cer_dwconv_fwd(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pt, pl, Ho, Wo,
+    rc = _fn("cer_dwconv_fwd", x)(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pt, pl, Ho, Wo,
                               _ptr(y), _stream())
     _check(rc, "cer_dwconv_fwd")
     return y
 
 
 def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
-    dy = _bf16(dy)
-    x = _bf16(x)
+    dy = _act(dy)
+    x = _act(x)
     B, H, W, GC = x.shape
     _, Ho, Wo, _ = dy.shape
     G = wref.G
@@ -854,7 +898,7 @@ def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
     dx = torch.empty_like(x) if need_dx else None
     wp, ws = wref.work_ptr()
     gp, gs = wref.grad_ptr()
-    rc = lib().cer_dwconv_bwd(_ptr(dy), _ptr(x), B, H, W, C, G, c_p(wp), ws, c_p(gp), gs, kh,
+    rc = _fn("cer_dwconv_bwd", dy)(_ptr(dy), _ptr(x), B, H, W, C, G, c_p(wp), ws, c_p(gp), gs, kh,
                               stride, pt, pl, Ho, Wo, _ptr(dx), _stream())
     _check(rc, "cer_dwconv_bwd")
     return dx
@@ -863,24 +907,24 @@ def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
 def avgpool_fwd(x, k, s, pad, count_pad):
     """k x k / s average pool; pad = int or (top, bottom, left, right) zero
     padding; count_pad: divide by k*k, else by the in-bounds tap count."""
-    x = _bf16(x)
+    x = _act(x)
     B, H, W, C = x.shape
     Ho, Wo = dw_out_hw(H, W, k, s, pad)
     pt, _, pl, _ = _pad4(pad)
-    y = torch.empty((B, Ho, Wo, C), dtype=torch.bfloat16, device=x.device)
-    rc = lib().cer_avgpool_fwd(_ptr(x), _ptr(y), B, H, W, C, Ho, Wo, k, s, pt, pl,
+    y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
+    rc = _fn("cer_avgpool_fwd", x)(_ptr(x), _ptr(y), B, H, W, C, Ho, Wo, k, s, pt, pl,
                                int(bool(count_pad)), _stream())
     _check(rc, "cer_avgpool_fwd")
     return y
 
 
 def avgpool_bwd(dy, xshape, k, s, pad, count_pad):
-    dy = _bf16(dy)
+    dy = _act(dy)
     B, H, W, C = xshape
     _, Ho, Wo, _ = dy.shape
     pt, _, pl, _ = _pad4(pad)
-    dx = torch.empty(xshape, dtype=torch.bfloat16, device=dy.device)
-    rc = lib().cer_avgpool_bwd(_ptr(dy), _ptr(dx), B, H, W, C, Ho, Wo, k, s, pt, pl,
+    dx = torch.empty(xshape, dtype=dy.dtype, device=dy.device)
+    rc = _fn("cer_avgpool_bwd", dy)(_ptr(dy), _ptr(dx), B, H, W, C, Ho, Wo, k, s, pt, pl,
                                int(bool(count_pad)), _stream())
     _check(rc, "cer_avgpool_bwd")
     return dx
@@ -889,10 +933,10 @@ def avgpool_bwd(dy, xshape, k, s, pad, count_pad):
 def embbag_fwd(idx, wref, bref, relu):
     G, B, nnz = idx.shape
     K, N = wref.spec.shape
-    y = torch.empty((B, G * N), dtype=torch.bfloat16, device=idx.device)
+    y = torch.empty((B, G * N), dtype=wref.arena.work.dtype, device=idx.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr()
-    rc = lib().cer_embbag_fwd(_ptr(idx.contiguous()), G, B, nnz, c_p(wp), ws, c_p(bp), bs, N,
+    rc = _fn("cer_embbag_fwd", y)(_ptr(idx.contiguous()), G, B, nnz, c_p(wp), ws, c_p(bp), bs, N,
                               1 if relu else 0, _ptr(y), _stream())
     _check(rc, "cer_embbag_fwd")
     return y
@@ -906,6 +950,6 @@ def embbag_bwd(dy, idx, y, wref, bref, relu):
         bref.grad().zero_()
     gp, gs = wref.grad_ptr()
     bp, bs = bref.grad_ptr()
-    rc = lib().cer_embbag_bwd(_ptr(_bf16(dy)), _ptr(y), _ptr(idx.contiguous()), G, B, nnz,
+    rc = _fn("cer_embbag_bwd", dy)(_ptr(_act(dy)), _ptr(y), _ptr(idx.contiguous()), G, B, nnz,
                               c_p(gp), gs, c_p(bp), bs, N, 1 if relu else 0, _stream())
     _check(rc, "cer_embbag_bwd")

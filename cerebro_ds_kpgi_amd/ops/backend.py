@@ -47,8 +47,9 @@ def use_hip(op, *tensors):
         if isinstance(t, torch.Tensor):
             if not t.is_cuda:
                 return False
-            # activation kernels are bf16; fp32 compute runs on the oracle path
-            if t.is_floating_point() and t.dtype != torch.bfloat16 and op not in ("adam", "gather"):
+            # activation kernels exist for bf16 (compute mode) and fp32
+            # (reference precision, 3-pass split-bf16 MFMA convolutions)
+            if t.is_floating_point() and t.dtype not in (torch.bfloat16, torch.float32):
                 return False
     return True
 

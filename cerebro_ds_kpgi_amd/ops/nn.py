@@ -541,8 +541,7 @@ class PackedEmbeddingBag(torch.autograd.Function):
         G = wref.G
         K, N = wref.spec.shape
         Gi, B, nnz = idx.shape
-        ctx.hip = hip_gate("embbag", wref.arena.compute_dtype == torch.bfloat16 and N % 8 == 0,
-                           idx)
+        ctx.hip = hip_gate("embbag", N % 8 == 0, idx)
         if ctx.hip:
             y = _hip().embbag_fwd(idx, wref, bref, relu)
         else:

@@ -63,7 +63,8 @@ class EngineOptions(object):
         self.scheduler = kw.get("scheduler", "rotation")
         self.n_train = kw.get("n_train", 0)
         self.n_valid = kw.get("n_valid", 0)
-        self.compute_dtype = kw.get("compute_dtype", "bf16")
+        # fp32 = the reference precision (TF 1.14 / PyTorch 1.4 defaults); bf16 opt-in
+        self.compute_dtype = kw.get("compute_dtype", "fp32")
         self.hop_optimizer_state = kw.get("hop_optimizer_state", True)
         self.l2 = kw.get("l2", True)
         self.use_graphs = kw.get("use_graphs", True)

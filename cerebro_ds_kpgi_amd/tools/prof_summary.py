@@ -17,7 +17,7 @@ import sys
 
 FAMILIES = [
     ("conv/linear GEMM (MFMA, NT: fwd)", r"igemm_nt|pipe_nt"),
-    ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad|pipe_nn"),
+    ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad|igemm_nn32|pipe_nn"),
     ("conv/linear wgrad (MFMA, TN; batched)", r"igemm_wgrad|pipe_wg|wgrad_batch"),
     ("weight transpose (dgrad)", r"transpose_w"),
     ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),

@@ -75,7 +75,7 @@ def get_main_parser():
                    help="ship Adam moments with the model (False = reset per sub-epoch, reference CTQ semantics)")
     p.add_argument("--l2_mode", choices=["adam_wd", "none"], default="adam_wd",
                    help="lambda as torch Adam weight_decay (reference DDP path) or a no-op (Keras path quirk)")
-    p.add_argument("--compute_dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--compute_dtype", choices=["bf16", "fp32"], default="fp32")
     p.add_argument("--optimizer", choices=["adam", "sgd"], default="adam",
                    help="per-config optimizer (reference: Adam); sgd = momentum 0.9, coupled L2")
     p.add_argument("--data_dtype", choices=["uint8", "fp32"], default="uint8")

@@ -42,25 +42,6 @@ __device__ __forceinline__ float act_bwd(float dy, float y, int code) {
   return dy;
 }
 
-__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
-  uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
-__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
-  uint4 u;
-  u.x = pack_bf2(v[0], v[1]);
-  u.y = pack_bf2(v[2], v[3]);
-  u.z = pack_bf2(v[4], v[5]);
-  u.w = pack_bf2(v[6], v[7]);
-  *reinterpret_cast<uint4*>(p) = u;
-}
-
 struct Map {
   int tc_n, tr_n, cb;  // threads along channels, row lanes, channels per block
 };
@@ -152,12 +133,13 @@ __device__ __forceinline__ void grid_sync(const GridBar& gb, unsigned ordinal) {
 constexpr int YM_NONE = 0, YM_Y = 1, YM_Z = 2;
 
 // forward scale / shift of 8 channels (bitwise the apply_fwd_tile values)
+template <typename T>
 __device__ __forceinline__ void bn_scale_shift(const Strided& gamma, const Strided& beta, int g,
                                                int cc, const float* mu, const float* is,
                                                float* sc, float* sh) {
   float ga[VEC], be[VEC];
-  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
-  load8((const bf16_t*)beta.p + g * beta.stride + cc, be);
+  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
+  ld8((const T*)beta.p + g * beta.stride + cc, be);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     sc[i] = is[i] * ga[i];
@@ -174,9 +156,9 @@ __device__ __forceinline__ float dz_of(float d, float yv, float xv, float sc, fl
 }
 
 // one (channel block cbk, row slab) tile; `red` = 2*BN_T*VEC floats of LDS
-template <int MODE, bool SC, int YM = YM_Y>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
+template <typename T, int MODE, bool SC, int YM = YM_Y>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
 __device__ __forceinline__ void partials_tile(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
     int64_t M, int C, int rows_per_slab, int act, const Map& mp, int cbk, int slab, float* red,
     const Strided& gamma = Strided{nullptr, 0}, const Strided& beta = Strided{nullptr, 0},
@@ -194,7 +176,7 @@ __device__ __forceinline__ void partials_tile(
     }
     if (YM == YM_Z) {
       const int g = c0 / Cper;
-      bn_scale_shift(gamma, beta, g, c0 - g * Cper, mu, is, sc, sh);
+      bn_scale_shift<T>(gamma, beta, g, c0 - g * Cper, mu, is, sc, sh);
     }
   }
   const int64_t r0 = (int64_t)slab * rows_per_slab;
@@ -211,10 +193,10 @@ __device__ __forceinline__ void partials_tile(
         const int64_t rr = r + (int64_t)u * mp.tr_n;
         ok[u] = rr < r1;
         if (ok[u]) {
-          load8(x + rr * C + c0, v[u]);
+          ld8(x + rr * C + c0, v[u]);
           if (MODE == 1) {
-            load8(dy + rr * C + c0, d[u]);
-            if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
+            ld8(dy + rr * C + c0, d[u]);
+            if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
           }
         }
       }
@@ -261,14 +243,14 @@ __device__ __forceinline__ void partials_tile(
   __syncthreads();  // `red` is reused by the next tile of a cooperative block
 }
 
-template <int MODE, int YM = YM_Y>
+template <typename T, int MODE, int YM = YM_Y>
 __global__ __launch_bounds__(BN_T) void bn_partials(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
     int64_t M, int C, int rows_per_slab, int act, Map mp, Strided gamma = Strided{nullptr, 0},
     Strided beta = Strided{nullptr, 0}, int Cper = 1) {
   __shared__ float red[2 * BN_T * VEC];
-  partials_tile<MODE, false, YM>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+  partials_tile<T, MODE, false, YM>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
                                  blockIdx.x, blockIdx.y, red, gamma, beta, Cper);
 }
 
@@ -389,9 +371,9 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
 // stage 3: elementwise apply (scale/shift per channel computed once per thread)
 // ---------------------------------------------------------------------------
 // MODE 0: train fwd, ws = (mean, invstd); MODE 1: eval fwd from running stats
-template <int MODE, bool SC, int AU = 2>   // AU: rows in flight per thread
+template <typename T, int MODE, bool SC, int AU = 2>   // AU: rows in flight per thread
 __device__ __forceinline__ void apply_fwd_tile(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, const Strided& gamma,
     const Strided& beta, int64_t M, int C, int Cper, int rows_per_slab, int act, const Map& mp,
@@ -411,7 +393,7 @@ __device__ __forceinline__ void apply_fwd_tile(
       is[i] = rsqrtf(rvar[g * rstat_stride + cc + i] + eps);
     }
   }
-  bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -420,8 +402,8 @@ __device__ __forceinline__ void apply_fwd_tile(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        load8(x + rr * C + c0, v[u]);
-        if (res) load8(res + rr * C + c0, rv[u]);
+        ld8(x + rr * C + c0, v[u]);
+        if (res) ld8(res + rr * C + c0, rv[u]);
       }
     }
 #pragma unroll
@@ -432,26 +414,26 @@ __device__ __forceinline__ void apply_fwd_tile(
 #pragma unroll
       for (int i = 0; i < VEC; ++i)
         o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
-      store8(y + rr * C + c0, o);
+      st8(y + rr * C + c0, o);
     }
   }
 }
 
-template <int MODE, int AU = 2>
+template <typename T, int MODE, int AU = 2>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y,
+    const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
     Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
-  apply_fwd_tile<MODE, false, AU>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
+  apply_fwd_tile<T, MODE, false, AU>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
                               Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
 }
 
-template <bool SC, int YM = YM_Y, int AU = 2>
+template <typename T, bool SC, int YM = YM_Y, int AU = 2>
 __device__ __forceinline__ void apply_bwd_tile(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
-    const Strided& gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
+    const Strided& gamma, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
     int Cper, int rows_per_slab, int act, const Map& mp, int cbk, int slab,
     const Strided& beta = Strided{nullptr, 0}) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
@@ -459,7 +441,7 @@ __device__ __forceinline__ void apply_bwd_tile(
   if (c0 >= C) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
-  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
+  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
   const float inv_m = 1.f / (float)M;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
@@ -469,7 +451,7 @@ __device__ __forceinline__ void apply_bwd_tile(
     k2[i] = ldf<SC>(ws + C + c0 + i) * inv_m;
     sdz[i] = ldf<SC>(ws + c0 + i) * inv_m;
   }
-  if (YM == YM_Z) bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -478,9 +460,9 @@ __device__ __forceinline__ void apply_bwd_tile(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        load8(dy + rr * C + c0, d[u]);
-        load8(x + rr * C + c0, xv[u]);
-        if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
+        ld8(dy + rr * C + c0, d[u]);
+        ld8(x + rr * C + c0, xv[u]);
+        if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
       }
     }
 #pragma unroll
@@ -494,19 +476,19 @@ __device__ __forceinline__ void apply_bwd_tile(
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
-      store8(dx + rr * C + c0, o);
-      if (dres) store8(dres + rr * C + c0, dz);
+      st8(dx + rr * C + c0, o);
+      if (dres) st8(dres + rr * C + c0, dz);
     }
   }
 }
 
-template <int YM, int AU = 2>
+template <typename T, int YM, int AU = 2>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
-    Strided gamma, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C,
+    Strided gamma, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
     int Cper, int rows_per_slab, int act, Map mp, Strided beta) {
-  apply_bwd_tile<false, YM, AU>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
+  apply_bwd_tile<T, false, YM, AU>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
                             rows_per_slab, act, mp, blockIdx.x, blockIdx.y, beta);
 }
 
@@ -581,10 +563,11 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
 
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
+template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
-    float* rvar, int64_t rstat_stride, float eps, float momentum, const bf16_t* __restrict__ x,
-    const bf16_t* __restrict__ res, bf16_t* __restrict__ y, Strided gamma, Strided beta,
+    float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
+    const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
     int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
@@ -614,7 +597,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     }
   }
   float sc[VEC], sh[VEC];
-  bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;
@@ -624,8 +607,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        load8(x + rr * C + c0, v[u]);
-        if (res) load8(res + rr * C + c0, rv[u]);
+        ld8(x + rr * C + c0, v[u]);
+        if (res) ld8(res + rr * C + c0, rv[u]);
       }
     }
 #pragma unroll
@@ -636,17 +619,17 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
 #pragma unroll
       for (int i = 0; i < VEC; ++i)
         o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
-      store8(y + rr * C + c0, o);
+      st8(y + rr * C + c0, o);
     }
   }
 }
 
-template <int YM>
+template <typename T, int YM>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     const float* __restrict__ part, int nslab, float* dgamma, float* dbeta, int64_t gstride,
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
-    Strided beta, bf16_t* __restrict__ dx, bf16_t* __restrict__ dres, int64_t M, int C, int Cper,
+    Strided beta, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C, int Cper,
     int rows_per_slab, int act, Map mp) {
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
@@ -663,7 +646,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     }
   }
   float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
-  load8((const bf16_t*)gamma.p + g * gamma.stride + cc, ga);
+  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
   const float inv_m = 1.f / (float)M;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
@@ -673,7 +656,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     k2[i] = b[i] * inv_m;
     sdz[i] = a[i] * inv_m;
   }
-  if (YM == YM_Z) bn_scale_shift(gamma, beta, g, cc, mu, is, sc, sh);
+  if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;
@@ -683,9 +666,9 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        load8(dy + rr * C + c0, d[u]);
-        load8(x + rr * C + c0, xv[u]);
-        if (YM == YM_Y) load8(y + rr * C + c0, yv[u]);
+        ld8(dy + rr * C + c0, d[u]);
+        ld8(x + rr * C + c0, xv[u]);
+        if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
       }
     }
 #pragma unroll
@@ -699,8 +682,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
-      store8(dx + rr * C + c0, o);
-      if (dres) store8(dres + rr * C + c0, dz);
+      st8(dx + rr * C + c0, o);
+      if (dres) st8(dres + rr * C + c0, dz);
     }
   }
 }
@@ -715,11 +698,12 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
 // partials -> finalize -> apply (3 -> 1).  Blocks grid-stride over the same
 // (channel block, row slab) tiles in every stage, so the backward apply
 // re-reads the rows its own block reduced (L2-warm).
+template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_fwd_coop(
     const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
     float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, float eps,
-    float momentum, const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
-    bf16_t* __restrict__ y, Strided gamma, Strided beta, int64_t M, int C, int Cper,
+    float momentum, const T* __restrict__ x, const T* __restrict__ res,
+    T* __restrict__ y, Strided gamma, Strided beta, int64_t M, int C, int Cper,
     int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
   const GridBar gb = grid_bar_open(bar);
   const int fin_tasks = (C + FIN_C - 1) / FIN_C;
@@ -728,20 +712,21 @@ __global__ __launch_bounds__(BN_T) void bn_fwd_coop(
                             C, Cper, eps, momentum, t);
   grid_sync(gb, 1);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    apply_fwd_tile<0, true>(x, res, y, ws, nullptr, nullptr, 0, 0.f, gamma, beta, M, C, Cper,
+    apply_fwd_tile<T, 0, true>(x, res, y, ws, nullptr, nullptr, 0, 0.f, gamma, beta, M, C, Cper,
                             rows_per_slab, act, mp, t % cblocks, t / cblocks);
 }
 
+template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_bwd_coop(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
+    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
-    float* dgamma, float* dbeta, int64_t gstride, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dres, float* __restrict__ ws, float* __restrict__ part, int64_t M, int C,
+    float* dgamma, float* dbeta, int64_t gstride, T* __restrict__ dx,
+    T* __restrict__ dres, float* __restrict__ ws, float* __restrict__ part, int64_t M, int C,
     int Cper, int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
   __shared__ float red[2 * BN_T * VEC];
   const GridBar gb = grid_bar_open(bar);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    partials_tile<1, true>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+    partials_tile<T, 1, true>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
                            t % cblocks, t / cblocks, red);
   grid_sync(gb, 1);
   const int fin_tasks = (C + FIN_C - 1) / FIN_C;
@@ -750,7 +735,7 @@ __global__ __launch_bounds__(BN_T) void bn_bwd_coop(
     finalize_bwd_task<true>(part, slabs, ws, dgamma, dbeta, gstride, C, Cper, t);
   grid_sync(gb, 2);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    apply_bwd_tile<true>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
+    apply_bwd_tile<T, true>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
                          act, mp, t % cblocks, t / cblocks);
 }
 
@@ -861,7 +846,7 @@ static int device_cus() {
   static int cache[64] = {0};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cache[dev]) hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev);
+  if (!cache[dev]) (void)hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev);
   return cache[dev];
 }
 
@@ -874,8 +859,9 @@ CER_API int64_t cer_bn_part_floats(int64_t M, int C) {
   return (int64_t)g.y * 2 * C;
 }
 
-static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
-                             int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
+template <typename T>
+static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
+                             int64_t gamma_stride, const T* beta, int64_t beta_stride,
                              float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
                              float* invstd_out, float* ws, float* part, int nslab, int64_t M,
                              int C, int Cper, float eps, float momentum, int act,
@@ -887,7 +873,7 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   if (nslab <= 0) {  // statistics not produced upstream: reduce x here
     make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
-    bn_partials<0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
+    bn_partials<T, 0><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr, part, M, C,
                                             rrows, 0, mp);
     nslab = (int)rg.y;
   }
@@ -895,7 +881,7 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     dim3 fg;
     int frows;
     make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
-    bn_apply_fwd_fold<<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
+    bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
                                                rstat_stride, eps, momentum, x, res, y,
                                                Strided{gamma, gamma_stride},
                                                Strided{beta, beta_stride}, M, C, Cper, frows, act,
@@ -904,7 +890,7 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   }
   if (coop_on()) {
     static int cap_cache[64] = {0};
-    const int cap = coop_capacity(bn_fwd_coop, cap_cache);
+    const int cap = coop_capacity(bn_fwd_coop<T>, cap_cache);
     unsigned* bar = coop_bar();
     dim3 cg;
     int crows;
@@ -912,7 +898,7 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
     const int ntiles = (int)(cg.x * cg.y);
     const int grid = coop_grid(ntiles, cap, 4 * device_cus());
     if (grid > 0 && bar) {
-      bn_fwd_coop<<<grid, BN_T, 0, stream>>>(part, nslab, ws, mean_out, invstd_out, rmean, rvar,
+      bn_fwd_coop<T><<<grid, BN_T, 0, stream>>>(part, nslab, ws, mean_out, invstd_out, rmean, rvar,
                                              rstat_stride, eps, momentum, x, res, y,
                                              Strided{gamma, gamma_stride},
                                              Strided{beta, beta_stride}, M, C, Cper, crows,
@@ -924,20 +910,21 @@ static int bn_fwd_train_impl(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
                                                           invstd_out, rmean, rvar, rstat_stride,
                                                           M, C, Cper, eps, momentum);
   if (apply_au() == 4)
-    bn_apply_fwd<0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+    bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                                 Strided{gamma, gamma_stride},
                                                 Strided{beta, beta_stride}, M, C, Cper, arows,
                                                 act, mp);
   else
-    bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+    bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                              Strided{gamma, gamma_stride},
                                              Strided{beta, beta_stride}, M, C, Cper, arows, act,
                                              mp);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
-                             int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
+template <typename T>
+static int cer_bn_fwd_train_t(const T* x, const T* res, T* y, const T* gamma,
+                             int64_t gamma_stride, const T* beta, int64_t beta_stride,
                              float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
                              float* invstd_out, float* ws, float* part, int64_t M, int C,
                              int Cper, float eps, float momentum, int act, hipStream_t stream) {
@@ -948,8 +935,9 @@ CER_API int cer_bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
 
 // same, with the per-slab (sum, sum^2) partials already produced by the
 // producing convolution's epilogue (cer_conv_fwd_stats)
-CER_API int cer_bn_fwd_train_part(const bf16_t* x, const bf16_t* res, bf16_t* y,
-                                  const bf16_t* gamma, int64_t gamma_stride, const bf16_t* beta,
+template <typename T>
+static int cer_bn_fwd_train_part_t(const T* x, const T* res, T* y,
+                                  const T* gamma, int64_t gamma_stride, const T* beta,
                                   int64_t beta_stride, float* rmean, float* rvar,
                                   int64_t rstat_stride, float* mean_out, float* invstd_out,
                                   float* ws, float* part, int nslab, int64_t M, int C, int Cper,
@@ -962,8 +950,9 @@ CER_API int cer_bn_fwd_train_part(const bf16_t* x, const bf16_t* res, bf16_t* y,
 
 // apply only: y = act(xhat * gamma + beta (+ res)) with ws = (mean, invstd)
 // already produced (conv-fused statistics, cer_conv_fwd_bnstat)
-CER_API int cer_bn_apply_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, const float* ws,
-                             const bf16_t* gamma, int64_t gamma_stride, const bf16_t* beta,
+template <typename T>
+static int cer_bn_apply_fwd_t(const T* x, const T* res, T* y, const float* ws,
+                             const T* gamma, int64_t gamma_stride, const T* beta,
                              int64_t beta_stride, int64_t M, int C, int Cper, int act,
                              hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
@@ -972,20 +961,21 @@ CER_API int cer_bn_apply_fwd(const bf16_t* x, const bf16_t* res, bf16_t* y, cons
   int arows;
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   if (apply_au() == 4)
-    bn_apply_fwd<0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+    bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                                 Strided{gamma, gamma_stride},
                                                 Strided{beta, beta_stride}, M, C, Cper, arows,
                                                 act, mp);
   else
-    bn_apply_fwd<0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+    bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                              Strided{gamma, gamma_stride},
                                              Strided{beta, beta_stride}, M, C, Cper, arows, act,
                                              mp);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const bf16_t* gamma,
-                            int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
+template <typename T>
+static int cer_bn_fwd_eval_t(const T* x, const T* res, T* y, const T* gamma,
+                            int64_t gamma_stride, const T* beta, int64_t beta_stride,
                             const float* rmean, const float* rvar, int64_t rstat_stride,
                             int64_t M, int C, int Cper, float eps, int act, hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
@@ -993,7 +983,7 @@ CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
   dim3 ag;
   int arows;
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  bn_apply_fwd<1><<<ag, BN_T, 0, stream>>>(x, res, y, nullptr, rmean, rvar, rstat_stride, eps,
+  bn_apply_fwd<T, 1><<<ag, BN_T, 0, stream>>>(x, res, y, nullptr, rmean, rvar, rstat_stride, eps,
                                            Strided{gamma, gamma_stride},
                                            Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
   return (int)hipGetLastError();
@@ -1001,10 +991,11 @@ CER_API int cer_bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, const
 
 // pre_nslab > 0: part already holds pre_nslab partials (computed in the
 // epilogue of the dgrad that produced dy): skip the partials pass
-static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
-                       const float* invstd, const bf16_t* gamma, int64_t gamma_stride,
-                       const bf16_t* beta, int64_t beta_stride, float* dgamma, float* dbeta,
-                       int64_t grad_stride, bf16_t* dx, bf16_t* dres, float* ws, float* part,
+template <typename T>
+static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
+                       const float* invstd, const T* gamma, int64_t gamma_stride,
+                       const T* beta, int64_t beta_stride, float* dgamma, float* dbeta,
+                       int64_t grad_stride, T* dx, T* dres, float* ws, float* part,
                        int pre_nslab, int64_t M, int C, int Cper, int act, hipStream_t stream) {
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
@@ -1015,12 +1006,12 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   if (pre_nslab <= 0 && coop_on()) {
     // same (channel block, slab) tiling as bn_partials: part has room for it
     static int cap_cache[64] = {0};
-    const int cap = coop_capacity(bn_bwd_coop, cap_cache);
+    const int cap = coop_capacity(bn_bwd_coop<T>, cap_cache);
     unsigned* bar = coop_bar();
     const int ntiles = (int)(rg.x * rg.y);
     const int grid = coop_grid(ntiles, cap, 4 * device_cus());
     if (grid > 0 && bar) {
-      bn_bwd_coop<<<grid, BN_T, 0, stream>>>(dy, x, y, mean, invstd, Strided{gamma, gamma_stride},
+      bn_bwd_coop<T><<<grid, BN_T, 0, stream>>>(dy, x, y, mean, invstd, Strided{gamma, gamma_stride},
                                              dgamma, dbeta, grad_stride, dx, dres, ws, part, M, C,
                                              Cper, rrows, (int)rg.x, ntiles, act, mp, bar);
       return (int)hipGetLastError();
@@ -1033,13 +1024,13 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
   const int nslab = pre_nslab > 0 ? pre_nslab : (int)rg.y;
   if (pre_nslab <= 0) {
     if (ym == YM_NONE)
-      bn_partials<1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
+      bn_partials<T, 1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
                                                        rrows, act, mp, gs, bs, Cper);
     else if (ym == YM_Z)
-      bn_partials<1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+      bn_partials<T, 1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                     act, mp, gs, bs, Cper);
     else
-      bn_partials<1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+      bn_partials<T, 1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                     act, mp, gs, bs, Cper);
   }
   if (nslab <= fold_max()) {
@@ -1047,16 +1038,16 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
     int frows;
     make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
     if (ym == YM_NONE)
-      bn_apply_bwd_fold<YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<T, YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                           grad_stride, dy, x, y, mean, invstd, gs,
                                                           bs, dx, dres, M, C, Cper, frows, act,
                                                           mp);
     else if (ym == YM_Z)
-      bn_apply_bwd_fold<YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<T, YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
                                                        dx, dres, M, C, Cper, frows, act, mp);
     else
-      bn_apply_bwd_fold<YM_Y><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+      bn_apply_bwd_fold<T, YM_Y><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
                                                        dx, dres, M, C, Cper, frows, act, mp);
     return (int)hipGetLastError();
@@ -1065,33 +1056,34 @@ static int bn_bwd_impl(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
                                                           grad_stride, C, Cper);
   if (ym == YM_NONE) {
     if (apply_au() == 4)
-      bn_apply_bwd<YM_NONE, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+      bn_apply_bwd<T, YM_NONE, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
                                                      C, Cper, arows, act, mp, bs);
     else
-      bn_apply_bwd<YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+      bn_apply_bwd<T, YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
                                                      C, Cper, arows, act, mp, bs);
   } else if (ym == YM_Z) {
     if (apply_au() == 4)
-      bn_apply_bwd<YM_Z, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+      bn_apply_bwd<T, YM_Z, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                   Cper, arows, act, mp, bs);
     else
-      bn_apply_bwd<YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+      bn_apply_bwd<T, YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                   Cper, arows, act, mp, bs);
   } else {
     if (apply_au() == 4)
-      bn_apply_bwd<YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+      bn_apply_bwd<T, YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                   Cper, arows, act, mp, bs);
     else
-      bn_apply_bwd<YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+      bn_apply_bwd<T, YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                   Cper, arows, act, mp, bs);
   }
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* mean,
-                       const float* invstd, const bf16_t* gamma, int64_t gamma_stride,
-                       const bf16_t* beta, int64_t beta_stride, float* dgamma, float* dbeta,
-                       int64_t grad_stride, bf16_t* dx, bf16_t* dres, float* ws, float* part,
+template <typename T>
+static int cer_bn_bwd_t(const T* dy, const T* x, const T* y, const float* mean,
+                       const float* invstd, const T* gamma, int64_t gamma_stride,
+                       const T* beta, int64_t beta_stride, float* dgamma, float* dbeta,
+                       int64_t grad_stride, T* dx, T* dres, float* ws, float* part,
                        int64_t M, int C, int Cper, int act, hipStream_t stream) {
   return bn_bwd_impl(dy, x, y, mean, invstd, gamma, gamma_stride, beta, beta_stride, dgamma,
                      dbeta, grad_stride, dx, dres, ws, part, 0, M, C, Cper, act, stream);
@@ -1099,13 +1091,67 @@ CER_API int cer_bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const
 
 // same, with the nslab (sum dz, sum dz*xhat) partials already in `part`
 // (cer_conv_dgrad_bnbwd)
-CER_API int cer_bn_bwd_part(const bf16_t* dy, const bf16_t* x, const bf16_t* y,
-                            const float* mean, const float* invstd, const bf16_t* gamma,
-                            int64_t gamma_stride, const bf16_t* beta, int64_t beta_stride,
-                            float* dgamma, float* dbeta, int64_t grad_stride, bf16_t* dx,
-                            bf16_t* dres, float* ws, float* part, int nslab, int64_t M, int C,
+template <typename T>
+static int cer_bn_bwd_part_t(const T* dy, const T* x, const T* y,
+                            const float* mean, const float* invstd, const T* gamma,
+                            int64_t gamma_stride, const T* beta, int64_t beta_stride,
+                            float* dgamma, float* dbeta, int64_t grad_stride, T* dx,
+                            T* dres, float* ws, float* part, int nslab, int64_t M, int C,
                             int Cper, int act, hipStream_t stream) {
   if (nslab <= 0) return (int)hipErrorInvalidValue;
   return bn_bwd_impl(dy, x, y, mean, invstd, gamma, gamma_stride, beta, beta_stride, dgamma,
                      dbeta, grad_stride, dx, dres, ws, part, nslab, M, C, Cper, act, stream);
 }
+
+// C entry points: bf16 (compute mode) and _f32 (reference-precision mode)
+// twins of every BatchNorm op, same arguments
+#define CER_BN_ENTRY_POINTS(T, SFX)                                                              \
+  CER_API int cer_bn_fwd_train##SFX(                                                             \
+      const T* x, const T* res, T* y, const T* gamma, int64_t gs, const T* beta, int64_t bs,    \
+      float* rmean, float* rvar, int64_t rstride, float* mean_out, float* invstd_out, float* ws, \
+      float* part, int64_t M, int C, int Cper, float eps, float momentum, int act,                \
+      hipStream_t stream) {                                                                      \
+    return cer_bn_fwd_train_t<T>(x, res, y, gamma, gs, beta, bs, rmean, rvar, rstride, mean_out, \
+                                 invstd_out, ws, part, M, C, Cper, eps, momentum, act, stream);  \
+  }                                                                                              \
+  CER_API int cer_bn_fwd_train_part##SFX(                                                        \
+      const T* x, const T* res, T* y, const T* gamma, int64_t gs, const T* beta, int64_t bs,    \
+      float* rmean, float* rvar, int64_t rstride, float* mean_out, float* invstd_out, float* ws, \
+      float* part, int nslab, int64_t M, int C, int Cper, float eps, float momentum, int act,    \
+      hipStream_t stream) {                                                                      \
+    return cer_bn_fwd_train_part_t<T>(x, res, y, gamma, gs, beta, bs, rmean, rvar, rstride,     \
+                                      mean_out, invstd_out, ws, part, nslab, M, C, Cper, eps,    \
+                                      momentum, act, stream);                                    \
+  }                                                                                              \
+  CER_API int cer_bn_apply_fwd##SFX(const T* x, const T* res, T* y, const float* ws,            \
+                                    const T* gamma, int64_t gs, const T* beta, int64_t bs,      \
+                                    int64_t M, int C, int Cper, int act, hipStream_t stream) {   \
+    return cer_bn_apply_fwd_t<T>(x, res, y, ws, gamma, gs, beta, bs, M, C, Cper, act, stream);   \
+  }                                                                                              \
+  CER_API int cer_bn_fwd_eval##SFX(const T* x, const T* res, T* y, const T* gamma, int64_t gs,  \
+                                   const T* beta, int64_t bs, const float* rmean,               \
+                                   const float* rvar, int64_t rstride, int64_t M, int C,         \
+                                   int Cper, float eps, int act, hipStream_t stream) {          \
+    return cer_bn_fwd_eval_t<T>(x, res, y, gamma, gs, beta, bs, rmean, rvar, rstride, M, C,      \
+                                Cper, eps, act, stream);                                         \
+  }                                                                                              \
+  CER_API int cer_bn_bwd##SFX(const T* dy, const T* x, const T* y, const float* mean,           \
+                              const float* invstd, const T* gamma, int64_t gs, const T* beta,    \
+                              int64_t bs, float* dgamma, float* dbeta, int64_t grad_stride,      \
+                              T* dx, T* dres, float* ws, float* part, int64_t M, int C,          \
+                              int Cper, int act, hipStream_t stream) {                          \
+    return cer_bn_bwd_t<T>(dy, x, y, mean, invstd, gamma, gs, beta, bs, dgamma, dbeta,           \
+                           grad_stride, dx, dres, ws, part, M, C, Cper, act, stream);            \
+  }                                                                                              \
+  CER_API int cer_bn_bwd_part##SFX(const T* dy, const T* x, const T* y, const float* mean,      \
+                                   const float* invstd, const T* gamma, int64_t gs,             \
+                                   const T* beta, int64_t bs, float* dgamma, float* dbeta,       \
+                                   int64_t grad_stride, T* dx, T* dres, float* ws, float* part,  \
+                                   int nslab, int64_t M, int C, int Cper, int act,               \
+                                   hipStream_t stream) {                                         \
+    return cer_bn_bwd_part_t<T>(dy, x, y, mean, invstd, gamma, gs, beta, bs, dgamma, dbeta,      \
+                                grad_stride, dx, dres, ws, part, nslab, M, C, Cper, act, stream);\
+  }
+
+CER_BN_ENTRY_POINTS(bf16_t, )
+CER_BN_ENTRY_POINTS(float, _f32)

@@ -29,6 +29,48 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// ---------------------------------------------------------------------------
+// Storage-dtype generic element access.  Every activation / parameter kernel
+// is a template over its storage type T (bf16_t: the bf16 compute mode,
+// float: the reference-precision fp32 mode); arithmetic is always fp32.
+// 8 consecutive elements = one 16-B (bf16) or two 16-B (fp32) accesses.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
+  uint4 u;
+  u.x = pack_bf2(v[0], v[1]);
+  u.y = pack_bf2(v[2], v[3]);
+  u.z = pack_bf2(v[4], v[5]);
+  u.w = pack_bf2(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+__device__ __forceinline__ float ld1(const bf16_t* p) { return bf2f(*p); }
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

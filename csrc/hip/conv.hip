@@ -151,10 +151,12 @@ struct WGParams {
   int splits;
 };
 
-static GatherGeom make_geom(const bf16_t* src, int B, int Ctot, int Cg, int Hs, int Ws, int Hm,
-                            int Wm, int kh, int kw, int st, int pad) {
-  GatherGeom g{src, Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad, 0u, {}, {}, {}, {}, {}, st, pad, Cg};
-  const uint64_t bytes = (uint64_t)B * Hs * Ws * Ctot * sizeof(bf16_t);
+// es: element size of the gathered tensor (2 = bf16, 4 = fp32)
+static GatherGeom make_geom(const void* src, int B, int Ctot, int Cg, int Hs, int Ws, int Hm,
+                            int Wm, int kh, int kw, int st, int pad, int es = 2) {
+  GatherGeom g{reinterpret_cast<const bf16_t*>(src), Ctot, Cg, Hs, Ws, Hm, Wm, kh, kw, st, pad,
+               0u, {}, {}, {}, {}, {}, st, pad, Cg};
+  const uint64_t bytes = (uint64_t)B * Hs * Ws * Ctot * (uint64_t)es;
   g.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   g.dWm = make_div((uint32_t)Wm);
   g.dHm = make_div((uint32_t)Hm);
@@ -228,8 +230,9 @@ __device__ __forceinline__ RowA row_init(const GatherGeom& g, int m, int M) {
   return a;
 }
 
-// byte offset of channel c of tap (r, s) for a row, or OOB (-> zeros)
-template <int GM>
+// byte offset of channel c of tap (r, s) for a row, or OOB (-> zeros);
+// ES = element size in bytes (2 bf16, 4 fp32)
+template <int GM, int ES = 2>
 __device__ __forceinline__ uint32_t a_off(const GatherGeom& g, const RowA& a, int r, int s, int c) {
   int hi, wi;
   uint32_t pix;
@@ -250,7 +253,7 @@ __device__ __forceinline__ uint32_t a_off(const GatherGeom& g, const RowA& a, in
     pix = ((uint32_t)a.pix + hq) * (uint32_t)g.Ws + wq;
   }
   const bool ok = ((unsigned)hi < (unsigned)g.Hs) & ((unsigned)wi < (unsigned)g.Ws);
-  return ok ? (pix * (uint32_t)g.Ctot + (uint32_t)c) * 2u : OOB;
+  return ok ? (pix * (uint32_t)g.Ctot + (uint32_t)c) * (uint32_t)ES : OOB;
 }
 
 // --- generic (unaligned) path ------------------------------------------------
@@ -314,8 +317,9 @@ __device__ __forceinline__ KPos kpos_init(const GatherGeom& g, int k) {
   return KPos{k - tap * g.Cg, r, tap - r * g.kw};
 }
 
+template <int STEP = BK>
 __device__ __forceinline__ void kpos_advance(const GatherGeom& g, KPos& kp) {
-  kp.c += BK;
+  kp.c += STEP;
   while (kp.c >= g.Cg) {
     kp.c -= g.Cg;
     if (++kp.s == g.kw) {
@@ -525,8 +529,9 @@ struct KRange {
   int kt0, kt1;
 };
 
+template <int STEP = BK>
 __device__ __forceinline__ KRange split_range(const NTParams& p, int split) {
-  const int KT = (p.K + BK - 1) / BK;
+  const int KT = (p.K + STEP - 1) / STEP;
   const int per = (KT + p.splits - 1) / p.splits;
   const int kt0 = split * per;
   return KRange{kt0, min(KT, kt0 + per)};
@@ -1519,24 +1524,663 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch(WGBatch b) {
     wgrad_pipe_body<BM, BN, 2>(p, work - b.start[i], lds);
 }
 
+// ===========================================================================
+// fp32 (reference-precision) path: 3-pass split-bf16 MFMA
+// ===========================================================================
+// The reference trains in fp32 (TF 1.14 / PyTorch 1.4 defaults).  In this
+// mode every operand and output stays fp32 in HBM; gfx950 has no xf32, and
+// its fp32 MFMA runs at 1/16 of the bf16 rate, so products go through the
+// bf16 matrix cores in three passes instead:
+//   v = hi + lo,  hi = bf16(v),  lo = bf16(v - hi)     (v - hi is exact)
+//   a * b ~= ah*bh + ah*bl + al*bh                      (al*bl ~ 2^-16 |ab| dropped)
+// with fp32 accumulation: per-product relative error <= ~2^-15, fp32 level
+// for training (tests: relative L2 error vs an fp64 reference <= 1e-4).
+// Operands are register-staged (global fp32 -> split -> LDS).  A stage
+// covers KS = 32 reduction elements and lands in the SAME LDS images as the
+// bf16 kernels: for K-contiguous (NT) rows hi sits in chunks 0-3 and lo in
+// chunks 4-7; for TN tiles hi fills reduction rows 0-31 and lo rows 32-63.
+// The bf16 fragment reads of substep kk = 0 / 1 thus return the hi / lo
+// fragments of the same 32 k, and each fragment pair takes three MFMAs.
+// Epilogues write fp32 straight from the accumulators (a lane holds 4
+// consecutive output channels of one row: one 16-B store).
+constexpr int KS = 32;
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  // gfx950 v_cvt_pk_bf16_f32 (round to nearest even, NaN preserving)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+
+// 8 fp32 (two 16-B loads) -> 8 bf16 hi + 8 bf16 lo
+__device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint4& hi, uint4& lo) {
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = __uint_as_float(w[2 * i]), x1 = __uint_as_float(w[2 * i + 1]);
+    const uint32_t hp = cvt_pk_bf16(x0, x1);
+    h[i] = hp;
+    l[i] = cvt_pk_bf16(x0 - __uint_as_float(hp << 16), x1 - __uint_as_float(hp & 0xffff0000u));
+  }
+  hi = make_uint4(h[0], h[1], h[2], h[3]);
+  lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+__device__ __forceinline__ uint4 f4_bits(const float* e) {
+  return make_uint4(__float_as_uint(e[0]), __float_as_uint(e[1]), __float_as_uint(e[2]),
+                    __float_as_uint(e[3]));
+}
+
+// per-element fp32 im2col gather of an 8-wide k chunk (unaligned operands)
+__device__ __forceinline__ void gather_chunk_slow32(const GatherGeom& g, int cfg, const RowPos& p,
+                                                    int k0, int K, int dgrad, uint4& c0,
+                                                    uint4& c1) {
+  const float* src = reinterpret_cast<const float*>(g.src);
+  float e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    e[i] = 0.f;
+    const int k = k0 + i;
+    if (k < K) {
+      const int tap = (int)fdiv((uint32_t)k, g.dCg), c = k - tap * g.Cg;
+      const int r = (int)fdiv((uint32_t)tap, g.dkw), s = tap - r * g.kw;
+      const int64_t off = src_pixel(g, p, r, s, dgrad);
+      if (off >= 0) e[i] = src[off + (int64_t)cfg * g.cfg_off + c];
+    }
+  }
+  c0 = f4_bits(e);
+  c1 = f4_bits(e + 4);
+}
+
+// 8 consecutive fp32 of a row (bounds per element), as two uint4
+__device__ __forceinline__ void load_row8_slow32(const float* src, int valid, uint4& c0,
+                                                 uint4& c1) {
+  float e[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) e[t] = t < valid ? src[t] : 0.f;
+  c0 = f4_bits(e);
+  c1 = f4_bits(e + 4);
+}
+
+// three MFMAs per fragment pair: (first operand, second operand) = (x, y)
+__device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const bf16x8& yh,
+                                       const bf16x8& yl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, yh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yh, acc, 0, 0, 0);
+}
+
+// A: NT image, B: NT image (forward)
+template <int BM, int BN>
+__device__ __forceinline__ void mma3_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                        int lane, f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+  bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc));
+    al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc + 4));
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    bh[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 16 * j + fr, fc));
+    bl[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 16 * j + fr, fc + 4));
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+}
+
+// A: NT image, B: TN image (dgrad)
+template <int BM, int BN>
+__device__ __forceinline__ void mma3_nn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                        int lane, f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+  bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc));
+    al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 16 * i + fr, fc + 4));
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    bh[j] = tn_frag<BN>(sb, 0, wn * TN + 16 * j, lane);
+    bl[j] = tn_frag<BN>(sb, KS, wn * TN + 16 * j, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+}
+
+// both TN images (wgrad)
+template <int BM, int BN>
+__device__ __forceinline__ void mma3_tn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                        int lane, f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    ah[i] = tn_frag<BM>(sa, 0, wm * TM + 16 * i, lane);
+    al[i] = tn_frag<BM>(sa, KS, wm * TM + 16 * i, lane);
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    bh[j] = tn_frag<BN>(sb, 0, wn * TN + 16 * j, lane);
+    bl[j] = tn_frag<BN>(sb, KS, wn * TN + 16 * j, lane);
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
+}
+
+// fp32 epilogue of the NT / NN kernels, straight from the accumulators:
+// lane (fr, fc) of wave (wm, wn) owns rows wm*TM + 16i + fr and channels
+// wn*TN + 16j + 4fc .. +3.  out = act(acc + bias) (+ addend), one 16-B
+// store per fragment; optional per-(M tile, channel) statistics partials:
+// forward BN (sum, sum^2) of the outputs (p.stats) or the BN-backward
+// (sum dz, sum dz*xhat) of a dgrad output (p.bb.part, BNBwdEpi).  xch: LDS
+// scratch of 4*BN floats.
+template <int BM, int BN>
+__device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
+                                      float* xch, int cfg, int m0, int n0, int wm, int wn,
+                                      int lane, int tid) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+  float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
+  const float* adb =
+      p.addend ? reinterpret_cast<const float*>(p.addend) + (int64_t)cfg * p.N : nullptr;
+  const BNBwdEpi& bb = p.bb;
+  const bool fstat = p.stats != nullptr;
+  const bool bstat = bb.part != nullptr;
+  const bool vec = ((p.N | p.ldc) & 3) == 0;
+  const float* zb = bstat ? reinterpret_cast<const float*>(bb.z) + (int64_t)cfg * p.N : nullptr;
+  const float* yb = bstat && bb.ym == 1 ? reinterpret_cast<const float*>(bb.y) + (int64_t)cfg * p.N
+                                       : nullptr;
+  float bc[FN][4], mu[FN][4], is[FN][4], sc[FN][4], sh[FN][4], s[FN][4], q[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+      const int nn = n < p.N ? n : p.N - 1;
+      bc[j][e] = p.bias ? reinterpret_cast<const float*>(p.bias)[(int64_t)cfg * p.bias_gstride + nn]
+                        : 0.f;
+      s[j][e] = q[j][e] = 0.f;
+      mu[j][e] = is[j][e] = sc[j][e] = sh[j][e] = 0.f;
+      if (bstat) {
+        const int64_t c = (int64_t)cfg * p.N + nn;
+        mu[j][e] = bb.mean[c];
+        is[j][e] = bb.invstd[c];
+        if (bb.ym == 2) {                   // YM_Z: the forward's scale / shift
+          const float ga = reinterpret_cast<const float*>(bb.gamma)[cfg * bb.gstride + nn];
+          const float be = reinterpret_cast<const float*>(bb.beta)[cfg * bb.bstride + nn];
+          sc[j][e] = is[j][e] * ga;
+          sh[j][e] = be - mu[j][e] * sc[j][e];
+        }
+      }
+    }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * TM + 16 * i + fr;
+    if (m >= p.M) continue;
+    int64_t orow = m;
+    if (p.o_st > 1) {
+      const RowPos r = decode_row(m, p.M, p.a);
+      orow = ((int64_t)r.b * p.o_H + (int64_t)r.y * p.o_st) * p.o_W + (int64_t)r.x * p.o_st;
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + 16 * j + 4 * fc;
+      if (n >= p.N) continue;
+      const int64_t go = orow * p.ldc + n;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bc[j][e];
+        v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
+      }
+      if (vec) {
+        if (adb) {
+          const float4 a = *reinterpret_cast<const float4*>(adb + go);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        }
+        *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < p.N) {
+            if (adb) v[e] += adb[go + e];
+            obase[go + e] = v[e];
+          }
+      }
+      if (fstat) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[j][e] += v[e];
+          q[j][e] += v[e] * v[e];
+        }
+      } else if (bstat) {      // host-gated: vec
+        const float4 z4 = *reinterpret_cast<const float4*>(zb + go);
+        const float zv[4] = {z4.x, z4.y, z4.z, z4.w};
+        float yv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (yb) {
+          const float4 y4 = *reinterpret_cast<const float4*>(yb + go);
+          yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float dz = v[e];
+          if (bb.ym == 2)
+            dz = (zv[e] * sc[j][e] + sh[j][e] + 0.f) > 0.f ? dz : 0.f;
+          else if (bb.ym == 1)
+            dz = bb.act == 6 ? ((yv[e] > 0.f && yv[e] < 6.f) ? dz : 0.f) : (yv[e] > 0.f ? dz : 0.f);
+          s[j][e] += dz;
+          q[j][e] += dz * (zv[e] - mu[j][e]) * is[j][e];
+        }
+      }
+    }
+  }
+  if (!fstat && !bstat) return;
+  // rows -> one deterministic partial per (M tile, channel): DPP over the 16
+  // lanes of equal fc, then the two M-direction waves meet in LDS
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sm = row16_sum(s[j][e]);
+      const float sq = row16_sum(q[j][e]);
+      if (fr == 0) {
+        const int nl = wn * TN + 16 * j + 4 * fc + e;
+        xch[(wm * 2) * BN + nl] = sm;
+        xch[(wm * 2 + 1) * BN + nl] = sq;
+      }
+    }
+  __syncthreads();
+  float* dst = (fstat ? p.stats : bb.part) + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  for (int t = tid; t < 2 * BN; t += NTHREADS) {
+    const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
+    if (n < p.N) dst[(int64_t)qd * p.ldc + n] = xch[qd * BN + nl] + xch[(2 + qd) * BN + nl];
+  }
+}
+
+// forward (and the unaligned-dgrad fallback through transposed weights):
+// y = act(im2col(x) W^T + b), fp32 in / out
+template <int BM, int BN, int GM>
+__global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
+  constexpr int CPR = KS / 8;                                  // 8-float chunks per row
+  constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
+  constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
+  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+#define SA(buf) (lds + (buf) * (BM * BK))
+#define SB(buf) (lds + 2 * BM * BK + (buf) * (BN * BK))
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;
+  work /= p.splits;
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range<KS>(p, split);
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int my_chunk = tid & (CPR - 1);
+  const float* wbase = reinterpret_cast<const float*>(p.w) + (int64_t)cfg * p.w_gstride;
+  const float* abase = reinterpret_cast<const float*>(p.a.src) + (int64_t)cfg * p.a.cfg_off;
+
+  RowPos rows[A_CH];
+  RowA rowa[A_CH];
+  __amdgpu_buffer_rsrc_t rA, rB;
+  if constexpr (GM != GM_SLOW) {
+    rA = make_rsrc(abase, p.a.bytes);
+    rB = make_rsrc(wbase, (uint32_t)p.N * (uint32_t)p.K * 4u);
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
+  } else {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
+  }
+  KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+  uint4 ra[2 * A_CH], rb[2 * B_CH];
+
+  auto load_tiles = [&](int kt) {
+    const int k0 = kt * KS + 8 * my_chunk;
+    if constexpr (GM != GM_SLOW) {
+      const bool kok = k0 < p.K;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
+        const uint32_t o = kok ? off : OOB;
+        ra[2 * i] = bload(rA, o);
+        ra[2 * i + 1] = bload(rA, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const int n = n0 + (tid + NTHREADS * i) / CPR;
+        const uint32_t o = (kok && n < p.N) ? (uint32_t)(n * p.K + k0) * 4u : OOB;
+        rb[2 * i] = bload(rB, o);
+        rb[2 * i + 1] = bload(rB, o + 16u);
+      }
+      kpos_advance<KS>(p.a, kp);
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i)
+        gather_chunk_slow32(p.a, cfg, rows[i], k0, p.K, p.dgrad, ra[2 * i], ra[2 * i + 1]);
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const int n = n0 + (tid + NTHREADS * i) / CPR;
+        load_row8_slow32(wbase + (int64_t)n * p.K + k0, n < p.N ? p.K - k0 : 0, rb[2 * i],
+                         rb[2 * i + 1]);
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = (tid + NTHREADS * i) / CPR;
+      uint4 h, l;
+      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
+      *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk + 4)) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = (tid + NTHREADS * i) / CPR;
+      uint4 h, l;
+      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk)) = h;
+      *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk + 4)) = l;
+    }
+  };
+
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  load_tiles(kr.kt0);
+  store_tiles(0);
+  __syncthreads();
+  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
+    const int cur = (kt - kr.kt0) & 1;
+    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
+    mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc);
+    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+#undef SA
+#undef SB
+}
+
+// dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
+// rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
+template <int BM, int BN, int GM>
+__global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, FastDiv dCout) {
+  constexpr int CPR = KS / 8;
+  constexpr int A_CH = BM * CPR / NTHREADS;
+  constexpr int B_CPR = BN / 8, B_CH = KS * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
+  constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
+  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;
+  work /= p.splits;
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range<KS>(p, split);
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int my_chunk = tid & (CPR - 1);
+  const int Cout = p.a.Cg, Cin = p.N;
+  const float* wbase = reinterpret_cast<const float*>(p.w) + (int64_t)cfg * p.w_gstride;
+  const float* abase = reinterpret_cast<const float*>(p.a.src) + (int64_t)cfg * p.a.cfg_off;
+  const int b_col = 8 * (tid % B_CPR), b_row0 = tid / B_CPR;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(abase, p.a.bytes);
+  const __amdgpu_buffer_rsrc_t rW =
+      make_rsrc(wbase, (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 4u);
+
+  RowA rowa[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
+  KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+  uint4 ra[2 * A_CH], rb[2 * B_CH];
+
+  auto load_tiles = [&](int kt) {
+    const int k0 = kt * KS + 8 * my_chunk;
+    const bool kok = k0 < p.K;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
+      const uint32_t o = kok ? off : OOB;
+      ra[2 * i] = bload(rA, o);
+      ra[2 * i + 1] = bload(rA, o + 16u);
+    }
+    kpos_advance<KS>(p.a, kp);
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int k = kt * KS + b_row0 + B_RSTEP * i;
+      const int c = n0 + b_col;
+      const int tap = (int)fdiv((uint32_t)k, dCout);
+      const int n = k - tap * Cout;
+      const uint32_t o = (k < p.K && c < Cin) ? (uint32_t)((n * T + tap) * Cin + c) * 4u : OOB;
+      rb[2 * i] = bload(rW, o);
+      rb[2 * i + 1] = bload(rW, o + 16u);
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    bf16_t* sa = lds + buf * (BM * BK);
+    bf16_t* sb = lds + 2 * BM * BK + buf * (BK * BN);
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = (tid + NTHREADS * i) / CPR;
+      uint4 h, l;
+      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk)) = h;
+      *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk + 4)) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = b_row0 + B_RSTEP * i;
+      uint4 h, l;
+      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
+      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+    }
+  };
+
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  load_tiles(kr.kt0);
+  store_tiles(0);
+  __syncthreads();
+  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
+    const int cur = (kt - kr.kt0) & 1;
+    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
+    mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane, acc);
+    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+}
+
+// wgrad tile body (fp32 operands): dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]
+template <int BM, int BN, int GM>
+__device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf16_t* lds) {
+  constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
+  constexpr int A_CH = KS * A_CPR / NTHREADS, B_CH = KS * B_CPR / NTHREADS;
+  constexpr int A_RSTEP = NTHREADS / A_CPR, B_RSTEP = NTHREADS / B_CPR;
+
+  const int tiles_k = (p.K + BN - 1) / BN;
+  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
+  const int cfg = work / (tiles * p.splits);
+  const int rem = work - cfg * tiles * p.splits;
+  const int split = rem / tiles, tile = rem - split * tiles;
+  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
+  const int n0 = tn_ * BM, k0 = tk * BN;
+  const int ms = split * p.m_per_split;
+  const int me = min(p.Mred, ms + p.m_per_split);
+  if (ms >= me) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wa = wid >> 1, wb = wid & 1;
+  const int a_col = 8 * (tid % A_CPR), b_col = 8 * (tid % B_CPR);
+  const int a_row0 = tid / A_CPR, b_row0 = tid / B_CPR;
+  const int kk0 = k0 + b_col;
+  const bool b_kok = kk0 < p.K;
+  KPos bk{0, 0, 0};
+  if (b_kok) bk = kpos_init(p.x, kk0);
+  uint4 ra[2 * A_CH], rb[2 * B_CH];
+  const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
+  const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
+  __amdgpu_buffer_rsrc_t rDY, rX;
+  if constexpr (GM != GM_SLOW) {
+    rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
+    rX = make_rsrc(xb, p.x.bytes);
+  }
+
+  auto load_tiles = [&](int mt) {
+    const int mbase = ms + mt * KS;
+    if constexpr (GM != GM_SLOW) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
+        const uint32_t o = (m < me && n < p.N) ? (uint32_t)(m * p.ldy + n) * 4u : OOB;
+        ra[2 * i] = bload(rDY, o);
+        ra[2 * i + 1] = bload(rDY, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
+        const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
+        const uint32_t o = b_kok ? off : OOB;
+        rb[2 * i] = bload(rX, o);
+        rb[2 * i + 1] = bload(rX, o + 16u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
+        load_row8_slow32(dyb + (int64_t)m * p.ldy + n, (m < me && n < p.N) ? p.N - n : 0,
+                         ra[2 * i], ra[2 * i + 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const int m = mbase + b_row0 + B_RSTEP * i;
+        const RowPos pos = decode_row(m, me, p.x);
+        if (b_kok && pos.ok) {
+          gather_chunk_slow32(p.x, cfg, pos, kk0, p.K, 0, rb[2 * i], rb[2 * i + 1]);
+        } else {
+          rb[2 * i] = make_uint4(0, 0, 0, 0);
+          rb[2 * i + 1] = make_uint4(0, 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    bf16_t* sa = lds + buf * (BK * BM);
+    bf16_t* sb = lds + 2 * BK * BM + buf * (BK * BN);
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = a_row0 + A_RSTEP * i;
+      uint4 h, l;
+      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(sa + tn_off<BM>(row, a_col)) = h;
+      *reinterpret_cast<uint4*>(sa + tn_off<BM>(row + KS, a_col)) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = b_row0 + B_RSTEP * i;
+      uint4 h, l;
+      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
+      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+    }
+  };
+
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  const int MT = (me - ms + KS - 1) / KS;
+  load_tiles(0);
+  store_tiles(0);
+  __syncthreads();
+  for (int mt = 0; mt < MT; ++mt) {
+    const int cur = mt & 1;
+    if (mt + 1 < MT) load_tiles(mt + 1);
+    mma3_tn<BM, BN>(lds + cur * (BK * BM), lds + 2 * BK * BM + cur * (BK * BN), wa, wb, lane, acc);
+    if (mt + 1 < MT) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
+  const int fr = lane & 15, fc = lane >> 4;
+  const bool split_k = p.splits > 1;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wa * TM + 16 * i + 4 * fc + e;
+        const int k = k0 + wb * TN + 16 * j + fr;
+        if (n < p.N && k < p.K) {
+          float* d = dwb + (int64_t)n * p.K + k;
+          if (split_k)
+            atomicAdd(d, acc[i][j][e]);
+          else
+            *d = acc[i][j][e];
+        }
+      }
+}
+
+template <int BM, int BN, int GM>
+__global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
+  wgrad_reg_body32<BM, BN, GM>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
+}
+
+// batched fp32 weight gradients (see wgrad_batch)
+template <int BM, int BN>
+__global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  int i = 0;
+  while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
+  const WGParams p = b.p[i];
+  wgrad_reg_body32<BM, BN, GM_FWD>(p, work - b.start[i], lds);
+}
+
 // ---------------------------------------------------------------------------
 // per-config weight transpose for dgrad: W[N][T][C] -> Wt[C][T][N]
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void transpose_w_kernel(const bf16_t* __restrict__ w,
+template <typename E>
+__global__ __launch_bounds__(256) void transpose_w_kernel(const E* __restrict__ w,
                                                           int64_t w_gstride,
-                                                          bf16_t* __restrict__ wt, int N,
+                                                          E* __restrict__ wt, int N,
                                                           int T, int C) {
-  __shared__ bf16_t tile[32][33];
+  __shared__ E tile[32][33];
   const int cfg = blockIdx.z;
   const int t = blockIdx.y;
   const int tiles_c = (C + 31) / 32;
   const int tn = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
-  const bf16_t* src = w + (int64_t)cfg * w_gstride;
-  bf16_t* dst = wt + (int64_t)cfg * N * T * C;
+  const E* src = w + (int64_t)cfg * w_gstride;
+  E* dst = wt + (int64_t)cfg * N * T * C;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   for (int yy = ty; yy < 32; yy += 8) {
     const int n = tn * 32 + yy, c = tc * 32 + tx;
-    tile[yy][tx] = (n < N && c < C) ? src[((int64_t)n * T + t) * C + c] : (bf16_t)0;
+    tile[yy][tx] = (n < N && c < C) ? src[((int64_t)n * T + t) * C + c] : (E)0;
   }
   __syncthreads();
   for (int yy = ty; yy < 32; yy += 8) {
@@ -1606,9 +2250,9 @@ static void tile_dims(int v, int& bm, int& bn) {
 
 // split count for a fwd / dgrad GEMM: enough blocks for ~1.5 waves of 256 CUs,
 // >= 4 K tiles per split, within the registered workspace
-static int nt_splits(const NTParams& p, int G, int bm, int bn) {
+static int nt_splits(const NTParams& p, int G, int bm, int bn, int ks) {
   const long tiles = ntiles(p.M, p.N, bm, bn) * G;
-  const int KT = (p.K + BK - 1) / BK;
+  const int KT = (p.K + ks - 1) / ks;
   int s = (int)((384 + tiles - 1) / tiles);
   if (s > 8) s = 8;
   if (s > KT / 4) s = KT / 4;
@@ -1619,10 +2263,10 @@ static int nt_splits(const NTParams& p, int G, int bm, int bn) {
   return s;
 }
 
-static void set_splits(NTParams& p, int G, int v) {
+static void set_splits(NTParams& p, int G, int v, int ks = BK) {
   int bm, bn;
   tile_dims(v, bm, bn);
-  p.splits = (v / 3) >= 2 ? nt_splits(p, G, bm, bn) : 1;
+  p.splits = (v / 3) >= 2 ? nt_splits(p, G, bm, bn, ks) : 1;
   p.skws = g_sk.ws;
   p.skcnt = g_sk.cnt;
 }
@@ -1668,10 +2312,46 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   return (int)hipGetLastError();
 }
 
-static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+// ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
+// LDS-DMA variant id maps to its register-staged twin (v - 3)
+template <int BM, int BN>
+static void launch_nt32_t(const NTParams& p, int G, bool fast, hipStream_t stream) {
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  if (fast)
+    igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+  else
+    igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+}
+
+static bool nt_fast32(const NTParams& p) {
+  return p.dgrad == 0 && (p.a.Cg % 8 == 0) && (p.a.Ctot % 8 == 0) && (p.K % 8 == 0) &&
+         p.a.bytes != 0 && (uint64_t)p.N * p.K * 4 < (1ull << 31);
+}
+
+static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
+
+static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
+  if (p.fin.cnt) return (int)hipErrorInvalidValue;   // fused finalize: bf16 path only
+  const bool fast = nt_fast32(p);
+  const int v = fp32_variant(choose(0, p.M, p.N, p.K, G, false));
+  set_splits(p, G, v, KS);
+  if (nslab) {
+    int bm, bn;
+    tile_dims(v, bm, bn);
+    *nslab = (int)((p.M + bm - 1) / bm);
+  }
+  switch (v % 3) {
+    case 0: launch_nt32_t<64, 64>(p, G, fast, stream); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, stream); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, stream); break;
+  }
+  return (int)hipGetLastError();
+}
+
+static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
-                         bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, const BNFinal* fin,
+                         void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
+                         int act, float* stats, int* nslab, const BNFinal* fin, bool f32,
                          hipStream_t stream);
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
@@ -1679,7 +2359,15 @@ CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
                          int act, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
-                       bias_gstride, act, nullptr, nullptr, nullptr, stream);
+                       bias_gstride, act, nullptr, nullptr, nullptr, false, stream);
+}
+
+CER_API int cer_conv_fwd_f32(const float* x, int B, int H, int W, int Cin, int G, const float* w,
+                             int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                             float* y, int Ho, int Wo, const float* bias, int64_t bias_gstride,
+                             int act, hipStream_t stream) {
+  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
+                       bias_gstride, act, nullptr, nullptr, nullptr, true, stream);
 }
 
 // forward + BN statistics partials (bias-free, no activation): part holds
@@ -1690,7 +2378,15 @@ CER_API int cer_conv_fwd_stats(const bf16_t* x, int B, int H, int W, int Cin, in
                                int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
                                int* nslab, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nslab, nullptr, stream);
+                       nullptr, 0, 0, part, nslab, nullptr, false, stream);
+}
+
+CER_API int cer_conv_fwd_stats_f32(const float* x, int B, int H, int W, int Cin, int G,
+                                   const float* w, int64_t w_gstride, int Cout, int kh, int kw,
+                                   int st, int pad, float* y, int Ho, int Wo, float* part,
+                                   int* nslab, hipStream_t stream) {
+  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
+                       nullptr, 0, 0, part, nslab, nullptr, true, stream);
 }
 
 // forward + BN statistics + BN finalize (mean / invstd / running stats) in
@@ -1703,7 +2399,7 @@ CER_API int cer_conv_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, i
                                 float momentum, hipStream_t stream) {
   BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nullptr, &f, stream);
+                       nullptr, 0, 0, part, nullptr, &f, false, stream);
 }
 
 // upper bound over tile choices: one slab per 64-row M tile
@@ -1711,30 +2407,30 @@ CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
   return ((M + 63) / 64) * 2 * (int64_t)C;
 }
 
-static int conv_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
-                         bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, const BNFinal* fin,
+                         void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
+                         int act, float* stats, int* nslab, const BNFinal* fin, bool f32,
                          hipStream_t stream) {
   NTParams p;
   p.fin = fin ? *fin : BNFinal{};
-  p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad);
+  p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, f32 ? 4 : 2);
   p.dgrad = 0;
-  p.w = w;
+  p.w = reinterpret_cast<const bf16_t*>(w);
   p.w_gstride = w_gstride;
-  p.out = y;
+  p.out = reinterpret_cast<bf16_t*>(y);
   p.ldc = G * Cout;
   p.M = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
-  p.bias = bias;
+  p.bias = reinterpret_cast<const bf16_t*>(bias);
   p.bias_gstride = bias_gstride;
   p.act = act;
   p.o_st = 1;
   p.o_H = Ho;
   p.o_W = Wo;
   p.stats = stats;
-  return run_nt(p, G, stream, nslab);
+  return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
 
 template <int BM, int BN>
@@ -1775,22 +2471,35 @@ static BNBwdEpi g_bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nul
                                 0, 0, 0};
 static int* g_bb_nslab = nullptr;
 
-CER_API void cer_conv_dgrad_bnbwd(float* part, const bf16_t* z, const bf16_t* y,
-                                  const float* mean, const float* invstd, const bf16_t* gamma,
-                                  int64_t gstride, const bf16_t* beta, int64_t bstride, int act,
+// z, y, gamma, beta: bf16 for cer_conv_dgrad, fp32 for cer_conv_dgrad_f32
+CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
+                                  const float* mean, const float* invstd, const void* gamma,
+                                  int64_t gstride, const void* beta, int64_t bstride, int act,
                                   int has_res, int* nslab_out) {
-  g_bb = BNBwdEpi{part, z, y, mean, invstd, gamma, gstride, beta, bstride,
-                  bn_mask_mode(act, has_res), act};
+  g_bb = BNBwdEpi{part, reinterpret_cast<const bf16_t*>(z), reinterpret_cast<const bf16_t*>(y),
+                  mean, invstd, reinterpret_cast<const bf16_t*>(gamma), gstride,
+                  reinterpret_cast<const bf16_t*>(beta), bstride, bn_mask_mode(act, has_res), act};
   g_bb_nslab = part ? nslab_out : nullptr;
 }
 
-CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, int G,
-                           const bf16_t* w, int64_t w_gstride, bf16_t* wt, int Cin, int kh,
-                           int kw, int st, int pad, bf16_t* dx, int H, int W,
-                           const bf16_t* addend, hipStream_t stream) {
+template <int BM, int BN>
+static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream) {
+  dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if (strided)
+    igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+  else
+    igemm_nn32<BM, BN, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+}
+
+static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int G, const void* w,
+                           int64_t w_gstride, void* wt, int Cin, int kh, int kw, int st, int pad,
+                           void* dx, int H, int W, const void* addend, bool f32,
+                           hipStream_t stream) {
   const int T = kh * kw;
+  const int es = f32 ? 4 : 2;
   NTParams p;
-  p.addend = addend;           // dx = dgrad + addend (nullptr: dx = dgrad)
+  p.addend = reinterpret_cast<const bf16_t*>(addend);  // dx = dgrad + addend (null: dx = dgrad)
   p.stats = nullptr;
   p.fin = BNFinal{};
   p.bias = nullptr;
@@ -1799,37 +2508,38 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   p.o_st = 1;
   p.o_H = H;
   p.o_W = W;
-  p.out = dx;
+  p.out = reinterpret_cast<bf16_t*>(dx);
   p.ldc = G * Cin;
   p.N = Cin;
   p.K = T * Cout;
   const bool aligned = (Cout % 8 == 0) && (Cin % 8 == 0) &&
-                       (uint64_t)B * Ho * Wo * G * Cout * 2 < (1ull << 31) &&
-                       (uint64_t)Cout * T * Cin * 2 < (1ull << 31);
+                       (uint64_t)B * Ho * Wo * G * Cout * es < (1ull << 31) &&
+                       (uint64_t)Cout * T * Cin * es < (1ull << 31);
   if (aligned) {
-    p.w = w;
+    p.w = reinterpret_cast<const bf16_t*>(w);
     p.w_gstride = w_gstride;
     bool strided = false;
     if (kh == 1 && kw == 1 && pad == 0 && st > 1) {
       // rows (b, ho, wo) of dy map to dx pixels (b, ho*st, wo*st); others get 0
       // (or the addend, which the kernel adds on the written pixels)
-      const size_t bytes = sizeof(bf16_t) * (size_t)B * H * W * G * Cin;
+      const size_t bytes = (size_t)es * B * H * W * G * Cin;
       if (addend)
         (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, stream);
       else
         (void)hipMemsetAsync(dx, 0, bytes, stream);
-      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0);
+      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0, es);
       p.dgrad = 0;
       p.M = B * Ho * Wo;
       p.o_st = st;
     } else {
-      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
+      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
       p.dgrad = 1;
       p.M = B * H * W;
       strided = st > 1;
     }
-    const int v = choose(1, p.M, p.N, p.K, G, Cout % 64 == 0);
-    set_splits(p, G, v);
+    int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
+    if (f32) v = fp32_variant(v);
+    set_splits(p, G, v, f32 ? KS : BK);
     const int kind = (v / 3) & 1;
     // BN-backward statistics: every dx pixel must come out of the epilogue
     // (a strided 1x1 dgrad leaves pixels at zero: fine without an addend)
@@ -1841,6 +2551,14 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
     } else if (g_bb_nslab) {
       *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
     }
+    if (f32) {
+      switch (v % 3) {
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream); break;
+      }
+      return (int)hipGetLastError();
+    }
     switch (v % 3) {
       case 0: launch_nn_t<64, 64>(p, G, T, kind, strided, stream); break;
       case 1: launch_nn_t<128, 128>(p, G, T, kind, strided, stream); break;
@@ -1850,13 +2568,36 @@ CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, in
   }
   if (g_bb_nslab) *g_bb_nslab = 0;       // fallback path: no BN statistics
   dim3 tg(((Cout + 31) / 32) * ((Cin + 31) / 32), T, G);
-  transpose_w_kernel<<<tg, 256, 0, stream>>>(w, w_gstride, wt, Cout, T, Cin);
-  p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad);
+  if (f32)
+    transpose_w_kernel<float><<<tg, 256, 0, stream>>>(reinterpret_cast<const float*>(w),
+                                                      w_gstride, reinterpret_cast<float*>(wt),
+                                                      Cout, T, Cin);
+  else
+    transpose_w_kernel<bf16_t><<<tg, 256, 0, stream>>>(reinterpret_cast<const bf16_t*>(w),
+                                                       w_gstride, reinterpret_cast<bf16_t*>(wt),
+                                                       Cout, T, Cin);
+  p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
   p.dgrad = 1;
-  p.w = wt;
+  p.w = reinterpret_cast<const bf16_t*>(wt);
   p.w_gstride = (int64_t)Cout * T * Cin;
   p.M = B * H * W;
-  return run_nt(p, G, stream);
+  return f32 ? run_nt32(p, G, stream) : run_nt(p, G, stream);
+}
+
+CER_API int cer_conv_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, int G,
+                           const bf16_t* w, int64_t w_gstride, bf16_t* wt, int Cin, int kh,
+                           int kw, int st, int pad, bf16_t* dx, int H, int W,
+                           const bf16_t* addend, hipStream_t stream) {
+  return conv_dgrad_impl(dy, B, Ho, Wo, Cout, G, w, w_gstride, wt, Cin, kh, kw, st, pad, dx, H, W,
+                         addend, false, stream);
+}
+
+CER_API int cer_conv_dgrad_f32(const float* dy, int B, int Ho, int Wo, int Cout, int G,
+                               const float* w, int64_t w_gstride, float* wt, int Cin, int kh,
+                               int kw, int st, int pad, float* dx, int H, int W,
+                               const float* addend, hipStream_t stream) {
+  return conv_dgrad_impl(dy, B, Ho, Wo, Cout, G, w, w_gstride, wt, Cin, kh, kw, st, pad, dx, H, W,
+                         addend, true, stream);
 }
 
 static int wg_variant(int N, int K, int G, bool fast) {
@@ -1922,10 +2663,58 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
   return (int)hipGetLastError();
 }
 
+// ---- fp32 weight gradients (register-staged 3-pass kernels) ----------------
+template <int BM, int BN>
+static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t stream) {
+  p.m_per_split = ((p.Mred + splits - 1) / splits + BK - 1) / BK * BK;
+  splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
+  p.splits = splits;
+  dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
+  if (fast)
+    igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+  else
+    igemm_wgrad32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+}
+
+static bool wg_fast32(int Cin, int Cout, const WGParams& p) {
+  return (Cin % 8 == 0) && (Cout % 8 == 0) && p.x.bytes != 0 &&
+         (uint64_t)p.Mred * p.ldy * 4 < (1ull << 31);
+}
+
+static void run_wg32(WGParams p, int G, int splits, bool fast, hipStream_t stream) {
+  const int v = choose(2, 0, p.N, p.K, G, false) % 3;
+  switch (v) {
+    case 0: launch_wg32_t<64, 64>(p, G, fast, splits, stream); break;
+    case 1: launch_wg32_t<128, 128>(p, G, fast, splits, stream); break;
+    default: launch_wg32_t<128, 64>(p, G, fast, splits, stream); break;
+  }
+}
+
+CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int G,
+                               const float* dy, int Ho, int Wo, int Cout, int kh, int kw, int st,
+                               int pad, float* dw, int64_t dw_gstride, int splits,
+                               hipStream_t stream) {
+  WGParams p;
+  p.x = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, 4);
+  p.dy = reinterpret_cast<const bf16_t*>(dy);
+  p.ldy = G * Cout;
+  p.dw = dw;
+  p.dw_gstride = dw_gstride;
+  p.Mred = B * Ho * Wo;
+  p.N = Cout;
+  p.K = kh * kw * Cin;
+  run_wg32(p, G, splits, wg_fast32(Cin, Cout, p), stream);
+  return (int)hipGetLastError();
+}
+
 // ---- batched (deferred) weight gradients ----------------------------------
+// one queue per dtype; a flush launches both
 static WGParams g_wgq[4096];
 static int g_wgq_G[4096];
 static int g_wgq_n = 0;
+static WGParams g_wgq32[4096];
+static int g_wgq32_G[4096];
+static int g_wgq32_n = 0;
 static int g_wgb_rows = 0;
 
 static int wgb_rows() {
@@ -1964,6 +2753,45 @@ CER_API int cer_wgrad_batch_add(const bf16_t* x, int B, int H, int W, int Cin, i
   return p.splits;
 }
 
+CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin, int G,
+                                    const float* dy, int Ho, int Wo, int Cout, int kh, int kw,
+                                    int st, int pad, float* dw, int64_t dw_gstride) {
+  if (g_wgq32_n >= 4096) return 0;
+  WGParams p;
+  p.x = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, 4);
+  p.dy = reinterpret_cast<const bf16_t*>(dy);
+  p.ldy = G * Cout;
+  p.dw = dw;
+  p.dw_gstride = dw_gstride;
+  p.Mred = B * Ho * Wo;
+  p.N = Cout;
+  p.K = kh * kw * Cin;
+  if (!wg_fast32(Cin, Cout, p)) return 0;
+  const int rows = wgb_rows();
+  p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
+  p.splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
+  g_wgq32_G[g_wgq32_n] = G;
+  g_wgq32[g_wgq32_n++] = p;
+  return p.splits;
+}
+
+template <int BM, int BN>
+static int wgb32_launch(hipStream_t stream) {
+  for (int b0 = 0; b0 < g_wgq32_n; b0 += WGB_MAX) {
+    WGBatch bt;
+    bt.n = g_wgq32_n - b0 < WGB_MAX ? g_wgq32_n - b0 : WGB_MAX;
+    int tot = 0;
+    for (int i = 0; i < bt.n; ++i) {
+      bt.p[i] = g_wgq32[b0 + i];
+      bt.start[i] = tot;
+      tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[b0 + i]);
+    }
+    bt.start[bt.n] = tot;
+    if (tot > 0) wgrad_batch32<BM, BN><<<tot, NTHREADS, 0, stream>>>(bt);
+  }
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN, int KIND>
 static int wgb_launch(hipStream_t stream) {
   for (int b0 = 0; b0 < g_wgq_n; b0 += WGB_MAX) {
@@ -1996,11 +2824,19 @@ CER_API int cer_wgrad_batch_flush(int v, int discard, hipStream_t stream) {
       default: rc = wgb_launch<64, 64, 0>(stream); break;
     }
   }
+  if (!discard && g_wgq32_n > 0 && rc == 0) {
+    switch (v % 3) {         // fp32: the register-staged tile of the same shape
+      case 1: rc = wgb32_launch<128, 128>(stream); break;
+      case 2: rc = wgb32_launch<128, 64>(stream); break;
+      default: rc = wgb32_launch<64, 64>(stream); break;
+    }
+  }
   g_wgq_n = 0;
+  g_wgq32_n = 0;
   return rc;
 }
 
-CER_API int cer_wgrad_batch_pending() { return g_wgq_n; }
+CER_API int cer_wgrad_batch_pending() { return g_wgq_n + g_wgq32_n; }
 
 // the split count the host should use (and whether dw needs zeroing); the
 // variant is re-derived exactly as cer_conv_wgrad will (fast path assumed
@@ -2021,25 +2857,23 @@ CER_API int cer_wgrad_splits(int Mred, int N, int K, int G) {
 // Weights are re-laid [N][kh][kw'][8] per step (zeros on padded taps /
 // channels); the wgrad runs on the same geometry and is folded back.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void stem_repack_kernel(const bf16_t* __restrict__ x,
-                                                          bf16_t* __restrict__ x4, int64_t P,
+template <typename E>
+__global__ __launch_bounds__(256) void stem_repack_kernel(const E* __restrict__ x,
+                                                          E* __restrict__ x4, int64_t P,
                                                           int G, int C) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, config)
   if (i >= P * G) return;
   const int64_t p = i / G;
   const int g = (int)(i - p * G);
-  const bf16_t* src = x + p * G * C + (int64_t)g * C;
-  uint16_t e[4] = {0, 0, 0, 0};
-  for (int c = 0; c < C; ++c) e[c] = src[c];
-  uint2 v;
-  v.x = e[0] | ((uint32_t)e[1] << 16);
-  v.y = e[2] | ((uint32_t)e[3] << 16);
-  *reinterpret_cast<uint2*>(x4 + ((int64_t)g * P + p) * 4) = v;
+  const E* src = x + p * G * C + (int64_t)g * C;
+  E* dst = x4 + ((int64_t)g * P + p) * 4;
+  for (int c = 0; c < 4; ++c) dst[c] = c < C ? src[c] : (E)0;
 }
 
-__global__ __launch_bounds__(256) void stem_pack_w_kernel(const bf16_t* __restrict__ w,
+template <typename E>
+__global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ w,
                                                           int64_t w_gstride,
-                                                          bf16_t* __restrict__ wp, int N, int kh,
+                                                          E* __restrict__ wp, int N, int kh,
                                                           int kw, int C, int kwp, int G) {
   const int64_t per = (int64_t)N * kh * kwp * 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -2053,7 +2887,7 @@ __global__ __launch_bounds__(256) void stem_pack_w_kernel(const bf16_t* __restri
   const int r = (int)(t % kh);
   const int n = (int)(t / kh);
   const int px = q >> 2, c = q & 3, s = 2 * sp + px - 1;
-  bf16_t v = 0;
+  E v = 0;
   if (s >= 0 && s < kw && c < C) v = w[g * w_gstride + (((int64_t)n * kh + r) * kw + s) * C + c];
   wp[i] = v;
 }
@@ -2089,7 +2923,7 @@ CER_API int64_t cer_stem_wpk_elems(int G, int Cout, int kh, int kw) {
   return (int64_t)G * Cout * kh * stem_kwp(kw) * 8;
 }
 
-static GatherGeom stem_geom(const bf16_t* x4, int B, int H, int W, int Ho, int Wo, int kh,
+static GatherGeom stem_geom(const void* x4, int B, int H, int W, int Ho, int Wo, int kh,
                             int kw, int pad) {
   const int kwp = stem_kwp(kw);
   GatherGeom g = make_geom(x4, B, 8, 8, H, W / 2, Ho, Wo, kh, kwp, 2, pad);
@@ -2099,26 +2933,36 @@ static GatherGeom stem_geom(const bf16_t* x4, int B, int H, int W, int Ho, int W
   return g;
 }
 
-static int stem_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
+static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
-                         bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
-                         int* nslab, const BNFinal* fin, hipStream_t stream) {
+                         void* x4, void* wpk, void* y, int Ho, int Wo, float* part,
+                         int* nslab, const BNFinal* fin, bool f32, hipStream_t stream) {
   if (!cer_stem_ok(Cin, W, kw, st, pad)) return (int)hipErrorInvalidValue;
   const int64_t P = (int64_t)B * H * W;
-  stem_repack_kernel<<<cer_blocks(P * G, 256), 256, 0, stream>>>(x, x4, P, G, Cin);
   const int kwp = stem_kwp(kw);
   const int64_t nw = (int64_t)G * Cout * kh * kwp * 8;
-  stem_pack_w_kernel<<<cer_blocks(nw, 256), 256, 0, stream>>>(w, w_gstride, wpk, Cout, kh, kw,
-                                                              Cin, kwp, G);
+  if (f32) {
+    stem_repack_kernel<float><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
+        reinterpret_cast<const float*>(x), reinterpret_cast<float*>(x4), P, G, Cin);
+    stem_pack_w_kernel<float><<<cer_blocks(nw, 256), 256, 0, stream>>>(
+        reinterpret_cast<const float*>(w), w_gstride, reinterpret_cast<float*>(wpk), Cout, kh, kw,
+        Cin, kwp, G);
+  } else {
+    stem_repack_kernel<bf16_t><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
+        reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(x4), P, G, Cin);
+    stem_pack_w_kernel<bf16_t><<<cer_blocks(nw, 256), 256, 0, stream>>>(
+        reinterpret_cast<const bf16_t*>(w), w_gstride, reinterpret_cast<bf16_t*>(wpk), Cout, kh,
+        kw, Cin, kwp, G);
+  }
   NTParams p;
   p.a = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
   // the whole [G][B][H][W/2][8] buffer is the buffer-load range
-  const uint64_t bytes = (uint64_t)G * P * 4 * 2;
+  const uint64_t bytes = (uint64_t)G * P * 4 * (f32 ? 4 : 2);
   p.a.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   p.dgrad = 0;
-  p.w = wpk;
+  p.w = reinterpret_cast<const bf16_t*>(wpk);
   p.w_gstride = (int64_t)Cout * kh * kwp * 8;
-  p.out = y;
+  p.out = reinterpret_cast<bf16_t*>(y);
   p.ldc = G * Cout;
   p.M = B * Ho * Wo;
   p.N = Cout;
@@ -2131,7 +2975,7 @@ static int stem_fwd_impl(const bf16_t* x, int B, int H, int W, int Cin, int G, c
   p.o_W = Wo;
   p.stats = part;
   p.fin = fin ? *fin : BNFinal{};
-  return run_nt(p, G, stream, nslab);
+  return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
 
 // repack + weight re-layout + forward conv (+ BN partials when part != null)
@@ -2140,10 +2984,19 @@ CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
                          bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
                          int* nslab, hipStream_t stream) {
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nslab, nullptr, stream);
+                       Wo, part, nslab, nullptr, false, stream);
 }
 
-// same with the BN finalize fused (see cer_conv_fwd_bnstat)
+// fp32 twin: x4 / wpk / y fp32 (same element counts)
+CER_API int cer_stem_fwd_f32(const float* x, int B, int H, int W, int Cin, int G, const float* w,
+                             int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
+                             float* x4, float* wpk, float* y, int Ho, int Wo, float* part,
+                             int* nslab, hipStream_t stream) {
+  return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
+                       Wo, part, nslab, nullptr, true, stream);
+}
+
+// same with the BN finalize fused (see cer_conv_fwd_bnstat; bf16 only)
 CER_API int cer_stem_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, int G,
                                 const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
                                 int st, int pad, bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho,
@@ -2152,38 +3005,56 @@ CER_API int cer_stem_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, i
                                 float eps, float momentum, hipStream_t stream) {
   BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nullptr, &f, stream);
+                       Wo, part, nullptr, &f, false, stream);
 }
 
 // dW of the stem from the repacked input; dwp: fp32 scratch of
 // cer_stem_wpk_elems floats (zeroed here when the reduction is split)
-CER_API int cer_stem_wgrad(const bf16_t* x4, int B, int H, int W, int Cin, int G,
-                           const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
-                           float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
+static int stem_wgrad_impl(const void* x4, int B, int H, int W, int Cin, int G, const void* dy,
+                           int Ho, int Wo, int Cout, int kh, int kw, int pad, float* dwp,
+                           float* dw, int64_t dw_gstride, bool f32, hipStream_t stream) {
   const int kwp = stem_kwp(kw);
   WGParams p;
   p.x = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
-  const uint64_t bytes = (uint64_t)G * B * H * W * 4 * 2;
+  const uint64_t bytes = (uint64_t)G * B * H * W * 4 * (f32 ? 4 : 2);
   p.x.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
-  p.dy = dy;
+  p.dy = reinterpret_cast<const bf16_t*>(dy);
   p.ldy = G * Cout;
   p.dw = dwp;
   p.dw_gstride = (int64_t)Cout * kh * kwp * 8;
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kwp * 8;
-  const bool fast = wg_fast(8, Cout, p);
-  const int v = wg_variant(p.N, p.K, G, fast);
+  const bool fast = f32 ? wg_fast32(8, Cout, p) : wg_fast(8, Cout, p);
+  const int v = wg_variant(p.N, p.K, G, fast && !f32);
   const int splits = wg_splits(p.Mred, p.N, p.K, G, v);
   if (splits > 1) (void)hipMemsetAsync(dwp, 0, sizeof(float) * (size_t)G * p.dw_gstride, stream);
-  const int kind = v / 3;
-  switch (v % 3) {
-    case 0: launch_wg_t<64, 64>(p, G, kind, fast, splits, stream); break;
-    case 1: launch_wg_t<128, 128>(p, G, kind, fast, splits, stream); break;
-    default: launch_wg_t<128, 64>(p, G, kind, fast, splits, stream); break;
+  if (f32) {
+    run_wg32(p, G, splits, fast, stream);
+  } else {
+    const int kind = v / 3;
+    switch (v % 3) {
+      case 0: launch_wg_t<64, 64>(p, G, kind, fast, splits, stream); break;
+      case 1: launch_wg_t<128, 128>(p, G, kind, fast, splits, stream); break;
+      default: launch_wg_t<128, 64>(p, G, kind, fast, splits, stream); break;
+    }
   }
   const int64_t n = (int64_t)G * Cout * kh * kw * Cin;
   stem_fold_grad_kernel<<<cer_blocks(n, 256), 256, 0, stream>>>(dwp, dw, dw_gstride, Cout, kh, kw,
                                                                 Cin, kwp, G);
   return (int)hipGetLastError();
+}
+
+CER_API int cer_stem_wgrad(const bf16_t* x4, int B, int H, int W, int Cin, int G,
+                           const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
+                           float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
+  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, pad, dwp, dw, dw_gstride,
+                         false, stream);
+}
+
+CER_API int cer_stem_wgrad_f32(const float* x4, int B, int H, int W, int Cin, int G,
+                               const float* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
+                               float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
+  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, pad, dwp, dw, dw_gstride,
+                         true, stream);
 }

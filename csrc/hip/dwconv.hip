@@ -26,46 +26,27 @@ namespace {
 constexpr int DW_V = 8;     // channels per thread
 constexpr int DW_X = 4;     // output columns per fwd thread
 
-__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
-  uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
-__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
-  uint4 u;
-  u.x = pack_bf2(v[0], v[1]);
-  u.y = pack_bf2(v[2], v[3]);
-  u.z = pack_bf2(v[4], v[5]);
-  u.w = pack_bf2(v[6], v[7]);
-  *reinterpret_cast<uint4*>(p) = u;
-}
-
 struct DWGeom {
   int B, H, W, C, G, Ho, Wo, pt, pl;
   int64_t w_gstride;
 };
 
 // filter row r of the 8 channels starting at packed channel gc0
-template <int K>
-__device__ __forceinline__ void load_wrow(const bf16_t* w, const DWGeom& d, int gc0, int r,
+template <int K, typename T>
+__device__ __forceinline__ void load_wrow(const T* w, const DWGeom& d, int gc0, int r,
                                           float (&wr)[K][DW_V]) {
   const int g = gc0 / d.C, c0 = gc0 - g * d.C;
-  const bf16_t* base = w + g * d.w_gstride + (int64_t)c0 * K * K + r * K;
+  const T* base = w + g * d.w_gstride + (int64_t)c0 * K * K + r * K;
 #pragma unroll
   for (int i = 0; i < DW_V; ++i)
 #pragma unroll
-    for (int s = 0; s < K; ++s) wr[s][i] = bf2f(base[i * K * K + s]);
+    for (int s = 0; s < K; ++s) wr[s][i] = ld1(base + i * K * K + s);
 }
 
-template <int K, int ST>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16_t* __restrict__ x,
-                                                     const bf16_t* __restrict__ w,
-                                                     bf16_t* __restrict__ y, DWGeom d) {
+template <int K, int ST, typename T>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x,
+                                                     const T* __restrict__ w,
+                                                     T* __restrict__ y, DWGeom d) {
   constexpr int NWIN = (DW_X - 1) * ST + K;
   const int GC = d.G * d.C, CV = GC / DW_V;
   const int xgroups = (d.Wo + DW_X - 1) / DW_X;
@@ -90,8 +71,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16_t* __restrict__ 
     const int hi = ho * ST - d.pt + r;
     if (hi < 0 || hi >= d.H) continue;
     float wr[K][DW_V];
-    load_wrow<K>(w, d, gc0, r, wr);
-    const bf16_t* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
+    load_wrow<K, T>(w, d, gc0, r, wr);
+    const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
     float win[NWIN][DW_V];
 #pragma unroll
     for (int j = 0; j < NWIN; ++j) {
@@ -117,10 +98,10 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-template <int K, int ST>
-__global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16_t* __restrict__ dy,
-                                                       const bf16_t* __restrict__ w,
-                                                       bf16_t* __restrict__ dx, DWGeom d) {
+template <int K, int ST, typename T>
+__global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
+                                                       const T* __restrict__ w,
+                                                       T* __restrict__ dx, DWGeom d) {
   const int GC = d.G * d.C, CV = GC / DW_V;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)d.B * d.H * d.W * CV;
@@ -139,7 +120,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16_t* __restrict_
     const int ho = hn / ST;
     if (ho >= d.Ho) continue;
     float wr[K][DW_V];
-    load_wrow<K>(w, d, gc0, r, wr);
+    load_wrow<K, T>(w, d, gc0, r, wr);
 #pragma unroll
     for (int s = 0; s < K; ++s) {
       const int wn = wi + d.pl - s;
@@ -157,9 +138,9 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const bf16_t* __restrict_
 
 // grid (GC / 8, row slabs, K / RB filter-row bands); 256 lanes stride over the
 // slab's output pixels, each accumulating RB x K taps x 8 channels
-template <int K, int RB>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16_t* __restrict__ x,
-                                                       const bf16_t* __restrict__ dy,
+template <int K, int RB, typename T>
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
+                                                       const T* __restrict__ dy,
                                                        float* __restrict__ dw,
                                                        int64_t dw_gstride, DWGeom d, int st,
                                                        int64_t pix_per_slab) {
@@ -236,57 +217,59 @@ bool dw_shape_ok(int C, int k, int st, int pt, int pl, int Ho, int Wo) {
          pl >= 0 && pt < k && pl < k && Ho > 0 && Wo > 0;
 }
 
-template <int K>
-void launch_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, const DWGeom& d, int st,
+template <int K, typename T>
+void launch_fwd(const T* x, const T* w, T* y, const DWGeom& d, int st,
                 hipStream_t stream) {
   const int64_t n = (int64_t)d.B * d.Ho * ((d.Wo + DW_X - 1) / DW_X) * (d.G * d.C / DW_V);
   if (st == 1)
-    dw_fwd_kernel<K, 1><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+    dw_fwd_kernel<K, 1, T><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
   else
-    dw_fwd_kernel<K, 2><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
+    dw_fwd_kernel<K, 2, T><<<cer_blocks(n, 256), 256, 0, stream>>>(x, w, y, d);
 }
 
-template <int K>
-void launch_dgrad(const bf16_t* dy, const bf16_t* w, bf16_t* dx, const DWGeom& d, int st,
+template <int K, typename T>
+void launch_dgrad(const T* dy, const T* w, T* dx, const DWGeom& d, int st,
                   hipStream_t stream) {
   const int64_t n = (int64_t)d.B * d.H * d.W * (d.G * d.C / DW_V);
   if (st == 1)
-    dw_dgrad_kernel<K, 1><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+    dw_dgrad_kernel<K, 1, T><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
   else
-    dw_dgrad_kernel<K, 2><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
+    dw_dgrad_kernel<K, 2, T><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
 }
 
 }  // namespace
 
 // pt / pl: top / left zero padding; Ho / Wo: output size (fixes bottom/right)
-CER_API int cer_dwconv_fwd(const bf16_t* x, int B, int H, int W, int C, int G, const bf16_t* w,
+template <typename T>
+static int dwconv_fwd_t(const T* x, int B, int H, int W, int C, int G, const T* w,
                            int64_t w_gstride, int k, int st, int pt, int pl, int Ho, int Wo,
-                           bf16_t* y, hipStream_t stream) {
+                           T* y, hipStream_t stream) {
   if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo)) return (int)hipErrorInvalidValue;
   const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
   if (k == 3)
-    launch_fwd<3>(x, w, y, d, st, stream);
+    launch_fwd<3, T>(x, w, y, d, st, stream);
   else if (k == 5)
-    launch_fwd<5>(x, w, y, d, st, stream);
+    launch_fwd<5, T>(x, w, y, d, st, stream);
   else
-    launch_fwd<7>(x, w, y, d, st, stream);
+    launch_fwd<7, T>(x, w, y, d, st, stream);
   return (int)hipGetLastError();
 }
 
 // dw must be zero on entry (accumulated with atomics); dx may be null
-CER_API int cer_dwconv_bwd(const bf16_t* dy, const bf16_t* x, int B, int H, int W, int C, int G,
-                           const bf16_t* w, int64_t w_gstride, float* dw, int64_t dw_gstride,
-                           int k, int st, int pt, int pl, int Ho, int Wo, bf16_t* dx,
+template <typename T>
+static int dwconv_bwd_t(const T* dy, const T* x, int B, int H, int W, int C, int G,
+                           const T* w, int64_t w_gstride, float* dw, int64_t dw_gstride,
+                           int k, int st, int pt, int pl, int Ho, int Wo, T* dx,
                            hipStream_t stream) {
   if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo)) return (int)hipErrorInvalidValue;
   const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
   if (dx) {
     if (k == 3)
-      launch_dgrad<3>(dy, w, dx, d, st, stream);
+      launch_dgrad<3, T>(dy, w, dx, d, st, stream);
     else if (k == 5)
-      launch_dgrad<5>(dy, w, dx, d, st, stream);
+      launch_dgrad<5, T>(dy, w, dx, d, st, stream);
     else
-      launch_dgrad<7>(dy, w, dx, d, st, stream);
+      launch_dgrad<7, T>(dy, w, dx, d, st, stream);
   }
   const int64_t P = (int64_t)B * Ho * Wo;
   const int cblocks = G * C / DW_V;
@@ -297,10 +280,27 @@ CER_API int cer_dwconv_bwd(const bf16_t* dy, const bf16_t* x, int B, int H, int 
   slabs = (P + per - 1) / per;
   dim3 grid(cblocks, (unsigned)slabs, bands);
   if (k == 3)
-    dw_wgrad_kernel<3, 3><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    dw_wgrad_kernel<3, 3, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
   else if (k == 5)
-    dw_wgrad_kernel<5, 5><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    dw_wgrad_kernel<5, 5, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
   else
-    dw_wgrad_kernel<7, 1><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    dw_wgrad_kernel<7, 1, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
   return (int)hipGetLastError();
 }
+
+#define CER_DW_ENTRY_POINTS(T, SFX)                                                              \
+  CER_API int cer_dwconv_fwd##SFX(const T* x, int B, int H, int W, int C, int G, const T* w,    \
+                                  int64_t w_gstride, int k, int st, int pt, int pl, int Ho,     \
+                                  int Wo, T* y, hipStream_t stream) {                           \
+    return dwconv_fwd_t<T>(x, B, H, W, C, G, w, w_gstride, k, st, pt, pl, Ho, Wo, y, stream);   \
+  }                                                                                              \
+  CER_API int cer_dwconv_bwd##SFX(const T* dy, const T* x, int B, int H, int W, int C, int G,   \
+                                  const T* w, int64_t w_gstride, float* dw, int64_t dw_gstride, \
+                                  int k, int st, int pt, int pl, int Ho, int Wo, T* dx,         \
+                                  hipStream_t stream) {                                         \
+    return dwconv_bwd_t<T>(dy, x, B, H, W, C, G, w, w_gstride, dw, dw_gstride, k, st, pt, pl,   \
+                           Ho, Wo, dx, stream);                                                 \
+  }
+
+CER_DW_ENTRY_POINTS(bf16_t, )
+CER_DW_ENTRY_POINTS(float, _f32)

@@ -1,6 +1,6 @@
 // Embedding-bag first layer of the Criteo MLP: a one-hot
 // input row with <= nnz active columns times a dense [K, N] kernel is the sum
-// of nnz kernel rows.  idx [G, B, nnz] int32 (-1 = padding), W_g [K, N] bf16
+// of nnz kernel rows.  idx [G, B, nnz] int32 (-1 = padding), W_g [K, N] bf16 / fp32
 // at w + g*w_gstride, bias_g [N].
 //   fwd : y[b, g*N + n] = act(bias_g[n] + sum_j W_g[idx[g,b,j], n])
 //   bwd : dz = act'(y) * dy ; dW_g[idx, :] += dz (fp32 atomics into the
@@ -12,24 +12,15 @@ namespace {
 
 constexpr int EB_V = 8;
 
-__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
-  uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
+template <typename T>
 __global__ __launch_bounds__(128) void embbag_fwd_kernel(
-    const int32_t* __restrict__ idx, int B, int nnz, const bf16_t* __restrict__ w,
-    int64_t w_gstride, const bf16_t* __restrict__ bias, int64_t b_gstride, int N, int act,
-    bf16_t* __restrict__ y) {
+    const int32_t* __restrict__ idx, int B, int nnz, const T* __restrict__ w,
+    int64_t w_gstride, const T* __restrict__ bias, int64_t b_gstride, int N, int act,
+    T* __restrict__ y) {
   const int b = blockIdx.x, g = blockIdx.y;
   const int G = gridDim.y;
   const int32_t* ids = idx + ((int64_t)g * B + b) * nnz;
-  const bf16_t* wg = w + g * w_gstride;
+  const T* wg = w + g * w_gstride;
   for (int n0 = threadIdx.x * EB_V; n0 < N; n0 += blockDim.x * EB_V) {
     float acc[EB_V];
     ld8(bias + g * b_gstride + n0, acc);
@@ -41,23 +32,17 @@ __global__ __launch_bounds__(128) void embbag_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < EB_V; ++i) acc[i] += v[i];
     }
-    uint4 o;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    if (act) {
 #pragma unroll
-    for (int i = 0; i < EB_V / 2; ++i) {
-      float a0 = acc[2 * i], a1 = acc[2 * i + 1];
-      if (act) {
-        a0 = fmaxf(a0, 0.f);
-        a1 = fmaxf(a1, 0.f);
-      }
-      ow[i] = pack_bf2(a0, a1);
+      for (int i = 0; i < EB_V; ++i) acc[i] = fmaxf(acc[i], 0.f);
     }
-    *reinterpret_cast<uint4*>(y + (int64_t)b * G * N + (int64_t)g * N + n0) = o;
+    st8(y + (int64_t)b * G * N + (int64_t)g * N + n0, acc);
   }
 }
 
+template <typename T>
 __global__ __launch_bounds__(128) void embbag_bwd_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ y, const int32_t* __restrict__ idx,
+    const T* __restrict__ dy, const T* __restrict__ y, const int32_t* __restrict__ idx,
     int B, int nnz, float* __restrict__ dw, int64_t dw_gstride, float* __restrict__ db,
     int64_t db_gstride, int N, int act) {
   const int b = blockIdx.x, g = blockIdx.y;
@@ -87,21 +72,39 @@ __global__ __launch_bounds__(128) void embbag_bwd_kernel(
 
 }  // namespace
 
-CER_API int cer_embbag_fwd(const int32_t* idx, int G, int B, int nnz, const bf16_t* w,
-                           int64_t w_gstride, const bf16_t* bias, int64_t b_gstride, int N,
-                           int act, bf16_t* y, hipStream_t stream) {
+template <typename T>
+static int embbag_fwd_t(const int32_t* idx, int G, int B, int nnz, const T* w,
+                           int64_t w_gstride, const T* bias, int64_t b_gstride, int N,
+                           int act, T* y, hipStream_t stream) {
   if (N % EB_V) return (int)hipErrorInvalidValue;
-  embbag_fwd_kernel<<<dim3(B, G), 128, 0, stream>>>(idx, B, nnz, w, w_gstride, bias, b_gstride,
+  embbag_fwd_kernel<T><<<dim3(B, G), 128, 0, stream>>>(idx, B, nnz, w, w_gstride, bias, b_gstride,
                                                     N, act, y);
   return (int)hipGetLastError();
 }
 
 // dw / db must be zero on entry
-CER_API int cer_embbag_bwd(const bf16_t* dy, const bf16_t* y, const int32_t* idx, int G, int B,
+template <typename T>
+static int embbag_bwd_t(const T* dy, const T* y, const int32_t* idx, int G, int B,
                            int nnz, float* dw, int64_t dw_gstride, float* db, int64_t db_gstride,
                            int N, int act, hipStream_t stream) {
   if (N % EB_V) return (int)hipErrorInvalidValue;
-  embbag_bwd_kernel<<<dim3(B, G), 128, 0, stream>>>(dy, y, idx, B, nnz, dw, dw_gstride, db,
+  embbag_bwd_kernel<T><<<dim3(B, G), 128, 0, stream>>>(dy, y, idx, B, nnz, dw, dw_gstride, db,
                                                     db_gstride, N, act);
   return (int)hipGetLastError();
 }
+
+#define CER_EMBBAG_ENTRY_POINTS(T, SFX)                                                          \
+  CER_API int cer_embbag_fwd##SFX(const int32_t* idx, int G, int B, int nnz, const T* w,        \
+                                  int64_t w_gstride, const T* bias, int64_t b_gstride, int N,   \
+                                  int act, T* y, hipStream_t stream) {                          \
+    return embbag_fwd_t<T>(idx, G, B, nnz, w, w_gstride, bias, b_gstride, N, act, y, stream);   \
+  }                                                                                              \
+  CER_API int cer_embbag_bwd##SFX(const T* dy, const T* y, const int32_t* idx, int G, int B,    \
+                                  int nnz, float* dw, int64_t dw_gstride, float* db,            \
+                                  int64_t db_gstride, int N, int act, hipStream_t stream) {     \
+    return embbag_bwd_t<T>(dy, y, idx, G, B, nnz, dw, dw_gstride, db, db_gstride, N, act,       \
+                           stream);                                                              \
+  }
+
+CER_EMBBAG_ENTRY_POINTS(bf16_t, )
+CER_EMBBAG_ENTRY_POINTS(float, _f32)

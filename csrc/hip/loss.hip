@@ -6,7 +6,7 @@
 // rank (-> top-1/top-5 hit, ties broken by index like a stable top-k),
 // the per-config mean loss, the metric accumulators (atomics into acc[g][4] =
 // {loss_sum, top1, top5, count}) and, when requested, dlogits =
-// (softmax - onehot) / B written in bf16 for the backward pass.
+// (softmax - onehot) / B written in the compute dtype for the backward pass.
 #include "common.h"
 
 template <typename T>
@@ -19,10 +19,10 @@ __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, int64_t i) { return
 constexpr int CE_THREADS = 256;
 constexpr int CE_MAXPER = 8;  // N <= 2048
 
-template <typename T>
+template <typename T, typename TD>
 __global__ __launch_bounds__(CE_THREADS) void softmax_ce_kernel(
     const T* __restrict__ logits, const int* __restrict__ labels, float* __restrict__ acc,
-    float* __restrict__ loss_out, bf16_t* __restrict__ dlogits, int B, int G, int N) {
+    float* __restrict__ loss_out, TD* __restrict__ dlogits, int B, int G, int N) {
   __shared__ float smem[16];
   const int b = blockIdx.x, g = blockIdx.y;
   const int64_t base = (int64_t)b * G * N + (int64_t)g * N;
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(CE_THREADS) void softmax_ce_kernel(
       int j = threadIdx.x + k * CE_THREADS;
       if (j < N) {
         float p = __expf(z[k] - mx) * inv_se;
-        dlogits[base + j] = f2bf((p - (j == lab ? 1.f : 0.f)) * inv_b);
+        st1(dlogits + base + j, (p - (j == lab ? 1.f : 0.f)) * inv_b);
       }
     }
   }
@@ -74,13 +74,25 @@ CER_API int cer_softmax_ce(const void* logits, int logits_bf16, const int* label
                            float* loss_out, bf16_t* dlogits, int B, int G, int N,
                            hipStream_t stream) {
   if (N > CE_THREADS * CE_MAXPER) return (int)hipErrorInvalidValue;
-  if (loss_out) hipMemsetAsync(loss_out, 0, sizeof(float) * G, stream);
+  if (loss_out) (void)hipMemsetAsync(loss_out, 0, sizeof(float) * G, stream);
   dim3 grid(B, G);
   if (logits_bf16)
-    softmax_ce_kernel<bf16_t><<<grid, CE_THREADS, 0, stream>>>(
+    softmax_ce_kernel<bf16_t, bf16_t><<<grid, CE_THREADS, 0, stream>>>(
         (const bf16_t*)logits, labels, acc, loss_out, dlogits, B, G, N);
   else
-    softmax_ce_kernel<float><<<grid, CE_THREADS, 0, stream>>>(
+    softmax_ce_kernel<float, bf16_t><<<grid, CE_THREADS, 0, stream>>>(
         (const float*)logits, labels, acc, loss_out, dlogits, B, G, N);
+  return (int)hipGetLastError();
+}
+
+// reference-precision mode: fp32 logits in, fp32 dlogits out
+CER_API int cer_softmax_ce_f32(const float* logits, const int* labels, float* acc,
+                               float* loss_out, float* dlogits, int B, int G, int N,
+                               hipStream_t stream) {
+  if (N > CE_THREADS * CE_MAXPER) return (int)hipErrorInvalidValue;
+  if (loss_out) (void)hipMemsetAsync(loss_out, 0, sizeof(float) * G, stream);
+  softmax_ce_kernel<float, float><<<dim3(B, G), CE_THREADS, 0, stream>>>(logits, labels, acc,
+                                                                          loss_out, dlogits, B, G,
+                                                                          N);
   return (int)hipGetLastError();
 }

@@ -1,5 +1,6 @@
 // Pooling + bias/activation elementwise kernels on packed NHWC (SURVEY.md
-// K10, K15).  All kernels move 8 channels (16 B of bf16) per thread.
+// K10, K15).  All kernels move 8 channels per thread (16 B in bf16, 32 B in fp32);
+// every op has a bf16 and an _f32 entry point.
 //
 // maxpool fwd stores the argmax window offset (uint8) per output element;
 // maxpool bwd is a deterministic *gather* (each input pixel sums the
@@ -8,27 +9,9 @@
 
 constexpr int PT = 256;
 
-__device__ __forceinline__ void ld8(const bf16_t* p, float* v) {
-  uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(w[i] << 16);
-    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-  }
-}
-
-__device__ __forceinline__ void st8(bf16_t* p, const float* v) {
-  uint4 u;
-  u.x = pack_bf2(v[0], v[1]);
-  u.y = pack_bf2(v[2], v[3]);
-  u.z = pack_bf2(v[4], v[5]);
-  u.w = pack_bf2(v[6], v[7]);
-  *reinterpret_cast<uint4*>(p) = u;
-}
-
-__global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const bf16_t* __restrict__ x,
-                                                         bf16_t* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x,
+                                                         T* __restrict__ y,
                                                          uint8_t* __restrict__ arg, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pad) {
@@ -73,9 +56,10 @@ __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const bf16_t* __restric
   *reinterpret_cast<uint2*>(arg + o) = packed;
 }
 
-__global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+template <typename T>
+__global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                          const uint8_t* __restrict__ arg,
-                                                         bf16_t* __restrict__ dx, int B, int H,
+                                                         T* __restrict__ dx, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
@@ -115,8 +99,9 @@ __global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const bf16_t* __restric
 }
 
 // global average pool: x [B, HW, C] -> y [B, C]
-__global__ __launch_bounds__(PT) void gavg_fwd_kernel(const bf16_t* __restrict__ x,
-                                                      bf16_t* __restrict__ y, int B, int HW,
+template <typename T>
+__global__ __launch_bounds__(PT) void gavg_fwd_kernel(const T* __restrict__ x,
+                                                      T* __restrict__ y, int B, int HW,
                                                       int C) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
   const int cv = C / 8;
@@ -136,8 +121,9 @@ __global__ __launch_bounds__(PT) void gavg_fwd_kernel(const bf16_t* __restrict__
   st8(y + (int64_t)b * C + c0, acc);
 }
 
-__global__ __launch_bounds__(PT) void gavg_bwd_kernel(const bf16_t* __restrict__ dy,
-                                                      bf16_t* __restrict__ dx, int B, int HW,
+template <typename T>
+__global__ __launch_bounds__(PT) void gavg_bwd_kernel(const T* __restrict__ dy,
+                                                      T* __restrict__ dx, int B, int HW,
                                                       int C) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
   const int cv = C / 8;
@@ -155,9 +141,10 @@ __global__ __launch_bounds__(PT) void gavg_bwd_kernel(const bf16_t* __restrict__
 }
 
 // bias + activation: y = act(x + bias[g][c]) over [M, C] packed channels
-__global__ __launch_bounds__(PT) void bias_act_fwd_kernel(const bf16_t* __restrict__ x,
-                                                          const bf16_t* __restrict__ bias,
-                                                          int64_t bstride, bf16_t* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(PT) void bias_act_fwd_kernel(const T* __restrict__ x,
+                                                          const T* __restrict__ bias,
+                                                          int64_t bstride, T* __restrict__ y,
                                                           int64_t M, int C, int Cper, int act) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
   const int cv = C / 8;
@@ -176,9 +163,10 @@ __global__ __launch_bounds__(PT) void bias_act_fwd_kernel(const bf16_t* __restri
 }
 
 // dz = act'(y) * dy  (written to dx) and per-channel partial sums of dz
-__global__ __launch_bounds__(PT) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
-                                                          const bf16_t* __restrict__ y,
-                                                          bf16_t* __restrict__ dx, float* ws,
+template <typename T>
+__global__ __launch_bounds__(PT) void bias_act_bwd_kernel(const T* __restrict__ dy,
+                                                          const T* __restrict__ y,
+                                                          T* __restrict__ dx, float* ws,
                                                           int64_t M, int C, int rows, int act) {
   const int c0 = (blockIdx.x * PT + threadIdx.x) * 8;
   if (c0 >= C) return;
@@ -211,22 +199,24 @@ __global__ void bias_grad_scatter(const float* ws, float* dbias, int64_t gstride
 }
 
 // scalar fallbacks for channel counts that are not multiples of 8 (N = 500, 10, 2 heads)
-__global__ __launch_bounds__(PT) void bias_act_fwd_scalar(const bf16_t* __restrict__ x,
-                                                          const bf16_t* __restrict__ bias,
-                                                          int64_t bstride, bf16_t* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(PT) void bias_act_fwd_scalar(const T* __restrict__ x,
+                                                          const T* __restrict__ bias,
+                                                          int64_t bstride, T* __restrict__ y,
                                                           int64_t M, int C, int Cper, int act) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
   if (t >= M * C) return;
   const int c = (int)(t % C);
   const int g = c / Cper;
-  float z = bf2f(x[t]) + bf2f(bias[g * bstride + (c - g * Cper)]);
+  float z = ld1(x + t) + ld1(bias + g * bstride + (c - g * Cper));
   z = act == 6 ? fminf(fmaxf(z, 0.f), 6.f) : (act ? fmaxf(z, 0.f) : z);
-  y[t] = f2bf(z);
+  st1(y + t, z);
 }
 
-__global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const bf16_t* __restrict__ dy,
-                                                          const bf16_t* __restrict__ y,
-                                                          bf16_t* __restrict__ dx, float* ws,
+template <typename T>
+__global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const T* __restrict__ dy,
+                                                          const T* __restrict__ y,
+                                                          T* __restrict__ dx, float* ws,
                                                           int64_t M, int C, int rows, int act) {
   const int c = blockIdx.x * PT + threadIdx.x;
   if (c >= C) return;
@@ -234,61 +224,67 @@ __global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const bf16_t* __restri
   const int64_t r1 = min(M, r0 + rows);
   float s = 0.f;
   for (int64_t r = r0; r < r1; ++r) {
-    const float d = bf2f(dy[r * C + c]), yv = bf2f(y[r * C + c]);
+    const float d = ld1(dy + r * C + c), yv = ld1(y + r * C + c);
     const float z = act == 6 ? ((yv > 0.f && yv < 6.f) ? d : 0.f) : (act ? (yv > 0.f ? d : 0.f) : d);
-    dx[r * C + c] = f2bf(z);
+    st1(dx + r * C + c, z);
     s += z;
   }
   atomicAdd(&ws[c], s);
 }
 
-CER_API int cer_maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* arg, int B, int H, int W, int C,
+template <typename T>
+static int cer_maxpool_fwd_t(const T* x, T* y, uint8_t* arg, int B, int H, int W, int C,
                             int Ho, int Wo, int k, int s, int pad, hipStream_t stream) {
   if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
   int64_t total = (int64_t)B * Ho * Wo * (C / 8);
-  maxpool_fwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, arg, B, H, W, C, Ho, Wo,
+  maxpool_fwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, arg, B, H, W, C, Ho, Wo,
                                                                k, s, pad);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_maxpool_bwd(const bf16_t* dy, const uint8_t* arg, bf16_t* dx, int B, int H,
+template <typename T>
+static int cer_maxpool_bwd_t(const T* dy, const uint8_t* arg, T* dx, int B, int H,
                             int W, int C, int Ho, int Wo, int k, int s, int pad,
                             hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   int64_t total = (int64_t)B * H * W * (C / 8);
-  maxpool_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, arg, dx, B, H, W, C, Ho, Wo,
+  maxpool_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, arg, dx, B, H, W, C, Ho, Wo,
                                                                k, s, pad);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_gavgpool_fwd(const bf16_t* x, bf16_t* y, int B, int HW, int C,
+template <typename T>
+static int cer_gavgpool_fwd_t(const T* x, T* y, int B, int HW, int C,
                              hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  gavg_fwd_kernel<<<cer_blocks((int64_t)B * (C / 8), PT), PT, 0, stream>>>(x, y, B, HW, C);
+  gavg_fwd_kernel<T><<<cer_blocks((int64_t)B * (C / 8), PT), PT, 0, stream>>>(x, y, B, HW, C);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_gavgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int HW, int C,
+template <typename T>
+static int cer_gavgpool_bwd_t(const T* dy, T* dx, int B, int HW, int C,
                              hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   int64_t total = (int64_t)B * HW * (C / 8);
-  gavg_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, HW, C);
+  gavg_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, HW, C);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bias_act_fwd(const bf16_t* x, const bf16_t* bias, int64_t bstride, bf16_t* y,
+template <typename T>
+static int cer_bias_act_fwd_t(const T* x, const T* bias, int64_t bstride, T* y,
                              int64_t M, int C, int Cper, int act, hipStream_t stream) {
   if (C % 8 || Cper % 8) {
-    bias_act_fwd_scalar<<<cer_blocks(M * C, PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
+    bias_act_fwd_scalar<T><<<cer_blocks(M * C, PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
                                                                   Cper, act);
     return (int)hipGetLastError();
   }
-  bias_act_fwd_kernel<<<cer_blocks(M * (C / 8), PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
+  bias_act_fwd_kernel<T><<<cer_blocks(M * (C / 8), PT), PT, 0, stream>>>(x, bias, bstride, y, M, C,
                                                                       Cper, act);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_bias_act_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, float* dbias,
+template <typename T>
+static int cer_bias_act_bwd_t(const T* dy, const T* y, T* dx, float* dbias,
                              int64_t gstride, float* ws, int64_t M, int C, int Cper, int act,
                              hipStream_t stream) {
   if (C % 8 || Cper % 8) {
@@ -297,8 +293,8 @@ CER_API int cer_bias_act_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, floa
     int64_t rows = (M + want - 1) / want;
     if (rows < 16) rows = 16;
     dim3 grid(cb, (unsigned)((M + rows - 1) / rows));
-    hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
-    bias_act_bwd_scalar<<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
+    (void)hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+    bias_act_bwd_scalar<T><<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
     bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
     return (int)hipGetLastError();
   }
@@ -307,8 +303,8 @@ CER_API int cer_bias_act_bwd(const bf16_t* dy, const bf16_t* y, bf16_t* dx, floa
   int64_t rows = (M + want - 1) / want;
   if (rows < 16) rows = 16;
   dim3 grid(cblocks, (unsigned)((M + rows - 1) / rows));
-  hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
-  bias_act_bwd_kernel<<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
+  (void)hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+  bias_act_bwd_kernel<T><<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
   bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
   return (int)hipGetLastError();
 }
@@ -328,8 +324,9 @@ __device__ __forceinline__ float avg_div(int ho, int wo, int H, int W, int k, in
   return n > 0 ? 1.f / (float)n : 0.f;
 }
 
-__global__ __launch_bounds__(PT) void avgpool_fwd_kernel(const bf16_t* __restrict__ x,
-                                                         bf16_t* __restrict__ y, int B, int H,
+template <typename T>
+__global__ __launch_bounds__(PT) void avgpool_fwd_kernel(const T* __restrict__ x,
+                                                         T* __restrict__ y, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pt, int pl, int count_pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
@@ -362,8 +359,9 @@ __global__ __launch_bounds__(PT) void avgpool_fwd_kernel(const bf16_t* __restric
 }
 
 // deterministic gather: each input pixel sums dy / divisor over the windows covering it
-__global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const bf16_t* __restrict__ dy,
-                                                         bf16_t* __restrict__ dx, int B, int H,
+template <typename T>
+__global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const T* __restrict__ dy,
+                                                         T* __restrict__ dx, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pt, int pl, int count_pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
@@ -395,24 +393,65 @@ __global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const bf16_t* __restric
   st8(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
 }
 
-CER_API int cer_avgpool_fwd(const bf16_t* x, bf16_t* y, int B, int H, int W, int C, int Ho,
+template <typename T>
+static int cer_avgpool_fwd_t(const T* x, T* y, int B, int H, int W, int C, int Ho,
                             int Wo, int k, int s, int pt, int pl, int count_pad,
                             hipStream_t stream) {
   if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
     return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)B * Ho * Wo * (C / 8);
-  avgpool_fwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, B, H, W, C, Ho, Wo, k, s,
+  avgpool_fwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, B, H, W, C, Ho, Wo, k, s,
                                                                pt, pl, count_pad);
   return (int)hipGetLastError();
 }
 
-CER_API int cer_avgpool_bwd(const bf16_t* dy, bf16_t* dx, int B, int H, int W, int C, int Ho,
+template <typename T>
+static int cer_avgpool_bwd_t(const T* dy, T* dx, int B, int H, int W, int C, int Ho,
                             int Wo, int k, int s, int pt, int pl, int count_pad,
                             hipStream_t stream) {
   if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
     return (int)hipErrorInvalidValue;
   const int64_t total = (int64_t)B * H * W * (C / 8);
-  avgpool_bwd_kernel<<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, H, W, C, Ho, Wo, k, s,
+  avgpool_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, H, W, C, Ho, Wo, k, s,
                                                                pt, pl, count_pad);
   return (int)hipGetLastError();
 }
+
+#define CER_POOL_ENTRY_POINTS(T, SFX)                                                            \
+  CER_API int cer_maxpool_fwd##SFX(const T* x, T* y, uint8_t* arg, int B, int H, int W, int C,  \
+                                   int Ho, int Wo, int k, int s, int pad, hipStream_t st) {      \
+    return cer_maxpool_fwd_t<T>(x, y, arg, B, H, W, C, Ho, Wo, k, s, pad, st);                   \
+  }                                                                                              \
+  CER_API int cer_maxpool_bwd##SFX(const T* dy, const uint8_t* arg, T* dx, int B, int H, int W, \
+                                   int C, int Ho, int Wo, int k, int s, int pad,                 \
+                                   hipStream_t st) {                                             \
+    return cer_maxpool_bwd_t<T>(dy, arg, dx, B, H, W, C, Ho, Wo, k, s, pad, st);                 \
+  }                                                                                              \
+  CER_API int cer_gavgpool_fwd##SFX(const T* x, T* y, int B, int HW, int C, hipStream_t st) {   \
+    return cer_gavgpool_fwd_t<T>(x, y, B, HW, C, st);                                            \
+  }                                                                                              \
+  CER_API int cer_gavgpool_bwd##SFX(const T* dy, T* dx, int B, int HW, int C, hipStream_t st) { \
+    return cer_gavgpool_bwd_t<T>(dy, dx, B, HW, C, st);                                          \
+  }                                                                                              \
+  CER_API int cer_bias_act_fwd##SFX(const T* x, const T* bias, int64_t bstride, T* y,           \
+                                    int64_t M, int C, int Cper, int act, hipStream_t st) {       \
+    return cer_bias_act_fwd_t<T>(x, bias, bstride, y, M, C, Cper, act, st);                      \
+  }                                                                                              \
+  CER_API int cer_bias_act_bwd##SFX(const T* dy, const T* y, T* dx, float* dbias,               \
+                                    int64_t gstride, float* ws, int64_t M, int C, int Cper,      \
+                                    int act, hipStream_t st) {                                   \
+    return cer_bias_act_bwd_t<T>(dy, y, dx, dbias, gstride, ws, M, C, Cper, act, st);            \
+  }                                                                                              \
+  CER_API int cer_avgpool_fwd##SFX(const T* x, T* y, int B, int H, int W, int C, int Ho, int Wo,\
+                                   int k, int s, int pt, int pl, int count_pad,                  \
+                                   hipStream_t st) {                                             \
+    return cer_avgpool_fwd_t<T>(x, y, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad, st);          \
+  }                                                                                              \
+  CER_API int cer_avgpool_bwd##SFX(const T* dy, T* dx, int B, int H, int W, int C, int Ho,      \
+                                   int Wo, int k, int s, int pt, int pl, int count_pad,          \
+                                   hipStream_t st) {                                             \
+    return cer_avgpool_bwd_t<T>(dy, dx, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad, st);        \
+  }
+
+CER_POOL_ENTRY_POINTS(bf16_t, )
+CER_POOL_ENTRY_POINTS(float, _f32)
