@@ -164,12 +164,6 @@ class PackedResNeXt(PackedNet):
 
 class PackedResNet50NoBN(PackedNet):
     KI = "tn0.01"
-    # Known issue (round 1): replaying this architecture's captured step
-    # produces non-finite weights from the second replay on, with the HIP and
-    # the PyTorch op backends alike, while eager steps are correct; reproduced
-    # by scripts/debug/valid_graph_nan4.py, root cause not yet found.  Run it
-    # eagerly until then (tests/test_kernels_gpu.py graph-vs-eager test).
-    graph_safe = False
 
     def __init__(self, num_classes=1000, input_hw=112):
         super(PackedResNet50NoBN, self).__init__()

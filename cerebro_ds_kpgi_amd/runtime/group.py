@@ -43,11 +43,12 @@ class PackGroup(object):
         self.store = store
         self.device = torch.device(device)
         self.dtype = compute_dtype
-        # HIP graphs only over our HIP kernels: with the PyTorch oracle backend
-        # (MIOpen convolutions) the second replay of a captured step already
-        # gives non-finite weights for every architecture
-        # (scripts/debug/nobn_bisect.py, CEREBRO_BACKEND=torch), so the oracle
-        # path always runs eagerly
+        # HIP graphs only over our HIP kernels.  A hipMemsetAsync captured
+        # into a HIP graph does not re-execute correctly from the second
+        # replay on (ROCm 7.x, scripts/debug/graph_memset_repro.py); our
+        # kernels therefore never memset on a launch path (csrc/hip/common.h
+        # cer_zero_async), but MIOpen's convolutions do, so the PyTorch
+        # oracle backend always runs eagerly
         self.use_graphs = (use_graphs and self.device.type == "cuda" and
                            get_backend() == "hip")
         self.l2 = l2
@@ -254,24 +255,33 @@ class _Working(object):
                 done += 1
 
     def read_metrics(self):
-        """(train, valid) per row: dict(loss, top1, top5, n) — one host sync."""
+        """(train, valid) per row: dict(loss, top1, top5, n) — one host sync.
+
+        Also the per-row non-finite guard: our ReLU epilogues (fmaxf) map NaN
+        to 0, so a NaN weight can hide behind finite losses; a row whose
+        state holds a non-finite value reports NaN losses (``finite`` False)
+        and the run log says so, instead of training on silently."""
+        fin = torch.isfinite(self.arena.state).all(dim=1)
         both = torch.stack([self.acc, self.vacc]).cpu()
+        fin = fin.cpu().tolist()
         out = []
         for row in range(self.G):
-            rec = {}
+            rec = {"finite": bool(fin[row])}
             for name, a in (("train", both[0, row]), ("valid", both[1, row])):
                 n = max(float(a[3]), 1.0)
-                rec[name] = {"loss": float(a[0]) / n, "top1": float(a[1]) / n,
-                             "top5": float(a[2]) / n, "n": int(a[3])}
+                rec[name] = {"loss": float(a[0]) / n if fin[row] else float("nan"),
+                             "top1": float(a[1]) / n, "top5": float(a[2]) / n, "n": int(a[3])}
+            if not fin[row]:
+                log_once("non-finite model state in {} row {} (config {})".format(
+                    self.group.arch, row, self.jobs[row][0] if row < len(self.jobs) else "?"))
             out.append(rec)
         return out
 
 
-# Graph-captured validation is off by default: replays of the captured
-# validation step can produce invalid ResNet-50 eval losses in later epochs
-# (tests/test_kernels_gpu.py, CER_VALID_GRAPH=1), root cause open; it showed
-# no measurable gain at N=1 (profiles/r1_ab_bn_links_gradjoin.md context).
-_VALID_GRAPH = os.environ.get("CER_VALID_GRAPH", "0") == "1"
+# Graph-captured validation (CER_VALID_GRAPH=0 runs it eagerly).  Its round-1
+# failures (invalid eval losses after an epoch boundary) had the same root
+# cause as the training-graph corruption: captured hipMemsetAsync nodes.
+_VALID_GRAPH = os.environ.get("CER_VALID_GRAPH", "1") == "1"
 
 
 def now():

@@ -117,3 +117,40 @@ __device__ __forceinline__ float block_max(float v, float* smem) {
 static inline int cer_blocks(int64_t n, int per_block) {
   return (int)((n + per_block - 1) / per_block);
 }
+
+// ---------------------------------------------------------------------------
+// Device fill / copy as KERNELS.  Never hipMemsetAsync / hipMemcpyAsync on a
+// launch path: captured into a HIP graph, a small hipMemsetAsync node does not
+// re-execute correctly from the second replay on (ROCm 7.x; 4 KB fill ->
+// garbage, scripts/debug/graph_memset_repro.py).  That was the root cause of
+// the round-1 graph-replay corruption (non-finite weights from replay 2).
+// A kernel node replays like every other kernel.
+// ---------------------------------------------------------------------------
+static __global__ __launch_bounds__(256) void cer_fill_kernel(uint8_t* __restrict__ dst,
+                                                              const uint8_t* __restrict__ src,
+                                                              size_t bytes, int vec) {
+  // src == nullptr: zero fill; vec: 16-B body (both pointers 16-B aligned) + byte tail
+  const size_t n16 = vec ? bytes / 16 : 0;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t k = i; k < n16; k += stride)
+    reinterpret_cast<uint4*>(dst)[k] = src ? reinterpret_cast<const uint4*>(src)[k]
+                                           : make_uint4(0u, 0u, 0u, 0u);
+  for (size_t k = n16 * 16 + i; k < bytes; k += stride) dst[k] = src ? src[k] : (uint8_t)0;
+}
+
+static inline void cer_launch_fill(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if (!bytes) return;
+  const int vec = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0);
+  int blocks = cer_blocks((int64_t)(vec ? (bytes + 15) / 16 : bytes), 256);
+  if (blocks > 4096) blocks = 4096;
+  cer_fill_kernel<<<blocks, 256, 0, stream>>>((uint8_t*)dst, (const uint8_t*)src, bytes, vec);
+}
+
+static inline void cer_zero_async(void* dst, size_t bytes, hipStream_t stream) {
+  cer_launch_fill(dst, nullptr, bytes, stream);
+}
+
+static inline void cer_copy_async(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  cer_launch_fill(dst, src, bytes, stream);
+}

@@ -2524,9 +2524,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       // (or the addend, which the kernel adds on the written pixels)
       const size_t bytes = (size_t)es * B * H * W * G * Cin;
       if (addend)
-        (void)hipMemcpyAsync(dx, addend, bytes, hipMemcpyDeviceToDevice, stream);
+        cer_copy_async(dx, addend, bytes, stream);
       else
-        (void)hipMemsetAsync(dx, 0, bytes, stream);
+        cer_zero_async(dx, bytes, stream);
       p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0, es);
       p.dgrad = 0;
       p.M = B * Ho * Wo;
@@ -3028,7 +3028,7 @@ static int stem_wgrad_impl(const void* x4, int B, int H, int W, int Cin, int G, 
   const bool fast = f32 ? wg_fast32(8, Cout, p) : wg_fast(8, Cout, p);
   const int v = wg_variant(p.N, p.K, G, fast && !f32);
   const int splits = wg_splits(p.Mred, p.N, p.K, G, v);
-  if (splits > 1) (void)hipMemsetAsync(dwp, 0, sizeof(float) * (size_t)G * p.dw_gstride, stream);
+  if (splits > 1) cer_zero_async(dwp, sizeof(float) * (size_t)G * p.dw_gstride, stream);
   if (f32) {
     run_wg32(p, G, splits, fast, stream);
   } else {

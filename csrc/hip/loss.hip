@@ -74,7 +74,7 @@ CER_API int cer_softmax_ce(const void* logits, int logits_bf16, const int* label
                            float* loss_out, bf16_t* dlogits, int B, int G, int N,
                            hipStream_t stream) {
   if (N > CE_THREADS * CE_MAXPER) return (int)hipErrorInvalidValue;
-  if (loss_out) (void)hipMemsetAsync(loss_out, 0, sizeof(float) * G, stream);
+  if (loss_out) cer_zero_async(loss_out, sizeof(float) * G, stream);
   dim3 grid(B, G);
   if (logits_bf16)
     softmax_ce_kernel<bf16_t, bf16_t><<<grid, CE_THREADS, 0, stream>>>(
@@ -90,7 +90,7 @@ CER_API int cer_softmax_ce_f32(const float* logits, const int* labels, float* ac
                                float* loss_out, float* dlogits, int B, int G, int N,
                                hipStream_t stream) {
   if (N > CE_THREADS * CE_MAXPER) return (int)hipErrorInvalidValue;
-  if (loss_out) (void)hipMemsetAsync(loss_out, 0, sizeof(float) * G, stream);
+  if (loss_out) cer_zero_async(loss_out, sizeof(float) * G, stream);
   softmax_ce_kernel<float, float><<<dim3(B, G), CE_THREADS, 0, stream>>>(logits, labels, acc,
                                                                           loss_out, dlogits, B, G,
                                                                           N);

@@ -293,7 +293,7 @@ static int cer_bias_act_bwd_t(const T* dy, const T* y, T* dx, float* dbias,
     int64_t rows = (M + want - 1) / want;
     if (rows < 16) rows = 16;
     dim3 grid(cb, (unsigned)((M + rows - 1) / rows));
-    (void)hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+    cer_zero_async(ws, sizeof(float) * C, stream);
     bias_act_bwd_scalar<T><<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
     bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
     return (int)hipGetLastError();
@@ -303,7 +303,7 @@ static int cer_bias_act_bwd_t(const T* dy, const T* y, T* dx, float* dbias,
   int64_t rows = (M + want - 1) / want;
   if (rows < 16) rows = 16;
   dim3 grid(cblocks, (unsigned)((M + rows - 1) / rows));
-  (void)hipMemsetAsync(ws, 0, sizeof(float) * C, stream);
+  cer_zero_async(ws, sizeof(float) * C, stream);
   bias_act_bwd_kernel<T><<<grid, PT, 0, stream>>>(dy, y, dx, ws, M, C, (int)rows, act);
   bias_grad_scatter<<<cer_blocks(C, 256), 256, 0, stream>>>(ws, dbias, gstride, C, Cper);
   return (int)hipGetLastError();

@@ -162,6 +162,16 @@ def test_graph_replay_matches_eager(model, bs):
             use_graphs=graphs))
         eng.run(2)
         losses.append([st["train_loss"] + st["valid_loss"] for st in eng.mst_state.values()])
+        if graphs:
+            ws = [w for g in eng.groups.values() for w in g._work.values()]
+            captured = any(w.graph is not None for w in ws)
+            # every family but the ones with a PyTorch-path op (grouped conv of
+            # ResNeXt, DenseNet's concat convs) must really replay a graph
+            if model not in ("resnext101",):
+                assert captured or all(w.eager_only for w in ws), model
+            if model in ("resnet50", "resnet50_nobn", "vgg16", "confA", "resnet18",
+                         "mobilenetv2"):
+                assert captured, "{}: no HIP graph was captured".format(model)
         eng.close()
     # every loss finite (train AND validation: the validation step is
     # graph-replayed too); the first round's training loss close — later
