@@ -25,8 +25,9 @@ vs_baseline = value / DA-Cerebro's aggregate img/s at the same worker count
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,6 +57,11 @@ def main():
                          "GPUs); the headline number always uses all 8")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # not launched by torchrun: start one rank per GPU ourselves, as child
+        # processes, BEFORE anything touches the GPU, and exit with their code
+        sys.exit(_spawn_ranks(args.gpus))
+
     import torch
     from cerebro_ds_kpgi_amd.ops import set_backend
     from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
@@ -65,6 +71,8 @@ def main():
 
     ctx = init_distributed()
     N = ctx.world
+    if N != args.gpus:
+        raise SystemExit("bench: --gpus {} but the job has {} ranks".format(args.gpus, N))
     backend = set_backend(args.backend)
     if args.workload == "criteo16":
         grid = dict(cat.param_grid_criteo)            # 2 lr x 2 lambda x 4 batch = 16
@@ -96,7 +104,7 @@ def main():
     sync()
     ctx.barrier()
     sync()
-    img0 = eng.train_images
+    img0, hop0, hopt0 = eng.train_images, eng.hop_bytes, eng.hop_time
     t0 = time.time()
     eng.run_steps(args.steps, args.steps_per_round, epoch_start=2)
     sync()
@@ -104,17 +112,21 @@ def main():
     sync()
     dt = time.time() - t0
     dt_max = ctx.allreduce_max(dt)
-    imgs = sum(ctx.all_gather_object(eng.train_images - img0))
+    per_rank = ctx.all_gather_object({"images": eng.train_images - img0,
+                                      "hop_bytes": eng.hop_bytes - hop0,
+                                      "hop_s": eng.hop_time - hopt0})
+    imgs = sum(r["images"] for r in per_rank)
     value = imgs / dt_max
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(N)
+        headline = (S == 8 and args.workload == "headline" and args.model == "resnet50"
+                    and args.dtype == "fp32")
         out = {
-            "metric": ("agg_train_images_per_sec_8cfg_resnet50_mop"
-                       if S == 8 and args.workload == "headline" else
-                       "diag_train_{}_per_sec_{}cfg_{}_mop".format(
+            "metric": ("agg_train_images_per_sec_8cfg_resnet50_mop" if headline else
+                       "diag_train_{}_per_sec_{}cfg_{}_mop_{}".format(
                            "samples" if args.workload == "criteo16" else "images", S,
-                           {"headline": "resnet50", "criteo16": "criteo_confA",
-                            "hetero8": "resnet50_vgg16"}[args.workload])),
+                           {"headline": args.model, "criteo16": "criteo_confA",
+                            "hetero8": "resnet50_vgg16"}[args.workload], args.dtype)),
             "value": round(value, 2),
             "unit": "samples/s" if args.workload == "criteo16" else "images/s",
             "n_gpus": N,
@@ -123,8 +135,7 @@ def main():
             "ms_per_step": round(1000.0 * dt_max / args.steps, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": (round(value / base, 3) if base and args.workload == "headline"
-                            else None),
+            "vs_baseline": round(value / base, 3) if base and headline else None,
             "dtype": args.dtype,
             "data": "synthetic",
             "config": {"model": {"headline": args.model, "criteo16": "confA",
@@ -141,12 +152,30 @@ def main():
             "baseline_makespan_s": ({1: 35440, 2: 17754, 4: 10229, 8: 5715}.get(N)
                                     if args.workload == "headline" else None),
             "backend": backend,
-            "hop_bytes_rank0": eng.hop_bytes,
+            "world_size": N,
+            "dist_backend": ctx.backend or "none",
+            "hop_bytes": sum(r["hop_bytes"] for r in per_rank),
+            "hop_ms_max": round(1000.0 * max(r["hop_s"] for r in per_rank), 3),
         }
         print(json.dumps(out))
         sys.stdout.flush()
     eng.close()
     shutdown(ctx)
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _spawn_ranks(n):
+    """``torch.distributed.run`` with n local ranks on 127.0.0.1 as a child
+    process (the driver's own launch shape); returns its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ))
 
 
 if __name__ == "__main__":

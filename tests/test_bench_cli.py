@@ -1,0 +1,38 @@
+"""bench.py contract on CPU: ``--gpus N`` really runs N ranks (gloo here,
+RCCL on the GPU node) and reports hop traffic."""
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + list(args),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                       timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_cpu():
+    out = _bench("--gpus", "2", "--backend", "torch", "--model", "tinycnn", "--steps", "4",
+                 "--warmup", "2", "--steps_per_round", "2", "--train_per_partition", "64")
+    assert out["n_gpus"] == 2 and out["world_size"] == 2
+    assert out["dist_backend"] == "gloo"
+    assert out["hop_bytes"] > 0                  # models hopped between the two ranks
+    assert out["metric"].startswith("diag_")     # not the headline model: diagnostic name
+    assert out["steps"] == 4 and out["value"] > 0
+
+
+def test_bench_one_rank_cpu():
+    out = _bench("--backend", "torch", "--model", "tinycnn", "--steps", "2", "--warmup", "1",
+                 "--steps_per_round", "2", "--train_per_partition", "64")
+    assert out["n_gpus"] == 1 and out["hop_bytes"] == 0
