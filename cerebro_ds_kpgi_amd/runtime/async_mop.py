@@ -1,0 +1,789 @@
+"""Event-driven (asynchronous) MOP runtime: work-conserving greedy scheduling
+and model hops overlapped with compute.
+
+The lock-step runtime (``engine.MOPEngine.run_round``) ends every sub-epoch
+with a barrier over all ranks, so a "greedy" schedule degenerates to
+rotation and a hop can only start once every GPU is done.  This runtime
+replaces the barrier with events (reference semantics:
+``cerebro_gpdb/ctq.py:448-508`` -- an idle worker immediately takes the next
+runnable (model, partition) pair; the client there busy-polls job
+processes, here workers post completion events):
+
+* **Coordinator** (a thread on rank 0) owns the scheduler.  Workers post
+  ``train_done`` (the model's state is final -- it is free to start its next
+  sub-epoch elsewhere while this worker still validates it) and ``job_done``
+  (train + validation finished, metrics attached -- the worker is free).
+  On every event the coordinator hands the next runnable pairs to idle
+  workers (greedy) or, for rotation (UDAF), starts the next lock-step round
+  once every worker is free -- but publishes that round's hops as soon as
+  every model's training is done, so the transfers overlap validation.
+* **Hop service** (a thread per rank): hops are published as one global
+  sequence ``hop/0, hop/1, ...``; every rank walks it in order and takes part
+  in the transfers it is an endpoint of (send from the parked home row /
+  receive into the home row), on its own HIP stream and its own process
+  group, so a transfer overlaps whatever the rank is computing.  One global
+  order makes every pair of endpoints meet in the same order: no deadlock.
+  The receiver's compute stream waits on the arrival event only when the
+  model is actually needed; ``hop_time`` counts that exposed wait, and
+  ``hop_busy_time`` the transfers themselves.
+* **Worker** (each rank's main thread): waits for its next assignment,
+  trains its jobs packed per pack group (kept resident in the working
+  arena: a job that stays on this GPU is a ``part_of_row`` change, no state
+  copy), posts the events, validates.
+
+Control messages ride a TCP key-value store (rank 0 hosts a
+``torch.distributed.TCPStore``; an in-process store at world size 1), data
+rides RCCL (gloo on CPU).  Fault handling: a ``SoftFault`` in a job sends
+its pairs back to the queue (the model's previous holder still has its
+pre-job state); anything else stops every rank with the error.
+Checkpoints are epoch-granular here (sub-epoch ``resume`` uses the
+lock-step runtime).
+"""
+
+import collections
+import datetime
+import json
+import os
+import threading
+import time
+
+import torch
+import torch.distributed as dist
+
+from ..scheduler.policies import GreedyScheduler, RotationScheduler
+from ..utils.keys import model_key
+
+
+# ---------------------------------------------------------------------------
+# key-value control channel
+# ---------------------------------------------------------------------------
+class LocalStore(object):
+    """In-process stand-in for TCPStore (world size 1): set / get / add / wait."""
+
+    def __init__(self):
+        self._d = {}
+        self._cv = threading.Condition()
+
+    def set(self, key, value):
+        with self._cv:
+            self._d[key] = value if isinstance(value, bytes) else str(value).encode()
+            self._cv.notify_all()
+
+    def add(self, key, n):
+        with self._cv:
+            v = int(self._d.get(key, b"0")) + int(n)
+            self._d[key] = str(v).encode()
+            self._cv.notify_all()
+            return v
+
+    def get(self, key, timeout=None):
+        with self._cv:
+            if not self._cv.wait_for(lambda: key in self._d, timeout):
+                raise TimeoutError("LocalStore: no key {}".format(key))
+            return self._d[key]
+
+    def delete_key(self, key):
+        with self._cv:
+            self._d.pop(key, None)
+
+
+class Channel(object):
+    """Typed JSON messages over the store.  Streams: per-rank assignments
+    ``a/<rank>/<k>``, the event log ``e/<i>`` (counter ``ne``), the global
+    hop sequence ``h/<i>``, and the final state ``final``.
+
+    A blocking TCPStore call holds the client's socket, so every thread
+    talks through its own client (``fork``)."""
+
+    def __init__(self, store, prefix, timeout, addr=None):
+        self.store = store
+        self.pfx = prefix
+        self.timeout = timeout
+        self.addr = addr
+
+    def fork(self):
+        if self.addr is None:
+            return Channel(self.store, self.pfx, self.timeout)
+        return Channel(tcp_client(self.addr, self.timeout), self.pfx, self.timeout, self.addr)
+
+    def _k(self, *parts):
+        return "/".join([self.pfx] + [str(p) for p in parts])
+
+    def _get(self, key):
+        if isinstance(self.store, LocalStore):
+            return self.store.get(key, timeout=self.timeout)
+        self.store.wait([key], datetime.timedelta(seconds=self.timeout))
+        return self.store.get(key)
+
+    def put(self, key_parts, obj):
+        self.store.set(self._k(*key_parts), json.dumps(obj).encode())
+
+    def take(self, key_parts):
+        return json.loads(self._get(self._k(*key_parts)).decode())
+
+    # events
+    def post_event(self, ev):
+        i = self.store.add(self._k("ne"), 1) - 1
+        self.put(("e", i), ev)
+
+    def event(self, i):
+        return self.take(("e", i))
+
+    # assignments / hops
+    def assign(self, rank, k, rec):
+        self.put(("a", rank, k), rec)
+
+    def assignment(self, rank, k):
+        return self.take(("a", rank, k))
+
+    def hop(self, h, rec):
+        self.put(("h", h), rec)
+
+    def next_hop(self, h):
+        return self.take(("h", h))
+
+    def put_final(self, obj):
+        self.put(("final",), obj)
+
+    def get_final(self):
+        return self.take(("final",))
+
+
+def tcp_client(addr, timeout):
+    """A client of the job's rendezvous store (MASTER_ADDR:MASTER_PORT, the
+    store ``torch.distributed`` was initialised from -- no new listener)."""
+    return dist.TCPStore(addr[0], addr[1], None, False,
+                         timeout=datetime.timedelta(seconds=timeout), wait_for_workers=False)
+
+
+def rendezvous_addr():
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = os.environ.get("MASTER_PORT")
+    return (host, int(port)) if port else None
+
+
+# ---------------------------------------------------------------------------
+# coordinator (rank 0)
+# ---------------------------------------------------------------------------
+class Coordinator(object):
+    """Scheduler owner, driven by completion events.
+
+    * greedy: an idle rank takes, per idle partition it owns, the first
+      runnable pair of the shuffled pair list (CTQ ``_get_runnable_model``);
+    * rotation: the UDAF round plan, executed as a data flow -- rank r runs
+      its share of round s+1 as soon as its round s is done and the models it
+      needs for s+1 are trained (no global barrier: a slow rank delays only
+      the ranks that wait for its models).  The visit order is exactly the
+      round plan's, so results equal the lock-step runtime's.  A model's hop
+      to its next partition is published the moment its training ends.
+
+    ``round_budget`` limits a rotation session to that many rounds with
+    ``steps_of(round)`` steps per job (``run_steps`` / the bench)."""
+
+    def __init__(self, eng, chan, sched, policy, first_epoch, num_epochs, mst_eval_fn=None,
+                 steps_of=None, round_budget=None):
+        self.eng = eng
+        self.chan = chan.fork()                        # this thread's own store client
+        self.sched = sched
+        self.policy = policy
+        self.first_epoch = first_epoch
+        self.num_epochs = num_epochs
+        self.mst_eval_fn = mst_eval_fn
+        self.steps_of = steps_of
+        self.round_budget = round_budget
+        self.world = eng.ctx.world
+        self.parts_of = collections.defaultdict(list)
+        for p in range(eng.P):
+            self.parts_of[eng.owner(p)].append(p)
+        self.k = collections.defaultdict(int)          # next assignment slot per rank
+        self.nhop = 0
+        self.nev = 0
+        self.batch = {}                                # rank -> running batch record
+        self.holder = dict(eng.holder)                 # committed state location
+        self.hop_sent = {}                             # model -> rank a hop already targets
+        self.retries = collections.Counter()
+        self.error = None
+        self.round_base = 0                            # rotation rounds of earlier epochs
+        self.rounds_done = 0
+        self.nbatch = 0                                # batches finished (greedy subepoch id)
+        self.thread = None
+
+    # -- plumbing ----------------------------------------------------------
+    def start(self):
+        self.thread = threading.Thread(target=self._main, name="cerebro-coordinator",
+                                       daemon=True)
+        self.thread.start()
+        return self
+
+    def join(self):
+        if self.thread is not None:
+            self.thread.join()
+
+    def _send(self, rank, rec):
+        self.chan.assign(rank, self.k[rank], rec)
+        self.k[rank] += 1
+
+    def _broadcast(self, rec):
+        for r in range(self.world):
+            self._send(r, rec)
+
+    def _next_event(self):
+        ev = self.chan.event(self.nev)
+        self.nev += 1
+        return ev
+
+    def _main(self):
+        try:
+            self._run()
+        except BaseException as e:          # never leave the workers waiting
+            self.error = "{}: {}".format(type(e).__name__, e)
+            try:
+                self._broadcast({"t": "stop", "error": self.error})
+                self.chan.hop(self.nhop, {"t": "stop"})
+            except Exception:
+                pass
+            return
+        self._broadcast({"t": "stop", "error": None})
+        self.chan.hop(self.nhop, {"t": "stop"})
+
+    def _budget_left(self):
+        return self.round_budget is None or self.rounds_done < self.round_budget
+
+    # -- epochs ------------------------------------------------------------
+    def _run(self):
+        eng = self.eng
+        epoch = self.first_epoch
+        self.last_epoch = epoch - 1
+        while self._budget_left() and (self.round_budget is not None or
+                                       epoch <= self.num_epochs):
+            active = [m for m in range(len(eng.coord_msts))
+                      if eng.mst_state[m]["state"] == "RUNNING"]
+            if not active:
+                break
+            sched = self.sched
+            sched.models = list(active)
+            sched.start_epoch(epoch)
+            self._broadcast({"t": "epoch", "epoch": epoch})
+            eng.coord_log("EPOCH:{}".format(epoch))
+            complete = self._run_epoch(epoch)
+            if not complete:
+                break                                  # bench budget hit mid-epoch
+            sched.monitor.check_epoch_complete(sched.models)
+            self._end_epoch(epoch)
+            self.last_epoch = epoch
+            epoch += 1
+
+    def _run_epoch(self, epoch):
+        """Returns False when a round budget stopped the epoch early."""
+        sched = self.sched
+        self.epoch_nbatch = 0
+        self._next_where = None
+        if self.policy == "rotation":
+            self.L = len(sched.rounds)
+            self.rnext = {r: 0 for r in range(self.world)}
+            self.where = [{m: p for p, m in rnd.items()} for rnd in sched.rounds]
+            for m in sched.models:
+                s0 = self._mnext(m)
+                if s0 is not None and self._round_allowed(s0):
+                    self._pre_hop(m, self.eng.owner(self.where[s0][m]))
+        self._pump(epoch)
+        while self.batch:
+            self._handle(self._next_event(), epoch)
+            self._pump(epoch)
+        if self.policy == "rotation":
+            done = min(self.rnext.values()) if self.rnext else 0
+            self.round_base += self.L
+            self.rounds_done = self.round_base if done >= self.L else self.round_base - self.L + done
+            return sched.epoch_done()
+        if not sched.epoch_done():
+            raise RuntimeError("greedy scheduler stalled with pending pairs {}".format(
+                sched.pending[:6]))
+        return True
+
+    def _round_allowed(self, s):
+        return self.round_budget is None or self.round_base + s < self.round_budget
+
+    # -- dispatch ----------------------------------------------------------
+    def _pump(self, epoch):
+        if self.policy == "rotation":
+            self._pump_rotation(epoch)
+        else:
+            self._pump_greedy(epoch)
+
+    def _pump_greedy(self, epoch):
+        sched = self.sched
+        for r in range(self.world):
+            if r in self.batch:
+                continue
+            jobs = []
+            for p in self.parts_of[r]:
+                if p in sched.idle_workers:
+                    m = sched.assign(p)
+                    if m is not None:
+                        jobs.append((m, p))
+            if jobs:
+                self._dispatch(r, jobs, epoch, self.round_base + self.epoch_nbatch)
+
+    def _pump_rotation(self, epoch):
+        sched = self.sched
+        for r in range(self.world):
+            if r in self.batch:
+                continue
+            s = self.rnext[r]
+            while s < self.L and self._round_allowed(s):
+                jobs = [(m, p) for p, m in sorted(sched.rounds[s].items())
+                        if self.eng.owner(p) == r and (m, p) in sched.pending]
+                if jobs:
+                    break
+                s += 1                                 # nothing of round s on this rank
+            self.rnext[r] = s
+            if s >= self.L or not self._round_allowed(s):
+                continue
+            if not all(m in sched.idle_models and self._mnext(m) == s for m, _ in jobs):
+                continue                               # a model it needs is not there yet
+            for m, p in jobs:
+                sched._start(m, p)
+            self._dispatch(r, jobs, epoch, self.round_base + s, rnd=s)
+
+    def _mnext(self, m):
+        """Rotation: the first round in which m still has a pending visit."""
+        pend = self.sched.pending
+        for s, where in enumerate(self.where):
+            p = where.get(m)
+            if p is not None and (m, p) in pend:
+                return s
+        return None
+
+    def _pre_hop(self, m, dst):
+        """Publish m's hop to ``dst`` now (its state is final); returns the
+        hop's sequence number (None: no transfer needed)."""
+        src = self.holder.get(m)
+        if src is None or src == dst:
+            return None
+        sent = self.hop_sent.get(m)
+        if sent is not None and sent[0] == dst:
+            return sent[1]
+        h = self.nhop
+        self.chan.hop(h, {"t": "hop", "m": m, "src": src, "dst": dst})
+        self.nhop += 1
+        self.hop_sent[m] = (dst, h)
+        return h
+
+    def _prefetch_next_epoch(self, m):
+        """Rotation, m's last visit of the epoch just ended: its first visit
+        of the next epoch is known when no ``mst_eval_fn`` can change the
+        active set -- start that hop now, behind this epoch's validation."""
+        if self.mst_eval_fn is not None or (self.round_budget is None and
+                                            self.sched.epoch >= self.num_epochs):
+            return
+        if getattr(self, "_next_where", None) is None:
+            nxt = RotationScheduler(list(self.sched.models), list(self.sched.workers))
+            nxt.start_epoch(self.sched.epoch + 1)
+            self._next_where = [{mm: p for p, mm in rnd.items()} for rnd in nxt.rounds]
+        for s, where in enumerate(self._next_where):
+            if m in where:
+                if self.round_budget is None or self.round_base + self.L + s < self.round_budget:
+                    self._pre_hop(m, self.eng.owner(where[m]))
+                return
+
+    def _dispatch(self, r, jobs, epoch, subepoch, rnd=None):
+        recs = []
+        for m, p in jobs:
+            src = self.holder.get(m)
+            recs.append([m, p, src, self._pre_hop(m, r)])
+        self.batch[r] = {"jobs": recs, "train_left": {m for m, _ in jobs},
+                         "subepoch": subepoch, "round": rnd}
+        steps = (self.steps_of(self.round_base + rnd)
+                 if (self.steps_of is not None and rnd is not None) else None)
+        self._send(r, {"t": "jobs", "epoch": epoch, "jobs": recs, "max_steps": steps,
+                       "subepoch": subepoch})
+
+    # -- events ------------------------------------------------------------
+    def _handle(self, ev, epoch):
+        eng = self.eng
+        t = ev["t"]
+        r = ev["rank"]
+        b = self.batch.get(r)
+        if t == "train_done":
+            for m in ev["models"]:
+                p = next(p for mm, p, _, _ in b["jobs"] if mm == m)
+                self.sched.release_model(m, p)
+                self.holder[m] = r
+                self.hop_sent.pop(m, None)
+                b["train_left"].discard(m)
+                if b["round"] is not None:
+                    s2 = self._mnext(m)
+                    if s2 is None:
+                        self._prefetch_next_epoch(m)
+                    elif self._round_allowed(s2):
+                        self._pre_hop(m, eng.owner(self.where[s2][m]))
+            return
+        if t != "job_done":
+            raise RuntimeError("unknown event {}".format(ev))
+        del self.batch[r]
+        if ev.get("fatal"):
+            raise RuntimeError("rank {} failed: {}".format(r, ev["error"]))
+        if ev.get("error"):                           # SoftFault: requeue the pairs
+            for m, p, src, _ in b["jobs"]:
+                if m not in b["train_left"]:
+                    continue                           # trained; only its metrics are lost
+                self.retries[(m, p)] += 1
+                if self.retries[(m, p)] > eng.o.max_retries:
+                    raise RuntimeError("pair {} failed {} times; giving up".format(
+                        (m, p), self.retries[(m, p)]))
+                self.sched.abort(m, p)
+                # the failed rank received every incoming state before it
+                # failed and its home rows hold the pre-job states
+                self.holder[m] = r
+                self.hop_sent.pop(m, None)
+                fj = {"status": "FAILED", "epoch": epoch, "subepoch": b["subepoch"],
+                      "attempt": self.retries[(m, p)] - 1, "rank": r, "partition": p,
+                      "error": ev["error"], "model_key": model_key(m, eng.coord_msts[m])}
+                eng.failures.append(fj)
+                eng.coord_log("JOB FAILED {} on partition {} (rank {}): {} -> requeued"
+                              .format(fj["model_key"], p, r, ev["error"]))
+            for m, p, _, _ in b["jobs"]:
+                self.sched.release_worker(p)
+            return
+        for m, p, _, _ in b["jobs"]:
+            self.sched.release_worker(p)
+        g = {"rank": r, "t_start": ev["t_start"], "t_hop": ev["t_hop"], "t_end": ev["t_end"]}
+        for res in ev["results"]:
+            eng._record_job(epoch, g, res, subepoch=b["subepoch"])
+        eng.round_idx += 1
+        self.epoch_nbatch += 1
+        if b["round"] is not None:
+            self.rnext[r] = b["round"] + 1
+
+    def _end_epoch(self, epoch):
+        eng = self.eng
+        eng._epoch_summary(epoch)
+        if eng.o.logs_root:
+            from .checkpoint import dump_infos
+            dump_infos(eng.o.logs_root, eng.models_info, eng.jobs_info)
+        if self.mst_eval_fn is not None:
+            stop, _, new_msts = self.mst_eval_fn(eng.mst_state)
+            for m in stop:
+                eng.mst_state[m]["state"] = "COMPLETED"
+            if new_msts:
+                ids = eng.coord_add_msts(new_msts)
+                self.sched.add_models(ids)
+                self._broadcast({"t": "add", "msts": new_msts})
+                for m in ids:
+                    self.holder[m] = None
+        if eng.o.ckpt_every != "none" and eng.o.models_root:
+            by_rank = collections.defaultdict(list)
+            for m in range(len(eng.coord_msts)):
+                h = self.holder.get(m)
+                by_rank[0 if h is None else h].append(m)
+            for r in range(self.world):
+                self._send(r, {"t": "ckpt", "epoch": epoch, "models": by_rank.get(r, [])})
+            acks = 0
+            while acks < self.world:
+                ev = self._next_event()
+                if ev["t"] != "ckpt_done":
+                    raise RuntimeError("unexpected event at checkpoint: {}".format(ev))
+                acks += 1
+            eng.write_resume(epoch, -1, True, None)
+
+
+# ---------------------------------------------------------------------------
+# hop service (every rank, world > 1)
+# ---------------------------------------------------------------------------
+class HopService(object):
+    """Walks the global hop sequence; sends from / receives into home rows on
+    its own stream and process group.  The send of a model whose training
+    just ended waits (on the device) for the parking copy only."""
+
+    def __init__(self, eng, chan, group):
+        self.eng = eng
+        self.chan = chan.fork()
+        self.group = group
+        self.rank = eng.ctx.rank
+        self.cuda = eng.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=eng.device) if self.cuda else None
+        self.final = {}                       # model -> cuda event of its last parking
+        self.arrived = {}                     # hop id -> [threading.Event, cuda event]
+        self.lock = threading.Lock()
+        self.quiet = threading.Lock()         # held while a transfer is in flight
+        self.bytes = 0
+        self.busy = 0.0
+        self.spans = []                       # (t0, t1) of every transfer
+        self.error = None
+        self.thread = None
+
+    def start(self):
+        self.thread = threading.Thread(target=self._main, name="cerebro-hops", daemon=True)
+        self.thread.start()
+        return self
+
+    def join(self):
+        if self.thread is not None:
+            self.thread.join()
+
+    def mark_final(self, m):
+        """Main thread: m's state is parked in its home row (enqueued)."""
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        with self.lock:
+            self.final[m] = ev
+
+    def wait_arrival(self, h):
+        """Main thread: block until hop ``h`` has landed (host side), then
+        order the compute stream after it (device side)."""
+        with self.lock:
+            slot = self.arrived.setdefault(h, [threading.Event(), None])
+        while not slot[0].wait(1.0):
+            if self.error:
+                raise RuntimeError("hop service failed: " + self.error)
+        if slot[1] is not None:
+            torch.cuda.current_stream().wait_event(slot[1])
+        with self.lock:
+            del self.arrived[h]
+
+    def _main(self):
+        try:
+            if self.cuda:
+                with torch.cuda.device(self.eng.device), torch.cuda.stream(self.stream):
+                    self._loop()
+            else:
+                self._loop()
+        except BaseException as e:
+            self.error = "{}: {}".format(type(e).__name__, e)
+
+    def _p2p(self, op, buf, peer, tag):
+        for w in dist.batch_isend_irecv([dist.P2POp(op, buf, peer, self.group, tag=tag)]):
+            w.wait()
+
+    def _loop(self):
+        from ..parallel.hop import HopChecksumError, checksum
+        eng = self.eng
+        h = 0
+        hopt = eng.o.hop_optimizer_state
+        while True:
+            rec = self.chan.next_hop(h)
+            hid = h
+            h += 1
+            if rec["t"] == "stop":
+                return
+            m, src, dst = rec["m"], rec["src"], rec["dst"]
+            if self.rank not in (src, dst):
+                continue
+            with self.quiet:
+                grp = eng.group_of[m]
+                row = grp.home.state[grp.home_row[m]]
+                buf = row if hopt else row[:grp.layout.n_master]
+                t0 = time.time()
+                with eng.tracer.span("hop", model=m, src=src, dst=dst):
+                    if self.rank == src:
+                        if eng.o.sim_hop_seconds:      # test hook: a slow link
+                            time.sleep(eng.o.sim_hop_seconds)
+                        with self.lock:
+                            ev = self.final.get(m)
+                        if ev is not None:
+                            self.stream.wait_event(ev)
+                        self._p2p(dist.isend, buf, dst, m)
+                        if eng.o.hop_check:
+                            self._p2p(dist.isend, checksum(buf), dst, 100000 + m)
+                        if self.cuda:
+                            self.stream.synchronize()   # transfer done (busy-time accounting)
+                        self.bytes += buf.numel() * buf.element_size()
+                    else:
+                        self._p2p(dist.irecv, buf, src, m)
+                        if eng.o.hop_check:
+                            sent = torch.empty(3, dtype=torch.float64, device=buf.device)
+                            self._p2p(dist.irecv, sent, src, 100000 + m)
+                            got = checksum(buf)
+                            if not torch.equal(got, sent):
+                                raise HopChecksumError(
+                                    "model {} arrived corrupted on rank {}: digest {} != sent {}"
+                                    .format(m, self.rank, got.tolist(), sent.tolist()))
+                        ev = None
+                        if self.cuda:
+                            ev = torch.cuda.Event()
+                            ev.record(self.stream)
+                            self.stream.synchronize()
+                        with self.lock:
+                            slot = self.arrived.setdefault(hid, [threading.Event(), None])
+                            slot[1] = ev
+                            slot[0].set()
+                t1 = time.time()
+            self.busy += t1 - t0
+            self.spans.append((t0, t1))
+
+
+# ---------------------------------------------------------------------------
+# worker (every rank's main thread)
+# ---------------------------------------------------------------------------
+def run_worker(eng, chan, hops):
+    """Execute this rank's assignment stream until ``stop``; returns the
+    coordinator's error (None on success)."""
+    rank = eng.ctx.rank
+    k = 0
+    while True:
+        rec = chan.assignment(rank, k)
+        k += 1
+        t = rec["t"]
+        if t == "stop":
+            return rec.get("error")
+        if t == "epoch":
+            eng.epoch = rec["epoch"]
+            eng.store.new_epoch(rec["epoch"])
+            continue
+        if t == "add":
+            if hops is not None:
+                with hops.quiet:                    # no transfer reads the old home arena
+                    eng.worker_add_msts(rec["msts"])
+            else:
+                eng.worker_add_msts(rec["msts"])
+            continue
+        if t == "ckpt":
+            for grp in eng.groups.values():
+                grp.park_all()
+            eng.checkpoint_all(rec["epoch"], models=rec["models"], holder_ok=True)
+            eng.writer.flush()
+            chan.post_event({"t": "ckpt_done", "rank": rank})
+            continue
+        assert t == "jobs", rec
+        _run_batch(eng, chan, hops, rec)
+
+
+def _run_batch(eng, chan, hops, rec):
+    from .engine import SoftFault
+    rank = eng.ctx.rank
+    tr = eng.tracer
+    t_start = time.time()
+    jobs = [tuple(j) for j in rec["jobs"]]         # (model, partition, holder, hop id)
+    models = [j[0] for j in jobs]
+    error = None
+    results, trained = [], 0
+    t_hop = t_start
+    try:
+        # arrivals: the compute stream waits for a hop only now
+        with tr.span("wait_arrival", subepoch=rec["subepoch"]):
+            for m, p, src, hid in jobs:
+                if hid is not None:
+                    hops.wait_arrival(hid)
+                    eng.group_of[m].invalidate(m)
+        t_hop = time.time()
+        eng.hop_time += t_hop - t_start
+        eng._fault_check_batch(rec["subepoch"])
+        per_group = collections.defaultdict(list)
+        for m, p, _, _ in jobs:
+            per_group[eng.group_of[m].key].append((m, eng.local_part(p)))
+        working = {}
+        for key, gj in per_group.items():
+            working[key] = eng.groups[key].begin_batch(gj)
+        steps_of = {}
+        for key, w in working.items():
+            grp = eng.groups[key]
+            w.prepare(eng.o.hop_optimizer_state)
+            B = grp.batch_size
+            steps = eng.n_train // B
+            if rec.get("max_steps"):
+                steps = min(steps, rec["max_steps"])
+            steps_of[key] = steps
+            with tr.span("train", sync=eng._sync, arch=key[0], G=w.G, steps=steps):
+                w.train_steps(steps)
+                delay = eng.o.sim_job_seconds
+                if delay:                            # test hook: heterogeneous job lengths
+                    time.sleep(max(delay[m % len(delay)] for m, _ in w.jobs))
+            trained += steps * B * w.G
+        # the states are final: park them (the home row is the committed
+        # copy a hop or a retry starts from), then free the models
+        for key in working:
+            eng.groups[key].park_all()
+        if hops is not None:
+            for m in models:
+                hops.mark_final(m)
+        chan.post_event({"t": "train_done", "rank": rank, "models": models})
+        for key, w in working.items():
+            grp = eng.groups[key]
+            B = grp.batch_size
+            vsteps = eng.n_valid // B
+            if rec.get("max_steps"):
+                full = max(eng.n_train // B, 1)
+                vsteps = max(1, -(-vsteps * steps_of[key] // full))
+            with tr.span("valid", sync=eng._sync, arch=key[0], G=w.G, steps=vsteps):
+                w.validate(vsteps)
+                mets = w.read_metrics()
+                if eng.o.sim_valid_seconds:
+                    time.sleep(eng.o.sim_valid_seconds)
+            for row, (m, lp) in enumerate(w.jobs):
+                results.append({"model": m, "dist_key": eng.store.pids[lp], "metrics": mets[row],
+                                "steps": steps_of[key], "batch": B, "partition": lp})
+    except SoftFault as e:
+        # every incoming state has arrived; the home rows hold the pre-job
+        # states, the working copies of this batch are void
+        error = str(e)
+        for grp in eng.groups.values():
+            grp.drop_residency(models)
+    except BaseException as e:
+        chan.post_event({"t": "job_done", "rank": rank, "error": "{}: {}".format(
+            type(e).__name__, e), "fatal": True, "results": [], "t_start": t_start,
+            "t_hop": t_start, "t_end": time.time()})
+        raise
+    if eng._sync is not None:
+        eng._sync()
+    if error is None:
+        eng.train_images += trained
+    with tr.span("report", subepoch=rec["subepoch"]):
+        chan.post_event({"t": "job_done", "rank": rank, "error": error, "fatal": False,
+                         "results": results, "t_start": t_start, "t_hop": t_hop,
+                         "t_end": time.time()})
+
+
+# ---------------------------------------------------------------------------
+# session driver
+# ---------------------------------------------------------------------------
+def run_session(eng, policy, first_epoch, num_epochs, mst_eval_fn=None, steps_of=None,
+                round_budget=None):
+    """One asynchronous run on every rank (collective); returns when the
+    coordinator stops.  Rank 0's coordinator state (metrics, holders) is
+    shared with every rank at the end."""
+    ctx = eng.ctx
+    chan = eng.control_channel()
+    hops = None
+    if ctx.world > 1:
+        hops = HopService(eng, chan, eng.hop_group()).start()
+    coord = None
+    if ctx.rank == 0:
+        eng.coord_begin()
+        coord = Coordinator(eng, chan, eng.async_scheduler(policy), policy, first_epoch,
+                            num_epochs, mst_eval_fn, steps_of, round_budget).start()
+    err = None
+    try:
+        err = run_worker(eng, chan, hops)
+    finally:
+        if coord is not None:
+            coord.join()
+        if hops is not None:
+            hops.join()
+    if coord is not None:
+        err = err or coord.error
+    for grp in eng.groups.values():
+        grp.park_all()
+    if hops is not None:
+        eng.hop_bytes += hops.bytes
+        eng.hop_busy_time += hops.busy
+        eng.hop_spans.extend(hops.spans)
+        if hops.error and not err:
+            err = "hop service: " + hops.error
+    # share rank 0's bookkeeping with every rank (JSON over the control store)
+    if ctx.rank == 0:
+        chan.put_final({
+            "holder": {str(m): h for m, h in coord.holder.items()},
+            "mst_state": {str(m): v for m, v in eng.mst_state.items()},
+            "jobs_info": {str(e): [[k[0], k[1], j] for k, j in jobs.items()]
+                          for e, jobs in eng.jobs_info.items()},
+            "models_info": dict(eng.models_info), "msts": eng.coord_msts,
+            "failures": eng.failures, "round_idx": eng.round_idx, "error": err,
+            "last_epoch": coord.last_epoch, "rounds_done": coord.rounds_done})
+    fin = chan.get_final()
+    ctx.barrier()
+    eng.coord_end(fin)
+    if fin["error"]:
+        raise RuntimeError("asynchronous MOP run failed: " + fin["error"])
+    return fin

@@ -84,6 +84,27 @@ class EngineOptions(object):
         self.max_retries = kw.get("max_retries", 2)
         self.resume = kw.get("resume", False)
         self.heartbeat = kw.get("heartbeat", 0)     # watchdog timeout (s); 0 = off
+        # runtime: "async" (event driven, hops overlapped with compute),
+        # "lockstep" (a barrier per sub-epoch) or "auto" (async unless a
+        # feature needs lock-step: sub-epoch checkpoints, task parallelism)
+        self.runtime = kw.get("runtime", os.environ.get("CER_RUNTIME", "auto"))
+        self.ctrl_timeout = kw.get("ctrl_timeout", 6 * 3600)
+        # test hook: extra seconds per job of config m (heterogeneous jobs)
+        self.sim_job_seconds = kw.get("sim_job_seconds", None)
+        self.sim_valid_seconds = kw.get("sim_valid_seconds", 0.0)
+        self.sim_hop_seconds = kw.get("sim_hop_seconds", 0.0)     # per hop (slow link)
+
+
+class _StepsPlan(object):
+    """Steps per job of a bench session: ``per`` per round, ``last`` in the
+    final one of ``n`` rounds (the coordinator passes the round index within
+    the epoch; it tracks the session's round count itself)."""
+
+    def __init__(self, per, last, n):
+        self.per, self.last, self.n = per, last, n
+
+    def __call__(self, session_round):
+        return self.last if session_round == self.n - 1 else self.per
 
 
 class SoftFault(RuntimeError):
@@ -149,7 +170,20 @@ class MOPEngine(object):
         self.train_images = 0
         self.round_idx = 0
         self.hop_bytes = 0
-        self.hop_time = 0.0
+        self.hop_time = 0.0          # exposed: time a rank waited for a hop
+        self.hop_busy_time = 0.0     # transfers themselves (async runtime)
+        self.hop_spans = []
+        self.coord_msts = None
+        self._asched = {}
+        self._chan = None
+        self._nsession = 0
+        self._hop_pg = None
+        if ctx.initialized and not self.task_parallel:
+            # async hops run on their own communicator (and their own thread)
+            import torch.distributed as dist
+            from ..parallel.hop import warm_p2p
+            self._hop_pg = dist.new_group(backend=ctx.backend)
+            warm_p2p(ctx.world, ctx.rank, self.device, group=self._hop_pg)
         self.epoch = 0
         self.failures = []
         self._fired = set()
@@ -215,6 +249,8 @@ class MOPEngine(object):
                 w.load_local(row, m)
         hopt = self.o.hop_optimizer_state
         t0 = time.time()
+        if moves and self.o.sim_hop_seconds and any(rank in (mv.src, mv.dst) for mv in moves):
+            time.sleep(self.o.sim_hop_seconds * sum(mv.src == rank for mv in moves))
         if moves:
             def send_buf(m):
                 st = self.group_of[m].state_row(m)
@@ -251,6 +287,15 @@ class MOPEngine(object):
             os._exit(3)
         raise RuntimeError(msg)
 
+    def _fault_check_batch(self, k):
+        """Async runtime: the injection hook keyed by the job's sub-epoch."""
+        saved = self.round_idx
+        self.round_idx = k
+        try:
+            self._fault_check()
+        finally:
+            self.round_idx = saved
+
     def _train_local(self, per_group, max_steps):
         """Train + validate every local pack group; returns (results, images)."""
         results = []
@@ -266,6 +311,9 @@ class MOPEngine(object):
                 steps = min(steps, max_steps)
             with tr.span("train", sync=self._sync, arch=key[0], G=w.G, steps=steps):
                 w.train_steps(steps)
+                if self.o.sim_job_seconds:           # test hook: heterogeneous job lengths
+                    d = self.o.sim_job_seconds
+                    time.sleep(max(d[m % len(d)] for m, _ in jobs))
             trained += steps * B * w.G
             vsteps = self.n_valid // B
             if max_steps is not None:
@@ -275,6 +323,8 @@ class MOPEngine(object):
             with tr.span("valid", sync=self._sync, arch=key[0], G=w.G, steps=vsteps):
                 w.validate(vsteps)
                 mets = w.read_metrics()
+                if self.o.sim_valid_seconds:
+                    time.sleep(self.o.sim_valid_seconds)
             for row, (m, lp) in enumerate(jobs):
                 results.append({"model": m, "dist_key": self.store.pids[lp], "metrics": mets[row],
                                 "steps": steps, "batch": B, "partition": lp})
@@ -346,11 +396,17 @@ class MOPEngine(object):
         self.train_images += trained
         return failed, trained
 
-    def _record_job(self, epoch, g, r):
+    def _bk_msts(self):
+        """Config list of the bookkeeping owner (the coordinator's during an
+        asynchronous session on rank 0)."""
+        return self.coord_msts if self.coord_msts is not None else self.msts
+
+    def _record_job(self, epoch, g, r, subepoch=None):
         m = r["model"]
         mets = r["metrics"]
+        sub = self.round_idx if subepoch is None else subepoch
         job = {"status": "SUCCESS", "epoch": epoch, "dist_key": r["dist_key"],
-               "model_key": model_key(m, self.msts[m]),
+               "model_key": model_key(m, self._bk_msts()[m]),
                "loss_train": mets["train"]["loss"], "metric_train": mets["train"]["top5"],
                "loss_valid": mets["valid"]["loss"], "metric_valid": mets["valid"]["top5"],
                "top1_train": mets["train"]["top1"], "top1_valid": mets["valid"]["top1"],
@@ -358,11 +414,11 @@ class MOPEngine(object):
                "start_time": g["t_start"], "end_time": g["t_end"],
                "init_time": 0.0, "train_time": g["t_end"] - g["t_hop"],
                "valid_time": 0.0, "exit_time": 0.0, "hop_time": g["t_hop"] - g["t_start"],
-               "subepoch": self.round_idx, "rank": g["rank"]}
+               "subepoch": sub, "rank": g["rank"]}
         self.jobs_info.setdefault(epoch, {})[(job["model_key"], r["dist_key"])] = job
         self.models_info[job["model_key"]].append(job)
         if self._metrics_path:
-            rec = {"epoch": epoch, "subepoch": self.round_idx, "cfg": job["model_key"],
+            rec = {"epoch": epoch, "subepoch": sub, "cfg": job["model_key"],
                    "partition": r["dist_key"], "rank": g["rank"],
                    "loss": job["loss_train"], "top1": job["top1_train"],
                    "top5": job["metric_train"], "valid_loss": job["loss_valid"],
@@ -386,8 +442,9 @@ class MOPEngine(object):
             a["v5"] += j["metric_valid"] * j["n_valid"]
             a["v1"] += j["top1_valid"] * j["n_valid"]
             a["nv"] += j["n_valid"]
-        for m in range(len(self.msts)):
-            mk = model_key(m, self.msts[m])
+        msts = self._bk_msts()
+        for m in range(len(msts)):
+            mk = model_key(m, msts[m])
             if mk not in agg:
                 continue
             a = agg[mk]
@@ -400,17 +457,18 @@ class MOPEngine(object):
             st["train_top1_error"].append(1 - a["t1"] / nt)
             st["valid_top1_error"].append(1 - a["v1"] / nv)
 
-    def checkpoint_all(self, epoch, models=None):
-        """Queue async checkpoints of the configs parked on this rank."""
+    def checkpoint_all(self, epoch, models=None, holder_ok=False):
+        """Queue async checkpoints of the configs parked on this rank
+        (``holder_ok``: the caller already picked this rank's configs)."""
         if not self.o.models_root:
             return
         os.makedirs(self.o.models_root, exist_ok=True)
         ids = range(len(self.msts)) if models is None else models
         for m in ids:
-            h = self.holder[m]
+            h = self.holder.get(m)
             if h is None:
                 h = 0
-            if h != self.ctx.rank:
+            if not holder_ok and h != self.ctx.rank:
                 continue
             grp = self.group_of[m]
             weights, opt = state_to_host(grp.layout, grp.state_row(m))
@@ -433,16 +491,23 @@ class MOPEngine(object):
             self.writer.flush()
             self.ctx.barrier()
             if self.ctx.rank == 0:
-                if self.o.logs_root:
-                    dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
-                st = {"epoch": epoch, "rounds_done": rounds_done, "epoch_done": epoch_done,
-                      "round_idx": self.round_idx, "msts": self.msts,
-                      "states": {str(m): self.mst_state[m]["state"] for m in self.mst_state},
-                      "sched_rng": sched_rng, "failures": self.failures}
-                path = os.path.join(self.o.models_root, RESUME_FILE)
-                with open(path + ".tmp", "w") as f:
-                    json.dump(st, f, default=str)
-                os.replace(path + ".tmp", path)
+                self.write_resume(epoch, rounds_done, epoch_done, sched_rng)
+
+    def write_resume(self, epoch, rounds_done, epoch_done, sched_rng):
+        """Publish ``resume.json`` (atomic rename); every checkpoint it names
+        is on disk already."""
+        if not self.o.models_root:
+            return
+        if self.o.logs_root:
+            dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
+        st = {"epoch": epoch, "rounds_done": rounds_done, "epoch_done": epoch_done,
+              "round_idx": self.round_idx, "msts": self._bk_msts(),
+              "states": {str(m): self.mst_state[m]["state"] for m in self.mst_state},
+              "sched_rng": sched_rng, "failures": self.failures}
+        path = os.path.join(self.o.models_root, RESUME_FILE)
+        with open(path + ".tmp", "w") as f:
+            json.dump(st, f, default=str)
+        os.replace(path + ".tmp", path)
 
     def _resume(self):
         """Load ``resume.json`` + checkpoints; returns (epoch, rounds_to_skip, rng)."""
@@ -478,11 +543,114 @@ class MOPEngine(object):
             return st["epoch"] + 1, 0, None
         return st["epoch"], st["rounds_done"], st.get("sched_rng")
 
+    # ------------------------------------------------------------------
+    # asynchronous runtime hooks (runtime.async_mop)
+    def use_async(self, sub_epoch_resume=False):
+        rt = self.o.runtime
+        if rt not in ("auto", "async", "lockstep"):
+            raise ValueError("unknown runtime {!r}".format(rt))
+        lock_only = (self.task_parallel or self.o.ckpt_every == "subepoch" or sub_epoch_resume
+                     or self.o.scheduler not in ("rotation", "greedy"))
+        if rt == "async" and lock_only:
+            raise ValueError("runtime='async' does not support scheduler={} / ckpt_every={} / "
+                             "sub-epoch resume".format(self.o.scheduler, self.o.ckpt_every))
+        return rt == "async" or (rt == "auto" and not lock_only)
+
+    def async_scheduler(self, policy):
+        """One scheduler per policy for the engine's lifetime (the greedy
+        shuffle RNG continues across epochs and sessions)."""
+        from ..scheduler.policies import GreedyScheduler, RotationScheduler
+        sch = self._asched.get(policy)
+        if sch is None:
+            ids = list(range(len(self._bk_msts())))
+            if policy == "rotation":
+                sch = RotationScheduler(ids, list(range(self.P)), seed=self.o.seed)
+            else:
+                sch = GreedyScheduler(ids, list(range(self.P)), seed=self.o.seed,
+                                      shuffle=self.o.shuffle)
+            self._asched[policy] = sch
+        return sch
+
+    def control_channel(self):
+        from .async_mop import Channel, LocalStore, rendezvous_addr, tcp_client
+        self._nsession += 1
+        # a fresh key space per session: the rendezvous store outlives engines
+        tok = self.ctx.broadcast_object(os.urandom(6).hex() if self.ctx.rank == 0 else None)
+        pfx = "cerebro_ctl/{}/{}".format(tok, self._nsession)
+        if self.ctx.world <= 1:
+            if self._chan is None:
+                self._chan = LocalStore()
+            return Channel(self._chan, pfx, self.o.ctrl_timeout)
+        if self._chan is None:
+            addr = rendezvous_addr()
+            if addr is None:
+                raise RuntimeError("asynchronous runtime needs MASTER_ADDR / MASTER_PORT")
+            self._chan = (tcp_client(addr, self.o.ctrl_timeout), addr)
+        return Channel(self._chan[0], pfx, self.o.ctrl_timeout, self._chan[1])
+
+    def hop_group(self):
+        return self._hop_pg
+
+    def coord_begin(self):
+        self.coord_msts = [dict(m) for m in self.msts]
+
+    def coord_log(self, msg):
+        self.log(msg)
+
+    def coord_add_msts(self, new_msts):
+        base = len(self.coord_msts)
+        self.coord_msts.extend(dict(m) for m in new_msts)
+        ids = list(range(base, len(self.coord_msts)))
+        for m in ids:
+            self.mst_state[m] = {"train_loss": [], "valid_loss": [], "train_top5_error": [],
+                                 "valid_top5_error": [], "train_top1_error": [],
+                                 "valid_top1_error": [], "state": "RUNNING"}
+        for sch in self._asched.values():
+            if sch is not None:
+                sch.add_models(ids)
+        return ids
+
+    def worker_add_msts(self, new_msts):
+        base = len(self.msts)
+        self.msts.extend(dict(m) for m in new_msts)
+        ids = list(range(base, len(self.msts)))
+        for m in ids:
+            self.holder[m] = None
+        self._build_groups(ids)
+        self.sched.add_models(ids)
+
+    def coord_end(self, fin):
+        """Adopt rank 0's end-of-session bookkeeping (JSON round trip)."""
+        self.holder = {int(m): h for m, h in fin["holder"].items()}
+        if self.coord_msts is None:          # ranks > 0
+            self.mst_state = {int(m): v for m, v in fin["mst_state"].items()}
+            self.jobs_info = {int(e): {(j[0], j[1]): j[2] for j in jobs}
+                              for e, jobs in fin["jobs_info"].items()}
+            self.models_info = collections.defaultdict(list, fin["models_info"])
+            self.failures = list(fin["failures"])
+            self.round_idx = fin["round_idx"]
+        self.coord_msts = None
+        assert len(self.msts) == len(fin["msts"]), "config lists diverged"
+
+    def _run_async(self, first, num_epochs, mst_eval_fn=None, steps_of=None, round_budget=None):
+        from .async_mop import run_session
+        policy = "greedy" if self.o.scheduler == "greedy" else "rotation"
+        return run_session(self, policy, first, num_epochs, mst_eval_fn, steps_of, round_budget)
+
     def run(self, num_epochs, mst_eval_fn=None):
         """Full semantic run: ``num_epochs`` MOP epochs (reference ``schedule``)."""
         t0 = time.time()
         first, skip, rng = (self._resume() if self.o.resume else (1, 0, None))
         hb = self._start_heartbeat()
+        if self.use_async(sub_epoch_resume=bool(skip or rng)):
+            try:
+                if first <= num_epochs:
+                    self._run_async(first, num_epochs, mst_eval_fn)
+                self.writer.flush()
+            finally:
+                if hb is not None:
+                    hb.stop()
+            return time.time() - t0
         try:
             for epoch in range(first, num_epochs + 1):
                 active = [m for m in range(len(self.msts))
@@ -589,6 +757,15 @@ class MOPEngine(object):
     def run_steps(self, total_steps, steps_per_round, epoch_start=1):
         """Bench mode: rounds of ``steps_per_round`` steps until ``total_steps``
         packed steps are done (the schedule continues across epochs)."""
+        if total_steps <= 0:
+            return 0
+        if self.use_async() and self.o.scheduler == "rotation":
+            n = -(-total_steps // steps_per_round)
+            last = total_steps - (n - 1) * steps_per_round
+            self._run_async(epoch_start, 1 << 30, None,
+                                  steps_of=_StepsPlan(steps_per_round, last, n),
+                                  round_budget=n)
+            return total_steps
         done = 0
         epoch = epoch_start
         while done < total_steps:

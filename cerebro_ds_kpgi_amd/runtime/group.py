@@ -61,12 +61,21 @@ class PackGroup(object):
                 self.home.init_model(self.home_row[m], seed_base + m)
         self._work = {}   # G -> _Working
         self.current = None
+        # asynchronous runtime: models whose latest state sits in a working
+        # arena row ({G: {model: row}}), and the subset not yet parked in
+        # their home rows.  A job that stays on this GPU then costs a
+        # part_of_row change, not a state copy in and out.
+        self.resident = {}
+        self.dirty = set()
+        self.n_loads = 0      # state copies home -> working row
+        self.n_parks = 0      # state copies working row -> home
 
     def add_models(self, model_ids, seed):
         """Grow the home arena for configs proposed mid-run (hyperopt)."""
         new = [m for m in model_ids if m not in self.home_row]
         if not new:
             return
+        self.park_all()
         old = self.home
         self.model_ids.extend(new)
         self.home_row = {m: i for i, m in enumerate(self.model_ids)}
@@ -79,7 +88,78 @@ class PackGroup(object):
 
     # ------------------------------------------------------------------
     def state_row(self, m):
+        self.park(m)
         return self.home.state[self.home_row[m]]
+
+    # -- residency (asynchronous runtime) -----------------------------------
+    def _where(self, m):
+        for G, rows in self.resident.items():
+            if m in rows:
+                return G, rows[m]
+        return None
+
+    def park(self, m):
+        """Copy m's working-row state to its home row if only the row has it."""
+        if m not in self.dirty:
+            return
+        G, row = self._where(m)
+        self.home.state[self.home_row[m]].copy_(self._work[G].arena.state[row])
+        self.dirty.discard(m)
+        self.n_parks += 1
+
+    def park_all(self):
+        for m in list(self.dirty):
+            self.park(m)
+
+    def invalidate(self, m):
+        """m's home row was just overwritten by an arriving hop."""
+        assert m not in self.dirty, m
+        for rows in self.resident.values():
+            rows.pop(m, None)
+
+    def drop_residency(self, models):
+        """Working copies of ``models`` are no longer valid (failed job)."""
+        for m in models:
+            self.dirty.discard(m)
+            for rows in self.resident.values():
+                rows.pop(m, None)
+
+    def begin_batch(self, jobs):
+        """Working set for jobs = [(model, local_partition)]: models already
+        resident in this working set keep their rows (only part_of_row
+        changes), other rows load from the home arena after their previous
+        residents are parked.  The batch's models are dirty afterwards."""
+        G = len(jobs)
+        w = self.working(G)
+        batch = {m for m, _ in jobs}
+        for G2, rows2 in self.resident.items():
+            if G2 != G:
+                for m in [m for m in rows2 if m in batch]:
+                    self.park(m)
+                    del rows2[m]
+        res = self.resident.setdefault(G, {})
+        rows = [None] * G
+        rest = []
+        for m, lp in jobs:
+            r = res.get(m)
+            if r is not None and rows[r] is None:
+                rows[r] = (m, lp)
+            else:
+                rest.append((m, lp))
+        for m2 in [m2 for m2 in res if m2 not in batch]:
+            self.park(m2)
+            del res[m2]
+        free = [i for i in range(G) if rows[i] is None]
+        for (m, lp), i in zip(rest, free):
+            rows[i] = (m, lp)
+        w.assign(rows)
+        for i, (m, _) in enumerate(rows):
+            if res.get(m) != i:
+                w.load_local(i, m)
+        self.resident[G] = {m: i for i, (m, _) in enumerate(rows)}
+        self.dirty |= batch
+        self.current = w
+        return w
 
     def working(self, G):
         w = self._work.get(G)
@@ -91,7 +171,10 @@ class PackGroup(object):
     def begin_round(self, jobs, recv_into=None):
         """jobs: list of (model_id, local_partition_index).  Returns the
         working set; rows whose state arrives by a hop are filled by the
-        caller through ``recv_buffer``."""
+        caller through ``recv_buffer``.  (Lock-step runtime: states are
+        copied in here and parked back by ``end_round``.)"""
+        self.park_all()
+        self.resident.clear()
         G = len(jobs)
         w = self.working(G)
         w.assign(jobs)
@@ -103,6 +186,7 @@ class PackGroup(object):
         w = self.current
         for row, (m, _) in enumerate(w.jobs):
             self.home.state[self.home_row[m]].copy_(w.arena.state[row])
+        self.n_parks += len(w.jobs)
         self.current = None
 
 
@@ -146,6 +230,7 @@ class _Working(object):
 
     def load_local(self, row, m):
         self.arena.state[row].copy_(self.group.state_row(m))
+        self.group.n_loads += 1
 
     def prepare(self, hop_optimizer_state):
         if not hop_optimizer_state:
@@ -206,7 +291,9 @@ class _Working(object):
                 return done
             streams.join()
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            # thread-local capture: the asynchronous runtime's hop thread keeps
+            # issuing RCCL transfers / stream syncs while this thread captures
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self._step()
         while done < nsteps:
             self.graph.replay()
@@ -245,7 +332,8 @@ class _Working(object):
                     # two graphs' temporaries alias: invalid eval results)
                     pool = (self.graph.pool() if self.graph is not None and
                             os.environ.get("CER_VG_SHARE", "0") == "1" else None)
-                    with torch.cuda.graph(self.vgraph, pool=pool):
+                    with torch.cuda.graph(self.vgraph, pool=pool,
+                                          capture_error_mode="thread_local"):
                         self._vstep()
             while done < nsteps:
                 if self.vgraph is not None and not self.veager:

@@ -124,6 +124,28 @@ class MOPScheduler(object):
         self.idle_models.add(model)
         self.idle_workers.add(worker)
 
+    # -- split completion (asynchronous runtime) --------------------------
+    # A sub-epoch job = train + validate.  Its model's state is final when
+    # training ends, so the model may start its next sub-epoch elsewhere
+    # while this worker still validates it; the worker frees after validation.
+    def release_model(self, model, worker):
+        """Training of (model, worker) done: the pair is done, the model idle."""
+        self.monitor.finish(model, worker)
+        self.idle_models.add(model)
+
+    def release_worker(self, worker):
+        self.idle_workers.add(worker)
+
+    def abort(self, model, worker):
+        """A failed job: the pair goes back to the front of the queue."""
+        if self.monitor.model_on.get(model) == worker:
+            del self.monitor.model_on[model]
+            del self.monitor.worker_has[worker]
+        if (model, worker) not in self.pending:
+            self.pending.insert(0, (model, worker))
+        self.idle_models.add(model)
+        self.idle_workers.add(worker)
+
     def assign_all_idle(self):
         """Offer every idle worker a job (worker order = id order, like CTQ's loop)."""
         out = []

@@ -66,6 +66,20 @@ class RotationScheduler(MOPScheduler):
             self.complete(m, w)
         self.subepoch += 1
 
+    # asynchronous runtime: the next round's map is known before the current
+    # round's workers are free (its hops start while they still validate)
+    def peek_round(self):
+        if self.subepoch >= len(self.rounds):
+            return None
+        return dict(self.rounds[self.subepoch])
+
+    def start_round(self):
+        """Start the peeked round (its workers must be free)."""
+        return self.next_round()
+
+    def end_round(self):
+        self.subepoch += 1
+
 
 class GreedyScheduler(MOPScheduler):
     def __init__(self, models, workers, seed=2018, shuffle=True):

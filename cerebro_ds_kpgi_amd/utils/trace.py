@@ -22,6 +22,15 @@ class Tracer(object):
         self.events = []
         self.t0 = time.time()
         self._lock = threading.Lock()
+        self._tids = {}
+
+    def _tid(self):
+        """One trace row per thread (main = 0; the asynchronous runtime's hop
+        and coordinator threads get their own rows)."""
+        name = threading.current_thread().name
+        if name not in self._tids:
+            self._tids[name] = 0 if name == "MainThread" else len(self._tids) + 1
+        return self._tids[name]
 
     def _us(self, t):
         return (t - self.t0) * 1e6
@@ -42,14 +51,15 @@ class Tracer(object):
             e = time.time()
             with self._lock:
                 self.events.append({"name": name, "cat": cat, "ph": "X", "ts": self._us(t),
-                                    "dur": (e - t) * 1e6, "pid": self.rank, "tid": 0,
-                                    "args": args})
+                                    "dur": (e - t) * 1e6, "pid": self.rank,
+                                    "tid": self._tid(), "args": args})
 
     def instant(self, name, **args):
         if self.enabled:
             with self._lock:
                 self.events.append({"name": name, "ph": "i", "ts": self._us(time.time()),
-                                    "pid": self.rank, "tid": 0, "s": "p", "args": args})
+                                    "pid": self.rank, "tid": self._tid(), "s": "p",
+                                    "args": args})
 
     def dump(self, directory):
         if not self.enabled or not directory:

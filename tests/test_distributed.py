@@ -37,7 +37,7 @@ def _msts():
     return out
 
 
-def _run(rank, world, port, outdir, slots, scheduler, hop_opt):
+def _run(rank, world, port, outdir, slots, scheduler, hop_opt, runtime="auto"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                        "CEREBRO_BACKEND": "torch", "CEREBRO_QUIET": "1"})
@@ -47,7 +47,7 @@ def _run(rank, world, port, outdir, slots, scheduler, hop_opt):
     ctx = init_distributed(device_type="cpu")
     eng = MOPEngine(_msts(), ctx, EngineOptions(
         n_train=64, n_valid=16, compute_dtype="fp32", slots_per_gpu=slots, scheduler=scheduler,
-        hop_optimizer_state=hop_opt, verbose=False, ckpt_every="none",
+        hop_optimizer_state=hop_opt, verbose=False, ckpt_every="none", runtime=runtime,
         models_root=os.path.join(outdir, "models"), logs_root=os.path.join(outdir, "logs")))
     eng.run(2)
     states = {}
@@ -65,12 +65,13 @@ def _run(rank, world, port, outdir, slots, scheduler, hop_opt):
     shutdown(ctx)
 
 
-def _launch(tmp, world, slots, scheduler="rotation", hop_opt=True):
+def _launch(tmp, world, slots, scheduler="rotation", hop_opt=True, runtime="auto"):
     port = _free_port()
     if world == 1:
-        _run(0, 1, port, tmp, slots, scheduler, hop_opt)
+        _run(0, 1, port, tmp, slots, scheduler, hop_opt, runtime)
     else:
-        mp.spawn(_run, args=(world, port, tmp, slots, scheduler, hop_opt), nprocs=world, join=True)
+        mp.spawn(_run, args=(world, port, tmp, slots, scheduler, hop_opt, runtime), nprocs=world,
+                 join=True)
     states = {}
     for r in range(world):
         states.update(torch.load(os.path.join(tmp, "states_{}.pt".format(r)), weights_only=True))
@@ -81,14 +82,19 @@ def _launch(tmp, world, slots, scheduler="rotation", hop_opt=True):
     return states, mst_state, hops
 
 
-@pytest.mark.parametrize("scheduler,hop_opt", [("rotation", True), ("greedy", False)])
-def test_two_rank_mop_matches_single_process(tmp_path, scheduler, hop_opt):
+# rotation runs on the asynchronous runtime (data-flow rounds, hops on their
+# own thread) and must reproduce the single-process visit order; the greedy
+# case pins the lock-step runtime, whose greedy plan is deterministic (the
+# asynchronous greedy order depends on event timing: test_async_runtime)
+@pytest.mark.parametrize("scheduler,hop_opt,runtime", [("rotation", True, "async"),
+                                                       ("greedy", False, "lockstep")])
+def test_two_rank_mop_matches_single_process(tmp_path, scheduler, hop_opt, runtime):
     a = tmp_path / "one"
     b = tmp_path / "two"
     a.mkdir()
     b.mkdir()
-    s1, m1, _ = _launch(str(a), 1, 4, scheduler, hop_opt)
-    s2, m2, hops = _launch(str(b), 2, 2, scheduler, hop_opt)
+    s1, m1, _ = _launch(str(a), 1, 4, scheduler, hop_opt, runtime)
+    s2, m2, hops = _launch(str(b), 2, 2, scheduler, hop_opt, runtime)
     assert hops["hop_bytes"] > 0                       # models really crossed ranks
     assert sorted(s1) == sorted(s2) == [0, 1, 2, 3]
     # packing 4 vs 2 configs per process changes CPU grouped-conv blocking, so

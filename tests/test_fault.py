@@ -86,7 +86,9 @@ def test_crash_then_resume_matches_uninterrupted(tmp_path, scheduler, monkeypatc
     monkeypatch.setenv("CEREBRO_BACKEND", "torch")
     monkeypatch.setenv("CEREBRO_QUIET", "1")
     torch.set_num_threads(2)
-    ref = _engine(str(tmp_path / "ref"), scheduler, ckpt_every="none")
+    # sub-epoch checkpoints run the lock-step runtime; the reference run too
+    # (the async runtime packs rows in another order: equal to float noise)
+    ref = _engine(str(tmp_path / "ref"), scheduler, ckpt_every="none", runtime="lockstep")
     ref.run(2)
     want = _states(ref)
     ref.close()
@@ -147,17 +149,20 @@ def test_heartbeat_watchdog_flags_silent_rank(tmp_path):
         assert json.load(f)["lost"] == [1]
 
 
-def test_trace_spans_and_metrics_jsonl(tmp_path, monkeypatch):
+@pytest.mark.parametrize("runtime", ["lockstep", "async"])
+def test_trace_spans_and_metrics_jsonl(tmp_path, monkeypatch, runtime):
     monkeypatch.setenv("CEREBRO_BACKEND", "torch")
     monkeypatch.setenv("CEREBRO_QUIET", "1")
     d = str(tmp_path)
-    eng = _engine(d, "rotation", ckpt_every="none", trace=True)
+    eng = _engine(d, "rotation", ckpt_every="none", trace=True, runtime=runtime)
     eng.run(1)
     eng.close()
     with open(os.path.join(d, "logs", "traces", "trace_rank0.json")) as f:
         ev = json.load(f)["traceEvents"]
     names = {e["name"] for e in ev}
-    assert {"hop", "train", "valid", "report"} <= names
+    # lock-step: a hop phase per round; async: the exposed wait for arrivals
+    assert {"hop" if runtime == "lockstep" else "wait_arrival", "train", "valid",
+            "report"} <= names
     assert sum(e["name"] == "train" for e in ev) == 4
     with open(os.path.join(d, "logs", "metrics.jsonl")) as f:
         rows = [json.loads(l) for l in f]
