@@ -1,8 +1,10 @@
 """Per-layer conv benchmark: our MFMA implicit-GEMM kernels vs MIOpen (PyTorch
-grouped conv on channels-last bf16), for every unique ResNet-50@112 conv
-shape of the packed G-config model.
+grouped conv on channels-last tensors), for every unique ResNet-50@112 conv
+shape of the packed G-config model, in bf16 or fp32 (the reference
+precision: 3-pass split-bf16 MFMA on our side, MIOpen's fp32 kernels on
+the other).
 
-    python -m cerebro_ds_kpgi_amd.tools.bench_conv --G 8 --B 32 [--json out.json]
+    python -m cerebro_ds_kpgi_amd.tools.bench_conv --G 8 --B 32 [--dtype fp32] [--json out.json]
 
 Reports time and TFLOP/s for fwd, dgrad and wgrad per shape, plus totals
 weighted by how often each shape occurs in ResNet-50.
@@ -58,23 +60,27 @@ def _time(fn, iters):
     return s.elapsed_time(e) / iters
 
 
-def bench_shape(shape, G, iters):
+def bench_shape(shape, G, iters, dtype=torch.bfloat16, miopen=True):
     B, H, W, cin, cout, k, st, pad = shape
     spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
     lay = ModelLayout([spec])
-    a = Arena(lay, G, "cuda", torch.bfloat16)
+    a = Arena(lay, G, "cuda", dtype)
     for g in range(G):
         a.init_model(g, g)
     ref = ParamRef(a, spec)
-    x = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+    x = torch.randn(B, H, W, G * cin, device="cuda").to(dtype)
     Ho = (H + 2 * pad - k) // st + 1
     Wo = (W + 2 * pad - k) // st + 1
-    dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(dtype)
     flops = 2.0 * B * Ho * Wo * cout * k * k * cin * G
     out = {}
     out["hip_fwd"] = _time(lambda: _hip.conv2d_fwd(x, ref, st, pad), iters)
     out["hip_dgrad"] = _time(lambda: _hip.conv2d_dgrad(dy, ref, x.shape, st, pad), iters)
     out["hip_wgrad"] = _time(lambda: _hip.conv2d_wgrad(x, dy, ref, st, pad), iters)
+    if not miopen:
+        out["tflops"] = {kk: flops / (v * 1e-3) / 1e12 for kk, v in out.items()}
+        out["gflop"] = flops / 1e9
+        return out
     w = ref.work().permute(0, 1, 4, 2, 3).reshape(G * cout, cin, k, k).contiguous(
         memory_format=torch.channels_last)
     xn = x.permute(0, 3, 1, 2)
@@ -131,7 +137,9 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default="")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant per shape")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     a = ap.parse_args(argv)
+    dtype = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     backend.set_backend("hip")
     if a.sweep:
         rows = sweep(resnet50_shapes(a.B), a.G, a.iters)
@@ -142,7 +150,7 @@ def main(argv=None):
     rows = []
     tot = collections.defaultdict(float)
     for shape, count in resnet50_shapes(a.B).items():
-        r = bench_shape(shape, a.G, a.iters)
+        r = bench_shape(shape, a.G, a.iters, dtype)
         r["shape"] = shape
         r["count"] = count
         rows.append(r)
@@ -156,7 +164,7 @@ def main(argv=None):
                   r["tflops"]["hip_wgrad"], r["tflops"]["miopen_wgrad"]), flush=True)
     hip = tot["hip_fwd"] + tot["hip_dgrad"] + tot["hip_wgrad"]
     mio = tot["miopen_fwd"] + tot["miopen_dgrad"] + tot["miopen_wgrad"]
-    summary = {"G": a.G, "B": a.B, "hip_ms_per_step": hip, "miopen_ms_per_step": mio,
+    summary = {"G": a.G, "B": a.B, "dtype": a.dtype, "hip_ms_per_step": hip, "miopen_ms_per_step": mio,
                "hip_tflops": 3 * tot["gflop"] / hip, "miopen_tflops": 3 * tot["gflop"] / mio,
                "fwd_ms": {"hip": tot["hip_fwd"], "miopen": tot["miopen_fwd"]},
                "dgrad_ms": {"hip": tot["hip_dgrad"], "miopen": tot["miopen_dgrad"]},
