@@ -14,9 +14,17 @@ own (HBM partition store, packed HIP models, fused step), so:
 * ``input_fn`` selects the data source: ``data.da.input_fn`` (or a catalog
   whose ``data_root`` holds a DA manifest) -> Direct-Access pages; anything
   else / ``None`` -> synthetic partitions of the dataset's shape;
-* ``model_fn`` / ``train_fn`` are accepted for source compatibility; the
-  model is built from each MST's ``model`` name (``models.registry``) and
-  trained by the native step.  A custom callable logs a notice;
+* ``model_fn``: ``None`` / ``native_model_fn`` build each MST's ``model``
+  from ``models.registry``.  A custom ``model_fn(mst)`` must return either an
+  architecture name or a ``models.common.PackedNet`` (our packed-model API:
+  ``ParamSpec`` declarations + a forward over ``ops.nn``); the returned
+  architecture is registered and trained by the native step.  The
+  reference's Keras closure ``model_fn(generator)(data, mst, purpose)`` cannot
+  run here and raises ``TypeError`` instead of being silently ignored;
+* ``train_fn``: ``None`` / ``native_train_fn`` = the fused HIP step
+  (forward, softmax-CE, backward, Adam).  Any other callable raises
+  ``NotImplementedError`` (the step is a captured HIP graph, not a Python
+  function of a Keras model);
 * ``workers`` / ``backend`` are accepted; the GPUs of the torchrun world are
   the workers; ``preload_data_to_mem`` is always true (HBM-resident);
 * ``mst_eval_fn(mst_state) -> (stop_list, update_list, new_msts)`` is called
@@ -53,6 +61,54 @@ def _is_da(input_fn, data_catalog):
     return bool(root) and os.path.exists(os.path.join(root, MANIFEST))
 
 
+def native_model_fn(mst):
+    """The framework's model factory (the default ``model_fn``)."""
+    return mst["model"]
+
+
+def native_train_fn(*a, **k):
+    """Marker for the native fused train step (the default ``train_fn``)."""
+    raise RuntimeError("native_train_fn is a marker; the engine runs the fused HIP step")
+
+
+native_model_fn._cerebro_native = True
+native_train_fn._cerebro_native = True
+
+
+def _adopt_model_fn(model_fn, msts):
+    """Apply a custom ``model_fn(mst)`` to every MST (see module docstring)."""
+    from .models.common import PackedNet
+    from .models.registry import MODEL_FACTORIES, dataset_of, register_model
+    out = []
+    for mst in msts:
+        try:
+            got = model_fn(mst)
+        except TypeError as e:
+            raise TypeError("schedule(): model_fn must be model_fn(mst) -> architecture name "
+                            "or PackedNet (a Keras model_fn(generator)(data, mst, purpose) "
+                            "closure cannot run on this framework): {}".format(e))
+        m = dict(mst)
+        if isinstance(got, str):
+            if got not in MODEL_FACTORIES:
+                raise ValueError("schedule(): model_fn returned unknown architecture {!r}"
+                                 .format(got))
+            m["model"] = got
+        elif isinstance(got, PackedNet):
+            import hashlib
+            cls = type(got)
+            sig = hashlib.sha1(repr([(s.name, s.shape) for s in got.layout.specs])
+                               .encode()).hexdigest()[:8]
+            name = "custom:{}.{}:{}".format(cls.__module__, cls.__qualname__, sig)
+            ds = getattr(got, "dataset", None) or dataset_of(mst.get("model", ""))
+            register_model(name, lambda mst=dict(mst): model_fn(mst), ds)
+            m["model"] = name
+        else:
+            raise TypeError("schedule(): model_fn returned {!r}; expected an architecture name "
+                            "or a PackedNet".format(type(got).__name__))
+        out.append(m)
+    return out
+
+
 def schedule(data_set_name=None, input_fn=None, model_fn=None, train_fn=None,
              initial_msts=None, mst_eval_fn=None, ckpt_root="", preload_data_to_mem=True,
              log_files_root="", backend="hip", data_catalog=None, workers=None,
@@ -60,9 +116,14 @@ def schedule(data_set_name=None, input_fn=None, model_fn=None, train_fn=None,
     msts = list(initial_msts or [])
     if not msts:
         raise ValueError("schedule() needs initial_msts")
-    for name, fn in (("model_fn", model_fn), ("train_fn", train_fn)):
-        if fn is not None and not getattr(fn, "_cerebro_native", False):
-            logs("schedule(): custom {} ignored; the native packed HIP step is used".format(name))
+    if train_fn is not None and not getattr(train_fn, "_cerebro_native", False):
+        raise NotImplementedError(
+            "schedule(): custom train_fn is not supported; the native fused step (forward, "
+            "softmax-CE, backward, Adam on HIP kernels) trains every config. Pass "
+            "train_fn=None or api.native_train_fn")
+    if model_fn is not None and not getattr(model_fn, "_cerebro_native", False):
+        msts = _adopt_model_fn(model_fn, msts)
+        logs("schedule(): model_fn -> architectures {}".format(sorted({m["model"] for m in msts})))
     ctx = ctx or init_distributed()
     loader = None
     if _is_da(input_fn, data_catalog):

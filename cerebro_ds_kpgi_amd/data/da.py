@@ -265,40 +265,101 @@ def input_fn(file_path, root=None, nthreads=16):
     return out
 
 
-def da_partition_loader(root, device, nthreads=16):
+class NonIntegralPixels(ValueError):
+    """A DA ImageNet partition holds float pixels that are not integers in
+    [0, 255]: storing it as uint8 in HBM would silently change the data."""
+
+
+def da_partition_loader(root, device, nthreads=16, stats=None):
     """Loader for ``PartitionStore``: DA partition -> HBM tensors (uint8
-    images / int32 active-column ids, int32 labels)."""
+    images / int32 active-column ids, int32 labels).
+
+    Buffers are detoasted + pglz-decoded by the C++ thread pool into pinned
+    host memory, then copied to the device and converted buffer by buffer on
+    a side copy stream (the caller's stream only waits at the end).  ImageNet
+    payloads are float32 pixels; they are stored as uint8 only after a
+    device-side check that every value is an integer in [0, 255]
+    (``NonIntegralPixels`` otherwise — never a silent quantisation).
+    ``stats`` (a dict) accumulates ETL timings: ``decode_s`` (C++ reader,
+    wall), ``h2d_s`` (copies + conversion, wall), ``payload_bytes``
+    (decompressed), ``stored_bytes`` (on disk, heap + TOAST) and ``buffers``."""
+    import time
     import torch
     man = load_manifest(root)
+    dev = torch.device(device)
+    cuda = dev.type == "cuda"
+    copy_stream = torch.cuda.Stream(device=dev) if cuda else None
+    st = stats if stats is not None else {}
+    for k in ("decode_s", "h2d_s", "payload_bytes", "stored_bytes", "buffers"):
+        st.setdefault(k, 0)
+
+    def convert(x, dataset):
+        if dataset == "imagenet":
+            q = x.round()
+            bad = ((q != x) | (x < 0) | (x > 255)).any()
+            return q.to(torch.uint8), bad
+        nnz = int((x[0] != 0).sum().item())
+        return torch.nonzero(x, as_tuple=False)[:, 1].view(x.shape[0], nnz).to(torch.int32), None
 
     def load_split(p, split):
         heap = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["relfilenode"]))
         toast = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["toast_relfilenode"]))
         shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
+        for path in (heap, toast):
+            seg = 0
+            f = path
+            while os.path.exists(f):
+                st["stored_bytes"] += os.path.getsize(f)
+                seg += 1
+                f = "{}.{}".format(path, seg)
+        t0 = time.perf_counter()
         r = DirectAccessReader(heap, toast)
-        recs = sorted(r.read(nthreads, pinned=(torch.device(device).type == "cuda")),
-                      key=lambda t: t[1])
+        recs = sorted(r.read(nthreads, pinned=cuda), key=lambda t: t[1])
         r.close()
-        xs, ys = [], []
-        for dk, bid, a, b in recs:
-            sh = shapes[(dk, bid)]
-            a = a if isinstance(a, torch.Tensor) else torch.from_numpy(a)
-            b = b if isinstance(b, torch.Tensor) else torch.from_numpy(b)
-            x = a.view(torch.float32).view(sh["independent_var_shape"]).to(device, non_blocking=True)
-            y = b.view(torch.int16).view(sh["dependent_var_shape"]).to(device, non_blocking=True)
-            xs.append(x)
-            ys.append(y)
-        x = torch.cat(xs)
-        y = torch.cat(ys).argmax(1).to(torch.int32)
-        if man["dataset"] == "imagenet":
-            x = x.round_().clamp_(0, 255).to(torch.uint8)
-        else:  # criteo one-hot -> active column ids
-            nnz = int((x[0] != 0).sum().item())
-            x = torch.nonzero(x, as_tuple=False)[:, 1].view(x.shape[0], nnz).to(torch.int32)
+        t1 = time.perf_counter()
+        st["decode_s"] += t1 - t0
+        xs, ys, bads = [], [], []
+        ctx = torch.cuda.stream(copy_stream) if cuda else _Null()
+        with ctx:
+            for dk, bid, a, b in recs:
+                sh = shapes[(dk, bid)]
+                a = a if isinstance(a, torch.Tensor) else torch.from_numpy(a)
+                b = b if isinstance(b, torch.Tensor) else torch.from_numpy(b)
+                st["payload_bytes"] += a.numel() * a.element_size() + b.numel() * b.element_size()
+                st["buffers"] += 1
+                x = a.view(torch.float32).view(sh["independent_var_shape"]).to(dev, non_blocking=True)
+                y = b.view(torch.int16).view(sh["dependent_var_shape"]).to(dev, non_blocking=True)
+                x, bad = convert(x, man["dataset"])
+                xs.append(x)
+                ys.append(y.argmax(1).to(torch.int32))
+                if bad is not None:
+                    bads.append(bad)
+            x = torch.cat(xs)
+            y = torch.cat(ys)
+            bad = torch.stack(bads).any() if bads else None
+        if cuda:
+            torch.cuda.current_stream(dev).wait_stream(copy_stream)
+            for t in (x, y):
+                t.record_stream(torch.cuda.current_stream(dev))
+        if bad is not None and bool(bad):           # one sync per split
+            raise NonIntegralPixels(
+                "DA partition {} ({}) holds non-integral or out-of-range pixel values; "
+                "the HBM store keeps images as uint8 — re-export integral 0..255 pixels "
+                "(raw images) instead of normalised floats".format(p, split))
+        st["h2d_s"] += time.perf_counter() - t1
         return x, y
 
     def loader(p):
         tx, ty = load_split(p, "train")
         vx, vy = load_split(p, "valid")
         return tx, ty, vx, vy
+    loader.stats = st
     return loader
+
+
+class _Null(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

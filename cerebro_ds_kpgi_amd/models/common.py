@@ -12,7 +12,7 @@ import os
 import torch
 
 from ..ops import nn as P
-from ..runtime.arena import ModelLayout, ParamRef, ParamSpec
+from ..runtime.arena import KerasBias, ModelLayout, ParamRef, ParamSpec
 
 
 class Conv(object):
@@ -50,7 +50,11 @@ class PackedNet(object):
 
     def __init__(self):
         self._specs = []
+        self._keras_extra = {}      # kernel spec name -> KerasBias (runtime.arena)
+        self.keras_order = None     # Keras get_weights() order when it differs from ours
         self.arena = None
+        # runtime.baselines.GradBuckets while DDP trains this net (bucket marks)
+        self.grad_buckets = None
         self.bn_momentum = 0.1
         self.bn_eps = 1e-5
         # BN backward partials in consumer dgrad epilogues (ops.nn.BNLink)
@@ -60,8 +64,14 @@ class PackedNet(object):
         self._specs.append(s)
         return s
 
+    def drop_bias(self, conv, bn):
+        """``conv`` has a bias in the Keras model that we do not store (it
+        feeds ``bn``); serialised blobs still carry it (as zeros)."""
+        name = conv.w.name.rsplit("/", 1)[0] + "/bias"
+        self._keras_extra[conv.w.name] = KerasBias(name, conv.cout, bn.rm.name)
+
     def build_layout(self):
-        self.layout = ModelLayout(self._specs)
+        self.layout = ModelLayout(self._specs, self._keras_extra, self.keras_order)
         return self.layout
 
     def bind(self, arena):
@@ -95,6 +105,17 @@ class PackedNet(object):
                              self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
                              self.bn_eps, self.anchor if anchor else None, join, res_join,
                              link_out and self.bn_links)
+
+    def bucket_mark(self, x, first_spec_above):
+        """Gradient-bucket boundary: in backward, once the gradient reaches
+        here, the gradients of every parameter from ``first_spec_above`` on
+        (arena order = forward order) are final and may be all-reduced while
+        the layers below run their backward."""
+        gb = self.grad_buckets
+        if gb is None or not torch.is_grad_enabled():
+            return x
+        off = first_spec_above.offset
+        return P.grad_mark(x, lambda: gb.ready_from(off))
 
     def dense(self, x, d, relu=False, anchor=False):
         return P.linear(x, self.ref(d.w), self.ref(d.b), relu, self.anchor if anchor else None)

@@ -27,7 +27,7 @@ class PackedConfA(PackedNet):
         self.num_classes = num_classes
         # Keras Dense kernel layout [in, out]: one contiguous row per input column
         self.w1 = self.spec(ParamSpec("dense_1/kernel", (in_dim, 1000), "weight", init="glorot",
-                                      fan_in=in_dim))
+                                      fan_in=in_dim, fmt="keras"))
         self.b1 = self.spec(ParamSpec("dense_1/bias", (1000,), "bias"))
         self.fc2 = Dense(self, "dense_2", 1000, 500)
         self.fc3 = Dense(self, "dense_3", 500, num_classes)
@@ -35,7 +35,9 @@ class PackedConfA(PackedNet):
 
     def forward(self, idx, training):
         x = P.embedding_bag(idx, self.ref(self.w1), self.ref(self.b1), relu=True, anchor=self.anchor)
+        x = self.bucket_mark(x, self.fc2.w)
         x = self.dense(x, self.fc2, relu=True)
+        x = self.bucket_mark(x, self.fc3.w)
         return self.dense(x, self.fc3)
 
 
@@ -53,5 +55,7 @@ class PackedSanity(PackedNet):
 
     def forward(self, x, training):
         x = self.dense(x, self.fc1, relu=True, anchor=True)
+        x = self.bucket_mark(x, self.fc2.w)
         x = self.dense(x, self.fc2, relu=True)
+        x = self.bucket_mark(x, self.fc3.w)
         return self.dense(x, self.fc3)

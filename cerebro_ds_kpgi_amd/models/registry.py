@@ -44,6 +44,17 @@ MODEL_FACTORIES = {
 }
 
 
+_CUSTOM_DATASETS = {}
+
+
+def register_model(name, factory, dataset="imagenet"):
+    """Add an architecture (a ``PackedNet`` factory) under ``name``; used by
+    ``api.schedule`` for user ``model_fn`` callables."""
+    MODEL_FACTORIES[name] = factory
+    _CUSTOM_DATASETS[name] = dataset
+    return name
+
+
 def create_model_from_mst(mst):
     name = mst["model"]
     if name not in MODEL_FACTORIES:
@@ -58,6 +69,8 @@ def pack_key(mst):
 
 
 def dataset_of(model_name):
+    if model_name in _CUSTOM_DATASETS:
+        return _CUSTOM_DATASETS[model_name]
     if model_name == "confA":
         return "criteo"
     if model_name == "sanity":

@@ -14,6 +14,12 @@ its gradient is identically zero; BN momentum/eps follow the reference's
 PyTorch trainer (0.1 / 1e-5).  Trainable parameters: 25 557 032 (= the
 torchvision count); Keras reports 25 583 592 trainable + 53 120 moving
 statistics = 25 636 712, the difference being the 26 560 conv biases.
+Serialised blobs (checkpoints, MA states) are nevertheless in the Keras
+``get_weights()`` layout: HWIO kernels, the dropped biases as zeros right
+after their kernels (a non-zero bias read from a Keras blob folds into the
+BN moving mean), and Keras's layer order, in which a projection block lists
+``..._branch2c, ..._branch1`` kernels before ``bn..._branch2c, bn..._branch1``
+(``runtime.arena.KerasBias``, ``runtime.serialize``).
 
 ResNet-18/34 (hyperopt grid, ``cerebro_gpdb/imagenetcat.py:100-105``) use
 basic blocks with the same stem; 101/152 bottleneck depths [3,4,23,3] /
@@ -63,11 +69,35 @@ class PackedResNet(PackedNet):
                 if bi == 0 and (stride != 1 or cin != cout):
                     blk["cs"] = Conv(self, name + "_branch1", cin, cout, 1, stride, 0)
                     blk["bs"] = BN(self, name.replace("res", "bn") + "_branch1", cout)
+                for c, b in (("c1", "b1"), ("c2", "b2"), ("c3", "b3"), ("cs", "bs")):
+                    if c in blk:
+                        self.drop_bias(blk[c], blk[b])
                 self.blocks.append(blk)
                 cin = cout
         self.feat = cin
         self.fc = Dense(self, "fc1000", cin, num_classes)
+        self.drop_bias(self.conv1, self.bn1)
+        self.keras_order = self._keras_layer_order()
         self.build_layout()
+
+    def _keras_layer_order(self):
+        """Keras lists layers by graph depth: in a projection block the two
+        convs feeding the add (last main-path conv, shortcut conv) come
+        before their two BatchNorms."""
+        def bn(b):
+            return [b.g.name, b.b.name, b.rm.name, b.rv.name]
+        order = [self.conv1.w.name] + bn(self.bn1)
+        last = "c3" if self.bottleneck else "c2"
+        lastb = "b3" if self.bottleneck else "b2"
+        for blk in self.blocks:
+            for c, b in (("c1", "b1"), ("c2", "b2"), ("c3", "b3")):
+                if c in blk and c != last:
+                    order += [blk[c].w.name] + bn(blk[b])
+            if "cs" in blk:
+                order += [blk[last].w.name, blk["cs"].w.name] + bn(blk[lastb]) + bn(blk["bs"])
+            else:
+                order += [blk[last].w.name] + bn(blk[lastb])
+        return order + [self.fc.w.name, self.fc.b.name]
 
     def forward(self, x, training):
         x = self.conv_bn(x, self.conv1, self.bn1, training, anchor=True)
@@ -95,5 +125,9 @@ class PackedResNet(PackedNet):
                 h = self.conv_bn(h, blk["c2"], blk["b2"], training, relu=True, residual=sc,
                                  res_join=rj, link_out=link_blk)
             x = h
+            if bi + 1 < nb:
+                x = self.bucket_mark(x, self.blocks[bi + 1]["c1"].w)
+            else:
+                x = self.bucket_mark(x, self.fc.w)
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

@@ -52,13 +52,18 @@ class PackedVGG16(PackedNet):
                                       act=1, anchor=self.anchor if first else None)
                 first = False
             x = P.maxpool2d(x, 2, 2, 0)
+            nxt = self.convs.index(blk) + 1
+            x = self.bucket_mark(x, self.convs[nxt][0][0].w if nxt < len(self.convs)
+                                 else self.fc1.w)
         B, H, W, GC = x.shape
         G = self.G
         C = GC // G
         # per-config flatten in (h, w, c) order: [B,H,W,G,C] -> [B,G,H,W,C]
         x = x.view(B, H, W, G, C).permute(0, 3, 1, 2, 4).reshape(B, G * H * W * C)
         x = self.dense(x, self.fc1, relu=True)
+        x = self.bucket_mark(x, self.fc2.w)
         x = self.dense(x, self.fc2, relu=True)
+        x = self.bucket_mark(x, self.fc3.w)
         return self.dense(x, self.fc3)
 
 

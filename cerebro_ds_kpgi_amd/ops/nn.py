@@ -743,3 +743,28 @@ class ReluAdd(torch.autograd.Function):
 def relu_add(a, b):
     """relu(a + b) in fp32 with one rounding (BN-free residual join)."""
     return ReluAdd.apply(a, b)
+
+
+class _GradMark(torch.autograd.Function):
+    """Identity whose backward calls ``fn`` first: by then every layer above
+    this point has issued its backward (their parameter gradients are final
+    once the queued weight-gradient kernels are flushed).  Used for the
+    bucketed DDP all-reduce overlapped with backward (runtime.baselines)."""
+
+    @staticmethod
+    def forward(ctx, x, fn):
+        ctx.fn = fn
+        y = x.view_as(x)
+        link = getattr(x, "_cer_bnlink", None)
+        if link is not None:           # keep the BN-link handoff to the consumer conv
+            y._cer_bnlink = link
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ctx.fn()
+        return dy, None
+
+
+def grad_mark(x, fn):
+    return _GradMark.apply(x, fn)

@@ -13,8 +13,13 @@ stamp is older than ``timeout`` and then
    it and the engine resumes from the last sub-epoch checkpoint
    (``runtime/engine.py`` ``--resume``).
 
-Heartbeats go over the store's TCP connection, not RCCL, so a rank wedged
-inside a collective is still detected.
+The stamp carries a *progress* record besides the time: the engine marks
+the start and end of every sub-epoch job (``progress(step, busy)``).  The
+beating thread is independent of the training thread, so a live stamp alone
+proves only that the process runs; a rank that has been inside one job for
+longer than ``stall_timeout`` (e.g. wedged in an RCCL call or a hung kernel)
+is flagged ``STALLED`` and handled like a lost one.  Idle ranks (waiting for
+an assignment) are never flagged as stalled.
 """
 
 import json
@@ -37,10 +42,13 @@ def default_store():
 
 class Heartbeat(object):
     def __init__(self, store, rank, world, interval=1.0, timeout=30.0, logs_root="",
-                 on_failure=None, prefix="cerebro_hb"):
+                 on_failure=None, prefix="cerebro_hb", stall_timeout=None):
         self.store = store
         self.rank, self.world = rank, world
         self.interval, self.timeout = interval, timeout
+        self.stall_timeout = stall_timeout
+        self._prog = [0, False, time.time()]      # step, busy, time of last change
+        self.stalled = []
         self.logs_root = logs_root
         self.on_failure = on_failure or self._die
         self.prefix = prefix
@@ -51,10 +59,15 @@ class Heartbeat(object):
     def _key(self, r):
         return "{}/{}".format(self.prefix, r)
 
-    def beat(self):
-        self.store.set(self._key(self.rank), repr(time.time()))
+    def progress(self, step, busy):
+        """Training thread: a job started (busy=True) or ended (False)."""
+        self._prog = [int(step), bool(busy), time.time()]
 
-    def ages(self):
+    def beat(self):
+        self.store.set(self._key(self.rank), json.dumps([time.time()] + self._prog))
+
+    def records(self):
+        """{rank: (stamp age, busy, seconds since the last progress mark)}."""
         now = time.time()
         out = {}
         for r in range(self.world):
@@ -63,14 +76,29 @@ class Heartbeat(object):
                 if not self.store.check([self._key(r)]):
                     out[r] = None
                     continue
-                out[r] = now - float(self.store.get(self._key(r)).decode())
+                t, _, busy, tp = json.loads(self.store.get(self._key(r)).decode())
+                out[r] = (now - t, busy, now - tp)
             except Exception:
-                out[r] = float("inf")
+                out[r] = (float("inf"), False, 0.0)
         return out
 
+    def ages(self):
+        return {r: (None if v is None else v[0]) for r, v in self.records().items()}
+
     def check(self):
-        """Ranks whose heartbeat is stale (never-started ranks are ignored)."""
-        return sorted(r for r, a in self.ages().items() if a is not None and a > self.timeout)
+        """Ranks whose heartbeat is stale, or that have been inside one job
+        for longer than ``stall_timeout`` (never-started ranks are ignored)."""
+        bad, stalled = [], []
+        for r, v in self.records().items():
+            if v is None:
+                continue
+            if v[0] > self.timeout:
+                bad.append(r)
+            elif self.stall_timeout and v[1] and v[2] > self.stall_timeout:
+                bad.append(r)
+                stalled.append(r)
+        self.stalled = stalled
+        return sorted(bad)
 
     def _beat_loop(self):
         while not self._stop.is_set():
@@ -92,11 +120,16 @@ class Heartbeat(object):
     def _report(self, lost):
         from ..utils.logging import logs
         for r in lost:
-            logs("WORKER {} LOST (no heartbeat for > {:.0f}s)".format(r, self.timeout))
+            if r in self.stalled:
+                logs("WORKER {} STALLED (inside one job for > {:.0f}s)".format(
+                    r, self.stall_timeout))
+            else:
+                logs("WORKER {} LOST (no heartbeat for > {:.0f}s)".format(r, self.timeout))
         if self.logs_root:
             os.makedirs(self.logs_root, exist_ok=True)
             with open(os.path.join(self.logs_root, "failed_workers.json"), "w") as f:
-                json.dump({"lost": lost, "time": time.time(), "timeout": self.timeout}, f)
+                json.dump({"lost": lost, "stalled": list(self.stalled), "time": time.time(),
+                           "timeout": self.timeout, "stall_timeout": self.stall_timeout}, f)
 
     def _die(self, lost):  # pragma: no cover - exercised in multi-process runs
         os._exit(EXIT_WORKER_LOST)

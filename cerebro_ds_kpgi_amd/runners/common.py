@@ -60,6 +60,7 @@ def _opts(args, scheduler, loader):
         dataset=("criteo" if args.criteo else None), store_loader=loader,
         trace=args.trace, resume=args.resume, max_retries=args.max_retries,
         heartbeat=args.heartbeat,
+        stall_timeout=args.stall_timeout,
         ckpt_every=args.ckpt_every or ("subepoch" if args.best_model_run else "epoch"))
 
 

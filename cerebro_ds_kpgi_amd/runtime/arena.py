@@ -30,9 +30,19 @@ ALIGN = 64  # elements: every tensor starts 256-B aligned in fp32, 128-B in bf16
 
 
 class ParamSpec(object):
-    __slots__ = ("name", "shape", "kind", "init", "fan_in", "offset", "numel")
+    """One tensor of one configuration.  ``fmt`` names how our storage order
+    maps to the Keras ``get_weights()`` array of the same tensor:
 
-    def __init__(self, name, shape, kind="weight", init="he", fan_in=None):
+    * ``conv``  ours (cout, kh, kw, cin)  -> Keras HWIO (kh, kw, cin, cout),
+    * ``dense`` ours (cout, cin)          -> Keras (cin, cout),
+    * ``dw``    ours (c, kh, kw)          -> Keras depthwise (kh, kw, c, 1),
+    * ``keras`` already in Keras order (biases, BN vectors, ...).
+
+    ``auto`` picks conv for 4-D weights, dw for 3-D weights, dense for 2-D
+    weights and keras otherwise."""
+    __slots__ = ("name", "shape", "kind", "init", "fan_in", "offset", "numel", "fmt")
+
+    def __init__(self, name, shape, kind="weight", init="he", fan_in=None, fmt="auto"):
         self.name = name
         self.shape = tuple(int(s) for s in shape)
         self.kind = kind          # weight | bias | gamma | beta | running_mean | running_var
@@ -40,10 +50,69 @@ class ParamSpec(object):
         self.fan_in = fan_in
         self.numel = int(np.prod(self.shape))
         self.offset = None
+        if fmt == "auto":
+            nd = len(self.shape)
+            fmt = ({4: "conv", 3: "dw", 2: "dense"}.get(nd, "keras") if kind == "weight"
+                   else "keras")
+        self.fmt = fmt
 
     @property
     def trainable(self):
         return self.kind not in ("running_mean", "running_var")
+
+    # ---- Keras get_weights() order (reference serialize_nd_weights blobs) ----
+    @property
+    def keras_shape(self):
+        s = self.shape
+        if self.fmt == "conv":
+            return (s[1], s[2], s[3], s[0])
+        if self.fmt == "dense":
+            return (s[1], s[0])
+        if self.fmt == "dw":
+            return (s[1], s[2], s[0], 1)
+        return s
+
+    def to_keras(self, flat):
+        """Our flat storage (numpy) -> the Keras-shaped array."""
+        a = np.asarray(flat).reshape(self.shape)
+        if self.fmt == "conv":
+            return np.ascontiguousarray(a.transpose(1, 2, 3, 0))
+        if self.fmt == "dense":
+            return np.ascontiguousarray(a.transpose(1, 0))
+        if self.fmt == "dw":
+            return np.ascontiguousarray(a.transpose(1, 2, 0))[..., None]
+        return a
+
+    def from_keras(self, arr):
+        """Keras-shaped array -> our flat storage order (numpy, 1-D)."""
+        a = np.asarray(arr, np.float32)
+        if tuple(a.shape) != self.keras_shape:
+            raise ValueError("{}: Keras shape {} != {}".format(self.name, a.shape,
+                                                              self.keras_shape))
+        if self.fmt == "conv":
+            a = a.transpose(3, 0, 1, 2)
+        elif self.fmt == "dense":
+            a = a.transpose(1, 0)
+        elif self.fmt == "dw":
+            a = a[..., 0].transpose(2, 0, 1)
+        return np.ascontiguousarray(a).reshape(-1)
+
+
+class KerasBias(object):
+    """A conv bias Keras has and we drop (the conv feeds a training-mode
+    BatchNorm, whose batch-mean subtraction cancels it exactly).  Serialised
+    as zeros; a non-zero bias read from a Keras blob is folded into the BN's
+    moving mean (``fold_into``), which is where Keras accumulated it."""
+    __slots__ = ("name", "shape", "fold_into")
+
+    def __init__(self, name, cout, fold_into):
+        self.name = name
+        self.shape = (int(cout),)
+        self.fold_into = fold_into
+
+    @property
+    def keras_shape(self):
+        return self.shape
 
 
 def _align(n):
@@ -53,7 +122,7 @@ def _align(n):
 class ModelLayout(object):
     """Ordered parameter specs of ONE configuration + their arena offsets."""
 
-    def __init__(self, specs):
+    def __init__(self, specs, keras_extra=None, keras_order=None):
         self.train_specs = [s for s in specs if s.trainable]
         self.buffer_specs = [s for s in specs if not s.trainable]
         off = 0
@@ -67,6 +136,17 @@ class ModelLayout(object):
         self.n_master = off
         self.by_name = {s.name: s for s in specs}
         self.specs = list(specs)
+        # Keras get_weights() entries: our specs (in ``keras_order`` when the
+        # architecture's Keras layer order differs from ours) plus the
+        # dropped conv biases, each right after its kernel
+        order = list(keras_order) if keras_order else [s.name for s in specs]
+        assert sorted(order) == sorted(self.by_name), "keras_order must list every spec once"
+        extra = dict(keras_extra or {})
+        self.keras_entries = []
+        for n in order:
+            self.keras_entries.append(self.by_name[n])
+            if n in extra:
+                self.keras_entries.append(extra[n])
 
     @property
     def num_params(self):
@@ -207,18 +287,17 @@ class Arena(object):
         self.wd[row] = float(wd)
 
     def row_weights_f32(self, row):
-        """Unpadded flat float32 weight blob (serialize_nd_weights order)."""
-        parts = [self.master[row, s.offset:s.offset + s.numel] for s in self.layout.specs]
-        return torch.cat(parts).detach().cpu().numpy().astype(np.float32)
+        """Flat float32 weight blob in the Keras ``serialize_nd_weights``
+        layout (``runtime.serialize.master_to_keras``)."""
+        from .serialize import master_to_keras
+        master = self.master[row].detach().cpu().numpy()
+        return np.concatenate([a.reshape(-1) for a in master_to_keras(self.layout, master)])
 
     def load_row_weights_f32(self, row, blob):
-        blob = np.asarray(blob, dtype=np.float32)
-        off = 0
-        for s in self.layout.specs:
-            self.master[row, s.offset:s.offset + s.numel].copy_(
-                torch.from_numpy(blob[off:off + s.numel]).to(self.device))
-            off += s.numel
-        assert off == blob.size, "weight blob size mismatch: {} vs {}".format(off, blob.size)
+        from .serialize import blob_to_master
+        self.master[row].copy_(torch.from_numpy(blob_to_master(self.layout,
+                                                               np.asarray(blob, np.float32)))
+                               .to(self.device))
         self.sync_work(row)
 
 

@@ -477,14 +477,15 @@ class Coordinator(object):
                 h = self.holder.get(m)
                 by_rank[0 if h is None else h].append(m)
             for r in range(self.world):
-                self._send(r, {"t": "ckpt", "epoch": epoch, "models": by_rank.get(r, [])})
+                self._send(r, {"t": "ckpt", "epoch": epoch, "models": by_rank.get(r, []),
+                               "version": eng.ckpt_version(epoch)})
             acks = 0
             while acks < self.world:
                 ev = self._next_event()
                 if ev["t"] != "ckpt_done":
                     raise RuntimeError("unexpected event at checkpoint: {}".format(ev))
                 acks += 1
-            eng.write_resume(epoch, -1, True, None)
+            eng.write_resume(epoch, -1, True, None, version=eng.ckpt_version(epoch))
 
 
 # ---------------------------------------------------------------------------
@@ -642,7 +643,8 @@ def run_worker(eng, chan, hops):
         if t == "ckpt":
             for grp in eng.groups.values():
                 grp.park_all()
-            eng.checkpoint_all(rec["epoch"], models=rec["models"], holder_ok=True)
+            eng.checkpoint_all(rec["epoch"], models=rec["models"], holder_ok=True,
+                               version=rec.get("version"))
             eng.writer.flush()
             chan.post_event({"t": "ckpt_done", "rank": rank})
             continue
@@ -660,6 +662,7 @@ def _run_batch(eng, chan, hops, rec):
     error = None
     results, trained = [], 0
     t_hop = t_start
+    eng.mark_progress(True)
     try:
         # arrivals: the compute stream waits for a hop only now
         with tr.span("wait_arrival", subepoch=rec["subepoch"]):
@@ -729,6 +732,7 @@ def _run_batch(eng, chan, hops, rec):
         eng._sync()
     if error is None:
         eng.train_images += trained
+    eng.mark_progress(False)
     with tr.span("report", subepoch=rec["subepoch"]):
         chan.post_event({"t": "job_done", "rank": rank, "error": error, "fatal": False,
                          "results": results, "t_start": t_start, "t_hop": t_hop,

@@ -9,10 +9,16 @@
   every epoch, as a MADlib fit transition does.
 * ``DDPEngine`` — synchronous data parallel per config (the reference's
   PyTorch DDP baseline, ``cerebro_gpdb/run_pytorchddp.py:204-519``): each
-  step every GPU computes gradients on its own partition's batch and the flat
-  gradient arena is all-reduced (one bucket per pack group) before the fused
-  Adam step.  Per-rank batch = the MST's batch size (reference default;
-  ``--pytorchddp_sanity`` divides it by the world size).
+  step every GPU computes gradients on its own partition's batch; the flat
+  gradient arena is all-reduced in buckets *during* backward
+  (``GradBuckets``: the models place bucket marks between blocks; when the
+  gradient flows past a mark, the queued weight-gradient kernels of the
+  layers above are flushed and their contiguous arena range is all-reduced
+  asynchronously by RCCL while the layers below run backward), and the fused
+  Adam step waits for the last bucket.  BatchNorm statistics stay per rank,
+  as in the reference (torch DDP without SyncBatchNorm).  Per-rank batch =
+  the MST's batch size (reference default; ``--pytorchddp_sanity`` divides
+  it by the world size).
 * Task parallelism (Hyperopt-Spark, D6) is ``MOPEngine`` with
   ``scheduler="task"``: data replicated on every GPU, whole models per GPU.
 
@@ -121,16 +127,73 @@ class MAEngine(_GroupEngine):
         return time.time() - t0
 
     def _average(self, w, count):
-        """w <- sum_r count_r * w_r / sum_r count_r over ranks (params + BN stats)."""
+        """w <- sum_r count_r * w_r / sum_r count_r over ranks (params + BN
+        stats): the reference's count-weighted merge (``madlib_keras_wrapper.py:
+        63-116``) as two RCCL all-reduces."""
         if not self.ctx.initialized:
             return
         master = w.arena.master
+        if getattr(self, "keep_pre_average", False):
+            self.pre_average = master.detach().clone()
         cnt = torch.tensor([float(count)], device=master.device)
         master.mul_(float(count))
-        dist.all_reduce(master)
+        # one contiguous state row per config ([G, R] rows; the master section
+        # of the whole arena is a strided view, which collectives reject)
+        works = [dist.all_reduce(master[g], async_op=True) for g in range(master.shape[0])]
         dist.all_reduce(cnt)
+        for wk in works:
+            wk.wait()
         master.div_(cnt)
         w.arena.sync_work()
+
+
+class GradBuckets(object):
+    """Bucketed gradient all-reduce overlapped with backward (DDP).
+
+    ``ready_from(lo)`` (called from a model's bucket mark in backward): the
+    gradients of arena columns ``[lo, hi)`` are final — flush the queued
+    weight-gradient kernels, then, once at least ``bucket_bytes`` are pending
+    (per config row), start an asynchronous all-reduce of each config row's
+    ``[lo, hi)`` slice.  RCCL's stream waits for everything issued so far on
+    the compute stream and runs beside the remaining backward.  ``finish()``
+    (before the optimizer) reduces the rest, makes the compute stream wait
+    for every bucket and averages.  Bucket sizes are per-link sized: ring
+    all-reduce over xGMI is bound by one link (~50 GB/s per direction), so
+    25-64 MB buckets keep ~1 ms transfers in flight behind the backward."""
+
+    def __init__(self, arena, world, bucket_bytes=32 << 20, group=None):
+        self.arena = arena
+        self.world = world
+        self.bucket_cols = max(1, bucket_bytes // 4)
+        self.group = group
+        self.hi = arena.layout.n_train
+        self.works = []
+        self.n_buckets = 0
+        self.bucket_log = []           # (lo, hi) per bucket of the last step
+
+    def ready_from(self, lo, force=False):
+        if lo >= self.hi or (not force and self.hi - lo < self.bucket_cols):
+            return
+        from ..ops import streams
+        streams.flush_wgrad()
+        g = self.arena.grad
+        for row in range(g.shape[0]):
+            self.works.append(dist.all_reduce(g[row, lo:self.hi], group=self.group,
+                                              async_op=True))
+        self.bucket_log.append((lo, self.hi))
+        self.n_buckets += 1
+        self.hi = lo
+
+    def finish(self, arena=None):
+        self.ready_from(0, force=True)
+        for w in self.works:
+            w.wait()
+        self.works = []
+        self.arena.grad.div_(self.world)
+        self.hi = self.arena.layout.n_train
+
+    def reset_log(self):
+        self.bucket_log = []
 
 
 class DDPEngine(_GroupEngine):
@@ -139,11 +202,6 @@ class DDPEngine(_GroupEngine):
     def run(self, num_epochs):
         t0 = time.time()
         world = self.ctx.world
-
-        def allreduce_grads(arena):
-            if self.ctx.initialized:
-                dist.all_reduce(arena.grad)
-                arena.grad.div_(world)
         for epoch in range(1, num_epochs + 1):
             self.store.new_epoch(epoch)
             per_model = {}
@@ -153,7 +211,11 @@ class DDPEngine(_GroupEngine):
                 for row, (m, _) in enumerate(jobs):
                     w.load_local(row, m)
                 w.prepare(hop_optimizer_state=True)
-                w.grad_hook = allreduce_grads
+                if self.ctx.initialized and world > 1:
+                    gb = GradBuckets(w.arena, world,
+                                     int(getattr(self.o, "ddp_bucket_mb", 32)) << 20)
+                    w.net.grad_buckets = gb
+                    w.grad_hook = gb.finish
                 B = grp.batch_size
                 steps = self.n_train // B
                 w.train_steps(steps)

@@ -52,8 +52,8 @@ from ..scheduler import make_scheduler
 from ..utils.keys import model_key, mst_2_str
 from ..utils.logging import logs
 from ..utils.trace import Tracer
-from .checkpoint import (AsyncWriter, ckpt_path, dump_infos, host_to_state, read_checkpoint,
-                         state_to_host, write_checkpoint)
+from .checkpoint import (AsyncWriter, HostStager, ckpt_path, dump_infos, host_to_state,
+                         publish_version, read_checkpoint, versioned, write_staged)
 from .group import PackGroup
 
 
@@ -84,6 +84,9 @@ class EngineOptions(object):
         self.max_retries = kw.get("max_retries", 2)
         self.resume = kw.get("resume", False)
         self.heartbeat = kw.get("heartbeat", 0)     # watchdog timeout (s); 0 = off
+        # a rank inside one sub-epoch job for longer than this is STALLED
+        # (0 = off; needs the heartbeat)
+        self.stall_timeout = kw.get("stall_timeout", 0)
         # runtime: "async" (event driven, hops overlapped with compute),
         # "lockstep" (a barrier per sub-epoch) or "auto" (async unless a
         # feature needs lock-step: sub-epoch checkpoints, task parallelism)
@@ -167,6 +170,9 @@ class MOPEngine(object):
                               "valid_top5_error": [], "train_top1_error": [],
                               "valid_top1_error": [], "state": "RUNNING"} for m in range(S)}
         self.writer = AsyncWriter()
+        self.stager = HostStager(self.device)
+        self.hb = None               # parallel.health.Heartbeat (when enabled)
+        self.ckpt_versions = {}      # config -> committed checkpoint version (rank 0)
         self.train_images = 0
         self.round_idx = 0
         self.hop_bytes = 0
@@ -334,6 +340,7 @@ class MOPEngine(object):
         """One sub-epoch; failed (config, partition) pairs are requeued."""
         pending = dict(rnd)
         trained = 0
+        self.mark_progress(True)
         for attempt in range(self.o.max_retries + 1):
             failed, images = self._attempt(pending, epoch, max_steps, attempt)
             trained += images
@@ -344,6 +351,7 @@ class MOPEngine(object):
             raise RuntimeError("sub-epoch {} failed {} times; giving up".format(
                 self.round_idx, self.o.max_retries + 1))
         self.round_idx += 1
+        self.mark_progress(False)
         return trained
 
     def _attempt(self, rnd, epoch, max_steps, attempt):
@@ -457,9 +465,11 @@ class MOPEngine(object):
             st["train_top1_error"].append(1 - a["t1"] / nt)
             st["valid_top1_error"].append(1 - a["v1"] / nv)
 
-    def checkpoint_all(self, epoch, models=None, holder_ok=False):
-        """Queue async checkpoints of the configs parked on this rank
-        (``holder_ok``: the caller already picked this rank's configs)."""
+    def checkpoint_all(self, epoch, models=None, holder_ok=False, version=None):
+        """Queue async checkpoints (files ``{key}@{version}``) of the configs
+        parked on this rank (``holder_ok``: the caller already picked this
+        rank's configs).  The rows are snapshotted on the device and copied
+        to pinned host memory on a side stream; nothing here waits."""
         if not self.o.models_root:
             return
         os.makedirs(self.o.models_root, exist_ok=True)
@@ -471,43 +481,61 @@ class MOPEngine(object):
             if not holder_ok and h != self.ctx.rank:
                 continue
             grp = self.group_of[m]
-            weights, opt = state_to_host(grp.layout, grp.state_row(m))
-            path = ckpt_path(self.o.models_root, m, self.msts[m])
+            staged = self.stager.stage(grp.state_row(m))
+            path = versioned(ckpt_path(self.o.models_root, m, self.msts[m]), version)
             meta = {"epoch": epoch, "subepoch": self.round_idx,
                     "model_key": model_key(m, self.msts[m]),
                     "mst": self.msts[m], "mst_str": mst_2_str(self.msts[m]),
                     "partitions_visited": sorted(
                         j["dist_key"] for j in self.jobs_info.get(epoch, {}).values()
                         if j["model_key"] == model_key(m, self.msts[m]))}
-            self.writer.submit(lambda p=path, w=weights, o=opt, mt=meta, L=grp.layout:
-                               write_checkpoint(p, L, w, o, mt))
+            self.writer.submit(lambda p=path, st=staged, mt=meta, L=grp.layout:
+                               write_staged(p, L, st, mt))
 
-    def _commit(self, epoch, rounds_done, epoch_done, sched_rng):
+    @staticmethod
+    def ckpt_version(epoch, rounds_done=-1):
+        return "e{}".format(epoch) if rounds_done < 0 else "e{}r{}".format(epoch, rounds_done)
+
+    def _commit(self, epoch, rounds_done, epoch_done, sched_rng, models=None):
         """Consistent restart point: every rank's checkpoint writes are on
-        disk before rank 0 publishes ``resume.json`` (atomic rename)."""
+        disk before rank 0 publishes ``resume.json`` (atomic rename) naming
+        them; superseded versions are dropped only after that."""
         if not self.o.models_root:
             return
         with self.tracer.span("checkpoint", epoch=epoch, rounds=rounds_done):
             self.writer.flush()
             self.ctx.barrier()
             if self.ctx.rank == 0:
-                self.write_resume(epoch, rounds_done, epoch_done, sched_rng)
+                self.write_resume(epoch, rounds_done, epoch_done, sched_rng, models=models,
+                                  version=self.ckpt_version(epoch, rounds_done))
 
-    def write_resume(self, epoch, rounds_done, epoch_done, sched_rng):
+    def write_resume(self, epoch, rounds_done, epoch_done, sched_rng, models=None, version=None):
         """Publish ``resume.json`` (atomic rename); every checkpoint it names
-        is on disk already."""
+        is on disk already.  ``models`` (None = all) were just written as
+        ``version``; afterwards their canonical CTQ files point at it."""
         if not self.o.models_root:
             return
+        changed = []
+        if version is not None:
+            ids = range(len(self._bk_msts())) if models is None else models
+            for m in ids:
+                if self.ckpt_versions.get(m) != version:
+                    self.ckpt_versions[m] = version
+                    changed.append(m)
         if self.o.logs_root:
             dump_infos(self.o.logs_root, self.models_info, self.jobs_info)
         st = {"epoch": epoch, "rounds_done": rounds_done, "epoch_done": epoch_done,
               "round_idx": self.round_idx, "msts": self._bk_msts(),
               "states": {str(m): self.mst_state[m]["state"] for m in self.mst_state},
-              "sched_rng": sched_rng, "failures": self.failures}
+              "sched_rng": sched_rng, "failures": self.failures,
+              "versions": {str(m): v for m, v in self.ckpt_versions.items()}}
         path = os.path.join(self.o.models_root, RESUME_FILE)
         with open(path + ".tmp", "w") as f:
             json.dump(st, f, default=str)
         os.replace(path + ".tmp", path)
+        msts = self._bk_msts()
+        for m in changed:
+            publish_version(ckpt_path(self.o.models_root, m, msts[m]), self.ckpt_versions[m])
 
     def _resume(self):
         """Load ``resume.json`` + checkpoints; returns (epoch, rounds_to_skip, rng)."""
@@ -519,10 +547,24 @@ class MOPEngine(object):
             st = json.load(f)
         if len(st["msts"]) > len(self.msts):
             self.add_msts(st["msts"][len(self.msts):])
+        versions = st.get("versions")
+        fresh = []
         for m in range(len(self.msts)):
-            weights, opt, _ = read_checkpoint(ckpt_path(self.o.models_root, m, self.msts[m]))
-            grp = self.group_of[m]
-            host_to_state(grp.layout, weights, opt, grp.state_row(m))
+            path = ckpt_path(self.o.models_root, m, self.msts[m])
+            if versions is not None:
+                v = versions.get(str(m))
+                path = versioned(path, v) if v else None
+                if v:
+                    self.ckpt_versions[m] = v
+            if path is None:
+                # never committed (e.g. more configs than partitions and a
+                # crash before its first round): the deterministic seeded
+                # initial state this engine built is exactly its start state
+                fresh.append(m)
+            else:
+                weights, opt, _ = read_checkpoint(path)
+                grp = self.group_of[m]
+                host_to_state(grp.layout, weights, opt, grp.state_row(m))
             self.holder[m] = None            # every rank now holds the same copy
             self.mst_state[m]["state"] = st["states"].get(str(m), "RUNNING")
         lr = self.o.logs_root
@@ -535,6 +577,9 @@ class MOPEngine(object):
         for e in sorted(self.jobs_info):
             if e < st["epoch"] or st["epoch_done"]:
                 self._epoch_summary(e)
+        if fresh:
+            self.log("RESUME: configs {} had no committed checkpoint: seeded initial state"
+                     .format(fresh))
         self.round_idx = st["round_idx"]
         self.failures = list(st.get("failures", []))
         self.log("RESUME: epoch {} after {} sub-epochs{}".format(
@@ -679,7 +724,7 @@ class MOPEngine(object):
                     if new_msts:
                         self.add_msts(new_msts)
                 if self.o.ckpt_every != "none":
-                    self.checkpoint_all(epoch)
+                    self.checkpoint_all(epoch, version=self.ckpt_version(epoch))
                     self._commit(epoch, -1, True, None)
             self.writer.flush()
         finally:
@@ -694,13 +739,20 @@ class MOPEngine(object):
         store = default_store()
         if store is None:
             return None
-        return Heartbeat(store, self.ctx.rank, self.ctx.world, timeout=self.o.heartbeat,
-                         logs_root=self.o.logs_root).start()
+        self.hb = Heartbeat(store, self.ctx.rank, self.ctx.world, timeout=self.o.heartbeat,
+                            logs_root=self.o.logs_root,
+                            stall_timeout=getattr(self.o, "stall_timeout", 0) or None).start()
+        return self.hb
+
+    def mark_progress(self, busy):
+        if self.hb is not None:
+            self.hb.progress(self.round_idx, busy)
 
     def _after_round(self, epoch, rnd, rounds_done, rng):
         if self.o.ckpt_every == "subepoch":
-            self.checkpoint_all(epoch, models=sorted(set(rnd.values())))
-            self._commit(epoch, rounds_done, False, rng)
+            models = sorted(set(rnd.values()))
+            self.checkpoint_all(epoch, models=models, version=self.ckpt_version(epoch, rounds_done))
+            self._commit(epoch, rounds_done, False, rng, models=models)
 
     def _run_task_epoch(self, epoch, active, max_steps=None, skip=0, rng=None):
         """Task parallel: models are pinned to ranks round-robin; in round r
@@ -794,6 +846,7 @@ class MOPEngine(object):
 
     def close(self):
         self.writer.close()
+        self.stager.clear()
         # release captured HIP graphs deterministically (device drained first)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)

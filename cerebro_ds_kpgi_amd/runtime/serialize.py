@@ -12,9 +12,14 @@ Byte-compatible with the reference's MADlib wrapper formats
 * ``deserialize_as_nd_weights(blob, shapes)`` -> list of arrays.
 
 ``arena_to_nd_weights`` / ``nd_weights_to_arena`` move one configuration's
-row of a packed arena to and from that list, in the layout's spec order
-(which is the Keras ``get_weights()`` order of the architecture), so blobs
-interoperate with ``runtime.checkpoint`` files and with MA merging.
+row of a packed arena to and from that list in the Keras ``get_weights()``
+layout (``master_to_keras`` / ``keras_to_master``): HWIO conv kernels,
+(in, out) dense kernels, (kh, kw, c, 1) depthwise kernels, the architecture's
+Keras layer order and the conv biases Keras has and we drop (zeros), so
+blobs interoperate with ``runtime.checkpoint`` files, with MA merging and
+with a Keras model of the same architecture.  The layer order of
+``keras.applications`` ResNet-50 is pinned by hand (there is no TF here to
+check it against: parity unpinned beyond the element count).
 """
 
 import numpy as np
@@ -67,26 +72,68 @@ def deserialize_as_nd_weights(blob, model_shapes):
 
 
 def model_shapes(layout):
-    return [tuple(s.shape) for s in layout.specs]
+    """Keras ``get_weights()`` shapes of one configuration (blob order)."""
+    return [tuple(e.keras_shape) for e in layout.keras_entries]
+
+
+def master_to_keras(layout, master):
+    """One configuration's master section (flat numpy, our storage order:
+    trainable params then BN statistics) -> the list of Keras arrays
+    (``get_weights()`` order and shapes; dropped conv biases as zeros)."""
+    from .arena import KerasBias
+    out = []
+    for e in layout.keras_entries:
+        if isinstance(e, KerasBias):
+            out.append(np.zeros(e.shape, np.float32))
+        else:
+            out.append(e.to_keras(master[e.offset:e.offset + e.numel]).astype(np.float32))
+    return out
+
+
+def keras_to_master(layout, weights):
+    """Inverse of ``master_to_keras``: a flat numpy master section.  A
+    non-zero dropped bias is folded into its BatchNorm's moving mean (Keras
+    accumulated the biased conv output there; our conv output lacks it)."""
+    from .arena import KerasBias
+    ents = layout.keras_entries
+    if len(weights) != len(ents):
+        raise ValueError("expected {} arrays, got {}".format(len(ents), len(weights)))
+    out = np.zeros(layout.n_master, np.float32)
+    folds = []
+    for e, w in zip(ents, weights):
+        if isinstance(e, KerasBias):
+            w = np.asarray(w, np.float32)
+            if tuple(w.shape) != e.shape:
+                raise ValueError("{}: shape {} != {}".format(e.name, w.shape, e.shape))
+            if np.any(w):
+                folds.append((e.fold_into, w))
+            continue
+        out[e.offset:e.offset + e.numel] = e.from_keras(w)
+    for name, b in folds:
+        s = layout.by_name[name]
+        out[s.offset:s.offset + s.numel] -= b
+    return out
+
+
+def weights_blob(layout, master):
+    """``serialize_nd_weights`` blob of one master section (numpy)."""
+    return serialize_nd_weights(master_to_keras(layout, master))
+
+
+def blob_to_master(layout, blob):
+    if isinstance(blob, np.ndarray):
+        blob = blob.astype("<f4").tobytes()
+    return keras_to_master(layout, deserialize_as_nd_weights(blob, model_shapes(layout)))
 
 
 def arena_to_nd_weights(arena, row):
-    """One configuration's weights (trainable + BN statistics) as a list of
-    arrays in spec order."""
-    master = arena.state[row].detach().to("cpu")
-    return [master[s.offset:s.offset + s.numel].numpy().reshape(s.shape).copy()
-            for s in arena.layout.specs]
+    """One configuration's weights (trainable + BN statistics) as the list
+    of Keras arrays."""
+    master = arena.state[row, :arena.layout.n_master].detach().to("cpu").numpy()
+    return master_to_keras(arena.layout, master)
 
 
 def nd_weights_to_arena(arena, row, weights):
-    specs = arena.layout.specs
-    if len(weights) != len(specs):
-        raise ValueError("expected {} arrays, got {}".format(len(specs), len(weights)))
-    out = torch.zeros(arena.layout.n_master, dtype=torch.float32)
-    for s, w in zip(specs, weights):
-        w = np.asarray(w, np.float32)
-        if tuple(w.shape) != tuple(s.shape):
-            raise ValueError("{}: shape {} != {}".format(s.name, w.shape, s.shape))
-        out[s.offset:s.offset + s.numel] = torch.from_numpy(w.reshape(-1))
+    out = torch.from_numpy(keras_to_master(arena.layout, weights))
     arena.state[row, :arena.layout.n_master].copy_(out.to(arena.state.device))
     arena.sync_work(row)

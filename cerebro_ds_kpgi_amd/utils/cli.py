@@ -96,6 +96,9 @@ def get_main_parser():
                    help="requeues of a (config, partition) pair after a recoverable failure")
     p.add_argument("--heartbeat", type=float, default=0.0,
                    help="watchdog timeout in seconds for worker heartbeats (0 = off)")
+    p.add_argument("--stall_timeout", type=float, default=0.0,
+                   help="flag a rank that stays inside one sub-epoch job longer than this "
+                        "many seconds (hung collective / kernel; 0 = off)")
     p.add_argument("--trace", action="store_true",
                    help="write chrome-trace spans (logs_root/traces) and 1 Hz system telemetry")
     p.add_argument("--da", action="store_true", help="read partitions through the Direct-Access page reader")

@@ -165,3 +165,32 @@ def test_da_export_to_filesystem(tmp_path):
     tx, ty, vx, vy = fs.fs_partition_loader(out, "imagenet", "cpu")(1)
     dx, dy, _, _ = da.da_partition_loader(root, "cpu")(1)
     assert np.array_equal(tx.numpy(), dx.numpy()) and np.array_equal(ty.numpy(), dy.numpy())
+
+
+def test_loader_refuses_normalised_float_pixels(tmp_path):
+    """uint8 HBM storage only for integral 0..255 pixels: a partition of
+    normalised floats raises instead of being quantised; ETL stats count."""
+    root = str(tmp_path / "gp")
+    man = da.write_dataset(root, "imagenet", 2, n_train=6, n_valid=3, buffer_size=4)
+    rng = np.random.default_rng(0)
+    bufs = []
+    for bid, (s0, e) in enumerate([(0, 4), (4, 6)]):
+        x = rng.random((e - s0, 112, 112, 3), dtype=np.float32)      # [0, 1) floats
+        y = np.zeros((e - s0, 1000), np.int16)
+        y[:, 3] = 1
+        bufs.append((bid, x, y))
+    d = da.seg_dir(root, 1, man["dboid"])
+    for f in os.listdir(d):
+        if f.startswith(str(da.TRAIN_RELFILENODE)) or f.startswith(str(da.TRAIN_TOAST)):
+            os.remove(os.path.join(d, f))
+    da.write_partition(os.path.join(d, str(da.TRAIN_RELFILENODE)),
+                       os.path.join(d, str(da.TRAIN_TOAST)), bufs, 1,
+                       toastrelid=da.TRAIN_TOAST, first_valueid=2 << 20)
+    stats = {}
+    loader = da.da_partition_loader(root, "cpu", stats=stats)
+    tx, ty, vx, vy = loader(0)
+    assert tx.dtype == __import__("torch").uint8 and tx.shape[0] == 6
+    assert stats["buffers"] == 3 and stats["payload_bytes"] > 6 * 112 * 112 * 3 * 4
+    assert stats["stored_bytes"] > 0 and stats["decode_s"] > 0
+    with pytest.raises(da.NonIntegralPixels):
+        loader(1)

@@ -12,6 +12,7 @@ import json
 import os
 import time
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
@@ -113,6 +114,67 @@ def test_crash_then_resume_matches_uninterrupted(tmp_path, scheduler, monkeypatc
     eng2.close()
 
 
+@pytest.mark.parametrize("crash_round", [1, 3])
+def test_resume_more_configs_than_partitions(tmp_path, monkeypatch, crash_round):
+    """S=4 configs on P=2 partitions: a crash in epoch 1 leaves configs that
+    never trained (no committed checkpoint); resume starts them from their
+    seeded initial state and ends bit-identical to an uninterrupted run."""
+    monkeypatch.setenv("CEREBRO_BACKEND", "torch")
+    monkeypatch.setenv("CEREBRO_QUIET", "1")
+    torch.set_num_threads(2)
+    ref = _engine(str(tmp_path / "ref"), "rotation", ckpt_every="none", runtime="lockstep",
+                  slots_per_gpu=2)
+    ref.run(1)
+    want = _states(ref)
+    ref.close()
+    d = str(tmp_path / "run")
+    eng = _engine(d, "rotation", ckpt_every="subepoch", slots_per_gpu=2,
+                  fault_inject="0:{}".format(crash_round))
+    with pytest.raises(RuntimeError, match="FAULT INJECTED"):
+        eng.run(1)
+    eng.close()
+    with open(os.path.join(d, "models", "resume.json")) as f:
+        st = json.load(f)
+    assert st["rounds_done"] == crash_round
+    if crash_round == 1:
+        assert len(st["versions"]) == 2          # half the configs never trained
+    eng2 = _engine(d, "rotation", ckpt_every="subepoch", slots_per_gpu=2, resume=True)
+    eng2.run(1)
+    got = _states(eng2)
+    for m in want:
+        assert torch.equal(got[m], want[m]), m
+    eng2.close()
+
+
+def test_interrupted_commit_keeps_previous_restart_point(tmp_path, monkeypatch):
+    """Files of a commit that never published resume.json are ignored: the
+    restart point stays the last complete commit, and publishing re-points
+    the canonical CTQ files and deletes superseded versions."""
+    from cerebro_ds_kpgi_amd.runtime.checkpoint import ckpt_path, read_checkpoint
+    monkeypatch.setenv("CEREBRO_BACKEND", "torch")
+    monkeypatch.setenv("CEREBRO_QUIET", "1")
+    d = str(tmp_path)
+    eng = _engine(d, "rotation", ckpt_every="epoch")
+    eng.run(1)
+    root = os.path.join(d, "models")
+    p0 = ckpt_path(root, 0, eng.msts[0])
+    w_committed = read_checkpoint(p0)[0].copy()
+    assert os.path.exists(p0 + "@e1") and os.path.samefile(p0, p0 + "@e1")
+    # a half-finished next commit: garbage weights under a newer version
+    with open(p0 + "@e2", "wb") as f:
+        f.write(np.full(w_committed.size, 7.0, "<f4").tobytes())
+    eng.close()
+    eng2 = _engine(d, "rotation", ckpt_every="epoch", resume=True)
+    assert eng2._resume()[0] == 2
+    grp = eng2.group_of[0]
+    np.testing.assert_array_equal(grp.home.row_weights_f32(grp.home_row[0]), w_committed)
+    eng2.run(2)
+    assert not os.path.exists(p0 + "@e1")
+    assert os.path.samefile(p0, p0 + "@e2") and os.path.exists(p0 + "@e2.json")
+    assert not np.all(read_checkpoint(p0)[0] == 7.0)
+    eng2.close()
+
+
 def test_epoch_resume_skips_finished_epochs(tmp_path, monkeypatch):
     monkeypatch.setenv("CEREBRO_BACKEND", "torch")
     monkeypatch.setenv("CEREBRO_QUIET", "1")
@@ -147,6 +209,32 @@ def test_heartbeat_watchdog_flags_silent_rank(tmp_path):
     assert seen == [[1]]
     with open(os.path.join(str(tmp_path), "failed_workers.json")) as f:
         assert json.load(f)["lost"] == [1]
+
+
+def test_watchdog_flags_rank_stalled_inside_a_job(tmp_path):
+    """The beating thread keeps stamping while the training thread hangs:
+    the progress record, not the stamp, reveals the stall; an idle rank is
+    not flagged."""
+    from cerebro_ds_kpgi_amd.parallel.health import Heartbeat
+    store = torch.distributed.HashStore()
+    seen = []
+    w0 = Heartbeat(store, 0, 3, interval=0.05, timeout=5.0, logs_root=str(tmp_path),
+                   on_failure=seen.append, stall_timeout=0.4)
+    w1 = Heartbeat(store, 1, 3, interval=0.05, timeout=5.0)
+    w2 = Heartbeat(store, 2, 3, interval=0.05, timeout=5.0)
+    for w in (w1, w2, w0):
+        w.start()
+    w1.progress(3, busy=True)              # rank 1 enters a job and never leaves
+    w2.progress(3, busy=False)             # rank 2 waits idle for work
+    deadline = time.time() + 5
+    while not seen and time.time() < deadline:
+        w0.progress(int(time.time() * 100), busy=True)    # rank 0 keeps making progress
+        time.sleep(0.05)
+    for w in (w0, w1, w2):
+        w.stop()
+    assert seen == [[1]]
+    with open(os.path.join(str(tmp_path), "failed_workers.json")) as f:
+        assert json.load(f)["stalled"] == [1]
 
 
 @pytest.mark.parametrize("runtime", ["lockstep", "async"])

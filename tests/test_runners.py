@@ -41,6 +41,33 @@ def test_schedule_facade_grid_search(tmp_path):
     assert all(len(s["train_loss"]) == 2 and s["state"] == "COMPLETED" for s in state.values())
 
 
+def test_schedule_custom_model_fn_and_train_fn(tmp_path):
+    """A custom model_fn(mst) -> PackedNet is registered and trained; a
+    Keras-style closure or a custom train_fn fails loudly."""
+    from cerebro_ds_kpgi_amd.api import schedule
+    from cerebro_ds_kpgi_amd.models.small import PackedTinyCNN
+    from cerebro_ds_kpgi_amd.selection.hyperopt_helper import mst_eval_fn
+
+    class Wide(PackedTinyCNN):
+        pass
+
+    built = []
+
+    def model_fn(mst):
+        built.append(mst["learning_rate"])
+        return Wide()
+    kw = dict(data_set_name="tiny", initial_msts=_tiny(2), mst_eval_fn=mst_eval_fn(1),
+              ctx=_ctx(), n_train=32, n_valid=16, compute_dtype="fp32", verbose=False,
+              slots_per_gpu=2)
+    state = schedule(model_fn=model_fn, **kw)
+    assert len(built) >= 2 and all(len(s["train_loss"]) == 1 for s in state.values())
+    with pytest.raises(NotImplementedError):
+        schedule(train_fn=lambda *a: None, **kw)
+    with pytest.raises(TypeError):
+        schedule(model_fn=lambda generator: (lambda data, mst, purpose: None), **dict(
+            kw, initial_msts=[dict(m, model=None) for m in _tiny(1)]))
+
+
 def test_async_tpe_over_mop():
     """Cerebro-hyperopt contract: configs finishing their epochs report to TPE
     and new configs join the running MOP until max_num_config."""
