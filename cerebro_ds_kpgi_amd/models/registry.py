@@ -17,7 +17,7 @@ from .nasnet import PackedNASNetMobile
 from .resnet import PackedResNet
 from .small import PackedMobileNetV2, PackedTinyCNN
 from .tf1zoo import PackedDenseNetTF1, PackedSqueezeNet
-from .vgg import PackedVGG16, PackedVGG19
+from .vgg import PackedVGG16, PackedVGG16Flat, PackedVGG16Torchvision, PackedVGG19
 from .zoo import PackedDenseNet, PackedMobileNetV1, PackedResNeXt, PackedResNet50NoBN
 
 MODEL_FACTORIES = {
@@ -30,6 +30,8 @@ MODEL_FACTORIES = {
     "resnext101": lambda: PackedResNeXt(101),
     "vgg16": lambda: PackedVGG16(),
     "vgg19": lambda: PackedVGG19(),
+    "vgg16_flat": lambda: PackedVGG16Flat(),
+    "vgg16_torchvision": lambda: PackedVGG16Torchvision(),
     "inceptionresnetv2": lambda: PackedVGG19(),
     "densenet121": lambda: PackedDenseNet(121),
     "densenet201": lambda: PackedDenseNet(201),
@@ -53,6 +55,11 @@ def register_model(name, factory, dataset="imagenet"):
     MODEL_FACTORIES[name] = factory
     _CUSTOM_DATASETS[name] = dataset
     return name
+
+
+# PyTorch-DDP baseline (reference run_pytorchddp.py:295-307): its "vgg16" is
+# torchvision's; its resnet50 (no conv biases) and confA are ours exactly
+TORCH_MODEL_NAMES = {"vgg16": "vgg16_torchvision"}
 
 
 def create_model_from_mst(mst):

@@ -9,6 +9,9 @@ DA-Cerebro / Cerebro standalone     MOP, greedy randomized scheduler
                                     (``--da`` reads Greenplum-format pages)
 UDAF (``madlib_keras_fit_multiple``) MOP, lock-step rotation scheduler
 CTQ                                 MOP, greedy scheduler (seeded shuffle)
+CTQ-Hyperopt                        TPE batches of ``--concurrency`` configs, one
+                                    fresh greedy-MOP session per batch
+                                    (``run_batched_hyperopt``)
 MA (``madlib_keras_fit``)           ``MAEngine`` (RCCL weighted averaging)
 PyTorch DDP / DA-DDP                ``DDPEngine`` (RCCL gradient all-reduce)
 Hyperopt-Spark                      MOP ``task`` scheduler + TPE batches
@@ -64,6 +67,62 @@ def _opts(args, scheduler, loader):
         ckpt_every=args.ckpt_every or ("subepoch" if args.best_model_run else "epoch"))
 
 
+class _BatchedRun(object):
+    """What ``run_approach`` reports for a batched TPE run."""
+
+    def __init__(self, msts, mst_state, images, etl):
+        self.msts, self.mst_state, self.train_images = msts, mst_state, images
+        self.data_load_time = etl
+
+
+def run_batched_hyperopt(args, ctx, loader, param_grid=None, engine_kw=None):
+    """CTQ-Hyperopt (reference ``run_ctq_hyperopt.py:122-160``): TPE proposes
+    ``concurrency`` configs, ONE greedy MOP session trains that batch for
+    ``num_epochs``, every config's last validation loss goes back to TPE
+    (by its own trial id), repeat until ``max_num_config`` trials exist.
+    Per-batch model/job logs: ``{logs_root}/models_info_grand.pkl`` /
+    ``jobs_info_grand.pkl`` ({batch: ...}) as in the reference."""
+    import pickle
+    import argparse
+    conc = args.concurrency or args.size or ctx.world
+    grid = param_grid or hh.param_grid_hyperopt
+    hp, msts, trials, domain, rand, _ = hh.init_hyperopt(grid, argparse.Namespace(size=conc))
+    start, end = 0, len(msts)
+    all_state, images, etl = {}, 0, 0.0
+    models_grand, jobs_grand = {}, {}
+    batch = 0
+    while True:
+        logs("STARTING BATCH:{}, FINISHED:{}".format(batch, start))
+        opts = _opts(args, "greedy", loader)
+        for k, v in (engine_kw or {}).items():
+            setattr(opts, k, v)
+        eng = MOPEngine(msts[start:end], ctx, opts)
+        etl += getattr(eng, "data_load_time", 0.0)
+        eng.run(args.num_epochs, mst_eval_fn=hh.mst_eval_fn(args.num_epochs))
+        losses = [eng.mst_state[i]["valid_loss"][-1] for i in range(end - start)]
+        hh.report_batch(trials, hp, start, end, losses)
+        for i in range(end - start):
+            all_state[start + i] = eng.mst_state[i]
+        images += eng.train_images
+        models_grand[batch] = dict(eng.models_info)
+        jobs_grand[batch] = dict(eng.jobs_info)
+        eng.close()
+        if ctx.rank == 0 and args.logs_root:
+            os.makedirs(args.logs_root, exist_ok=True)
+            with open(os.path.join(args.logs_root, "models_info_grand.pkl"), "wb") as f:
+                pickle.dump(models_grand, f)
+            with open(os.path.join(args.logs_root, "jobs_info_grand.pkl"), "wb") as f:
+                pickle.dump(jobs_grand, f)
+        logs("ENDING BATCH:{}, FINISHED:{}".format(batch, end))
+        batch += 1
+        if len(hp) >= args.max_num_config:
+            break
+        n = min(conc, args.max_num_config - len(hp))
+        hp, msts, start, end = hh.hyperopt_add_one_batch_configs(
+            None, hp, msts, domain, trials, n, rand=rand)
+    return _BatchedRun(msts, all_state, images, etl)
+
+
 def run_approach(approach, argv=None, shuffle=True):
     args, msts = main_prepare(argv, shuffle=shuffle, verbose=True)
     if not args.run:
@@ -83,13 +142,19 @@ def run_approach(approach, argv=None, shuffle=True):
         mon = SysMonitor(os.path.join(args.logs_root, "sys_logs")).start()
     loader = _loader(args, ctx.device)
     tpe_state = None
-    if args.hyperopt and approach not in ("ma", "ddp"):
+    if approach == "ctq_hyperopt":
+        eng = run_batched_hyperopt(args, ctx, loader)
+    elif args.hyperopt and approach not in ("ma", "ddp"):
         # initial batch proposed by TPE (model ids == trial order)
         tpe_state = hh.init_hyperopt(args=args)
         msts = tpe_state[1]
-    if approach in ("ma",):
+    if approach == "ctq_hyperopt":
+        pass
+    elif approach in ("ma",):
         eng = MAEngine(msts, ctx, _opts(args, "rotation", loader))
     elif approach in ("ddp",):
+        from ..models.registry import TORCH_MODEL_NAMES
+        msts = [dict(m, model=TORCH_MODEL_NAMES.get(m["model"], m["model"])) for m in msts]
         eng = DDPEngine(msts, ctx, _opts(args, "rotation", loader))
     else:
         sched = {"udaf": "rotation", "ctq": "greedy", "cerebro": args.scheduler,
@@ -97,7 +162,9 @@ def run_approach(approach, argv=None, shuffle=True):
         eng = MOPEngine(msts, ctx, _opts(args, sched, loader))
     etl = getattr(eng, "data_load_time", 0.0)
     mst_eval = None
-    if isinstance(eng, MOPEngine):
+    if approach == "ctq_hyperopt":
+        pass
+    elif isinstance(eng, MOPEngine):
         if tpe_state is not None:
             hp, _, trials, domain, rand, _ = tpe_state
             mst_eval = hh.mst_eval_fn_hyperopt(args.num_epochs, hp, trials, domain,

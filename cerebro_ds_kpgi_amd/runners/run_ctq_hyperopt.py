@@ -1,4 +1,5 @@
-"""CTQ-Hyperopt (reference run_ctq_hyperopt.py)."""
+"""CTQ-Hyperopt (reference run_ctq_hyperopt.py): batched TPE, one greedy
+MOP session per batch of ``--concurrency`` configs."""
 
 import sys
 
@@ -6,7 +7,7 @@ from .common import run_approach
 
 
 def main(argv=None):
-    return run_approach("ctq", argv, shuffle=False)
+    return run_approach("ctq_hyperopt", argv, shuffle=False)
 
 
 if __name__ == "__main__":

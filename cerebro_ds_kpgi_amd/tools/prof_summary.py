@@ -58,12 +58,7 @@ def _rows(con, last_steps):
     return sorted(rows, key=lambda r: -r[2])
 
 
-def summarize(path, steps=None, title=None, last_steps=None):
-    con = sqlite3.connect(find_db(path))
-    rows = _rows(con, last_steps)
-    if last_steps:
-        steps = last_steps
-    total = sum(r[2] for r in rows)
+def _families(rows):
     fam = {}
     for name, calls, dur, avg in rows:
         key = "other"
@@ -74,6 +69,23 @@ def summarize(path, steps=None, title=None, last_steps=None):
         f = fam.setdefault(key, [0, 0.0])
         f[0] += calls
         f[1] += dur
+    return fam
+
+
+def family_ms(path, last_steps):
+    """{family: ms per step} over the last ``last_steps`` steps."""
+    con = sqlite3.connect(find_db(path))
+    fam = _families(_rows(con, last_steps))
+    return {k: v[1] / 1000.0 / last_steps for k, v in fam.items()}
+
+
+def summarize(path, steps=None, title=None, last_steps=None, roofline=None):
+    con = sqlite3.connect(find_db(path))
+    rows = _rows(con, last_steps)
+    if last_steps:
+        steps = last_steps
+    total = sum(r[2] for r in rows)
+    fam = _families(rows)
     out = []
     out.append("# {}".format(title or "rocprofv3 kernel summary"))
     out.append("")
@@ -97,7 +109,13 @@ def summarize(path, steps=None, title=None, last_steps=None):
         short = name if len(name) < 90 else name[:87] + "..."
         out.append("| `{}` | {} | {:.2f} | {:.1f} | {:.1f}% |".format(
             short.replace("|", "\\|"), calls, dur / 1000.0, avg, 100.0 * dur / total))
-    return "\n".join(out) + "\n"
+    text = "\n".join(out) + "\n"
+    if roofline and steps:
+        from .roofline import roofline_md
+        arch, configs, batch, dtype = roofline
+        text += "\n" + roofline_md({k: v[1] / 1000.0 / steps for k, v in fam.items()},
+                                   arch, configs, batch, dtype)
+    return text
 
 
 if __name__ == "__main__":
@@ -107,5 +125,11 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--last-steps", type=int, default=None)
     ap.add_argument("--title", default=None)
+    ap.add_argument("--roofline", default=None,
+                    help="arch,configs,batch,dtype (e.g. resnet50,8,32,fp32): append a roofline")
     a = ap.parse_args()
-    sys.stdout.write(summarize(a.path, a.steps, a.title, a.last_steps))
+    rl = None
+    if a.roofline:
+        arch, c, b, dt = a.roofline.split(",")
+        rl = (arch, int(c), int(b), dt)
+    sys.stdout.write(summarize(a.path, a.steps, a.title, a.last_steps, rl))

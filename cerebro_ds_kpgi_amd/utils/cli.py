@@ -38,6 +38,8 @@ def get_main_parser():
     p.add_argument("--load", action="store_true")
     p.add_argument("--db_name", type=str, default="cerebro")
     p.add_argument("--size", type=int, default=8)
+    p.add_argument("--concurrency", type=int, default=0,
+                   help="CTQ-Hyperopt: configs per TPE batch (default: --size)")
     p.add_argument("--num_epochs", type=int, default=10)
     p.add_argument("--drill_down_hetro", action="store_true")
     p.add_argument("--drill_down_model_size", action="store_true")

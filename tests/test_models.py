@@ -16,6 +16,8 @@ COUNTS = {
     "resnet18": (11689512, 9600),
     "vgg16": (54471464, 0),               # 14 714 688 conv + 39 756 776 dense (flatten 4608)
     "vgg19": (59781160, 0),
+    "vgg16_flat": (69151528, 0),          # vgg16tfk.py: SAME pools -> flatten 4x4x512
+    "vgg16_torchvision": (138357544, 0),  # torchvision.models.vgg16 (DDP baseline)
     "inceptionresnetv2": (59781160, 0),   # the reference's name for VGG19
     "mobilenetv1": (4231976, 21888),
     "mobilenetv2": (3504872, 34112),
@@ -42,7 +44,7 @@ def test_parameter_counts(name):
 
 @pytest.mark.parametrize("name", ["vgg19", "mobilenetv1", "densenet121", "resnext101",
                                   "resnet50_nobn", "nasnetmobile", "squeezenet",
-                                  "densenet_tf1"])
+                                  "densenet_tf1", "vgg16_flat", "vgg16_torchvision"])
 def test_packed_forward_backward(name):
     from cerebro_ds_kpgi_amd.models import create_model_from_mst
     from cerebro_ds_kpgi_amd.ops import set_backend

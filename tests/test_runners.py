@@ -89,6 +89,33 @@ def test_async_tpe_over_mop():
     assert len(trials.completed()) == 6
 
 
+def test_ctq_hyperopt_batches(tmp_path):
+    """CTQ-Hyperopt: batches of `concurrency` configs, one MOP session each,
+    every trial reported before the next batch is proposed."""
+    import argparse
+    import pickle
+    from cerebro_ds_kpgi_amd.runners.common import run_batched_hyperopt
+    grid = {"learning_rate": [1e-4, 1e-1], "lambda_value": [1e-4], "batch_size": [8, 8],
+            "model": ["tinycnn"]}
+    args = argparse.Namespace(concurrency=2, size=2, max_num_config=5, num_epochs=1,
+                              logs_root=str(tmp_path), criteo=False)
+    ctx = _ctx()
+    import cerebro_ds_kpgi_amd.runners.common as C
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions
+    orig = C._opts
+    C._opts = lambda a, sched, loader: EngineOptions(
+        scheduler=sched, n_train=32, n_valid=16, compute_dtype="fp32", verbose=False,
+        ckpt_every="none", slots_per_gpu=2)
+    try:
+        run = run_batched_hyperopt(args, ctx, None, param_grid=grid)
+    finally:
+        C._opts = orig
+    assert len(run.msts) == 5 and len(run.mst_state) == 5
+    assert all(len(s["valid_loss"]) == 1 for s in run.mst_state.values())
+    with open(os.path.join(str(tmp_path), "models_info_grand.pkl"), "rb") as f:
+        assert sorted(pickle.load(f)) == [0, 1, 2]          # batches of 2, 2, 1
+
+
 @pytest.mark.parametrize("engine", ["ma", "ddp", "task"])
 def test_baseline_engines_train(engine):
     from cerebro_ds_kpgi_amd.runtime.baselines import DDPEngine, MAEngine
