@@ -52,6 +52,10 @@ def main():
                     help="headline = BASELINE.json's metric; criteo16 / hetero8 = the other "
                          "BASELINE configs (16-config Criteo confA grid; {ResNet-50, VGG-16} x "
                          "{lr, batch}), reported as diag_* metrics")
+    ap.add_argument("--da", action="store_true",
+                    help="diagnostic: write the synthetic partitions as Greenplum-format DA "
+                         "pages first (untimed) and load them through the C++ page / TOAST / "
+                         "pglz reader; the ETL is reported separately (etl_da)")
     ap.add_argument("--configs", type=int, default=0,
                     help="diagnostic: train only the first K configs (per-GPU work of N = 8/K "
                          "GPUs); the headline number always uses all 8")
@@ -88,10 +92,24 @@ def main():
     B = max(m["batch_size"] for m in msts)
     n_train = max(args.train_per_partition, B * args.steps_per_round)
     n_valid = max(B, int(round(n_train * cat.IMAGENET_VALID_TOTAL / cat.IMAGENET_TRAIN_TOTAL)))
+    loader, da_stats, da_root = None, None, None
+    if args.da:
+        import tempfile
+        from cerebro_ds_kpgi_amd.data import da
+        da_root = ctx.broadcast_object(tempfile.mkdtemp(prefix="cer_da_") if ctx.rank == 0
+                                       else None)
+        if ctx.rank == 0:
+            da.write_dataset(da_root, "criteo" if args.workload == "criteo16" else "imagenet",
+                             max(1, S // N) * N, n_train, n_valid)
+        ctx.barrier()
+        da_stats = {}
+        loader = da.da_partition_loader(da_root, ctx.device, stats=da_stats)
     opts = EngineOptions(slots_per_gpu=max(1, S // N), scheduler="rotation", n_train=n_train,
                          n_valid=n_valid, compute_dtype=args.dtype, use_graphs=not args.no_graphs,
-                         verbose=False, ckpt_every="none")
+                         verbose=False, ckpt_every="none", store_loader=loader)
+    t_etl = time.time()
     eng = MOPEngine(msts, ctx, opts)
+    t_etl = time.time() - t_etl
     sync = (torch.cuda.synchronize if ctx.device.type == "cuda" else (lambda: None))
 
     # warm-up (includes HIP-graph capture), untimed; then open every RCCL
@@ -137,7 +155,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(value / base, 3) if base and headline else None,
             "dtype": args.dtype,
-            "data": "synthetic",
+            "data": "synthetic via DA pages (C++ reader)" if args.da else "synthetic",
             "config": {"model": {"headline": args.model, "criteo16": "confA",
                                  "hetero8": "resnet50+vgg16"}[args.workload],
                        "global_batch": sum(m["batch_size"] for m in msts), "seq_len": None,
@@ -157,9 +175,22 @@ def main():
             "hop_bytes": sum(r["hop_bytes"] for r in per_rank),
             "hop_ms_max": round(1000.0 * max(r["hop_s"] for r in per_rank), 3),
         }
+        if da_stats is not None:
+            st = da_stats
+            out["etl_da"] = {"engine_setup_s": round(t_etl, 3), "decode_s": round(st["decode_s"], 3),
+                             "h2d_s": round(st["h2d_s"], 3),
+                             "payload_GB": round(st["payload_bytes"] / 1e9, 3),
+                             "stored_GB": round(st["stored_bytes"] / 1e9, 3),
+                             "decode_GBps": round(st["payload_bytes"] / 1e9 /
+                                                  max(st["decode_s"], 1e-9), 2),
+                             "h2d_GBps": round(st["payload_bytes"] / 1e9 /
+                                               max(st["h2d_s"], 1e-9), 2)}
         print(json.dumps(out))
         sys.stdout.flush()
     eng.close()
+    if da_root and ctx.rank == 0:
+        import shutil
+        shutil.rmtree(da_root, ignore_errors=True)
     shutdown(ctx)
 
 

@@ -24,7 +24,9 @@ from . import streams
 
 _LIB = None
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libcerebro_hip.so")
+# CER_HIP_LIB: an A/B twin built by ``tools.build --variant`` (file name in _lib/)
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib",
+                        os.environ.get("CER_HIP_LIB", "libcerebro_hip.so"))
 
 IMPLEMENTED = {"adam", "loss", "gather"}
 _RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}

@@ -185,6 +185,14 @@ def run_approach(approach, argv=None, shuffle=True):
                    "epochs": args.num_epochs, "makespan_s": makespan, "etl_s": etl,
                    "train_images": images, "agg_img_per_s": images / max(train_s, 1e-9),
                    "mst_state": {str(k): v for k, v in eng.mst_state.items()}}
+        st = getattr(loader, "stats", None)
+        if st and st.get("buffers"):
+            # Direct-Access ETL (rank 0's partitions): C++ page walk + detoast +
+            # pglz into pinned memory, then pinned -> HBM copies + conversion
+            summary["etl_da"] = dict(
+                st, payload_GB=st["payload_bytes"] / 1e9, stored_GB=st["stored_bytes"] / 1e9,
+                decode_GBps=st["payload_bytes"] / 1e9 / max(st["decode_s"], 1e-9),
+                h2d_GBps=st["payload_bytes"] / 1e9 / max(st["h2d_s"], 1e-9))
         logs("SUMMARY {}".format(json.dumps({k: v for k, v in summary.items()
                                               if k != "mst_state"})))
         if args.logs_root:

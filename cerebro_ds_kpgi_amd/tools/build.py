@@ -60,13 +60,18 @@ def _build(kind, srcs, headers, out, compiler, flags, link_flags, jobs):
     return out
 
 
-def build_hip(jobs=8):
+def build_hip(jobs=8, variant="", defines=()):
+    """``variant`` + ``defines`` (e.g. ``pf1``, ``["CER_FP32_PF=1"]``) build an
+    A/B twin ``libcerebro_hip_{variant}.so`` loaded with ``CER_HIP_LIB``."""
     srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.hip")))
     if not srcs:
         return None
     headers = glob.glob(os.path.join(ROOT, "csrc", "hip", "*.h"))
-    out = os.path.join(LIBDIR, "libcerebro_hip.so")
-    return _build("hip", srcs, headers, out, HIPCC, HIP_FLAGS, [], jobs)
+    name = "libcerebro_hip{}.so".format("_" + variant if variant else "")
+    out = os.path.join(LIBDIR, name)
+    flags = HIP_FLAGS + ["-D" + d for d in defines]
+    return _build("hip" + ("_" + variant if variant else ""), srcs, headers, out, HIPCC, flags,
+                  [], jobs)
 
 
 def build_da(jobs=8):
@@ -83,4 +88,13 @@ def build_all(jobs=8):
 
 
 if __name__ == "__main__":
-    print(build_all(int(sys.argv[1]) if len(sys.argv) > 1 else 8))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("jobs", nargs="?", type=int, default=8)
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    if a.variant:
+        print(build_hip(a.jobs, a.variant, a.defines))
+    else:
+        print(build_all(a.jobs))

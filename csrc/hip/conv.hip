@@ -30,6 +30,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -1612,6 +1614,54 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yh, acc, 0, 0, 0);
 }
 
+// fp32 K loop: register-staged operands through a double-buffered LDS
+// image, ONE barrier per KS-deep step.  With CER_FP32_PF = 2 two register
+// sets alternate, so the global loads of step k+2 are issued before the
+// MFMAs of step k and land in LDS only at the end of step k+1: two steps of
+// MFMA work (2 x 768 cycles per wave at 128x128) cover the L2 / HBM latency
+// instead of one.  ``load(k, S)`` / ``store(buf, S)`` take the register set
+// as a std::integral_constant so every index stays compile-time (no
+// scratch); ``mma(buf)`` consumes LDS buffer ``buf`` (0 / 1 by step parity).
+// 128x128 tiles stay at one set: the second one (+32 VGPRs) would push them
+// past the 256-VGPR budget of 2 workgroups per CU (spills).
+#ifndef CER_FP32_PF
+#define CER_FP32_PF 2
+#endif
+template <int BM, int BN>
+constexpr int fp32_sets() { return BM * BN > 128 * 64 ? 1 : CER_FP32_PF; }
+using RS0 = std::integral_constant<int, 0>;
+
+template <int SETS, typename Load, typename Store, typename Mma>
+__device__ __forceinline__ void kloop32(int k0, int k1, Load&& load, Store&& store, Mma&& mma) {
+  using RS1 = std::integral_constant<int, (SETS > 1 ? 1 : 0)>;
+  load(k0, RS0{});
+  store(0, RS0{});
+  if constexpr (SETS > 1) {
+    if (k0 + 1 < k1) load(k0 + 1, RS1{});
+    __syncthreads();
+    for (int kt = k0; kt < k1; kt += 2) {
+      if (kt + 2 < k1) load(kt + 2, RS0{});
+      mma(0);
+      if (kt + 1 < k1) store(1, RS1{});
+      __syncthreads();
+      if (kt + 1 >= k1) break;
+      if (kt + 3 < k1) load(kt + 3, RS1{});
+      mma(1);
+      if (kt + 2 < k1) store(0, RS0{});
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    for (int kt = k0; kt < k1; ++kt) {
+      const int cur = (kt - k0) & 1;
+      if (kt + 1 < k1) load(kt + 1, RS0{});
+      mma(cur);
+      if (kt + 1 < k1) store(cur ^ 1, RS0{});
+      __syncthreads();
+    }
+  }
+}
+
 // A: NT image, B: NT image (forward)
 template <int BM, int BN>
 __device__ __forceinline__ void mma3_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
@@ -1850,9 +1900,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  uint4 ra[2 * A_CH], rb[2 * B_CH];
+  constexpr int SETS = fp32_sets<BM, BN>();
+  uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
-  auto load_tiles = [&](int kt) {
+  auto load_tiles = [&](int kt, auto S) {
+    constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
     if constexpr (GM != GM_SLOW) {
       const bool kok = k0 < p.K;
@@ -1860,35 +1912,36 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
       for (int i = 0; i < A_CH; ++i) {
         const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
         const uint32_t o = kok ? off : OOB;
-        ra[2 * i] = bload(rA, o);
-        ra[2 * i + 1] = bload(rA, o + 16u);
+        ra[s][2 * i] = bload(rA, o);
+        ra[s][2 * i + 1] = bload(rA, o + 16u);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const int n = n0 + (tid + NTHREADS * i) / CPR;
         const uint32_t o = (kok && n < p.N) ? (uint32_t)(n * p.K + k0) * 4u : OOB;
-        rb[2 * i] = bload(rB, o);
-        rb[2 * i + 1] = bload(rB, o + 16u);
+        rb[s][2 * i] = bload(rB, o);
+        rb[s][2 * i + 1] = bload(rB, o + 16u);
       }
       kpos_advance<KS>(p.a, kp);
     } else {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i)
-        gather_chunk_slow32(p.a, cfg, rows[i], k0, p.K, p.dgrad, ra[2 * i], ra[2 * i + 1]);
+        gather_chunk_slow32(p.a, cfg, rows[i], k0, p.K, p.dgrad, ra[s][2 * i], ra[s][2 * i + 1]);
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const int n = n0 + (tid + NTHREADS * i) / CPR;
-        load_row8_slow32(wbase + (int64_t)n * p.K + k0, n < p.N ? p.K - k0 : 0, rb[2 * i],
-                         rb[2 * i + 1]);
+        load_row8_slow32(wbase + (int64_t)n * p.K + k0, n < p.N ? p.K - k0 : 0, rb[s][2 * i],
+                         rb[s][2 * i + 1]);
       }
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, auto S) {
+    constexpr int s = decltype(S)::value;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -1896,7 +1949,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < B_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -1904,16 +1957,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
 
   f32x4 acc[BM / 32][BN / 32];
   zero_acc<BM, BN>(acc);
-  load_tiles(kr.kt0);
-  store_tiles(0);
-  __syncthreads();
-  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
-    const int cur = (kt - kr.kt0) & 1;
-    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
-    mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc);
-    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
-    __syncthreads();
-  }
+  kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
+          [&](int cur) { mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
   if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
 #undef SA
@@ -1955,17 +2000,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  uint4 ra[2 * A_CH], rb[2 * B_CH];
+  constexpr int SETS = fp32_sets<BM, BN>();
+  uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
-  auto load_tiles = [&](int kt) {
+  auto load_tiles = [&](int kt, auto S) {
+    constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
     const bool kok = k0 < p.K;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
       const uint32_t o = kok ? off : OOB;
-      ra[2 * i] = bload(rA, o);
-      ra[2 * i + 1] = bload(rA, o + 16u);
+      ra[s][2 * i] = bload(rA, o);
+      ra[s][2 * i + 1] = bload(rA, o + 16u);
     }
     kpos_advance<KS>(p.a, kp);
 #pragma unroll
@@ -1975,18 +2022,19 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
       const int tap = (int)fdiv((uint32_t)k, dCout);
       const int n = k - tap * Cout;
       const uint32_t o = (k < p.K && c < Cin) ? (uint32_t)((n * T + tap) * Cin + c) * 4u : OOB;
-      rb[2 * i] = bload(rW, o);
-      rb[2 * i + 1] = bload(rW, o + 16u);
+      rb[s][2 * i] = bload(rW, o);
+      rb[s][2 * i + 1] = bload(rW, o + 16u);
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, auto S) {
+    constexpr int s = decltype(S)::value;
     bf16_t* sa = lds + buf * (BM * BK);
     bf16_t* sb = lds + 2 * BM * BK + buf * (BK * BN);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk + 4)) = l;
     }
@@ -1994,7 +2042,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
     }
@@ -2002,16 +2050,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
 
   f32x4 acc[BM / 32][BN / 32];
   zero_acc<BM, BN>(acc);
-  load_tiles(kr.kt0);
-  store_tiles(0);
-  __syncthreads();
-  for (int kt = kr.kt0; kt < kr.kt1; ++kt) {
-    const int cur = (kt - kr.kt0) & 1;
-    if (kt + 1 < kr.kt1) load_tiles(kt + 1);
+  kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, [&](int cur) {
     mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane, acc);
-    if (kt + 1 < kr.kt1) store_tiles(cur ^ 1);
-    __syncthreads();
-  }
+  });
   if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
   epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
 }
@@ -2041,7 +2082,8 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   const bool b_kok = kk0 < p.K;
   KPos bk{0, 0, 0};
   if (b_kok) bk = kpos_init(p.x, kk0);
-  uint4 ra[2 * A_CH], rb[2 * B_CH];
+  constexpr int SETS = fp32_sets<BM, BN>();
+  uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
   const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
   const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
   __amdgpu_buffer_rsrc_t rDY, rX;
@@ -2050,52 +2092,54 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     rX = make_rsrc(xb, p.x.bytes);
   }
 
-  auto load_tiles = [&](int mt) {
+  auto load_tiles = [&](int mt, auto S) {
+    constexpr int s = decltype(S)::value;
     const int mbase = ms + mt * KS;
     if constexpr (GM != GM_SLOW) {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
         const uint32_t o = (m < me && n < p.N) ? (uint32_t)(m * p.ldy + n) * 4u : OOB;
-        ra[2 * i] = bload(rDY, o);
-        ra[2 * i + 1] = bload(rDY, o + 16u);
+        ra[s][2 * i] = bload(rDY, o);
+        ra[s][2 * i + 1] = bload(rDY, o + 16u);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
         const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
         const uint32_t o = b_kok ? off : OOB;
-        rb[2 * i] = bload(rX, o);
-        rb[2 * i + 1] = bload(rX, o + 16u);
+        rb[s][2 * i] = bload(rX, o);
+        rb[s][2 * i + 1] = bload(rX, o + 16u);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
         load_row8_slow32(dyb + (int64_t)m * p.ldy + n, (m < me && n < p.N) ? p.N - n : 0,
-                         ra[2 * i], ra[2 * i + 1]);
+                         ra[s][2 * i], ra[s][2 * i + 1]);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const int m = mbase + b_row0 + B_RSTEP * i;
         const RowPos pos = decode_row(m, me, p.x);
         if (b_kok && pos.ok) {
-          gather_chunk_slow32(p.x, cfg, pos, kk0, p.K, 0, rb[2 * i], rb[2 * i + 1]);
+          gather_chunk_slow32(p.x, cfg, pos, kk0, p.K, 0, rb[s][2 * i], rb[s][2 * i + 1]);
         } else {
-          rb[2 * i] = make_uint4(0, 0, 0, 0);
-          rb[2 * i + 1] = make_uint4(0, 0, 0, 0);
+          rb[s][2 * i] = make_uint4(0, 0, 0, 0);
+          rb[s][2 * i + 1] = make_uint4(0, 0, 0, 0);
         }
       }
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, auto S) {
+    constexpr int s = decltype(S)::value;
     bf16_t* sa = lds + buf * (BK * BM);
     bf16_t* sb = lds + 2 * BK * BM + buf * (BK * BN);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = a_row0 + A_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(ra[2 * i], ra[2 * i + 1], h, l);
+      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sa + tn_off<BM>(row, a_col)) = h;
       *reinterpret_cast<uint4*>(sa + tn_off<BM>(row + KS, a_col)) = l;
     }
@@ -2103,7 +2147,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(rb[2 * i], rb[2 * i + 1], h, l);
+      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
     }
@@ -2112,16 +2156,9 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   f32x4 acc[BM / 32][BN / 32];
   zero_acc<BM, BN>(acc);
   const int MT = (me - ms + KS - 1) / KS;
-  load_tiles(0);
-  store_tiles(0);
-  __syncthreads();
-  for (int mt = 0; mt < MT; ++mt) {
-    const int cur = mt & 1;
-    if (mt + 1 < MT) load_tiles(mt + 1);
+  kloop32<SETS>(0, MT, load_tiles, store_tiles, [&](int cur) {
     mma3_tn<BM, BN>(lds + cur * (BK * BM), lds + 2 * BK * BM + cur * (BK * BN), wa, wb, lane, acc);
-    if (mt + 1 < MT) store_tiles(cur ^ 1);
-    __syncthreads();
-  }
+  });
 
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;

@@ -33,8 +33,34 @@ def test_da_cerebro_standalone_end_to_end(tmp_path):
     blobs = sorted(p for p in os.listdir(models) if p.endswith("model:resnet50"))
     assert len(blobs) == 8
     w = np.fromfile(str(models / blobs[0]), dtype=np.float32)
-    assert w.size == 25557032 + 53120 and np.isfinite(w).all()
+    # Keras get_weights() layout: 25 583 592 trainable (conv biases as zeros) + 53 120 stats
+    assert w.size == 25636712 and np.isfinite(w).all()
     jobs = [j for ep in json.loads((logs / "jobs_info.json").read_text()).values()
             for j in ep.values()]
     assert len(jobs) == 64 and all(j["status"] == "SUCCESS" for j in jobs)   # 8 cfg x 8 part.
     assert all(np.isfinite(j["loss_train"]) for j in jobs)
+
+
+def test_criteo_da_cerebro_standalone_end_to_end(tmp_path):
+    """BASELINE config 3 path: the 16-config Criteo confA grid through the
+    DA page/pglz reader (one-hot float32 payload -> 39 active ids per row in
+    HBM) and MOP on the HIP embedding-bag / linear / loss kernels."""
+    from cerebro_ds_kpgi_amd.data import da
+    from cerebro_ds_kpgi_amd.ops import _hip
+    from cerebro_ds_kpgi_amd.runners import run_da_cerebro_standalone
+    _hip.lib()
+    root = str(tmp_path / "da")
+    da.write_dataset(root, "criteo", 8, n_train=1024, n_valid=512, buffer_size=256)
+    logs = tmp_path / "run_logs" / "cerebro-da-criteo"
+    run_da_cerebro_standalone.main([
+        "--run", "--num_epochs", "1", "--criteo", "--size", "1", "--slots_per_gpu", "8",
+        "--da", "--da_root", root, "--train_per_partition", "1024",
+        "--valid_per_partition", "512", "--backend", "hip", "--logs_root", str(logs),
+        "--models_root", str(tmp_path / "models")])
+    summ = json.loads((logs / "summary.json").read_text())
+    assert summ["configs"] == 16
+    assert summ["train_images"] > 0 and summ["etl_da"]["buffers"] == 8 * (4 + 2)
+    assert summ["etl_da"]["decode_GBps"] > 0 and summ["etl_da"]["h2d_GBps"] > 0
+    jobs = [j for ep in json.loads((logs / "jobs_info.json").read_text()).values()
+            for j in ep.values()]
+    assert len(jobs) == 16 * 8 and all(np.isfinite(j["loss_train"]) for j in jobs)
