@@ -1637,17 +1637,20 @@ __device__ __forceinline__ void kloop32(int k0, int k1, Load&& load, Store&& sto
   load(k0, RS0{});
   store(0, RS0{});
   if constexpr (SETS > 1) {
-    if (k0 + 1 < k1) load(k0 + 1, RS1{});
+    // loads past k1 are issued anyway (their offsets are out of range, the
+    // buffer loads return zeros): no branch around a load, so the compiler
+    // keeps counted vmcnt waits instead of draining at every join
+    load(k0 + 1, RS1{});
     __syncthreads();
     for (int kt = k0; kt < k1; kt += 2) {
-      if (kt + 2 < k1) load(kt + 2, RS0{});
+      load(kt + 2, RS0{});
       mma(0);
-      if (kt + 1 < k1) store(1, RS1{});
+      store(1, RS1{});
       __syncthreads();
       if (kt + 1 >= k1) break;
-      if (kt + 3 < k1) load(kt + 3, RS1{});
+      load(kt + 3, RS1{});
       mma(1);
-      if (kt + 2 < k1) store(0, RS0{});
+      store(0, RS0{});
       __syncthreads();
     }
   } else {
