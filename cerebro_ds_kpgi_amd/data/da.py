@@ -280,8 +280,11 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     payloads are float32 pixels; they are stored as uint8 only after a
     device-side check that every value is an integer in [0, 255]
     (``NonIntegralPixels`` otherwise — never a silent quantisation).
-    ``stats`` (a dict) accumulates ETL timings: ``decode_s`` (C++ reader,
-    wall), ``h2d_s`` (copies + conversion, wall), ``payload_bytes``
+    ``loader.prefetch(pids)`` (called by the partition store) lets up to four
+    (partition, split) decodes run ahead on a thread pool.
+    ``stats`` (a dict) accumulates ETL timings: ``decode_s`` (wall time the
+    consumer waited for the C++ reader), ``h2d_s`` (copies + conversion,
+    wall), ``payload_bytes``
     (decompressed), ``stored_bytes`` (on disk, heap + TOAST) and ``buffers``."""
     import time
     import torch
@@ -301,21 +304,50 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
         nnz = int((x[0] != 0).sum().item())
         return torch.nonzero(x, as_tuple=False)[:, 1].view(x.shape[0], nnz).to(torch.int32), None
 
-    def load_split(p, split):
+    # decode pipeline: the C++ reader releases the GIL, so up to WINDOW
+    # (partition, split) decodes run concurrently ahead of the consumer
+    # (bounded: each holds its decompressed payload in pinned memory)
+    import concurrent.futures as cf
+    WINDOW = 4
+    jobs, futs = [], {}
+    pool = cf.ThreadPoolExecutor(max_workers=WINDOW)
+
+    def decode(p, split, threads):
         heap = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["relfilenode"]))
         toast = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["toast_relfilenode"]))
-        shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
+        stored = 0
         for path in (heap, toast):
             seg = 0
             f = path
             while os.path.exists(f):
-                st["stored_bytes"] += os.path.getsize(f)
+                stored += os.path.getsize(f)
                 seg += 1
                 f = "{}.{}".format(path, seg)
-        t0 = time.perf_counter()
         r = DirectAccessReader(heap, toast)
-        recs = sorted(r.read(nthreads, pinned=cuda), key=lambda t: t[1])
+        recs = sorted(r.read(threads, pinned=cuda), key=lambda t: t[1])
         r.close()
+        return recs, stored
+
+    def prefetch(pids):
+        """The store's partitions, in load order: start decoding ahead."""
+        del jobs[:]
+        jobs.extend((p, sp) for p in pids for sp in ("train", "valid"))
+
+    def fetch(p, split):
+        key = (p, split)
+        if key in jobs:
+            i = jobs.index(key)
+            for k in jobs[i:i + WINDOW]:
+                if k not in futs:
+                    futs[k] = pool.submit(decode, k[0], k[1], max(2, nthreads // WINDOW))
+        fut = futs.pop(key, None)
+        return fut.result() if fut is not None else decode(p, split, nthreads)
+
+    def load_split(p, split):
+        shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
+        t0 = time.perf_counter()
+        recs, stored = fetch(p, split)
+        st["stored_bytes"] += stored
         t1 = time.perf_counter()
         st["decode_s"] += t1 - t0
         xs, ys, bads = [], [], []
@@ -352,8 +384,11 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     def loader(p):
         tx, ty = load_split(p, "train")
         vx, vy = load_split(p, "valid")
+        if jobs and not futs and (p, "valid") == jobs[-1]:
+            pool.shutdown(wait=False)
         return tx, ty, vx, vy
     loader.stats = st
+    loader.prefetch = prefetch
     return loader
 
 

@@ -42,6 +42,8 @@ class PartitionStore(object):
         self.local = {p: i for i, p in enumerate(self.pids)}
         self.seed = seed
         parts = []
+        if loader is not None and hasattr(loader, "prefetch"):
+            loader.prefetch(self.pids)
         for p in self.pids:
             if loader is not None:
                 tx, ty, vx, vy = loader(p)
