@@ -116,6 +116,32 @@ struct BNBwdEpi {
   int ym, act;                  // mask mode (bn.hip YM_*) and activation code
 };
 
+// BN-apply prologue (fp32 kernels): the gathered activation is the INPUT z of
+// a training-mode BatchNorm whose output y = act(z * scale + shift) is never
+// materialised; the operand load applies it per element (padding taps stay
+// 0, i.e. y's zero padding).  scsh = [2][ld] fp32 (scale | shift) per packed
+// channel (bn.hip cer_bn_finalize_scsh); scsh == nullptr: off.
+struct BNPro {
+  const float* scsh;
+  int ld;       // packed channels of the gathered tensor (G * Cg)
+  int act;      // 0 none, 1 relu, 6 relu6
+};
+
+// BN-apply prologue for the NEXT fp32 forward / weight-gradient calls (until
+// cleared with scsh == nullptr): the activation argument of those calls is a
+// BatchNorm input z, the convolution consumes act(z * scale + shift).  Only
+// the aligned (fast-gather) kernels implement it: a call that would take the
+// generic gather returns hipErrorInvalidValue instead of ignoring it.
+static BNPro g_pro = BNPro{nullptr, 0, 0};
+
+CER_API void cer_conv_set_prologue(const float* scsh, int ld, int act) {
+  g_pro = BNPro{scsh, ld, act};
+}
+
+__device__ __forceinline__ float pro_act(float v, int act) {
+  return act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (act ? fmaxf(v, 0.f) : v);
+}
+
 struct NTParams {
   GatherGeom a;
   int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
@@ -139,6 +165,7 @@ struct NTParams {
                                    // input gradient joins here instead of in an add kernel)
   BNBwdEpi bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
                          0, 0};
+  BNPro pro = BNPro{nullptr, 0, 0};   // fp32 fwd: BN-apply prologue on the gathered A operand
 };
 
 
@@ -151,6 +178,7 @@ struct WGParams {
   int Mred, N, K;
   int m_per_split;
   int splits;
+  BNPro pro = BNPro{nullptr, 0, 0};   // fp32: BN-apply prologue on the gathered x (BNPro)
 };
 
 // es: element size of the gathered tensor (2 = bf16, 4 = fp32)
@@ -1570,6 +1598,24 @@ __device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint
   lo = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
+// y = valid ? act(z * sc + sh) : 0 on two uint4 of fp32 (8 channels)
+__device__ __forceinline__ void pro_apply(uint4& a, uint4& b, const uint4 (&ss)[4], bool valid,
+                                          int act) {
+  uint32_t* x0 = reinterpret_cast<uint32_t*>(&a);
+  uint32_t* x1 = reinterpret_cast<uint32_t*>(&b);
+  const uint32_t* sc = reinterpret_cast<const uint32_t*>(&ss[0]);
+  const uint32_t* sh = reinterpret_cast<const uint32_t*>(&ss[2]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float v0 = pro_act(fmaf(__uint_as_float(x0[e]), __uint_as_float(sc[e]),
+                                  __uint_as_float(sh[e])), act);
+    const float v1 = pro_act(fmaf(__uint_as_float(x1[e]), __uint_as_float(sc[4 + e]),
+                                  __uint_as_float(sh[4 + e])), act);
+    x0[e] = valid ? __float_as_uint(v0) : 0u;
+    x1[e] = valid ? __float_as_uint(v1) : 0u;
+  }
+}
+
 __device__ __forceinline__ uint4 f4_bits(const float* e) {
   return make_uint4(__float_as_uint(e[0]), __float_as_uint(e[1]), __float_as_uint(e[2]),
                     __float_as_uint(e[3]));
@@ -1865,7 +1911,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out
-template <int BM, int BN, int GM>
+template <int BM, int BN, int GM, bool PRO = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
@@ -1905,6 +1951,14 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
   constexpr int SETS = fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
+  // BN-apply prologue: (scale, shift) of the chunk's 8 channels per set and
+  // the per-chunk "not padding" flags; loaded unconditionally (a null table
+  // has a 0-byte range: zeros, no branch around the loads)
+  constexpr bool pro = PRO && GM != GM_SLOW;     // compile-time: no registers otherwise
+  uint4 rs[pro ? SETS : 1][4];
+  bool av[pro ? SETS : 1][A_CH];
+  __amdgpu_buffer_rsrc_t rP;
+  if constexpr (pro) rP = make_rsrc(p.pro.scsh, (uint32_t)p.pro.ld * 8u);
 
   auto load_tiles = [&](int kt, auto S) {
     constexpr int s = decltype(S)::value;
@@ -1915,8 +1969,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
       for (int i = 0; i < A_CH; ++i) {
         const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
         const uint32_t o = kok ? off : OOB;
+        if constexpr (pro) av[s][i] = o != OOB;
         ra[s][2 * i] = bload(rA, o);
         ra[s][2 * i + 1] = bload(rA, o + 16u);
+      }
+      if constexpr (pro) {
+        const uint32_t po = (uint32_t)(cfg * p.a.Cg + kp.c) * 4u;
+        rs[s][0] = bload(rP, po);
+        rs[s][1] = bload(rP, po + 16u);
+        rs[s][2] = bload(rP, po + (uint32_t)p.pro.ld * 4u);
+        rs[s][3] = bload(rP, po + (uint32_t)p.pro.ld * 4u + 16u);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
@@ -1944,6 +2006,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
+      if constexpr (pro) pro_apply(ra[s][2 * i], ra[s][2 * i + 1], rs[s], av[s][i], p.pro.act);
       split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk + 4)) = l;
@@ -2061,7 +2124,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
 }
 
 // wgrad tile body (fp32 operands): dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]
-template <int BM, int BN, int GM>
+template <int BM, int BN, int GM, bool PRO = false>
 __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf16_t* lds) {
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
   constexpr int A_CH = KS * A_CPR / NTHREADS, B_CH = KS * B_CPR / NTHREADS;
@@ -2094,6 +2157,18 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
     rX = make_rsrc(xb, p.x.bytes);
   }
+  // BN-apply prologue on x (see BNPro): a thread's B chunk covers the same 8
+  // channels for the whole reduction, so (scale, shift) load once
+  constexpr bool pro = PRO && GM != GM_SLOW;
+  uint4 rs[4];
+  bool bv[pro ? SETS : 1][B_CH];
+  if constexpr (pro) {
+    const float* ps = p.pro.scsh + cfg * p.x.Cg + bk.c;
+    rs[0] = *reinterpret_cast<const uint4*>(ps);
+    rs[1] = *reinterpret_cast<const uint4*>(ps + 4);
+    rs[2] = *reinterpret_cast<const uint4*>(ps + p.pro.ld);
+    rs[3] = *reinterpret_cast<const uint4*>(ps + p.pro.ld + 4);
+  }
 
   auto load_tiles = [&](int mt, auto S) {
     constexpr int s = decltype(S)::value;
@@ -2111,6 +2186,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
         const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
         const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
         const uint32_t o = b_kok ? off : OOB;
+        if constexpr (pro) bv[s][i] = o != OOB;
         rb[s][2 * i] = bload(rX, o);
         rb[s][2 * i + 1] = bload(rX, o + 16u);
       }
@@ -2150,6 +2226,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
+      if constexpr (pro) pro_apply(rb[s][2 * i], rb[s][2 * i + 1], rs, bv[s][i], p.pro.act);
       split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
@@ -2185,21 +2262,21 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
       }
 }
 
-template <int BM, int BN, int GM>
+template <int BM, int BN, int GM, bool PRO = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
-  wgrad_reg_body32<BM, BN, GM>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
+  wgrad_reg_body32<BM, BN, GM, PRO>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
 }
 
 // batched fp32 weight gradients (see wgrad_batch)
-template <int BM, int BN>
+template <int BM, int BN, bool PRO = false>
 __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
   const int work = xcd_remap(blockIdx.x, gridDim.x);
   int i = 0;
   while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
   const WGParams p = b.p[i];
-  wgrad_reg_body32<BM, BN, GM_FWD>(p, work - b.start[i], lds);
+  wgrad_reg_body32<BM, BN, GM_FWD, PRO>(p, work - b.start[i], lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -2358,7 +2435,10 @@ template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, hipStream_t stream) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if (fast)
-    igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+    if (p.pro.scsh)
+      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
 }
@@ -2373,6 +2453,8 @@ static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   if (p.fin.cnt) return (int)hipErrorInvalidValue;   // fused finalize: bf16 path only
   const bool fast = nt_fast32(p);
+  p.pro = g_pro;
+  if (p.pro.scsh && !fast) return (int)hipErrorInvalidValue;
   const int v = fp32_variant(choose(0, p.M, p.N, p.K, G, false));
   set_splits(p, G, v, KS);
   if (nslab) {
@@ -2393,6 +2475,7 @@ static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
                          void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
                          int act, float* stats, int* nslab, const BNFinal* fin, bool f32,
                          hipStream_t stream);
+
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
@@ -2711,7 +2794,10 @@ static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t 
   p.splits = splits;
   dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
   if (fast)
-    igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+    if (p.pro.scsh)
+      igemm_wgrad32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_wgrad32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
 }
@@ -2743,6 +2829,8 @@ CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
+  p.pro = g_pro;
+  if (p.pro.scsh && !wg_fast32(Cin, Cout, p)) return (int)hipErrorInvalidValue;
   run_wg32(p, G, splits, wg_fast32(Cin, Cout, p), stream);
   return (int)hipGetLastError();
 }
@@ -2806,6 +2894,7 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
+  p.pro = g_pro;
   if (!wg_fast32(Cin, Cout, p)) return 0;
   const int rows = wgb_rows();
   p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
@@ -2815,20 +2904,31 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   return p.splits;
 }
 
-template <int BM, int BN>
-static int wgb32_launch(hipStream_t stream) {
-  for (int b0 = 0; b0 < g_wgq32_n; b0 += WGB_MAX) {
+template <int BM, int BN, bool PRO>
+static void wgb32_launch_sel(hipStream_t stream) {
+  int idx[4096];
+  int n = 0;
+  for (int k = 0; k < g_wgq32_n; ++k)
+    if ((g_wgq32[k].pro.scsh != nullptr) == PRO) idx[n++] = k;
+  for (int b0 = 0; b0 < n; b0 += WGB_MAX) {
     WGBatch bt;
-    bt.n = g_wgq32_n - b0 < WGB_MAX ? g_wgq32_n - b0 : WGB_MAX;
+    bt.n = n - b0 < WGB_MAX ? n - b0 : WGB_MAX;
     int tot = 0;
     for (int i = 0; i < bt.n; ++i) {
-      bt.p[i] = g_wgq32[b0 + i];
+      const int k = idx[b0 + i];
+      bt.p[i] = g_wgq32[k];
       bt.start[i] = tot;
-      tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[b0 + i]);
+      tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[k]);
     }
     bt.start[bt.n] = tot;
-    if (tot > 0) wgrad_batch32<BM, BN><<<tot, NTHREADS, 0, stream>>>(bt);
+    if (tot > 0) wgrad_batch32<BM, BN, PRO><<<tot, NTHREADS, 0, stream>>>(bt);
   }
+}
+
+template <int BM, int BN>
+static int wgb32_launch(hipStream_t stream) {
+  wgb32_launch_sel<BM, BN, false>(stream);
+  wgb32_launch_sel<BM, BN, true>(stream);
   return (int)hipGetLastError();
 }
 
