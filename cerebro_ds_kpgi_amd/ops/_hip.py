@@ -41,6 +41,10 @@ _SIGS = {
                       c_p, c_i, c_f, c_f, c_f, c_i, c_p],
     "cer_sgd_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p, c_p, c_i,
                      c_f, c_i, c_p],
+    "cer_adam_step_split": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64,
+                            c_p, c_p, c_i, c_f, c_f, c_f, c_i, c_p],
+    "cer_split_image": [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_p],
+    "cer_conv_set_wsplit": [c_p, c_i64],
     "cer_softmax_ce": [c_p, c_i, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_gather_images": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p],
 }
@@ -86,9 +90,28 @@ def _check(rc, name):
 
 
 # ---------------------------------------------------------------------------
+def split_image(arena, row=None):
+    """Rewrite the pre-split weight image (``Arena.wsplit``) of one row (or
+    all) from the fp32 params — after init, load, hop or a host-side update."""
+    src, dst = arena.params, arena.wsplit
+    g0, G = (0, arena.G) if row is None else (row, 1)
+    rc = lib().cer_split_image(c_p(src[g0].data_ptr()), src.stride(0), c_p(dst[g0].data_ptr()),
+                               dst.stride(0), arena.layout.n_train, G, _stream())
+    _check(rc, "cer_split_image")
+
+
 def adam_step(arena, beta1, beta2, eps, l2):
     L = arena.layout
     st = arena.state
+    if arena.wsplit is not None:
+        sp = arena.wsplit
+        rc = lib().cer_adam_step_split(
+            _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
+            _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
+            _ptr(sp), sp.stride(0), _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps,
+            int(bool(l2)), _stream())
+        _check(rc, "cer_adam_step_split")
+        return
     work = arena.work if arena.work is not arena.params else None
     rc = lib().cer_adam_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
@@ -108,6 +131,8 @@ def sgd_step(arena, momentum, l2):
         _ptr(work), work.stride(0) if work is not None else 0,
         _ptr(arena.lr), _ptr(arena.wd), arena.G, float(momentum), int(bool(l2)), _stream())
     _check(rc, "cer_sgd_step")
+    if arena.wsplit is not None:
+        split_image(arena)
 
 
 def softmax_ce_fwd(logits, labels, acc, G, need_grad=True):
@@ -344,12 +369,38 @@ def tuned_variants():
     return dict(_TUNED)
 
 
+class _WSplit(object):
+    """``with _WSplit(wref):`` the next fp32 conv forward / dgrad reads the
+    pre-split (hi | lo bf16) image of these weights that the optimizer keeps
+    next to the fp32 params (``Arena.wsplit``; conv.hip cer_conv_set_wsplit)
+    instead of splitting them while staging.  No-op without an image."""
+    __slots__ = ("ptr", "stride")
+
+    def __init__(self, wref):
+        img = getattr(wref.arena, "wsplit", None) if wref is not None else None
+        self.ptr = None
+        if img is not None:
+            self.ptr = img.data_ptr() + wref.spec.offset * img.element_size()
+            self.stride = img.stride(0)
+
+    def __enter__(self):
+        if self.ptr is not None:
+            lib().cer_conv_set_wsplit(c_p(self.ptr), self.stride)
+
+    def __exit__(self, *a):
+        if self.ptr is not None:
+            lib().cer_conv_set_wsplit(None, 0)
+        return False
+
+
 def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,
-                     act):
+                     act, wref=None):
     _splitk_ready(x.device)
     def launch():
-        rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
-                                _ptr(y), Ho, Wo, c_p(bp), bs, _act_code(act), _stream())
+        with _WSplit(wref):
+            rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
+                                        stride, pad, _ptr(y), Ho, Wo, c_p(bp), bs,
+                                        _act_code(act), _stream())
         _check(rc, "cer_conv_fwd")
     _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
@@ -371,7 +422,8 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     y = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
-    _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs, act)
+    _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs, act,
+                     wref=wref)
     return y
 
 
@@ -395,9 +447,10 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _splitk_ready(x.device)
 
     def launch():
-        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride,
-                                      pad, _ptr(z), Ho, Wo, _ptr(part), ctypes.byref(nslab),
-                                      _stream())
+        with _WSplit(wref):
+            rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
+                                              stride, pad, _ptr(z), Ho, Wo, _ptr(part),
+                                              ctypes.byref(nslab), _stream())
         _check(rc, "cer_conv_fwd_stats")
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
@@ -541,9 +594,11 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
         _check(rc, "cer_stem_fwd_bnstat")
     else:
         def tune():
-            _check(_fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
-                                            stride, pad, _ptr(z), Ho, Wo, _ptr(part),
-                                            ctypes.byref(nslab), _stream()), "cer_conv_fwd_stats")
+            with _WSplit(wref):
+                rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
+                                                  kh, kw, stride, pad, _ptr(z), Ho, Wo,
+                                                  _ptr(part), ctypes.byref(nslab), _stream())
+            _check(rc, "cer_conv_fwd_stats")
         _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), tune, x.dtype)
         if not fused_fin:
             tune()
@@ -622,15 +677,17 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend=None, bnstats=False):
+                       addend=None, bnstats=False, wref=None):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
     wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
 
     def launch():
-        rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh,
-                                  kw, stride, pad, _ptr(dx), H, W, _ptr(addend), _stream())
+        with _WSplit(wref):
+            rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
+                                           cin, kh, kw, stride, pad, _ptr(dx), H, W,
+                                           _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
             launch, dy.dtype)
@@ -655,7 +712,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
         assert addend.shape == dx.shape
     if bnlink is None:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend)
+                           addend, wref=wref)
         return dx
     link, ybn = bnlink
     L = lib()
@@ -669,7 +726,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
                            1 if link.has_res else 0, ctypes.byref(nslab))
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend, bnstats=True)
+                           addend, bnstats=True, wref=wref)
     finally:
         L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
     if nslab.value > 0:
@@ -902,7 +959,7 @@ def linear_fwd(x, wref, bref, act):
     y = torch.empty((B, G * N), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
-    _conv_fwd_launch(x, B, 1, 1, K, G, wp, ws, N, 1, 1, 1, 0, y, 1, 1, bp, bs, act)
+    _conv_fwd_launch(x, B, 1, 1, K, G, wp, ws, N, 1, 1, 1, 0, y, 1, 1, bp, bs, act, wref=wref)
     return y
 
 
@@ -918,7 +975,7 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
         return None
     dx = torch.empty((B, G * K), dtype=dy.dtype, device=dy.device)
     wp, ws = wref.work_ptr()
-    _conv_dgrad_launch(dz, B, 1, 1, N, G, wp, ws, K, 1, 1, 1, 0, dx, 1, 1)
+    _conv_dgrad_launch(dz, B, 1, 1, N, G, wp, ws, K, 1, 1, 1, 0, dx, 1, 1, wref=wref)
     return dx
 
 

@@ -36,8 +36,7 @@ def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
         bc2 = 1 - torch.pow(torch.full_like(t, beta2), t)
         denom = v.sqrt() / bc2.sqrt() + eps
         p.sub_((arena.lr.unsqueeze(1) / bc1) * m / denom)
-        if arena.work is not arena.params:
-            arena.work.copy_(p)
+        arena.sync_work()
         if arena.grad_clean:
             arena.grad.zero_()
 
@@ -65,8 +64,7 @@ def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
         else:
             upd = g
         p.sub_(arena.lr.unsqueeze(1) * upd)
-        if arena.work is not arena.params:
-            arena.work.copy_(p)
+        arena.sync_work()
         if arena.grad_clean:
             arena.grad.zero_()
 

@@ -41,7 +41,26 @@ __global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step
   if (g < G) state[g * row_stride + off_step] += 1.0f;
 }
 
-template <bool WRITE_BF16, bool NT = false>
+// 8 fp32 -> the split image chunk [8 x bf16 hi | 8 x bf16 lo] (conv.hip
+// cer_conv_set_wsplit): hi = bf16(v), lo = bf16(v - hi)
+__device__ __forceinline__ void store_split8(uint32_t* dst, const float* v) {
+  uint4 h, l;
+  uint32_t* hw = reinterpret_cast<uint32_t*>(&h);
+  uint32_t* lw = reinterpret_cast<uint32_t*>(&l);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t hp = pack_bf2(v[2 * k], v[2 * k + 1]);
+    hw[k] = hp;
+    lw[k] = pack_bf2(v[2 * k] - __uint_as_float(hp << 16),
+                     v[2 * k + 1] - __uint_as_float(hp & 0xffff0000u));
+  }
+  reinterpret_cast<uint4*>(dst)[0] = h;
+  reinterpret_cast<uint4*>(dst)[1] = l;
+}
+
+// work modes: 0 none (fp32 compute reads the params), 1 bf16 shadow,
+// 2 split image of the params (fp32 compute with pre-split weights)
+template <bool WRITE_BF16, bool NT = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void adam_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
@@ -84,7 +103,9 @@ __global__ __launch_bounds__(256) void adam_kernel(
   st4<NT>(pp, p[0]); st4<NT>(pp + 1, p[1]);
   st4<NT>(mp, m[0]); st4<NT>(mp + 1, m[1]);
   st4<NT>(vp, v[0]); st4<NT>(vp + 1, v[1]);
-  if (WRITE_BF16) {
+  if (SPLIT) {
+    store_split8(reinterpret_cast<uint32_t*>(work) + g * work_stride + i, pf);
+  } else if (WRITE_BF16) {
     uint4 o;
     o.x = pack_bf2(pf[0], pf[1]);
     o.y = pack_bf2(pf[2], pf[3]);
@@ -92,6 +113,45 @@ __global__ __launch_bounds__(256) void adam_kernel(
     o.w = pack_bf2(pf[6], pf[7]);
     *reinterpret_cast<uint4*>(work + g * work_stride + i) = o;
   }
+}
+
+// Adam that also writes the split image of the updated params: ``split`` =
+// [G][n_train] 32-bit slots, ``split_stride`` in slots
+CER_API int cer_adam_step_split(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
+                                int64_t off_v, int64_t off_step, float* grad,
+                                int64_t grad_stride, int zero_grad, void* split,
+                                int64_t split_stride, const float* lr, const float* wd, int G,
+                                float b1, float b2, float eps, int l2, hipStream_t stream) {
+  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  dim3 grid(cer_blocks(n_train / 8, 256), G);
+  adam_kernel<false, false, true><<<grid, 256, 0, stream>>>(
+      state, row_stride, n_train, off_m, off_v, off_step, grad, grad_stride, zero_grad,
+      reinterpret_cast<bf16_t*>(split), split_stride, lr, wd, b1, b2, eps, l2);
+  return (int)hipGetLastError();
+}
+
+// split image of fp32 params (after init / load / hop): [G][n] -> [G][n] slots
+__global__ void split_image_kernel(const float* __restrict__ src, int64_t src_stride,
+                                   uint32_t* __restrict__ dst, int64_t dst_stride, int64_t n) {
+  const int g = blockIdx.y;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  float v[8];
+  const float4* sp = reinterpret_cast<const float4*>(src + g * src_stride + i);
+  const float4 a = sp[0], b = sp[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  store_split8(dst + g * dst_stride + i, v);
+}
+
+CER_API int cer_split_image(const float* src, int64_t src_stride, void* dst, int64_t dst_stride,
+                            int64_t n, int G, hipStream_t stream) {
+  if (n % 8 != 0) return (int)hipErrorInvalidValue;
+  dim3 grid(cer_blocks(n / 8, 256), G);
+  split_image_kernel<<<grid, 256, 0, stream>>>(src, src_stride,
+                                               reinterpret_cast<uint32_t*>(dst), dst_stride, n);
+  return (int)hipGetLastError();
 }
 
 CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,

@@ -138,6 +138,20 @@ CER_API void cer_conv_set_prologue(const float* scsh, int ld, int act) {
   g_pro = BNPro{scsh, ld, act};
 }
 
+// Pre-split weights for the NEXT fp32 forward / dgrad call (then cleared by
+// the caller): an image of the same tensor with every 8 consecutive elements
+// stored as [8 x bf16 hi | 8 x bf16 lo] (32 B, the optimizer writes it,
+// optim: cer_adam_step_split), so its byte offsets equal the fp32 tensor's
+// and the B-operand staging skips the hi/lo split.  Used only by the aligned
+// (fast) kernels; fallbacks keep reading the fp32 weights.
+static const void* g_wsplit = nullptr;
+static int64_t g_wsplit_stride = 0;
+
+CER_API void cer_conv_set_wsplit(const void* wsplit, int64_t stride) {
+  g_wsplit = wsplit;
+  g_wsplit_stride = stride;
+}
+
 __device__ __forceinline__ float pro_act(float v, int act) {
   return act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (act ? fmaxf(v, 0.f) : v);
 }
@@ -1911,7 +1925,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out
-template <int BM, int BN, int GM, bool PRO = false>
+template <int BM, int BN, int GM, bool PRO = false, bool WS = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
@@ -2015,7 +2029,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < B_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      if constexpr (WS) {            // pre-split weight image: (hi, lo) as loaded
+        h = rb[s][2 * i];
+        l = rb[s][2 * i + 1];
+      } else {
+        split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      }
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -2033,7 +2052,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM>
+template <int BM, int BN, int GM, bool WS = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
@@ -2108,7 +2127,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      if constexpr (WS) {            // pre-split weight image: (hi, lo) as loaded
+        h = rb[s][2 * i];
+        l = rb[s][2 * i + 1];
+      } else {
+        split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      }
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
       *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
     }
@@ -2432,15 +2456,19 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
-static void launch_nt32_t(const NTParams& p, int G, bool fast, hipStream_t stream) {
+static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, hipStream_t stream) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
-  if (fast)
-    if (p.pro.scsh)
-      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
-    else
-      igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
-  else
+  if (!fast)
     igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (p.pro.scsh)
+    if (ws)
+      igemm_nt32<BM, BN, GM_FWD, true, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (ws)
+    igemm_nt32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+  else
+    igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
 }
 
 static bool nt_fast32(const NTParams& p) {
@@ -2455,6 +2483,11 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   const bool fast = nt_fast32(p);
   p.pro = g_pro;
   if (p.pro.scsh && !fast) return (int)hipErrorInvalidValue;
+  const bool ws = fast && g_wsplit != nullptr;
+  if (ws) {
+    p.w = reinterpret_cast<const bf16_t*>(g_wsplit);
+    p.w_gstride = g_wsplit_stride;
+  }
   const int v = fp32_variant(choose(0, p.M, p.N, p.K, G, false));
   set_splits(p, G, v, KS);
   if (nslab) {
@@ -2463,9 +2496,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = (int)((p.M + bm - 1) / bm);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, stream); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, stream); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, stream); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, stream); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, stream); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, ws, stream); break;
   }
   return (int)hipGetLastError();
 }
@@ -2606,11 +2639,17 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 }
 
 template <int BM, int BN>
-static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream) {
+static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, bool ws,
+                          hipStream_t stream) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
   if (strided)
-    igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    if (ws)
+      igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    else
+      igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+  else if (ws)
+    igemm_nn32<BM, BN, GM_DG1, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
   else
     igemm_nn32<BM, BN, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
 }
@@ -2675,10 +2714,15 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
     }
     if (f32) {
+      const bool ws = g_wsplit != nullptr;
+      if (ws) {
+        p.w = reinterpret_cast<const bf16_t*>(g_wsplit);
+        p.w_gstride = g_wsplit_stride;
+      }
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, ws, stream); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, ws, stream); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, ws, stream); break;
       }
       return (int)hipGetLastError();
     }

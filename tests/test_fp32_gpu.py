@@ -55,6 +55,7 @@ def _make(specs, G, seed=0):
             a.master_view(s).uniform_(-0.5, 1.5)
         if s.kind == "running_var":
             a.master_view(s).uniform_(0.5, 2.0)
+    a.sync_work()
     return a, {s.name: ParamRef(a, s) for s in specs}
 
 
@@ -122,6 +123,68 @@ def test_conv_fp32_vs_fp64(case):
     print("conv", case, "rel err y/dx/dw = %.2e %.2e %.2e" % e)
     assert max(e) < TOL, e
     assert _fp32_conv_ran()
+
+
+def _split_ref(p):
+    """fp32 -> the pre-split image [8 x bf16 hi | 8 x bf16 lo] per 8 values
+    (round-to-nearest-even bf16, as the kernels' cvt), as int32 words."""
+    p = p.contiguous()
+    hi = p.to(torch.bfloat16)
+    lo = (p - hi.float()).to(torch.bfloat16)
+    n = p.shape[-1]
+    img = torch.cat([hi.view(*p.shape[:-1], n // 8, 8), lo.view(*p.shape[:-1], n // 8, 8)], -1)
+    return img.reshape(*p.shape[:-1], 2 * n).view(torch.int32)
+
+
+def test_presplit_weight_image_tracks_params():
+    """Arena.wsplit == split(params) after init, after an Adam step and after
+    a host-side write + sync_work (the image the fp32 conv kernels read)."""
+    from cerebro_ds_kpgi_amd.ops.optim import optimizer_step
+    spec = ParamSpec("w", (64, 3, 3, 64), "weight", fan_in=576)
+    a, refs = _make([spec], 3)
+    if a.wsplit is None:
+        pytest.skip("CER_W_SPLIT=0")
+    assert torch.equal(a.wsplit, _split_ref(a.params))
+    for g in range(3):
+        a.set_hparams(g, 1e-3, 1e-4)
+    a.grad.normal_()
+    optimizer_step(a, "adam")
+    torch.cuda.synchronize()
+    assert torch.equal(a.wsplit, _split_ref(a.params))
+    a.params[1].mul_(0.5)
+    a.sync_work(1)
+    assert torch.equal(a.wsplit, _split_ref(a.params))
+
+
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[2], CONV_CASES[4], CONV_CASES[8]])
+def test_conv_presplit_weights_match_in_kernel_split(case):
+    """The conv fwd / dgrad with the pre-split image give the same result as
+    splitting the fp32 weights in the kernel (same rounding; only split-K
+    accumulation order may differ)."""
+    B, H, W, cin, cout, k, s, p, G = case
+    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+    a, refs = _make([spec], G)
+    if a.wsplit is None:
+        pytest.skip("CER_W_SPLIT=0")
+    torch.manual_seed(1)
+    x = torch.randn(B, H, W, G * cin, device="cuda")
+    outs = []
+    for use in (True, False):
+        keep = a.wsplit
+        if not use:
+            a.wsplit = None
+        try:
+            xx = x.clone().requires_grad_(True)
+            y = P.conv2d(xx, refs["w"], s, p)
+            torch.manual_seed(3)
+            y.backward(torch.randn_like(y))
+            torch.cuda.synchronize()
+            outs.append((y.detach(), xx.grad))
+        finally:
+            a.wsplit = keep
+    e = (_rel(outs[0][0], outs[1][0]), _rel(outs[0][1], outs[1][1]))
+    print("presplit", case, "rel diff y/dx = %.2e %.2e" % e)
+    assert max(e) < 1e-6, e
 
 
 @pytest.mark.parametrize("act,res,stem", [(True, False, False), (True, True, False),
