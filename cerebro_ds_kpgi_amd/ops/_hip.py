@@ -316,7 +316,12 @@ def _splitk_ready(device):
 
 # fp32 mode: register-staged 3-pass kernels only (an LDS-DMA id maps to its
 # register-staged twin in conv.hip), so only these ids are distinct
-FP32_VARIANTS = (0, 1, 2, 6, 7, 8)
+# fp32 variants per op: the forward also has the LDS-DMA ring kernels
+# (conv.hip pipe_nt32: 3-5, split-K 9-11); dgrad / wgrad register-staged only
+# (CER_FP32_RING=0 leaves the ring kernels out of the forward autotune)
+FP32_VARIANTS = {0: tuple(range(12)) if os.environ.get("CER_FP32_RING", "1") != "0"
+                 else (0, 1, 2, 6, 7, 8),
+                 1: (0, 1, 2, 6, 7, 8), 2: (0, 1, 2, 6, 7, 8)}
 
 
 def _select(op, key, launch, dtype, after_tune=None):
@@ -330,7 +335,7 @@ def _select(op, key, launch, dtype, after_tune=None):
     if v is None:
         v = -1
         if _tune_enabled() and not torch.cuda.is_current_stream_capturing():
-            cands = FP32_VARIANTS if dtype == torch.float32 else range(NVARIANTS)
+            cands = FP32_VARIANTS[op] if dtype == torch.float32 else range(NVARIANTS)
             v = _autotune(op, launch, after=after_tune, variants=cands)
         _TUNED[(op, key)] = v
     lib().cer_conv_set_variant(op, v)

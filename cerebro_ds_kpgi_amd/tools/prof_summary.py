@@ -27,7 +27,7 @@ FAMILIES = [
     ("adam (fused, flat arena)", r"adam"),
     ("softmax-CE + metrics", r"softmax_ce"),
     ("batch gather (HBM store)", r"gather_images"),
-    ("memset/copy (runtime)", r"__amd_rocclr|fillBuffer|copyBuffer"),
+    ("memset/copy (runtime)", r"__amd_rocclr|fillBuffer|copyBuffer|cer_fill_kernel"),
     ("torch elementwise glue", r"at::native"),
 ]
 
@@ -58,14 +58,17 @@ def _rows(con, last_steps):
     return sorted(rows, key=lambda r: -r[2])
 
 
+def family(name):
+    for label, pat in FAMILIES:
+        if re.search(pat, name):
+            return label
+    return "other"
+
+
 def _families(rows):
     fam = {}
     for name, calls, dur, avg in rows:
-        key = "other"
-        for label, pat in FAMILIES:
-            if re.search(pat, name):
-                key = label
-                break
+        key = family(name)
         f = fam.setdefault(key, [0, 0.0])
         f[0] += calls
         f[1] += dur

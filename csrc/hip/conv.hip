@@ -1687,39 +1687,69 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const
 #ifndef CER_FP32_PF
 #define CER_FP32_PF 2
 #endif
+#ifndef CER_FP32_PF_SMALL
+#define CER_FP32_PF_SMALL CER_FP32_PF
+#endif
+#ifndef CER_FP32_PF_BIG
+#define CER_FP32_PF_BIG 1
+#endif
 template <int BM, int BN>
-constexpr int fp32_sets() { return BM * BN > 128 * 64 ? 1 : CER_FP32_PF; }
+constexpr int fp32_sets() {
+  return BM * BN > 128 * 64 ? CER_FP32_PF_BIG : BM * BN > 64 * 64 ? CER_FP32_PF : CER_FP32_PF_SMALL;
+}
 using RS0 = std::integral_constant<int, 0>;
 
 template <int SETS, typename Load, typename Store, typename Mma>
 __device__ __forceinline__ void kloop32(int k0, int k1, Load&& load, Store&& store, Mma&& mma) {
-  using RS1 = std::integral_constant<int, (SETS > 1 ? 1 : 0)>;
-  load(k0, RS0{});
-  store(0, RS0{});
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, (1 % SETS)>;
+  using I2 = std::integral_constant<int, (2 % SETS)>;
+  using I3 = std::integral_constant<int, (3 % SETS)>;
+  load(k0, I0{});
+  store(0, I0{});
   if constexpr (SETS > 1) {
-    // loads past k1 are issued anyway (their offsets are out of range, the
-    // buffer loads return zeros): no branch around a load, so the compiler
-    // keeps counted vmcnt waits instead of draining at every join
-    load(k0 + 1, RS1{});
+    // register ring of SETS sets: the loads of step k + SETS are issued (into
+    // the set step k just emptied) before the MFMAs of step k and land in LDS
+    // at the end of step k + SETS - 1, so SETS steps of MFMA work cover the
+    // load latency.  Loads past k1 are issued anyway (out-of-range offsets,
+    // the buffer loads return zeros): no branch around a load, so the
+    // compiler keeps counted vmcnt waits instead of draining at every join;
+    // the breaks below are loop exits only.
+    load(k0 + 1, I1{});
+    if constexpr (SETS > 2) load(k0 + 2, I2{});
+    if constexpr (SETS > 3) load(k0 + 3, I3{});
     __syncthreads();
-    for (int kt = k0; kt < k1; kt += 2) {
-      load(kt + 2, RS0{});
-      mma(0);
-      store(1, RS1{});
+    auto step = [&](int k, auto U, auto U1) {
+      load(k + SETS, U);
+      const int buf = (k - k0) & 1;
+      mma(buf);
+      store(buf ^ 1, U1);
       __syncthreads();
+    };
+    for (int kt = k0; kt < k1; kt += SETS) {
+      step(kt, I0{}, I1{});
       if (kt + 1 >= k1) break;
-      load(kt + 3, RS1{});
-      mma(1);
-      store(0, RS0{});
-      __syncthreads();
+      if constexpr (SETS == 2) {
+        step(kt + 1, I1{}, I0{});
+      } else {
+        step(kt + 1, I1{}, I2{});
+        if (kt + 2 >= k1) break;
+        if constexpr (SETS == 3) {
+          step(kt + 2, I2{}, I0{});
+        } else {
+          step(kt + 2, I2{}, I3{});
+          if (kt + 3 >= k1) break;
+          step(kt + 3, I3{}, I0{});
+        }
+      }
     }
   } else {
     __syncthreads();
     for (int kt = k0; kt < k1; ++kt) {
       const int cur = (kt - k0) & 1;
-      if (kt + 1 < k1) load(kt + 1, RS0{});
+      if (kt + 1 < k1) load(kt + 1, I0{});
       mma(cur);
-      if (kt + 1 < k1) store(cur ^ 1, RS0{});
+      if (kt + 1 < k1) store(cur ^ 1, I0{});
       __syncthreads();
     }
   }
@@ -2048,6 +2078,120 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
 #undef SA
 #undef SB
+}
+
+// ---- fp32 LDS-DMA ring (forward): operand tiles go global -> LDS as fp32
+// by buffer_load ... lds (no VGPR staging, no ds_write pass) into an S-stage
+// ring; each wave splits its fragments into (hi, lo) bf16 right after the
+// ds_read.  A 32-deep fp32 stage has the byte geometry of a 64-deep bf16
+// stage (rows of 8 swizzled 16-B chunks), so the DMA addressing and the
+// ring driver are the bf16 pipe_nt's.  The split moves from the staging
+// pass (once per element) to the fragment reads (once per element per wave
+// reading it: 2x the cvt work) in exchange for the LDS write traffic, which
+// costs 2.5x a read per byte on the VGPR -> LDS path.  Requires Cg % 32 == 0.
+template <int BM, int BN>
+__device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                             int lane, f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  const int fr = lane & 15, fc = lane >> 4;
+  bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int row = wn * TN + 16 * j + fr;
+    const uint4 x0 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 2 * fc));
+    const uint4 x1 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 2 * fc + 1));
+    uint4 h, l;
+    split_hi_lo(x0, x1, h, l);
+    bh[j] = __builtin_bit_cast(bf16x8, h);
+    bl[j] = __builtin_bit_cast(bf16x8, l);
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int row = wm * TM + 16 * i + fr;
+    const uint4 x0 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 2 * fc));
+    const uint4 x1 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 2 * fc + 1));
+    uint4 h, l;
+    split_hi_lo(x0, x1, h, l);
+    ah[i] = __builtin_bit_cast(bf16x8, h);
+    al[i] = __builtin_bit_cast(bf16x8, l);
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+}
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
+  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
+  constexpr int STAGE = (BM + BN) * BK;             // bf16 units = (BM + BN) x 32 fp32
+  constexpr int EPI = 8 * BN;
+  constexpr int LDS_ELEMS = S * STAGE > EPI ? S * STAGE : EPI;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
+  int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = work % p.splits;
+  work /= p.splits;
+  const int cfg = work / tiles, tile = work - cfg * tiles;
+  const KRange kr = split_range<KS>(p, split);
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const float* abase = reinterpret_cast<const float*>(p.a.src) + (int64_t)cfg * p.a.cfg_off;
+  const float* wbase = reinterpret_cast<const float*>(p.w) + (int64_t)cfg * p.w_gstride;
+  const auto rA = make_rsrc(abase, p.a.bytes);
+  const auto rB = make_rsrc(wbase, (uint32_t)p.N * (uint32_t)p.K * 4u);
+
+  RowA arow[AJ];
+  int achan[AJ];
+  uint32_t boff[BJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    const int row = (wid * AJ + j) * 8 + (lane >> 3);
+    achan[j] = 4 * ((lane & 7) ^ ((row >> 1) & 7));
+    arow[j] = row_init<GM_FWD>(p.a, m0 + row, p.M);
+  }
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    const int row = (wid * BJ + j) * 8 + (lane >> 3);
+    const int n = n0 + row;
+    boff[j] = n < p.N ? (uint32_t)(n * p.K + 4 * ((lane & 7) ^ ((row >> 1) & 7))) * 4u : OOB;
+  }
+  // tap / channel of the next K tile to issue (Cg % 32 == 0: a 32-deep tile
+  // never straddles taps)
+  int tc = (kr.kt0 * KS) % p.a.Cg, tr = (kr.kt0 * KS) / p.a.Cg;
+  int ts = tr % p.a.kw;
+  tr /= p.a.kw;
+  auto issue = [&](int kt, int st) {
+    bf16_t* sa = lds + st * STAGE;
+    bf16_t* sb = sa + BM * BK;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+      glds16(rA, sa + (wid * AJ + j) * 512, a_off<GM_FWD, 4>(p.a, arow[j], tr, ts, tc + achan[j]),
+             0);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j)
+      glds16(rB, sb + (wid * BJ + j) * 512, boff[j], (uint32_t)kt * (KS * 4));
+    tc += KS;
+    if (tc == p.a.Cg) {
+      tc = 0;
+      if (++ts == p.a.kw) {
+        ts = 0;
+        ++tr;
+      }
+    }
+  };
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
+    mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+  });
+  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
 }
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
@@ -2456,9 +2600,18 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
-static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, hipStream_t stream) {
+static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, int kind,
+                          hipStream_t stream) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
-  if (!fast)
+  if (kind == 1) {
+    // 128x128: two stages keep 2 workgroups per CU (3 x 32 KiB would not)
+    if constexpr (BM * BN <= 128 * 64)
+      if (p.K / KS >= 3) {
+        pipe_nt32<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(p);
+        return;
+      }
+    pipe_nt32<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
+  } else if (!fast)
     igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
   else if (p.pro.scsh)
     if (ws)
@@ -2478,6 +2631,8 @@ static bool nt_fast32(const NTParams& p) {
 
 static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 
+// fp32 forward variants: 0-2 register-staged, 3-5 LDS-DMA ring (pipe_nt32),
+// 6-8 register-staged split-K, 9-11 ring split-K (v % 3 = tile shape)
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   if (p.fin.cnt) return (int)hipErrorInvalidValue;   // fused finalize: bf16 path only
   const bool fast = nt_fast32(p);
@@ -2488,7 +2643,11 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     p.w = reinterpret_cast<const bf16_t*>(g_wsplit);
     p.w_gstride = g_wsplit_stride;
   }
-  const int v = fp32_variant(choose(0, p.M, p.N, p.K, G, false));
+  // the ring kernel has no prologue / pre-split-weight form
+  const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh && !ws;
+  int v = choose(0, p.M, p.N, p.K, G, ring_ok);
+  if (!fast) v = fp32_variant(v);
+  const int kind = (v / 3) & 1;
   set_splits(p, G, v, KS);
   if (nslab) {
     int bm, bn;
@@ -2496,9 +2655,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = (int)((p.M + bm - 1) / bm);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, stream); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, stream); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, ws, stream); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, kind, stream); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, kind, stream); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, ws, kind, stream); break;
   }
   return (int)hipGetLastError();
 }

@@ -125,6 +125,30 @@ def test_conv_fp32_vs_fp64(case):
     assert _fp32_conv_ran()
 
 
+@pytest.mark.parametrize("v", [3, 4, 5, 9, 10, 11])
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[2], CONV_CASES[5],
+                                  CONV_CASES[7], (2, 9, 11, 32, 40, 3, 2, 1, 2)])
+def test_conv_fwd_lds_ring_fp32_vs_fp64(case, v):
+    """The fp32 LDS-DMA ring forward kernels (pipe_nt32, every tile shape,
+    with and without split-K), pinned, vs an fp64 conv."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    B, H, W, cin, cout, k, s, p, G = case
+    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+    a, refs = _make([spec], G)
+    torch.manual_seed(1)
+    x = torch.randn(B, H, W, G * cin, device="cuda")
+    _hip.conv_set_variant(0, v)
+    try:
+        y = P.conv2d(x, refs["w"], s, p)
+        torch.cuda.synchronize()
+    finally:
+        _hip.conv_set_variant(0, -1)
+    y64 = F.conv2d(_nchw(x.double()), _w64(refs["w"]), None, s, p, 1, G)
+    e = _rel(y, _nhwc(y64))
+    print("ring fwd", case, v, "rel err %.2e" % e)
+    assert e < TOL, e
+
+
 def _split_ref(p):
     """fp32 -> the pre-split image [8 x bf16 hi | 8 x bf16 lo] per 8 values
     (round-to-nearest-even bf16, as the kernels' cvt), as int32 words."""
