@@ -314,14 +314,16 @@ def _splitk_ready(device):
     _SPLITK["_current"] = key
 
 
-# fp32 mode: register-staged 3-pass kernels only (an LDS-DMA id maps to its
-# register-staged twin in conv.hip), so only these ids are distinct
 # fp32 variants per op: the forward also has the LDS-DMA ring kernels
 # (conv.hip pipe_nt32: 3-5, split-K 9-11); dgrad / wgrad register-staged only
-# (CER_FP32_RING=0 leaves the ring kernels out of the forward autotune)
-FP32_VARIANTS = {0: tuple(range(12)) if os.environ.get("CER_FP32_RING", "1") != "0"
-                 else (0, 1, 2, 6, 7, 8),
-                 1: (0, 1, 2, 6, 7, 8), 2: (0, 1, 2, 6, 7, 8)}
+# (CER_FP32_RING=0 leaves the ring kernels out of the forward autotune).
+# 12-23 are the 32x32x16-MFMA ("wide") twins of ids 0-11 of every op
+# (CER_FP32_WIDE=0 leaves them out).
+_FWD32 = tuple(range(12)) if os.environ.get("CER_FP32_RING", "1") != "0" else (0, 1, 2, 6, 7, 8)
+_REG32 = (0, 1, 2, 6, 7, 8)
+FP32_VARIANTS = {0: _FWD32, 1: _REG32, 2: (0, 1, 2)}
+if os.environ.get("CER_FP32_WIDE", "1") != "0":
+    FP32_VARIANTS = {op: vs + tuple(12 + v for v in vs) for op, vs in FP32_VARIANTS.items()}
 
 
 def _select(op, key, launch, dtype, after_tune=None):
@@ -349,7 +351,7 @@ def _autotune(op, launch, reps=3, passes=None, after=None, variants=None):
     if passes is None:
         passes = int(os.environ.get("CER_TUNE_PASSES", "2"))
     variants = list(range(NVARIANTS) if variants is None else variants)
-    best_t = [None] * NVARIANTS
+    best_t = dict.fromkeys(variants)
     for _ in range(max(1, passes)):
         for v in variants:
             L.cer_conv_set_variant(op, v)

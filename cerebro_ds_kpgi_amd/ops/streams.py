@@ -20,6 +20,12 @@ are plain stream/event operations, so a captured HIP graph keeps the fork /
 join as parallel branches.  Small steps (the one-config-per-GPU case at 8
 GPUs) leave most CUs idle during a dgrad; the wgrads fill them.
 
+Chunked batches (``CER_WGB_CHUNK=n``, default 0 = one batch at the end):
+every n queued layers the batch launched so far goes to the side stream
+(forked from the current stream at that point), so the multi-layer wgrad
+kernels of the upper layers run while the dgrad / BN-backward chain of the
+lower ones is still issuing; ``join`` waits for them before the optimizer.
+
 Tensors read by a side-stream launch are ``record_stream``-ed so the caching
 allocator does not hand their memory to the main stream while the wgrad may
 still read it.  ``CER_WGRAD_STREAM=0`` keeps everything on one stream.
@@ -36,8 +42,10 @@ _PENDING = set()
 
 _BATCH = os.environ.get("CER_WGRAD_BATCH", "1") != "0"
 _BATCH_VARIANT = int(os.environ.get("CER_WGB_VARIANT", "1"))   # reg 128x128 (A/B in profiles/)
+_CHUNK = int(os.environ.get("CER_WGB_CHUNK", "0"))
 _DEFER = 0
 _HELD = []          # operands of queued wgrads (alive until the flush)
+_NQ = 0             # layers queued since the last flush
 
 
 def batching():
@@ -46,7 +54,18 @@ def batching():
 
 
 def hold(*tensors):
+    """Keep a queued layer's operands alive until its batch is launched; with
+    ``CER_WGB_CHUNK`` every n-th layer launches the batch on the side stream."""
+    global _NQ
     _HELD.extend(t for t in tensors if t is not None)
+    _NQ += 1
+    if _CHUNK > 0 and _NQ >= _CHUNK and torch.cuda.is_available():
+        flush_wgrad(side=True)
+
+
+def set_chunk(n):
+    global _CHUNK
+    _CHUNK = int(n)
 
 
 def set_batch_variant(v):
@@ -70,11 +89,23 @@ def deferred_wgrad(enabled=True):
                 flush_wgrad()
 
 
-def flush_wgrad(discard=False):
+def flush_wgrad(discard=False, side=False):
+    global _NQ
     if not _HELD:
         return
     from . import _hip
-    rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 1 if discard else 0, _hip._stream())
+    _NQ = 0
+    if side and not discard:
+        cur = torch.cuda.current_stream()
+        dev = cur.device.index
+        st = _side(dev)
+        st.wait_stream(cur)              # the fork: every queued dy is issued by now
+        rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 0, _hip.c_p(st.cuda_stream))
+        for t in _HELD:
+            t.record_stream(st)
+        _PENDING.add(dev)
+    else:
+        rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 1 if discard else 0, _hip._stream())
     del _HELD[:]
     _hip._check(rc, "cer_wgrad_batch_flush")
 

@@ -98,35 +98,53 @@ def bench_shape(shape, G, iters, dtype=torch.bfloat16, miopen=True):
 VARIANTS = {0: "reg64", 1: "reg128", 2: "reg128x64", 3: "dma64", 4: "dma128", 5: "dma128x64"}
 
 
-def sweep(shapes, G, iters):
-    """Time every kernel variant of every op on every shape (HIP only)."""
+def _vname(v):
+    """conv.hip variant id -> name (fp32 forward: 12-23 = 32x32x16-MFMA twins)."""
+    w, v = ("w", v - 12) if v >= 12 else ("", v)
+    return "{}{}{}{}".format(w, "sk" if v >= 6 else "", "dma" if (v // 3) & 1 else "reg",
+                             ("64", "128", "128x64")[v % 3])
+
+
+def sweep(shapes, G, iters, dtype=torch.bfloat16, ops_sel=(0, 1, 2)):
+    """Time every kernel variant of every op on every shape (HIP only).
+    Returns the rows plus, per op, the count-weighted step time of the best
+    variant per shape among ids < 12 ("narrow") and among all ids."""
     out = []
+    tot = collections.defaultdict(float)
     for shape, count in shapes.items():
         B, H, W, cin, cout, k, st, pad = shape
         if cin % 8:
             continue
         spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
-        a = Arena(ModelLayout([spec]), G, "cuda", torch.bfloat16)
+        a = Arena(ModelLayout([spec]), G, "cuda", dtype)
         for g in range(G):
             a.init_model(g, g)
         ref = ParamRef(a, spec)
-        x = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
+        x = torch.randn(B, H, W, G * cin, device="cuda").to(dtype)
         Ho = (H + 2 * pad - k) // st + 1
         Wo = (W + 2 * pad - k) // st + 1
-        dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(torch.bfloat16)
+        dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(dtype)
         row = {"shape": shape, "count": count}
         ops = {0: lambda: _hip.conv2d_fwd(x, ref, st, pad),
                1: lambda: _hip.conv2d_dgrad(dy, ref, x.shape, st, pad),
                2: lambda: _hip.conv2d_wgrad(x, dy, ref, st, pad)}
-        for op, fn in ops.items():
-            for v in VARIANTS:
+        for op in ops_sel:
+            fn = ops[op]
+            vs = _hip.FP32_VARIANTS[op] if dtype == torch.float32 else tuple(VARIANTS)
+            times = {}
+            for v in vs:
                 _hip.conv_set_variant(op, v)
-                row["{}:{}".format(op, VARIANTS[v])] = _time(fn, iters)
+                times[v] = _time(fn, iters)
+                row["{}:{}".format(op, _vname(v))] = times[v]
             _hip.conv_set_variant(op, -1)
-            row["{}:auto".format(op)] = _time(fn, iters)
+            narrow = min(t for v, t in times.items() if v < 12)
+            tot["{}:narrow".format(op)] += count * narrow
+            tot["{}:all".format(op)] += count * min(times.values())
+            row["{}:best".format(op)] = _vname(min(times, key=times.get))
         out.append(row)
-        print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()}),
+        print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()}),
               flush=True)
+    print("SWEEP_TOTAL_MS", json.dumps({k: round(v, 3) for k, v in tot.items()}), flush=True)
     return out
 
 
@@ -138,11 +156,13 @@ def main(argv=None):
     ap.add_argument("--json", default="")
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant per shape")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--ops", default="0,1,2", help="ops to sweep: 0 fwd, 1 dgrad, 2 wgrad")
     a = ap.parse_args(argv)
     dtype = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     backend.set_backend("hip")
     if a.sweep:
-        rows = sweep(resnet50_shapes(a.B), a.G, a.iters)
+        rows = sweep(resnet50_shapes(a.B), a.G, a.iters, dtype,
+                     tuple(int(o) for o in a.ops.split(",")))
         if a.json:
             with open(a.json, "w") as f:
                 json.dump(rows, f, indent=1, default=str)

@@ -1693,9 +1693,16 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const
 #ifndef CER_FP32_PF_BIG
 #define CER_FP32_PF_BIG 1
 #endif
-template <int BM, int BN>
+// The wide (32x32x16) 128x128 forward holds ~45 fewer VGPRs than the
+// 16x16x32 one (169 vs 215 at one set), but a second set still spills (256
+// VGPRs + 28-204 B scratch), so it stays at one (knob kept for A/B builds).
+#ifndef CER_FP32W_PF_BIG
+#define CER_FP32W_PF_BIG 1
+#endif
+template <int BM, int BN, bool WIDE = false>
 constexpr int fp32_sets() {
-  return BM * BN > 128 * 64 ? CER_FP32_PF_BIG : BM * BN > 64 * 64 ? CER_FP32_PF : CER_FP32_PF_SMALL;
+  return BM * BN > 128 * 64 ? (WIDE ? CER_FP32W_PF_BIG : CER_FP32_PF_BIG)
+                            : BM * BN > 64 * 64 ? CER_FP32_PF : CER_FP32_PF_SMALL;
 }
 using RS0 = std::integral_constant<int, 0>;
 
@@ -1953,9 +1960,368 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   }
 }
 
+// ---- wide-MFMA form of the fp32 forward (v_mfma_f32_32x32x16_bf16) --------
+// Same staging, LDS images and K loop as the 16x16x32 kernels; only the
+// fragment reads, the accumulator layout and the epilogue differ.  Why: the
+// fp32 kernels are bound by the VALU work of the hi/lo split, which can only
+// issue in the cycles an MFMA leaves the SIMD's vector port free -- 8 of the
+// 16 cycles of a 16x16x32 but 24 of the 32 of a 32x32x16 (MI355X_MICROARCH
+// "vector-instruction ISSUE cost").  Per stage the same FLOPs therefore leave
+// 1.5x the VALU slack for the split (e.g. 128x128: 2304 vs 1536 cycles per
+// wave-step against ~1700 of split work).
+// Operand maps (32x32x16): lane l (r = l & 31, h = l >> 5) holds
+// X[row r][k = 8h + j]; the weight fragment goes FIRST, so D[n][m] comes out
+// with the output row m = r on the lane and channels 8q + 4h + e (q = reg >> 2,
+// e = reg & 3) in the registers: one 16-B store per register quad.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int BM, int BN, bool WIDE>
+struct AccT {
+  using type = f32x4[BM / 32][BN / 32];
+};
+template <int BM, int BN>
+struct AccT<BM, BN, true> {
+  using type = f32x16[BM / 64][BN / 64];
+};
+
+template <int BM, int BN>
+__device__ __forceinline__ void zero_accw(f32x16 (&acc)[BM / 64][BN / 64]) {
+#pragma unroll
+  for (int i = 0; i < BM / 64; ++i)
+#pragma unroll
+    for (int j = 0; j < BN / 64; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+}
+
+__device__ __forceinline__ f32x16 mfma3w(const bf16x8& xh, const bf16x8& xl, const bf16x8& yh,
+                                         const bf16x8& yl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, yh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, yl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, yh, acc, 0, 0, 0);
+}
+
+// NT x NT images (hi in chunks 0-3, lo in 4-7): two 16-deep substeps
+template <int BM, int BN>
+__device__ __forceinline__ void mma3w_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                         int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
+      al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 2 * s + h));
+      bl[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 4 + 2 * s + h));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma3w(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+  }
+}
+
+// fp32 ring images (32 fp32 per row as 8 swizzled 16-B chunks): the k of
+// substep s, half h are fp32 16s + 8h .. +7 = chunks 4s + 2h, 4s + 2h + 1
+template <int BM, int BN>
+__device__ __forceinline__ void mma3w_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                              int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * TN + 32 * j + r;
+      const uint4 x0 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 4 * s + 2 * h));
+      const uint4 x1 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 4 * s + 2 * h + 1));
+      uint4 hh, ll;
+      split_hi_lo(x0, x1, hh, ll);
+      bh[j] = __builtin_bit_cast(bf16x8, hh);
+      bl[j] = __builtin_bit_cast(bf16x8, ll);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * TM + 32 * i + r;
+      const uint4 x0 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 4 * s + 2 * h));
+      const uint4 x1 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 4 * s + 2 * h + 1));
+      uint4 hh, ll;
+      split_hi_lo(x0, x1, hh, ll);
+      ah[i] = __builtin_bit_cast(bf16x8, hh);
+      al[i] = __builtin_bit_cast(bf16x8, ll);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma3w(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+  }
+}
+
+// TN image of the wide kernels: [reduction rows][COLS] bf16, 8-B column
+// chunks XOR-swizzled per row so that the 32x32x16 transposed fragment read
+// (tn_frag32: per 32-lane half, rows q = 0..3 x 8 consecutive 8-B chunks) hits
+// 64 distinct banks; the XOR is even, so the 16-B staging stores stay whole.
+//   COLS 128 (256-B rows, all rows on the same banks): chunk ^ 8 (row & 3)
+//   COLS  64 (128-B rows, odd rows on the other half): chunk ^ 8 ((row >> 1) & 1)
+template <int COLS>
+__device__ __forceinline__ int tn_off_w(int row, int col) {  // col multiple of 4
+  const int sw = COLS == 128 ? 8 * (row & 3) : 8 * ((row >> 1) & 1);
+  return row * COLS + 4 * ((col >> 2) ^ sw);
+}
+
+// B-operand map of the 32x32x16 MFMA from a TN image: lane l (r = l & 31,
+// h = l >> 5) gets element j = 0..7 of reduction row row0 + 8h + j at column
+// col_base + r.  ds_read_b64_tr_b16 transposes a 4-row x 16-column block
+// across 16 lanes (lane i supplies row i >> 2, columns 4 (i & 3) .. +3 and
+// receives column i), so each 16-lane group g = (l >> 4) & 1 reads columns
+// col_base + 16g .. +15, rows +0..3 then +4..7.
+template <int COLS>
+__device__ __forceinline__ bf16x8 tn_frag32(const bf16_t* tile, int row0, int col_base, int lane) {
+  const int h = lane >> 5, g = (lane >> 4) & 1, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int col = col_base + 16 * g + 4 * pp;
+  const bf16_t* p0 = tile + tn_off_w<COLS>(row0 + 8 * h + q, col);
+  const bf16_t* p1 = tile + tn_off_w<COLS>(row0 + 8 * h + 4 + q, col);
+  s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+  s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p1));
+  s16x8 t = __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, t);
+}
+
+// A: NT image, B: TN image (tn_off_w; hi rows 0-31, lo rows 32-63) -- dgrad
+template <int BM, int BN>
+__device__ __forceinline__ void mma3w_nn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                         int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
+      al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = tn_frag32<BN>(sb, 16 * s, wn * TN + 32 * j, lane);
+      bl[j] = tn_frag32<BN>(sb, KS + 16 * s, wn * TN + 32 * j, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma3w(bh[j], bl[j], ah[i], al[i], acc[i][j]);
+  }
+}
+
+// both TN images (tn_off_w) -- wgrad: D[n][k], k on the lane
+template <int BM, int BN>
+__device__ __forceinline__ void mma3w_tn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                         int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ah[i] = tn_frag32<BM>(sa, 16 * s, wm * TM + 32 * i, lane);
+      al[i] = tn_frag32<BM>(sa, KS + 16 * s, wm * TM + 32 * i, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = tn_frag32<BN>(sb, 16 * s, wn * TN + 32 * j, lane);
+      bl[j] = tn_frag32<BN>(sb, KS + 16 * s, wn * TN + 32 * j, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = mfma3w(ah[i], al[i], bh[j], bl[j], acc[i][j]);
+  }
+}
+
+// split-K seam of the wide kernels (splitk_reduce with the 32x32 accumulators)
+template <int BM, int BN>
+__device__ __forceinline__ bool splitk_reduce_w(const NTParams& p,
+                                                f32x16 (&acc)[BM / 64][BN / 64], int tile_id,
+                                                int split, int tid) {
+  constexpr int FI = BM / 64, FJ = BN / 64, NA = FI * FJ * 16;
+  __shared__ int sk_flag;
+  float* base = p.skws + (int64_t)tile_id * p.splits * (NA * NTHREADS);
+  float* mine = base + (int64_t)split * (NA * NTHREADS);
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        st_sc1(mine + ((i * FJ + j) * 16 + e) * NTHREADS + tid, acc[i][j][e]);
+  if (!last_arriver(p.skcnt + tile_id, (unsigned)p.splits, &sk_flag)) return false;
+  zero_accw<BM, BN>(acc);
+  for (int sp = 0; sp < p.splits; ++sp) {
+    const float* src = base + (int64_t)sp * (NA * NTHREADS);
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          acc[i][j][e] += ld_sc1(src + ((i * FJ + j) * 16 + e) * NTHREADS + tid);
+  }
+  return true;
+}
+
+// fp32 epilogue of the wide NT / NN kernels (epi32 with the 32x32 layout):
+// out = act(acc + bias) (+ addend), and optionally the forward BN partials
+// (sum, sum^2) or a dgrad output's BN-backward partials (sum dz, sum dz*xhat,
+// BNBwdEpi) per (M tile, channel).  Walks one 32-channel block j at a time so
+// only 16 channels of per-channel state are live next to the accumulators.
+// xch: LDS scratch of 4*BN floats.
+template <int BM, int BN, bool BSTAT = false>
+__device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM / 64][BN / 64],
+                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
+                                       int lane, int tid) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+  float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
+  const float* adb =
+      p.addend ? reinterpret_cast<const float*>(p.addend) + (int64_t)cfg * p.N : nullptr;
+  const BNBwdEpi& bb = p.bb;
+  const bool fstat = p.stats != nullptr;
+  const bool bstat = BSTAT && bb.part != nullptr;   // compile-time off in the forward kernels
+  const bool vec = ((p.N | p.ldc) & 3) == 0;
+  const float* zb = bstat ? reinterpret_cast<const float*>(bb.z) + (int64_t)cfg * p.N : nullptr;
+  const float* yb = bstat && bb.ym == 1 ? reinterpret_cast<const float*>(bb.y) + (int64_t)cfg * p.N
+                                       : nullptr;
+  int64_t orow[FM];
+  bool rok[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * TM + 32 * i + r;
+    rok[i] = m < p.M;
+    orow[i] = m;
+    if (p.o_st > 1 && rok[i]) {
+      const RowPos rp = decode_row(m, p.M, p.a);
+      orow[i] = ((int64_t)rp.b * p.o_H + (int64_t)rp.y * p.o_st) * p.o_W + (int64_t)rp.x * p.o_st;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int nb = n0 + wn * TN + 32 * j + 4 * h;       // + 8q + e
+    float bc[4][4], s[4][4], q[4][4], mu[4][4], is[4][4], sc[4][4], sh[4][4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = nb + 8 * g + e;
+        const int nn = n < p.N ? n : p.N - 1;
+        bc[g][e] = p.bias
+                       ? reinterpret_cast<const float*>(p.bias)[(int64_t)cfg * p.bias_gstride + nn]
+                       : 0.f;
+        s[g][e] = q[g][e] = 0.f;
+        mu[g][e] = is[g][e] = sc[g][e] = sh[g][e] = 0.f;
+        if (bstat) {
+          const int64_t c = (int64_t)cfg * p.N + nn;
+          mu[g][e] = bb.mean[c];
+          is[g][e] = bb.invstd[c];
+          if (bb.ym == 2) {                   // YM_Z: the forward's scale / shift
+            const float ga = reinterpret_cast<const float*>(bb.gamma)[cfg * bb.gstride + nn];
+            const float be = reinterpret_cast<const float*>(bb.beta)[cfg * bb.bstride + nn];
+            sc[g][e] = is[g][e] * ga;
+            sh[g][e] = be - mu[g][e] * sc[g][e];
+          }
+        }
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (!rok[i]) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = nb + 8 * g;
+        if (n >= p.N) continue;
+        const int64_t go = orow[i] * p.ldc + n;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][4 * g + e] + bc[g][e];
+          v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
+        }
+        if (vec) {
+          if (adb) {
+            const float4 a = *reinterpret_cast<const float4*>(adb + go);
+            v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          }
+          *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) {
+              if (adb) v[e] += adb[go + e];
+              obase[go + e] = v[e];
+            }
+        }
+        if (fstat) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s[g][e] += v[e];
+            q[g][e] += v[e] * v[e];
+          }
+        } else if (bstat) {      // host-gated: vec
+          const float4 z4 = *reinterpret_cast<const float4*>(zb + go);
+          const float zv[4] = {z4.x, z4.y, z4.z, z4.w};
+          float yv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (yb) {
+            const float4 y4 = *reinterpret_cast<const float4*>(yb + go);
+            yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float dz = v[e];
+            if (bb.ym == 2)
+              dz = (zv[e] * sc[g][e] + sh[g][e] + 0.f) > 0.f ? dz : 0.f;
+            else if (bb.ym == 1)
+              dz = bb.act == 6 ? ((yv[e] > 0.f && yv[e] < 6.f) ? dz : 0.f) : (yv[e] > 0.f ? dz : 0.f);
+            s[g][e] += dz;
+            q[g][e] += dz * (zv[e] - mu[g][e]) * is[g][e];
+          }
+        }
+      }
+    }
+    if (fstat || bstat) {
+      // rows live on the 32 lanes of equal h: DPP sum over 16, then xor 16
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float sm = row16_sum(s[g][e]);
+          float sq = row16_sum(q[g][e]);
+          sm += __shfl_xor(sm, 16, 64);
+          sq += __shfl_xor(sq, 16, 64);
+          if (r == 0) {
+            const int nl = wn * TN + 32 * j + 8 * g + 4 * h + e;
+            xch[(wm * 2) * BN + nl] = sm;
+            xch[(wm * 2 + 1) * BN + nl] = sq;
+          }
+        }
+    }
+  }
+  if (!fstat && !bstat) return;
+  __syncthreads();
+  float* dst = (fstat ? p.stats : bb.part) + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  for (int t = tid; t < 2 * BN; t += NTHREADS) {
+    const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
+    if (n < p.N) dst[(int64_t)qd * p.ldc + n] = xch[qd * BN + nl] + xch[(2 + qd) * BN + nl];
+  }
+}
+
 // forward (and the unaligned-dgrad fallback through transposed weights):
-// y = act(im2col(x) W^T + b), fp32 in / out
-template <int BM, int BN, int GM, bool PRO = false, bool WS = false>
+// y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
+template <int BM, int BN, int GM, bool PRO = false, bool WS = false, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
@@ -1993,7 +2359,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = fp32_sets<BM, BN>();
+  constexpr int SETS = fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
   // BN-apply prologue: (scale, shift) of the chunk's 8 channels per set and
   // the per-chunk "not padding" flags; loaded unconditionally (a null table
@@ -2070,12 +2436,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     }
   };
 
-  f32x4 acc[BM / 32][BN / 32];
-  zero_acc<BM, BN>(acc);
-  kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
-          [&](int cur) { mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
-  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  typename AccT<BM, BN, WIDE>::type acc;
+  if constexpr (WIDE) {
+    zero_accw<BM, BN>(acc);
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
+                  [&](int cur) { mma3w_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
+    if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  } else {
+    zero_acc<BM, BN>(acc);
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
+                  [&](int cur) { mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
+    if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  }
 #undef SA
 #undef SB
 }
@@ -2121,7 +2495,7 @@ __device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb,
     for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(bh[j], bl[j], ah[i], al[i], acc[i][j]);
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
   constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
   constexpr int STAGE = (BM + BN) * BK;             // bf16 units = (BM + BN) x 32 fp32
@@ -2185,18 +2559,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
       }
     }
   };
-  f32x4 acc[BM / 32][BN / 32];
-  zero_acc<BM, BN>(acc);
-  ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
-    mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
-  });
-  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  typename AccT<BM, BN, WIDE>::type acc;
+  if constexpr (WIDE) {
+    zero_accw<BM, BN>(acc);
+    ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
+      mma3w_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+    });
+    if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  } else {
+    zero_acc<BM, BN>(acc);
+    ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
+      mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+    });
+    if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  }
 }
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WS = false>
+template <int BM, int BN, int GM, bool WS = false, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
@@ -2277,22 +2660,38 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
       } else {
         split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       }
-      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
-      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+      if constexpr (WIDE) {
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
+      } else {
+        *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
+        *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+      }
     }
   };
 
-  f32x4 acc[BM / 32][BN / 32];
-  zero_acc<BM, BN>(acc);
-  kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, [&](int cur) {
-    mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane, acc);
-  });
-  if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-  epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  typename AccT<BM, BN, WIDE>::type acc;
+  if constexpr (WIDE) {
+    zero_accw<BM, BN>(acc);
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, [&](int cur) {
+      mma3w_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane,
+                       acc);
+    });
+    if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32w<BM, BN, true>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  } else {
+    zero_acc<BM, BN>(acc);
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, [&](int cur) {
+      mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane,
+                      acc);
+    });
+    if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
+    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+  }
 }
 
 // wgrad tile body (fp32 operands): dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]
-template <int BM, int BN, int GM, bool PRO = false>
+template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
 __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf16_t* lds) {
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
   constexpr int A_CH = KS * A_CPR / NTHREADS, B_CH = KS * B_CPR / NTHREADS;
@@ -2387,8 +2786,13 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
       const int row = a_row0 + A_RSTEP * i;
       uint4 h, l;
       split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
-      *reinterpret_cast<uint4*>(sa + tn_off<BM>(row, a_col)) = h;
-      *reinterpret_cast<uint4*>(sa + tn_off<BM>(row + KS, a_col)) = l;
+      if constexpr (WIDE) {
+        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row, a_col)) = h;
+        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row + KS, a_col)) = l;
+      } else {
+        *reinterpret_cast<uint4*>(sa + tn_off<BM>(row, a_col)) = h;
+        *reinterpret_cast<uint4*>(sa + tn_off<BM>(row + KS, a_col)) = l;
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -2396,55 +2800,88 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
       uint4 h, l;
       if constexpr (pro) pro_apply(rb[s][2 * i], rb[s][2 * i + 1], rs, bv[s][i], p.pro.act);
       split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
-      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
-      *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+      if constexpr (WIDE) {
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
+      } else {
+        *reinterpret_cast<uint4*>(sb + tn_off<BN>(row, b_col)) = h;
+        *reinterpret_cast<uint4*>(sb + tn_off<BN>(row + KS, b_col)) = l;
+      }
     }
   };
 
-  f32x4 acc[BM / 32][BN / 32];
-  zero_acc<BM, BN>(acc);
   const int MT = (me - ms + KS - 1) / KS;
-  kloop32<SETS>(0, MT, load_tiles, store_tiles, [&](int cur) {
-    mma3_tn<BM, BN>(lds + cur * (BK * BM), lds + 2 * BK * BM + cur * (BK * BN), wa, wb, lane, acc);
-  });
-
-  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
-  const int fr = lane & 15, fc = lane >> 4;
   const bool split_k = p.splits > 1;
+  if constexpr (WIDE) {
+    f32x16 acc[BM / 64][BN / 64];
+    zero_accw<BM, BN>(acc);
+    kloop32<SETS>(0, MT, load_tiles, store_tiles, [&](int cur) {
+      mma3w_tn<BM, BN>(lds + cur * (BK * BM), lds + 2 * BK * BM + cur * (BK * BN), wa, wb, lane,
+                       acc);
+    });
+    // D[n][k]: k = lane & 31 (32 consecutive k per register: 128-B stores)
+    constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+    const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = n0 + wa * TM + 16 * i + 4 * fc + e;
-        const int k = k0 + wb * TN + 16 * j + fr;
-        if (n < p.N && k < p.K) {
-          float* d = dwb + (int64_t)n * p.K + k;
-          if (split_k)
-            atomicAdd(d, acc[i][j][e]);
-          else
-            *d = acc[i][j][e];
+        for (int e = 0; e < 16; ++e) {
+          const int n = n0 + wa * TM + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+          const int k = k0 + wb * TN + 32 * j + r;
+          if (n < p.N && k < p.K) {
+            float* d = dwb + (int64_t)n * p.K + k;
+            if (split_k)
+              atomicAdd(d, acc[i][j][e]);
+            else
+              *d = acc[i][j][e];
+          }
         }
-      }
+  } else {
+    f32x4 acc[BM / 32][BN / 32];
+    zero_acc<BM, BN>(acc);
+    kloop32<SETS>(0, MT, load_tiles, store_tiles, [&](int cur) {
+      mma3_tn<BM, BN>(lds + cur * (BK * BM), lds + 2 * BK * BM + cur * (BK * BN), wa, wb, lane,
+                      acc);
+    });
+    constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+    const int fr = lane & 15, fc = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + wa * TM + 16 * i + 4 * fc + e;
+          const int k = k0 + wb * TN + 16 * j + fr;
+          if (n < p.N && k < p.K) {
+            float* d = dwb + (int64_t)n * p.K + k;
+            if (split_k)
+              atomicAdd(d, acc[i][j][e]);
+            else
+              *d = acc[i][j][e];
+          }
+        }
+  }
 }
 
-template <int BM, int BN, int GM, bool PRO = false>
+template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
-  wgrad_reg_body32<BM, BN, GM, PRO>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
+  wgrad_reg_body32<BM, BN, GM, PRO, WIDE>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
 }
 
 // batched fp32 weight gradients (see wgrad_batch)
-template <int BM, int BN, bool PRO = false>
+template <int BM, int BN, bool PRO = false, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
   const int work = xcd_remap(blockIdx.x, gridDim.x);
   int i = 0;
   while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
   const WGParams p = b.p[i];
-  wgrad_reg_body32<BM, BN, GM_FWD, PRO>(p, work - b.start[i], lds);
+  wgrad_reg_body32<BM, BN, GM_FWD, PRO, WIDE>(p, work - b.start[i], lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -2510,7 +2947,10 @@ static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) 
 static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
   if (g_variant[op] >= 0) {
     int v = g_variant[op];
+    const int wide = v >= 12 ? 12 : 0;              // fp32 32x32x16-MFMA twins: 12-23
+    v -= wide;
     if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
+    v += wide;
     if (((v / 3) & 1) && !pipe_ok) v -= 3;
     return v;
   }
@@ -2581,6 +3021,7 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   const bool fast = nt_fast(p);
   const bool pipe_ok = fast && p.a.Cg % 64 == 0;
   int v = choose(0, p.M, p.N, p.K, G, pipe_ok);
+  if (v >= 12) v -= 12;                             // wide ids: fp32 kernels only
   if (!fast) v = (v >= 6 ? 6 : 0) + v % 3;         // generic gather: register-staged only
   set_splits(p, G, v);
   const int kind = (v / 3) & 1;
@@ -2601,8 +3042,23 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, int kind,
-                          hipStream_t stream) {
+                          hipStream_t stream, bool wide = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  if (wide) {                      // 32x32x16 MFMA twins (no prologue / pre-split forms)
+    if (kind == 1) {
+      if constexpr (BM * BN <= 128 * 64)
+        if (p.K / KS >= 3) {
+          pipe_nt32<BM, BN, 3, true><<<grid, NTHREADS, 0, stream>>>(p);
+          return;
+        }
+      pipe_nt32<BM, BN, 2, true><<<grid, NTHREADS, 0, stream>>>(p);
+    } else if (!fast) {
+      igemm_nt32<BM, BN, GM_SLOW, false, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+    } else {
+      igemm_nt32<BM, BN, GM_FWD, false, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+    }
+    return;
+  }
   if (kind == 1) {
     // 128x128: two stages keep 2 workgroups per CU (3 x 32 KiB would not)
     if constexpr (BM * BN <= 128 * 64)
@@ -2632,7 +3088,8 @@ static bool nt_fast32(const NTParams& p) {
 static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 
 // fp32 forward variants: 0-2 register-staged, 3-5 LDS-DMA ring (pipe_nt32),
-// 6-8 register-staged split-K, 9-11 ring split-K (v % 3 = tile shape)
+// 6-8 register-staged split-K, 9-11 ring split-K (v % 3 = tile shape);
+// 12-23: the same twelve on the 32x32x16 MFMA (wide) kernels
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   if (p.fin.cnt) return (int)hipErrorInvalidValue;   // fused finalize: bf16 path only
   const bool fast = nt_fast32(p);
@@ -2646,6 +3103,14 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   // the ring kernel has no prologue / pre-split-weight form
   const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh && !ws;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
+  bool wide = false;
+  if (v >= 12) {
+    v -= 12;
+    // no prologue / pre-split-weight forms; BN-backward statistics (the
+    // unaligned-dgrad fallback) only in the NN kernels' wide epilogue
+    wide = !p.pro.scsh && !ws && p.bb.part == nullptr;
+    if (((v / 3) & 1) && !ring_ok) v -= 3;
+  }
   if (!fast) v = fp32_variant(v);
   const int kind = (v / 3) & 1;
   set_splits(p, G, v, KS);
@@ -2655,9 +3120,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = (int)((p.M + bm - 1) / bm);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, kind, stream); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, kind, stream); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, ws, kind, stream); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, kind, stream, wide); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, kind, stream, wide); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, ws, kind, stream, wide); break;
   }
   return (int)hipGetLastError();
 }
@@ -2799,9 +3264,16 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, bool ws,
-                          hipStream_t stream) {
+                          hipStream_t stream, bool wide = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if (wide) {                      // 32x32x16 MFMA twins (no pre-split-weight form)
+    if (strided)
+      igemm_nn32<BM, BN, GM_DGS, false, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    else
+      igemm_nn32<BM, BN, GM_DG1, false, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    return;
+  }
   if (strided)
     if (ws)
       igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
@@ -2859,6 +3331,11 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       strided = st > 1;
     }
     int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
+    bool wide = false;
+    if (v >= 12) {                        // fp32 32x32x16-MFMA twins of 0-11
+      v -= 12;
+      wide = f32 && g_wsplit == nullptr;
+    }
     if (f32) v = fp32_variant(v);
     set_splits(p, G, v, f32 ? KS : BK);
     const int kind = (v / 3) & 1;
@@ -2879,9 +3356,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
         p.w_gstride = g_wsplit_stride;
       }
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, ws, stream); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, ws, stream); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, ws, stream); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, ws, stream, wide); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, ws, stream, wide); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, ws, stream, wide); break;
       }
       return (int)hipGetLastError();
     }
@@ -2927,7 +3404,8 @@ CER_API int cer_conv_dgrad_f32(const float* dy, int B, int Ho, int Wo, int Cout,
 }
 
 static int wg_variant(int N, int K, int G, bool fast) {
-  const int v = choose(2, 0, N, K, G, fast);
+  int v = choose(2, 0, N, K, G, fast);
+  if (v >= 12) v -= 12;                             // same tile as its wide twin
   return fast ? v : v % 3;
 }
 
@@ -2991,12 +3469,18 @@ CER_API int cer_conv_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
 
 // ---- fp32 weight gradients (register-staged 3-pass kernels) ----------------
 template <int BM, int BN>
-static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t stream) {
+static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t stream,
+                          bool wide = false) {
   p.m_per_split = ((p.Mred + splits - 1) / splits + BK - 1) / BK * BK;
   splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
   p.splits = splits;
   dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
-  if (fast)
+  if (wide && !p.pro.scsh)   // 32x32x16-MFMA twins
+    if (fast)
+      igemm_wgrad32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else
+      igemm_wgrad32<BM, BN, GM_SLOW, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (fast)
     if (p.pro.scsh)
       igemm_wgrad32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     else
@@ -3011,11 +3495,12 @@ static bool wg_fast32(int Cin, int Cout, const WGParams& p) {
 }
 
 static void run_wg32(WGParams p, int G, int splits, bool fast, hipStream_t stream) {
-  const int v = choose(2, 0, p.N, p.K, G, false) % 3;
-  switch (v) {
-    case 0: launch_wg32_t<64, 64>(p, G, fast, splits, stream); break;
-    case 1: launch_wg32_t<128, 128>(p, G, fast, splits, stream); break;
-    default: launch_wg32_t<128, 64>(p, G, fast, splits, stream); break;
+  const int vv = choose(2, 0, p.N, p.K, G, false);
+  const bool wide = vv >= 12;
+  switch (vv % 3) {
+    case 0: launch_wg32_t<64, 64>(p, G, fast, splits, stream, wide); break;
+    case 1: launch_wg32_t<128, 128>(p, G, fast, splits, stream, wide); break;
+    default: launch_wg32_t<128, 64>(p, G, fast, splits, stream, wide); break;
   }
 }
 
@@ -3107,7 +3592,7 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   return p.splits;
 }
 
-template <int BM, int BN, bool PRO>
+template <int BM, int BN, bool PRO, bool WIDE = false>
 static void wgb32_launch_sel(hipStream_t stream) {
   int idx[4096];
   int n = 0;
@@ -3124,13 +3609,16 @@ static void wgb32_launch_sel(hipStream_t stream) {
       tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[k]);
     }
     bt.start[bt.n] = tot;
-    if (tot > 0) wgrad_batch32<BM, BN, PRO><<<tot, NTHREADS, 0, stream>>>(bt);
+    if (tot > 0) wgrad_batch32<BM, BN, PRO, WIDE><<<tot, NTHREADS, 0, stream>>>(bt);
   }
 }
 
 template <int BM, int BN>
-static int wgb32_launch(hipStream_t stream) {
-  wgb32_launch_sel<BM, BN, false>(stream);
+static int wgb32_launch(hipStream_t stream, bool wide = false) {
+  if (wide)                  // no prologue form of the wide kernels
+    wgb32_launch_sel<BM, BN, false, true>(stream);
+  else
+    wgb32_launch_sel<BM, BN, false>(stream);
   wgb32_launch_sel<BM, BN, true>(stream);
   return (int)hipGetLastError();
 }
@@ -3158,7 +3646,7 @@ static int wgb_launch(hipStream_t stream) {
 CER_API int cer_wgrad_batch_flush(int v, int discard, hipStream_t stream) {
   int rc = 0;
   if (!discard && g_wgq_n > 0) {
-    switch (v) {
+    switch (v >= 12 ? v % 3 : v) {
       case 1: rc = wgb_launch<128, 128, 0>(stream); break;
       case 2: rc = wgb_launch<128, 64, 0>(stream); break;
       case 3: rc = wgb_launch<64, 64, 1>(stream); break;
@@ -3168,10 +3656,11 @@ CER_API int cer_wgrad_batch_flush(int v, int discard, hipStream_t stream) {
     }
   }
   if (!discard && g_wgq32_n > 0 && rc == 0) {
+    const bool wide = v >= 12;   // fp32: 12-14 = 32x32x16-MFMA tiles
     switch (v % 3) {         // fp32: the register-staged tile of the same shape
-      case 1: rc = wgb32_launch<128, 128>(stream); break;
-      case 2: rc = wgb32_launch<128, 64>(stream); break;
-      default: rc = wgb32_launch<64, 64>(stream); break;
+      case 1: rc = wgb32_launch<128, 128>(stream, wide); break;
+      case 2: rc = wgb32_launch<128, 64>(stream, wide); break;
+      default: rc = wgb32_launch<64, 64>(stream, wide); break;
     }
   }
   g_wgq_n = 0;

@@ -94,8 +94,11 @@ def test_async_greedy_makespan_matches_simulator(tmp_path):
                             for s in range(200))
     sim_r = simulate_rotation(RUNTIMES, world)
     print("measured", got, "simulated greedy", sim_g, "rotation", sim_r)
-    # work conserving: within 10 % of the event simulation of the same policy
-    assert got["greedy_async"] <= 1.10 * sim_g
+    # work conserving: within 10 % of the event simulation of the same policy.
+    # A loaded host (pytest -n) stretches every sleep-based job alike; the
+    # lock-step rotation run measures that stretch, so scale the bound by it
+    slow = max(1.0, got["rotation_lockstep"] / sim_r)
+    assert got["greedy_async"] <= 1.10 * sim_g * slow
     # and faster than lock-step rotation (simulated and measured)
     assert got["greedy_async"] < got["rotation_lockstep"]
     assert got["rotation_lockstep"] >= 0.95 * sim_r

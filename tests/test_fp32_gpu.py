@@ -149,6 +149,108 @@ def test_conv_fwd_lds_ring_fp32_vs_fp64(case, v):
     assert e < TOL, e
 
 
+@pytest.mark.parametrize("v", list(range(12, 24)))
+@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[2], CONV_CASES[5],
+                                  CONV_CASES[6], CONV_CASES[7], CONV_CASES[8],
+                                  (2, 9, 11, 32, 40, 3, 2, 1, 2), (3, 6, 5, 8, 12, 3, 1, 0, 3)])
+def test_conv_fwd_wide_mfma_fp32_vs_fp64(case, v):
+    """The 32x32x16-MFMA forward twins (igemm_nt32 / pipe_nt32 WIDE: every
+    tile shape, register-staged and ring, with and without split-K, aligned
+    and generic gathers), pinned, vs an fp64 conv."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    B, H, W, cin, cout, k, s, p, G = case
+    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+    a, refs = _make([spec], G)
+    torch.manual_seed(1)
+    x = torch.randn(B, H, W, G * cin, device="cuda")
+    _hip.conv_set_variant(0, v)
+    try:
+        y = P.conv2d(x, refs["w"], s, p)
+        torch.cuda.synchronize()
+    finally:
+        _hip.conv_set_variant(0, -1)
+    y64 = F.conv2d(_nchw(x.double()), _w64(refs["w"]), None, s, p, 1, G)
+    e = _rel(y, _nhwc(y64))
+    print("wide fwd", case, v, "rel err %.2e" % e)
+    assert e < TOL, e
+
+
+@pytest.mark.parametrize("v", [12, 13, 14, 18, 19, 20])
+def test_conv_bn_unit_wide_fwd_fp32_vs_fp64(v):
+    """BN statistics from the wide forward epilogue (epi32w's 32-lane row
+    reduction): the fused unit with the forward pinned to a wide variant."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(0, v)
+    try:
+        test_conv_bn_unit_fp32_vs_fp64(True, True, False)
+    finally:
+        _hip.conv_set_variant(0, -1)
+
+
+@pytest.mark.parametrize("vd,vw", [(12, 12), (13, 13), (14, 14), (18, 12), (19, 13), (20, 14)])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_bwd_wide_mfma_fp32_vs_fp64(case, vd, vw):
+    """The 32x32x16-MFMA dgrad (igemm_nn32 WIDE, tn_frag32 transposed reads of
+    the tn_off_w image) and wgrad (wgrad_reg_body32 WIDE) twins, pinned, on
+    every conv case (incl. split-K, strided, generic-gather fallbacks)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(1, vd)
+    _hip.conv_set_variant(2, vw)
+    try:
+        test_conv_fp32_vs_fp64(case)
+    finally:
+        _hip.conv_set_variant(1, -1)
+        _hip.conv_set_variant(2, -1)
+
+
+@pytest.mark.parametrize("vb", [12, 13, 14])
+def test_wgrad_batch_wide_fp32_vs_fp64(vb):
+    """Batched (deferred) fp32 weight gradients on the wide kernels
+    (cer_wgrad_batch_flush with ids 12-14) over three layers at once."""
+    from cerebro_ds_kpgi_amd.ops import streams
+    cases = [CONV_CASES[0], CONV_CASES[1], CONV_CASES[5]]
+    keep = streams._BATCH_VARIANT
+    streams.set_batch_variant(vb)
+    try:
+        errs = []
+        made = []
+        for (B, H, W, cin, cout, k, s, p, G) in cases:
+            spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+            a, refs = _make([spec], G)
+            torch.manual_seed(1)
+            x = torch.randn(B, H, W, G * cin, device="cuda").requires_grad_(True)
+            made.append((a, refs, x, (B, H, W, cin, cout, k, s, p, G)))
+        with streams.deferred_wgrad():
+            for a, refs, x, c in made:
+                y = P.conv2d(x, refs["w"], c[6], c[7])
+                torch.manual_seed(3)
+                y.backward(torch.randn_like(y))
+        torch.cuda.synchronize()
+        for a, refs, x, (B, H, W, cin, cout, k, s, p, G) in made:
+            torch.manual_seed(3)
+            w64 = _w64(refs["w"]).requires_grad_(True)
+            y64 = F.conv2d(_nchw(x.detach().double()), w64, None, s, p, 1, G)
+            y64.backward(_nchw(torch.randn(y64.shape[0], y64.shape[2], y64.shape[3], y64.shape[1],
+                                           device="cuda").double()))
+            dw64 = w64.grad.view(G, cout, cin, k, k).permute(0, 1, 3, 4, 2)
+            errs.append(_rel(a.grad.view(G, -1)[:, :dw64[0].numel()], dw64.reshape(G, -1)))
+    finally:
+        streams.set_batch_variant(keep)
+    print("wgrad batch wide", vb, ["%.1e" % e for e in errs])
+    assert max(errs) < TOL, errs
+
+
+@pytest.mark.parametrize("vd", [12, 13, 14])
+def test_bn_link_dgrad_epilogue_wide_fp32(vd):
+    """BN-backward partials from the wide dgrad epilogue (epi32w BSTAT)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(1, vd)
+    try:
+        test_bn_link_dgrad_epilogue_fp32()
+    finally:
+        _hip.conv_set_variant(1, -1)
+
+
 def _split_ref(p):
     """fp32 -> the pre-split image [8 x bf16 hi | 8 x bf16 lo] per 8 values
     (round-to-nearest-even bf16, as the kernels' cvt), as int32 words."""

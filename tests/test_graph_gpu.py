@@ -27,10 +27,21 @@ def _hip_backend():
     yield
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_fwd_bwd_graph_replays_equal_eager(dtype):
+@pytest.mark.parametrize("dtype,chunk", [(torch.float32, 0), (torch.bfloat16, 0),
+                                         (torch.float32, 16), (torch.float32, 5)])
+def test_fwd_bwd_graph_replays_equal_eager(dtype, chunk):
     """Captured fwd+bwd (no optimizer, fixed batch): every replay's gradient
-    arena equals the eager one (same kernels, same variants)."""
+    arena equals the eager one (same kernels, same variants).  chunk > 0:
+    the batched wgrads launch every ``chunk`` layers on the side stream
+    (streams.CER_WGB_CHUNK), a fork / join inside the captured graph; the
+    eager gradient must also match the one-batch-at-the-end gradient."""
+    try:
+        _graph_replays(dtype, chunk)
+    finally:
+        streams.set_chunk(0)
+
+
+def _graph_replays(dtype, chunk):
     from cerebro_ds_kpgi_amd.models import create_model_from_mst
     from cerebro_ds_kpgi_amd.ops.loss import softmax_ce
     from cerebro_ds_kpgi_amd.runtime import Arena
@@ -58,6 +69,15 @@ def test_fwd_bwd_graph_replays_equal_eager(dtype):
     step()
     torch.cuda.synchronize()
     ge = a.grad.clone()
+    if chunk:
+        streams.set_chunk(chunk)
+        for _ in range(2):
+            a.master.copy_(m0)
+            step()
+        torch.cuda.synchronize()
+        rel = ((a.grad.double() - ge.double()).norm() / ge.double().norm()).item()
+        assert rel < 1e-3, rel
+        ge = a.grad.clone()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
         step()
