@@ -62,14 +62,19 @@ def init_distributed(backend="auto", device_type="auto", timeout_s=1800):
     if device_type == "auto":
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # one process per GPU; more local ranks than GPUs (a rehearsal of the
+        # multi-rank path on a small box) wrap around onto the same devices
+        ndev = torch.cuda.device_count()
+        dev_idx = local_rank % ndev if ndev > 0 else local_rank
+        torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
     else:
         device = torch.device("cpu")
     if world <= 1:
         return DistContext(0, 1, 0, device, None, None)
     if backend == "auto":
-        backend = "nccl" if device.type == "cuda" else "gloo"
+        backend = os.environ.get("CER_DIST_BACKEND",
+                                 "nccl" if device.type == "cuda" else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     kw = {}
