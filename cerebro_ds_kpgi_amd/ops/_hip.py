@@ -204,6 +204,7 @@ _SIGS.update({
     "cer_wgrad_batch_add": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                             c_p, c_i64],
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
+    "cer_wgrad_batch_set_grid": [c_i],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_set_fold": [c_i],

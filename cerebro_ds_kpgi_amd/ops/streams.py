@@ -43,9 +43,19 @@ _PENDING = set()
 _BATCH = os.environ.get("CER_WGRAD_BATCH", "1") != "0"
 _BATCH_VARIANT = int(os.environ.get("CER_WGB_VARIANT", "1"))   # reg 128x128 (A/B in profiles/)
 _CHUNK = int(os.environ.get("CER_WGB_CHUNK", "0"))
+# blocks of a side-stream wgrad batch (0 = one per work item): a small grid
+# walks its tiles persistently on a few CUs, leaving the rest to the dgrad chain
+_SIDE_GRID = int(os.environ.get("CER_WGB_GRID", "0"))
+# adaptive split (deferred_wgrad(side_frac=f)): the first f of a step's layers
+# (by the previous step's count) go to the side stream as one batch on
+# SPLIT_GRID blocks; the rest launch at the end as usual
+_SPLIT_GRID = int(os.environ.get("CER_WGB_SPLIT_GRID", "96"))
 _DEFER = 0
 _HELD = []          # operands of queued wgrads (alive until the flush)
 _NQ = 0             # layers queued since the last flush
+_NSTEP = 0          # layers queued in the current deferred block
+_LAST = {}          # ... in the previous block of the same key
+_CUR = (0, 0)       # (chunk, grid) in force for the current block
 
 
 def batching():
@@ -56,16 +66,25 @@ def batching():
 def hold(*tensors):
     """Keep a queued layer's operands alive until its batch is launched; with
     ``CER_WGB_CHUNK`` every n-th layer launches the batch on the side stream."""
-    global _NQ
+    global _NQ, _NSTEP
     _HELD.extend(t for t in tensors if t is not None)
     _NQ += 1
-    if _CHUNK > 0 and _NQ >= _CHUNK and torch.cuda.is_available():
+    _NSTEP += 1
+    global _CUR
+    chunk = _CUR[0] if _DEFER else _CHUNK
+    if chunk > 0 and _NQ >= chunk and torch.cuda.is_available():
         flush_wgrad(side=True)
+        if _DEFER and len(_CUR) > 2:           # adaptive split: one side batch per step
+            _CUR = (0, 0)
 
 
-def set_chunk(n):
-    global _CHUNK
+def set_chunk(n, grid=None):
+    """Side-stream wgrad batches every ``n`` layers (0: off); ``grid`` caps
+    their blocks (None: keep, 0: one block per work item)."""
+    global _CHUNK, _SIDE_GRID
     _CHUNK = int(n)
+    if grid is not None:
+        _SIDE_GRID = int(grid)
 
 
 def set_batch_variant(v):
@@ -74,11 +93,29 @@ def set_batch_variant(v):
 
 
 @contextlib.contextmanager
-def deferred_wgrad(enabled=True):
-    """Queue HIP weight gradients issued inside the block; flush them on exit."""
-    global _DEFER
+def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
+    """Queue HIP weight gradients issued inside the block; flush them on exit.
+
+    ``side_frac`` > 0 (and no ``CER_WGB_CHUNK`` override): once that fraction
+    of the previous block's layer count (same ``key``) is queued, the batch so
+    far launches ONCE on the side stream on a capped grid
+    (``CER_WGB_SPLIT_GRID`` blocks) and overlaps the rest of backward; the
+    remaining layers launch at the end as usual, with the full grid
+    (profiles/r2_ab_wgrad_chunk.md: +2 % with 8 packed configs, slower with 1;
+    a capped grid for the tail batch, or more side batches, lose 10-25 %)."""
+    global _DEFER, _CUR, _NSTEP
     on = enabled and _BATCH
     if on:
+        if _DEFER == 0:
+            if _CHUNK > 0:
+                _CUR = (_CHUNK, _SIDE_GRID)
+            elif side_frac > 0 and _LAST.get(key, 0) > 1:
+                # ONE side batch of the first ceil(frac * n) layers; the rest
+                # launches at the end on the current stream with the full grid
+                _CUR = (-(-int(round(side_frac * 1000)) * _LAST[key] // 1000), _SPLIT_GRID, 1)
+            else:
+                _CUR = (0, 0)
+            _NSTEP = 0
         _DEFER += 1
     try:
         yield
@@ -87,9 +124,11 @@ def deferred_wgrad(enabled=True):
             _DEFER -= 1
             if _DEFER == 0:
                 flush_wgrad()
+                _LAST[key] = _NSTEP
+                _CUR = (0, 0)
 
 
-def flush_wgrad(discard=False, side=False):
+def flush_wgrad(discard=False, side=False, grid=None):
     global _NQ
     if not _HELD:
         return
@@ -100,7 +139,16 @@ def flush_wgrad(discard=False, side=False):
         dev = cur.device.index
         st = _side(dev)
         st.wait_stream(cur)              # the fork: every queued dy is issued by now
-        rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 0, _hip.c_p(st.cuda_stream))
+        L = _hip.lib()
+        if grid is None:
+            grid = _CUR[1] if _DEFER else _SIDE_GRID
+        if grid:
+            L.cer_wgrad_batch_set_grid(grid)
+        try:
+            rc = L.cer_wgrad_batch_flush(_BATCH_VARIANT, 0, _hip.c_p(st.cuda_stream))
+        finally:
+            if grid:
+                L.cer_wgrad_batch_set_grid(0)
         for t in _HELD:
             t.record_stream(st)
         _PENDING.add(dev)

@@ -245,8 +245,11 @@ class _Working(object):
         g = self.group
         gather_batch(g.store, True, self.part_of_row, self.cursor, g.batch_size, self.x, self.y)
         # weight gradients are queued during backward and launched as a few
-        # multi-layer kernels when the block exits (ops.streams)
-        with streams.deferred_wgrad(self.x.device.type == "cuda"):
+        # multi-layer kernels when the block exits (ops.streams); with >=
+        # _SIDE_MIN_G packed configs the first half of them runs on the side
+        # stream during the rest of backward
+        frac = _SIDE_FRAC if self.G >= _SIDE_MIN_G else 0.0
+        with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self)):
             logits = self.net.forward(self.x, True)
             loss = softmax_ce(logits, self.y, self.acc, self.G)
             loss.sum().backward()
@@ -371,6 +374,12 @@ class _Working(object):
             out.append(rec)
         return out
 
+
+# Side-stream share of the batched weight gradients (ops.streams
+# deferred_wgrad side_frac) for packs of at least _SIDE_MIN_G configs
+# (measured: +2 % at 8, +1 % at 4, -3 % at 1 config; r2_ab_wgrad_chunk.md)
+_SIDE_FRAC = float(os.environ.get("CER_WGB_SIDE_FRAC", "0.5"))
+_SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "4"))
 
 # Graph-captured validation (CER_VALID_GRAPH=0 runs it eagerly).  Its round-1
 # failures (invalid eval losses after an epoch boundary) had the same root

@@ -2875,13 +2875,22 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
 
 // batched fp32 weight gradients (see wgrad_batch)
 template <int BM, int BN, bool PRO = false, bool WIDE = false>
+// A grid smaller than the batch's work items (cer_wgrad_batch_set_grid: a
+// side-stream batch that should leave most CUs to the dgrad chain) walks the
+// items persistently, block-strided; the full grid takes one item per block
+// in XCD-aware order.
 __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
-  int i = 0;
-  while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
-  const WGParams p = b.p[i];
-  wgrad_reg_body32<BM, BN, GM_FWD, PRO, WIDE>(p, work - b.start[i], lds);
+  const int total = b.start[b.n];
+  const int nwg = (int)gridDim.x;
+  for (int w = blockIdx.x; w < total; w += nwg) {
+    const int work = nwg >= total ? xcd_remap(w, nwg) : w;
+    int i = 0;
+    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
+    const WGParams p = b.p[i];
+    wgrad_reg_body32<BM, BN, GM_FWD, PRO, WIDE>(p, work - b.start[i], lds);
+    if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3604,6 +3613,10 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   return p.splits;
 }
 
+// grid cap of the next fp32 batch flushes (0 = one block per work item)
+static int g_wgb_grid = 0;
+CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
+
 template <int BM, int BN, bool PRO, bool WIDE = false>
 static void wgb32_launch_sel(hipStream_t stream) {
   int idx[4096];
@@ -3621,7 +3634,8 @@ static void wgb32_launch_sel(hipStream_t stream) {
       tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[k]);
     }
     bt.start[bt.n] = tot;
-    if (tot > 0) wgrad_batch32<BM, BN, PRO, WIDE><<<tot, NTHREADS, 0, stream>>>(bt);
+    const int grid = g_wgb_grid > 0 && g_wgb_grid < tot ? g_wgb_grid : tot;
+    if (tot > 0) wgrad_batch32<BM, BN, PRO, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
   }
 }
 

@@ -28,17 +28,22 @@ def _hip_backend():
 
 
 @pytest.mark.parametrize("dtype,chunk", [(torch.float32, 0), (torch.bfloat16, 0),
-                                         (torch.float32, 16), (torch.float32, 5)])
+                                         (torch.float32, 16), (torch.float32, 5),
+                                         (torch.float32, (8, 48)), (torch.float32, "half")])
 def test_fwd_bwd_graph_replays_equal_eager(dtype, chunk):
     """Captured fwd+bwd (no optimizer, fixed batch): every replay's gradient
     arena equals the eager one (same kernels, same variants).  chunk > 0:
     the batched wgrads launch every ``chunk`` layers on the side stream
     (streams.CER_WGB_CHUNK), a fork / join inside the captured graph; the
-    eager gradient must also match the one-batch-at-the-end gradient."""
+    eager gradient must also match the one-batch-at-the-end gradient.
+    (n, g): chunks of n layers whose batches run persistently on g blocks;
+    "half": the adaptive split the runtime uses for packs of >= 4 configs
+    (deferred_wgrad side_frac=0.5: the first half of the previous step's
+    layers on the side stream, capped grid)."""
     try:
         _graph_replays(dtype, chunk)
     finally:
-        streams.set_chunk(0)
+        streams.set_chunk(0, grid=0)
 
 
 def _graph_replays(dtype, chunk):
@@ -57,9 +62,11 @@ def _graph_replays(dtype, chunk):
     y = torch.randint(0, 1000, (G, B), device="cuda", dtype=torch.int32)
     acc = torch.zeros(G, 4, device="cuda")
 
+    frac = [0.0]
+
     def step():
         a.grad.zero_()
-        with streams.deferred_wgrad(True):
+        with streams.deferred_wgrad(True, side_frac=frac[0], key="graph_test"):
             softmax_ce(net.forward(x, True), y, acc, G).sum().backward()
         streams.join()
     m0 = a.master.clone()
@@ -69,8 +76,12 @@ def _graph_replays(dtype, chunk):
     step()
     torch.cuda.synchronize()
     ge = a.grad.clone()
+    if chunk == "half":
+        frac[0] = 0.5
+    elif chunk:
+        n, grid = chunk if isinstance(chunk, tuple) else (chunk, 0)
+        streams.set_chunk(n, grid=grid)
     if chunk:
-        streams.set_chunk(chunk)
         for _ in range(2):
             a.master.copy_(m0)
             step()
