@@ -121,6 +121,20 @@ def adam_step(arena, beta1, beta2, eps, l2):
     _check(rc, "cer_adam_step")
 
 
+def adam_step_range(arena, lo, hi, beta1, beta2, eps, l2, inc_step):
+    """Adam over parameters [lo, hi) of every row on the current stream
+    (fp32 arenas without a shadow / split image)."""
+    L = arena.layout
+    st = arena.state
+    assert arena.work is arena.params and arena.wsplit is None
+    rc = lib().cer_adam_step_range(
+        _ptr(st), st.stride(0), int(lo), int(hi), L.off_m, L.off_v, L.off_step,
+        _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
+        _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)),
+        int(bool(inc_step)), _stream())
+    _check(rc, "cer_adam_step_range")
+
+
 def sgd_step(arena, momentum, l2):
     L = arena.layout
     st = arena.state
@@ -205,6 +219,8 @@ _SIGS.update({
                             c_p, c_i64],
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_set_grid": [c_i],
+    "cer_adam_step_range": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p,
+                            c_p, c_i, c_f, c_f, c_f, c_i, c_i, c_p],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_set_fold": [c_i],
@@ -759,7 +775,7 @@ def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad
         if splits > 0:
             if splits > 1 and not wref.arena.grad_clean:
                 wref.grad().zero_()
-            streams.hold(x, dy)
+            streams.hold(x, dy, grad_ptr=gp)
             return
 
     def launch():

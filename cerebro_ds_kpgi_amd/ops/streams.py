@@ -56,6 +56,8 @@ _NQ = 0             # layers queued since the last flush
 _NSTEP = 0          # layers queued in the current deferred block
 _LAST = {}          # ... in the previous block of the same key
 _CUR = (0, 0)       # (chunk, grid) in force for the current block
+_SPANS = []         # grad pointers of the layers queued since the last flush
+_HOOK = None        # deferred_wgrad(hook=...): pre() before / after(ptrs) behind a side batch
 
 
 def batching():
@@ -63,14 +65,16 @@ def batching():
     return _DEFER > 0
 
 
-def hold(*tensors):
+def hold(*tensors, grad_ptr=None):
     """Keep a queued layer's operands alive until its batch is launched; with
-    ``CER_WGB_CHUNK`` every n-th layer launches the batch on the side stream."""
-    global _NQ, _NSTEP
+    ``CER_WGB_CHUNK`` every n-th layer launches the batch on the side stream.
+    ``grad_ptr``: where the layer's gradient lands (handed to the hook)."""
+    global _NQ, _NSTEP, _CUR
     _HELD.extend(t for t in tensors if t is not None)
+    if grad_ptr is not None:
+        _SPANS.append(grad_ptr)
     _NQ += 1
     _NSTEP += 1
-    global _CUR
     chunk = _CUR[0] if _DEFER else _CHUNK
     if chunk > 0 and _NQ >= chunk and torch.cuda.is_available():
         flush_wgrad(side=True)
@@ -93,7 +97,7 @@ def set_batch_variant(v):
 
 
 @contextlib.contextmanager
-def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
+def deferred_wgrad(enabled=True, side_frac=0.0, key=None, hook=None):
     """Queue HIP weight gradients issued inside the block; flush them on exit.
 
     ``side_frac`` > 0 (and no ``CER_WGB_CHUNK`` override): once that fraction
@@ -102,8 +106,13 @@ def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
     (``CER_WGB_SPLIT_GRID`` blocks) and overlaps the rest of backward; the
     remaining layers launch at the end as usual, with the full grid
     (profiles/r2_ab_wgrad_chunk.md: +2 % with 8 packed configs, slower with 1;
-    a capped grid for the tail batch, or more side batches, lose 10-25 %)."""
-    global _DEFER, _CUR, _NSTEP
+    a capped grid for the tail batch, or more side batches, lose 10-25 %).
+
+    ``hook`` (adaptive split only): ``hook.pre()`` runs on the current stream
+    just before the fork and ``hook.after(grad_ptrs)`` on the side stream right
+    behind the side batch (the runtime starts the optimizer update of the
+    layers whose gradients are final there, runtime/group.py)."""
+    global _DEFER, _CUR, _NSTEP, _HOOK
     on = enabled and _BATCH
     if on:
         if _DEFER == 0:
@@ -116,6 +125,8 @@ def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
             else:
                 _CUR = (0, 0)
             _NSTEP = 0
+            _HOOK = hook if len(_CUR) > 2 else None
+            del _SPANS[:]
         _DEFER += 1
     try:
         yield
@@ -126,6 +137,7 @@ def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
                 flush_wgrad()
                 _LAST[key] = _NSTEP
                 _CUR = (0, 0)
+                _HOOK = None
 
 
 def flush_wgrad(discard=False, side=False, grid=None):
@@ -134,10 +146,15 @@ def flush_wgrad(discard=False, side=False, grid=None):
         return
     from . import _hip
     _NQ = 0
+    spans = list(_SPANS)
+    del _SPANS[:]
     if side and not discard:
         cur = torch.cuda.current_stream()
         dev = cur.device.index
         st = _side(dev)
+        hook = _HOOK if _DEFER else None
+        if hook is not None:
+            hook.pre()
         st.wait_stream(cur)              # the fork: every queued dy is issued by now
         L = _hip.lib()
         if grid is None:
@@ -149,6 +166,9 @@ def flush_wgrad(discard=False, side=False, grid=None):
         finally:
             if grid:
                 L.cer_wgrad_batch_set_grid(0)
+        if hook is not None:
+            with torch.cuda.stream(st):
+                hook.after(spans)
         for t in _HELD:
             t.record_stream(st)
         _PENDING.add(dev)

@@ -185,6 +185,27 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
   return (int)hipGetLastError();
 }
 
+// Adam over the parameter range [lo, hi) of every row (an update split
+// across streams: the range whose gradients are final early runs on a side
+// stream while backward finishes the rest).  inc_step: also advance the step
+// counters (exactly once per step, before any range reads them); fp32
+// compute only (no shadow / split image).
+CER_API int cer_adam_step_range(float* state, int64_t row_stride, int64_t lo, int64_t hi,
+                                int64_t off_m, int64_t off_v, int64_t off_step, float* grad,
+                                int64_t grad_stride, int zero_grad, const float* lr,
+                                const float* wd, int G, float b1, float b2, float eps, int l2,
+                                int inc_step, hipStream_t stream) {
+  if (lo % 8 || hi % 8 || hi < lo) return (int)hipErrorInvalidValue;
+  if (inc_step)
+    adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  if (hi == lo) return (int)hipGetLastError();
+  dim3 grid(cer_blocks((hi - lo) / 8, 256), G);
+  adam_kernel<false><<<grid, 256, 0, stream>>>(state + lo, row_stride, hi - lo, off_m, off_v,
+                                                off_step - lo, grad + lo, grad_stride, zero_grad,
+                                                nullptr, 0, lr, wd, b1, b2, eps, l2);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // SGD with momentum, torch.optim.SGD semantics (dampening 0, no Nesterov):
 //   g += wd * p;  buf = mu * buf + g;  p -= lr * buf
