@@ -219,6 +219,7 @@ _SIGS.update({
                             c_p, c_i64],
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_set_grid": [c_i],
+    "cer_wgrad_batch_set_rows": [c_i],
     "cer_adam_step_range": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p,
                             c_p, c_i, c_f, c_f, c_f, c_i, c_i, c_p],
     "cer_wgrad_batch_pending": [],

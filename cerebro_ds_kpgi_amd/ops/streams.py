@@ -82,6 +82,18 @@ def hold(*tensors, grad_ptr=None):
             _CUR = (0, 0)
 
 
+_ROWS = [None]
+
+
+def set_batch_rows(rows):
+    """Rows of the reduction per split for the next queued fp32/bf16 wgrads
+    (0: the library default, CER_WGB_ROWS or 1024)."""
+    if _ROWS[0] != rows:
+        from . import _hip
+        _hip.lib().cer_wgrad_batch_set_rows(int(rows))
+        _ROWS[0] = rows
+
+
 def set_chunk(n, grid=None):
     """Side-stream wgrad batches every ``n`` layers (0: off); ``grid`` caps
     their blocks (None: keep, 0: one block per work item)."""

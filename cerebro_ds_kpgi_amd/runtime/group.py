@@ -251,6 +251,8 @@ class _Working(object):
         # stream during the rest of backward
         frac = _SIDE_FRAC if self.G >= _SIDE_MIN_G else 0.0
         hook = self._adam_split() if frac else None
+        if self.x.device.type == "cuda" and get_backend() == "hip":
+            streams.set_batch_rows(_WIDE_ROWS if self.G >= _SIDE_MIN_G else 0)
         with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self),
                                     hook=hook):
             logits = self.net.forward(self.x, True)
@@ -403,6 +405,9 @@ class _Working(object):
 # (measured: +2 % at 8, +1 % at 4, -3 % at 1 config; r2_ab_wgrad_chunk.md)
 _SIDE_FRAC = float(os.environ.get("CER_WGB_SIDE_FRAC", "0.5"))
 _SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "4"))
+# wgrad-batch rows per split for those packs (fewer, longer splits: +1 % at
+# 8 configs; one-config packs keep 1024, where 2048 is 1-2.5 % slower)
+_WIDE_ROWS = int(os.environ.get("CER_WGB_ROWS_WIDE", "2048"))
 
 # Optimizer update split across streams with the side wgrad batch (below).
 # Measured neutral-to-slower (profiles/r2_ab_wgrad_chunk.md): off by default.

@@ -3554,6 +3554,12 @@ static int g_wgq32_G[4096];
 static int g_wgq32_n = 0;
 static int g_wgb_rows = 0;
 
+// rows per split of the next queued wgrads (0: CER_WGB_ROWS / 1024); the
+// runtime sets it per packed step (more rows for wider packs, A/B in profiles/)
+CER_API void cer_wgrad_batch_set_rows(int rows) {
+  g_wgb_rows = rows > 0 ? (rows < BK ? BK : rows / BK * BK) : 0;
+}
+
 static int wgb_rows() {
   if (!g_wgb_rows) {
     const char* e = getenv("CER_WGB_ROWS");
