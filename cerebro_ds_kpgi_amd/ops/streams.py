@@ -20,11 +20,18 @@ are plain stream/event operations, so a captured HIP graph keeps the fork /
 join as parallel branches.  Small steps (the one-config-per-GPU case at 8
 GPUs) leave most CUs idle during a dgrad; the wgrads fill them.
 
-Chunked batches (``CER_WGB_CHUNK=n``, default 0 = one batch at the end):
-every n queued layers the batch launched so far goes to the side stream
-(forked from the current stream at that point), so the multi-layer wgrad
-kernels of the upper layers run while the dgrad / BN-backward chain of the
-lower ones is still issuing; ``join`` waits for them before the optimizer.
+Split batches (default for packs of >= 4 configs, ``deferred_wgrad(side_frac=
+0.5)`` from runtime/group.py): once half of the previous step's layer count
+is queued, that batch -- the upper stages' wgrads -- launches ONCE on the
+side stream (forked from the current stream at that point) on a capped,
+persistent grid (``CER_WGB_SPLIT_GRID`` = 96 blocks), so it runs on a slice
+of the CUs while the dgrad / BN-backward chain of the lower stages keeps the
+rest; the remaining layers launch at the end on the current stream with the
+full grid; ``join`` waits for the side batch before the optimizer.  Measured
+(profiles/r2_ab_wgrad_chunk.md): +1.6 % at 8 packed configs, +1.3 % at 4;
+one-config packs keep the single batch (a split costs them 3 %), as do more
+or smaller side batches and capped tail batches (10-25 % slower).
+``CER_WGB_CHUNK=n`` / ``CER_WGB_GRID`` force fixed chunks (A/B only).
 
 Tensors read by a side-stream launch are ``record_stream``-ed so the caching
 allocator does not hand their memory to the main stream while the wgrad may
