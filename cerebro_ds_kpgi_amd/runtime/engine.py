@@ -39,7 +39,6 @@ import collections
 import json
 import math
 import os
-import pickle
 import time
 
 import torch
@@ -49,6 +48,7 @@ from ..data.store import PartitionStore
 from ..models import dataset_of, pack_key
 from ..parallel.hop import execute_moves, plan_moves, validate_plan
 from ..scheduler import make_scheduler
+from ..utils import safe_pickle
 from ..utils.keys import model_key, mst_2_str
 from ..utils.logging import logs
 from ..utils.trace import Tracer
@@ -571,9 +571,9 @@ class MOPEngine(object):
         if lr and os.path.exists(os.path.join(lr, "jobs_info.pkl")):
             # files this framework wrote itself (dump_infos)
             with open(os.path.join(lr, "jobs_info.pkl"), "rb") as f:
-                self.jobs_info = pickle.load(f)
+                self.jobs_info = safe_pickle.load(f)
             with open(os.path.join(lr, "models_info.pkl"), "rb") as f:
-                self.models_info = collections.defaultdict(list, pickle.load(f))
+                self.models_info = collections.defaultdict(list, safe_pickle.load(f))
         for e in sorted(self.jobs_info):
             if e < st["epoch"] or st["epoch_done"]:
                 self._epoch_summary(e)

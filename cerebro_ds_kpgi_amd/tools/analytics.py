@@ -34,9 +34,10 @@ import datetime
 import glob
 import json
 import os
-import pickle
 
 import numpy as np
+
+from ..utils import safe_pickle
 
 TIME_FORMAT = "%Y-%m-%d %H:%M:%S"
 
@@ -117,7 +118,7 @@ def load_models_info(logs_root):
     p = os.path.join(logs_root, "models_info.pkl")
     if os.path.exists(p):
         with open(p, "rb") as f:          # written by runtime.checkpoint.dump_infos
-            return pickle.load(f)
+            return safe_pickle.load(f)
     return {}
 
 

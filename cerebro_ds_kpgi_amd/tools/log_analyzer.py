@@ -29,7 +29,8 @@ import datetime
 import glob
 import json
 import os
-import pickle
+
+from ..utils import safe_pickle
 
 TIME_FORMAT = "%Y-%m-%d %H:%M:%S"
 CATEGORIES = ("initialization", "data_transmission", "model_hopping", "train_valid",
@@ -59,7 +60,7 @@ def _load_jobs(logs_root):
     p = os.path.join(logs_root, "jobs_info.pkl")
     if os.path.exists(p):
         with open(p, "rb") as f:        # written by runtime.checkpoint.dump_infos
-            return pickle.load(f)
+            return safe_pickle.load(f)
     p = os.path.join(logs_root, "jobs_info.json")
     if os.path.exists(p):
         with open(p) as f:
