@@ -708,20 +708,26 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
     wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
 
-    def launch():
+    def launch(out=dx):
         with _WSplit(wref):
             rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
-                                           cin, kh, kw, stride, pad, _ptr(dx), H, W,
+                                           cin, kh, kw, stride, pad, _ptr(out), H, W,
                                            _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
+    # an in-place accumulation (dx IS the addend) must not be repeated by the
+    # autotune's timing launches: those write a scratch dx instead
+    inplace = addend is not None and addend.data_ptr() == dx.data_ptr()
+    tune = (lambda: launch(torch.empty_like(dx))) if inplace else launch
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
-            launch, dy.dtype)
+            tune, dy.dtype)
     launch()
 
 
 def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     """dx of the conv; ``addend`` (same shape and dtype as dx) is added in the
-    GEMM epilogue (the other consumer's gradient of a shared input).
+    GEMM epilogue (the other consumer's gradient of a shared input).  For a
+    strided 1x1 conv the addend is CONSUMED: dx accumulates into its storage
+    (the caller, ops.nn's GradJoin, owns it and uses it nowhere else).
     ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
     output y this conv consumed — the epilogue also computes that BN's
     backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink)."""
@@ -730,11 +736,20 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     _, H, W, _ = xshape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
-    dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
     wp, ws = wref.work_ptr()
     if addend is not None:
         addend = _same(addend, dy)
-        assert addend.shape == dx.shape
+        assert addend.shape == (B, H, W, G * cin)
+    # strided 1x1 dgrad with an addend (the second input gradient of a ResNet
+    # stage's first block): accumulate in place into the addend, which is the
+    # other consumer's freshly computed dx parked in a GradJoin and used
+    # nowhere else -- the kernel then only touches the 1/4 of the pixels it
+    # computes, instead of first copying the whole addend into a new dx
+    if (addend is not None and bnlink is None and kh == 1 and kw == 1 and pad == 0
+            and stride > 1 and addend.is_contiguous()):
+        dx = addend
+    else:
+        dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
     if bnlink is None:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
                            addend, wref=wref)

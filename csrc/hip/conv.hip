@@ -3337,10 +3337,11 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       // rows (b, ho, wo) of dy map to dx pixels (b, ho*st, wo*st); others get 0
       // (or the addend, which the kernel adds on the written pixels)
       const size_t bytes = (size_t)es * B * H * W * G * Cin;
-      if (addend)
-        cer_copy_async(dx, addend, bytes, stream);
-      else
+      if (addend) {
+        if (addend != dx) cer_copy_async(dx, addend, bytes, stream);   // in place: nothing to copy
+      } else {
         cer_zero_async(dx, bytes, stream);
+      }
       p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, Ho, Wo, 1, 1, 1, 0, es);
       p.dgrad = 0;
       p.M = B * Ho * Wo;

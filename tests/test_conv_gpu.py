@@ -542,10 +542,17 @@ def test_dgrad_addend_equals_dgrad_plus_add(case):
     dy = torch.randn(B, Ho, Wo, G * cout, device="cuda").to(torch.bfloat16)
     add = torch.randn(B, H, W, G * cin, device="cuda").to(torch.bfloat16)
     xshape = (B, H, W, G * cin)
-    fused = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add)
+    fused = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add.clone())
     plain = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p) + add
     torch.cuda.synchronize()
     assert torch.equal(fused, plain)
+    if k == 1 and p == 0 and s > 1:
+        # strided 1x1: the addend is consumed, dx accumulates into its storage
+        add2 = add.clone()
+        again = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add2)
+        torch.cuda.synchronize()
+        assert again.data_ptr() == add2.data_ptr()
+        assert torch.equal(again, plain)
 
 
 def test_resnet50_gradjoin_on_gpu(monkeypatch):
