@@ -745,8 +745,10 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     # other consumer's freshly computed dx parked in a GradJoin and used
     # nowhere else -- the kernel then only touches the 1/4 of the pixels it
     # computes, instead of first copying the whole addend into a new dx
-    if (addend is not None and bnlink is None and kh == 1 and kw == 1 and pad == 0
-            and stride > 1 and addend.is_contiguous()):
+    # (a BN link does not change this: conv.hip computes no BN-backward
+    # statistics in a strided dgrad with an addend, the BN runs its own pass)
+    if (addend is not None and kh == 1 and kw == 1 and pad == 0 and stride > 1
+            and addend.is_contiguous()):
         dx = addend
     else:
         dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
