@@ -62,9 +62,21 @@ def init_distributed(backend="auto", device_type="auto", timeout_s=1800):
     if device_type == "auto":
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
-        # one process per GPU; more local ranks than GPUs (a rehearsal of the
-        # multi-rank path on a small box) wrap around onto the same devices
+        # one process per GPU.  More local ranks than GPUs is refused unless
+        # CER_ALLOW_DEVICE_WRAP=1 (a rehearsal of the multi-rank path on a
+        # small box, gloo data plane): the ranks then share devices, and a
+        # result of such a run must not be mistaken for an N-GPU one
         ndev = torch.cuda.device_count()
+        if ndev > 0 and local_rank >= ndev:
+            if os.environ.get("CER_ALLOW_DEVICE_WRAP") != "1":
+                raise RuntimeError(
+                    "local rank {} but only {} GPU(s) visible; set CER_ALLOW_DEVICE_WRAP=1 "
+                    "(with CER_DIST_BACKEND=gloo) to rehearse several ranks per GPU"
+                    .format(local_rank, ndev))
+            import sys
+            sys.stderr.write("cerebro: rank {} (local {}) wraps onto cuda:{} of {} GPU(s) "
+                             "(CER_ALLOW_DEVICE_WRAP rehearsal)\n".format(
+                                 rank, local_rank, local_rank % ndev, ndev))
         dev_idx = local_rank % ndev if ndev > 0 else local_rank
         torch.cuda.set_device(dev_idx)
         device = torch.device("cuda", dev_idx)

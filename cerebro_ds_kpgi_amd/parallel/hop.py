@@ -137,3 +137,39 @@ def warm_p2p(world, rank, device, group=None):
             raise RuntimeError("p2p warm-up: rank {} got {} from {}".format(rank, float(r[0]), peer))
     return len(bufs)
 
+
+
+def pair_groups(world, rank, backend, device):
+    """One process group per unordered rank pair, created collectively (every
+    rank calls ``new_group`` for every pair, in the same order), each warmed
+    by a tiny exchange so no RCCL connection setup lands in a real hop.
+    Returns {peer: group} for this rank.
+
+    Two-rank communicators are what lets the asynchronous hop service run
+    transfers of different pairs concurrently: on one shared communicator
+    RCCL executes point-to-point operations in issue order, so a rank's
+    receive from r-1 and send to r+1 would serialise (and the ring's sends
+    would chain through every rank).  With xGMI every pair of the 8 GPUs has
+    its own link, so concurrent pairs do not share bandwidth either."""
+    links = {}
+    for i in range(world):
+        for j in range(i + 1, world):
+            g = dist.new_group(ranks=[i, j], backend=backend)
+            if rank in (i, j):
+                links[j if rank == i else i] = g
+    # warm every link, pairs in one global order (deadlock-free)
+    for i in range(world):
+        for j in range(i + 1, world):
+            if rank not in (i, j):
+                continue
+            peer = j if rank == i else i
+            s = torch.full((16,), float(rank), device=device)
+            r = torch.empty(16, device=device)
+            ops = [dist.P2POp(dist.isend, s, peer, links[peer], tag=910000 + rank),
+                   dist.P2POp(dist.irecv, r, peer, links[peer], tag=910000 + peer)]
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+            if float(r[0]) != float(peer):
+                raise RuntimeError("hop link warm-up: rank {} got {} from {}".format(
+                    rank, float(r[0]), peer))
+    return links

@@ -183,13 +183,13 @@ class MOPEngine(object):
         self._asched = {}
         self._chan = None
         self._nsession = 0
-        self._hop_pg = None
+        self._hop_links = {}
         if ctx.initialized and not self.task_parallel:
-            # async hops run on their own communicator (and their own thread)
-            import torch.distributed as dist
-            from ..parallel.hop import warm_p2p
-            self._hop_pg = dist.new_group(backend=ctx.backend)
-            warm_p2p(ctx.world, ctx.rank, self.device, group=self._hop_pg)
+            # async hops: one communicator per rank pair (and a stream and a
+            # thread per peer, async_mop.HopService), so transfers between
+            # different pairs run concurrently
+            from ..parallel.hop import pair_groups
+            self._hop_links = pair_groups(ctx.world, ctx.rank, ctx.backend, self.device)
         self.epoch = 0
         self.failures = []
         self._fired = set()
@@ -633,8 +633,9 @@ class MOPEngine(object):
             self._chan = (tcp_client(addr, self.o.ctrl_timeout), addr)
         return Channel(self._chan[0], pfx, self.o.ctrl_timeout, self._chan[1])
 
-    def hop_group(self):
-        return self._hop_pg
+    def hop_links(self):
+        """{peer rank: process group of (this rank, peer)} for the hops."""
+        return self._hop_links
 
     def coord_begin(self):
         self.coord_msts = [dict(m) for m in self.msts]

@@ -202,3 +202,45 @@ def test_async_greedy_requeues_soft_fault(tmp_path):
         out = json.load(f)
     assert out["failures"] and all(f["rank"] == 1 for f in out["failures"])
     assert out["finite"] and set(out["epochs"].values()) == {2}
+
+
+# ---------------------------------------------------------------------------
+def _ring_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
+    ctx = init_distributed(device_type="cpu")
+    eng = _engine(ctx, world, 1, scheduler="rotation", runtime="async", trace=True,
+                  hop_check=True, sim_job_seconds=[0.05], sim_hop_seconds=0.1)
+    ctx.barrier()
+    eng.run(1)
+    _pairs_once(eng, world, world)
+    with open(os.path.join(outdir, "ring_{}.json".format(rank)), "w") as f:
+        json.dump({"spans": eng.hop_spans, "bytes": eng.hop_bytes}, f)
+    eng.close()
+    shutdown(ctx)
+
+
+def test_async_rotation_ring_shift_is_one_phase(tmp_path):
+    """8 ranks, rotation: at every sub-epoch boundary each rank sends its
+    model to the next rank and receives one from the previous.  With a
+    forced 0.1 s per transfer a boundary's eight sends overlap (one phase,
+    <= 2 x 0.1 s), instead of chaining through the ring (~0.8 s) as they did
+    when every rank walked its transfers one at a time on one communicator."""
+    world = 8
+    mp.spawn(_ring_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    sends = []
+    for r in range(world):
+        d = json.load(open(tmp_path / "ring_{}.json".format(r)))
+        assert d["bytes"] > 0
+        sends.append(sorted((s[0], s[1]) for s in d["spans"] if s[2] == "send"))
+    nb = min(len(s) for s in sends)
+    assert nb >= world - 1, [len(s) for s in sends]
+    phases = []
+    for k in range(nb):
+        t0 = min(s[k][0] for s in sends)
+        t1 = max(s[k][1] for s in sends)
+        phases.append(t1 - t0)
+        # spans of different ranks overlap: every send starts before the
+        # first one of the boundary has ended + one transfer
+    print("ring-shift phases (s):", [round(p, 3) for p in phases])
+    assert statistics.median(phases) <= 2 * 0.1, phases
