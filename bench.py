@@ -169,6 +169,13 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(value / base, 3) if base and headline else None,
             "dtype": args.dtype,
+            # how the conv / linear products are computed: fp32 storage and
+            # accumulation with 3-pass split-bf16 MFMA products (hi*hi + hi*lo
+            # + lo*hi, ~2^-16 relative per product; every op within 1e-4
+            # relative L2 of fp64, tests/test_fp32_gpu.py) on our HIP kernels
+            "math": ({"fp32": "3xbf16-split MFMA, fp32 accumulate/storage",
+                      "bf16": "bf16 MFMA, fp32 accumulate"}[args.dtype]
+                     if backend == "hip" else "PyTorch-ROCm/MIOpen " + args.dtype),
             "data": "synthetic via DA pages (C++ reader)" if args.da else "synthetic",
             "config": {"model": {"headline": args.model, "criteo16": "confA",
                                  "hetero8": "resnet50+vgg16"}[args.workload],

@@ -310,7 +310,20 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     import concurrent.futures as cf
     WINDOW = 4
     jobs, futs = [], {}
-    pool = cf.ThreadPoolExecutor(max_workers=WINDOW)
+    # the decode pool lives while a prefetch window is open: created lazily
+    # on the first submit, shut down once the window drains (every prefetched
+    # job consumed), re-created by the next store that uses this loader
+    pool = [None]
+
+    def submit(*a):
+        if pool[0] is None:
+            pool[0] = cf.ThreadPoolExecutor(max_workers=WINDOW)
+        return pool[0].submit(*a)
+
+    def drain():
+        if pool[0] is not None and not futs:
+            pool[0].shutdown(wait=False)
+            pool[0] = None
 
     def decode(p, split, threads):
         heap = os.path.join(seg_dir(root, p, man["dboid"]), str(man[split]["relfilenode"]))
@@ -331,6 +344,10 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     def prefetch(pids):
         """The store's partitions, in load order: start decoding ahead."""
         del jobs[:]
+        for f in futs.values():                 # a previous window never consumed
+            f.cancel()
+        futs.clear()
+        drain()
         jobs.extend((p, sp) for p in pids for sp in ("train", "valid"))
 
     def fetch(p, split):
@@ -339,7 +356,7 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
             i = jobs.index(key)
             for k in jobs[i:i + WINDOW]:
                 if k not in futs:
-                    futs[k] = pool.submit(decode, k[0], k[1], max(2, nthreads // WINDOW))
+                    futs[k] = submit(decode, k[0], k[1], max(2, nthreads // WINDOW))
         fut = futs.pop(key, None)
         return fut.result() if fut is not None else decode(p, split, nthreads)
 
@@ -385,7 +402,7 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
         tx, ty = load_split(p, "train")
         vx, vy = load_split(p, "valid")
         if jobs and not futs and (p, "valid") == jobs[-1]:
-            pool.shutdown(wait=False)
+            drain()
         return tx, ty, vx, vy
     loader.stats = st
     loader.prefetch = prefetch

@@ -41,10 +41,6 @@ _SIGS = {
                       c_p, c_i, c_f, c_f, c_f, c_i, c_p],
     "cer_sgd_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p, c_p, c_i,
                      c_f, c_i, c_p],
-    "cer_adam_step_split": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64,
-                            c_p, c_p, c_i, c_f, c_f, c_f, c_i, c_p],
-    "cer_split_image": [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_p],
-    "cer_conv_set_wsplit": [c_p, c_i64],
     "cer_softmax_ce": [c_p, c_i, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_gather_images": [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_p, c_p],
 }
@@ -90,28 +86,9 @@ def _check(rc, name):
 
 
 # ---------------------------------------------------------------------------
-def split_image(arena, row=None):
-    """Rewrite the pre-split weight image (``Arena.wsplit``) of one row (or
-    all) from the fp32 params — after init, load, hop or a host-side update."""
-    src, dst = arena.params, arena.wsplit
-    g0, G = (0, arena.G) if row is None else (row, 1)
-    rc = lib().cer_split_image(c_p(src[g0].data_ptr()), src.stride(0), c_p(dst[g0].data_ptr()),
-                               dst.stride(0), arena.layout.n_train, G, _stream())
-    _check(rc, "cer_split_image")
-
-
 def adam_step(arena, beta1, beta2, eps, l2):
     L = arena.layout
     st = arena.state
-    if arena.wsplit is not None:
-        sp = arena.wsplit
-        rc = lib().cer_adam_step_split(
-            _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
-            _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
-            _ptr(sp), sp.stride(0), _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps,
-            int(bool(l2)), _stream())
-        _check(rc, "cer_adam_step_split")
-        return
     work = arena.work if arena.work is not arena.params else None
     rc = lib().cer_adam_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
@@ -119,20 +96,6 @@ def adam_step(arena, beta1, beta2, eps, l2):
         _ptr(work), work.stride(0) if work is not None else 0,
         _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)), _stream())
     _check(rc, "cer_adam_step")
-
-
-def adam_step_range(arena, lo, hi, beta1, beta2, eps, l2, inc_step):
-    """Adam over parameters [lo, hi) of every row on the current stream
-    (fp32 arenas without a shadow / split image)."""
-    L = arena.layout
-    st = arena.state
-    assert arena.work is arena.params and arena.wsplit is None
-    rc = lib().cer_adam_step_range(
-        _ptr(st), st.stride(0), int(lo), int(hi), L.off_m, L.off_v, L.off_step,
-        _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
-        _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)),
-        int(bool(inc_step)), _stream())
-    _check(rc, "cer_adam_step_range")
 
 
 def sgd_step(arena, momentum, l2):
@@ -145,8 +108,6 @@ def sgd_step(arena, momentum, l2):
         _ptr(work), work.stride(0) if work is not None else 0,
         _ptr(arena.lr), _ptr(arena.wd), arena.G, float(momentum), int(bool(l2)), _stream())
     _check(rc, "cer_sgd_step")
-    if arena.wsplit is not None:
-        split_image(arena)
 
 
 def softmax_ce_fwd(logits, labels, acc, G, need_grad=True):
@@ -211,7 +172,6 @@ _SIGS.update({
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
-    "cer_bn_set_coop": [c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
     "cer_bn_bwd_part": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p,
                         c_p, c_p, c_p, c_i, c_i64, c_i, c_i, c_i, c_p],
@@ -220,8 +180,6 @@ _SIGS.update({
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_set_grid": [c_i],
     "cer_wgrad_batch_set_rows": [c_i],
-    "cer_adam_step_range": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p,
-                            c_p, c_i, c_f, c_f, c_f, c_i, c_i, c_p],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_set_fold": [c_i],
@@ -230,12 +188,6 @@ _SIGS.update({
                            c_p, c_i, c_i, c_p, c_p, c_p],
     "cer_conv_stats_floats": [c_i64, c_i],
     "cer_stem_ok": [c_i, c_i, c_i, c_i, c_i],
-    "cer_conv_fwd_bnstat": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
-                            c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f,
-                            c_p],
-    "cer_stem_fwd_bnstat": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
-                            c_p, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64,
-                            c_f, c_f, c_p],
     "cer_bn_apply_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i64, c_i, c_i, c_i, c_p],
     "cer_stem_wpk_elems": [c_i, c_i, c_i, c_i],
     "cer_stem_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
@@ -394,38 +346,13 @@ def tuned_variants():
     return dict(_TUNED)
 
 
-class _WSplit(object):
-    """``with _WSplit(wref):`` the next fp32 conv forward / dgrad reads the
-    pre-split (hi | lo bf16) image of these weights that the optimizer keeps
-    next to the fp32 params (``Arena.wsplit``; conv.hip cer_conv_set_wsplit)
-    instead of splitting them while staging.  No-op without an image."""
-    __slots__ = ("ptr", "stride")
-
-    def __init__(self, wref):
-        img = getattr(wref.arena, "wsplit", None) if wref is not None else None
-        self.ptr = None
-        if img is not None:
-            self.ptr = img.data_ptr() + wref.spec.offset * img.element_size()
-            self.stride = img.stride(0)
-
-    def __enter__(self):
-        if self.ptr is not None:
-            lib().cer_conv_set_wsplit(c_p(self.ptr), self.stride)
-
-    def __exit__(self, *a):
-        if self.ptr is not None:
-            lib().cer_conv_set_wsplit(None, 0)
-        return False
-
-
 def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,
                      act, wref=None):
     _splitk_ready(x.device)
     def launch():
-        with _WSplit(wref):
-            rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
-                                        stride, pad, _ptr(y), Ho, Wo, c_p(bp), bs,
-                                        _act_code(act), _stream())
+        rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
+                                    stride, pad, _ptr(y), Ho, Wo, c_p(bp), bs,
+                                    _act_code(act), _stream())
         _check(rc, "cer_conv_fwd")
     _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
@@ -472,37 +399,13 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _splitk_ready(x.device)
 
     def launch():
-        with _WSplit(wref):
-            rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
-                                              stride, pad, _ptr(z), Ho, Wo, _ptr(part),
-                                              ctypes.byref(nslab), _stream())
+        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
+                                          stride, pad, _ptr(z), Ho, Wo, _ptr(part),
+                                          ctypes.byref(nslab), _stream())
         _check(rc, "cer_conv_fwd_stats")
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
     return z, part, nslab.value
-
-
-_COUNTERS = {}
-_COUNTER_SLOTS = 1 << 16
-
-
-def _counters(device):
-    """Zeroed arrival counters shared by every fused conv+BN launch on a
-    device (each launch's last arriver re-zeroes its slots; allocated once so
-    captured HIP graphs keep a valid address)."""
-    key = str(device)
-    c = _COUNTERS.get(key)
-    if c is None:
-        c = torch.zeros(_COUNTER_SLOTS, dtype=torch.int32, device=device)
-        _COUNTERS[key] = c
-    return c
-
-
-# CER_BN_FUSED_FINALIZE=1: BN finalize by the last-arriving conv tile of each
-# channel column (one launch fewer per layer; slower on MI355X at ResNet-50
-# sizes because the arriving tile serialises the slab reduction) — default
-# off: conv epilogue partials + the parallel finalize kernel.
-_FUSED_FINALIZE = os.environ.get("CER_BN_FUSED_FINALIZE", "0") == "1"
 
 
 def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps):
@@ -587,65 +490,35 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     _splitk_ready(dev)
     z = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=dev)
     part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dev)
-    mean = torch.empty(C, dtype=torch.float32, device=dev)
-    invstd = torch.empty(C, dtype=torch.float32, device=dev)
-    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
-    cnt = _counters(dev)
-    assert G * ((cout + 63) // 64) <= cnt.numel()
     wp, wstr = wref.work_ptr()
-    rmp, rs = rmref.master_ptr()
-    rvp, _ = rvref.master_ptr()
     nslab = ctypes.c_int(0)
-    x4 = wpk = None
-    fused_fin = _FUSED_FINALIZE and x.dtype == torch.bfloat16   # bf16 kernels only
     if stem:
         x4 = torch.empty((G, B, H, W, 4), dtype=x.dtype, device=dev)
         wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
                           device=dev)
 
-        def tune():        # statistics-only twin (no running-stat side effects)
+        def launch():        # conv + BN statistics partials (no running-stat side effects)
             _check(_fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                       stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
                                       _ptr(part), ctypes.byref(nslab), _stream()), "cer_stem_fwd")
-        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), tune, x.dtype)
-        if not fused_fin:
-            tune()
-            return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                                 momentum, eps) + (x4, None)
-        rc = L.cer_stem_fwd_bnstat(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride,
-                                   pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
-                                   _ptr(cnt), _ptr(ws), _ptr(mean), _ptr(invstd), c_p(rmp),
-                                   c_p(rvp), rs, eps, momentum, _stream())
-        _check(rc, "cer_stem_fwd_bnstat")
-    else:
-        def tune():
-            with _WSplit(wref):
-                rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
-                                                  kh, kw, stride, pad, _ptr(z), Ho, Wo,
-                                                  _ptr(part), ctypes.byref(nslab), _stream())
-            _check(rc, "cer_conv_fwd_stats")
-        _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), tune, x.dtype)
-        if not fused_fin:
-            tune()
-            if fold_out:
-                mean, invstd, scsh = bn_finalize_scsh(part, nslab.value, z, gref, bref, rmref,
-                                                      rvref, momentum, eps)
-                return z, z, mean, invstd, None, scsh
-            return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                                 momentum, eps) + (None, None)
-        rc = L.cer_conv_fwd_bnstat(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride,
-                                   pad, _ptr(z), Ho, Wo, _ptr(part), _ptr(cnt), _ptr(ws),
-                                   _ptr(mean), _ptr(invstd), c_p(rmp), c_p(rvp), rs, eps,
-                                   momentum, _stream())
-        _check(rc, "cer_conv_fwd_bnstat")
-    y = torch.empty_like(z)
-    gp, gs = gref.work_ptr()
-    bp, bs = bref.work_ptr()
-    res = _same(residual, x) if residual is not None else None
-    rc = _fn("cer_bn_apply_fwd", z)(_ptr(z), _ptr(res), _ptr(y), _ptr(ws), c_p(gp), gs, c_p(bp), bs, M,
-                            C, cout, _act_code(act), _stream())
-    _check(rc, "cer_bn_apply_fwd")
-    return y, z, mean, invstd, x4, None
+        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype)
+        launch()
+        return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
+                             momentum, eps) + (x4, None)
+
+    def launch():
+        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
+                                          kh, kw, stride, pad, _ptr(z), Ho, Wo,
+                                          _ptr(part), ctypes.byref(nslab), _stream())
+        _check(rc, "cer_conv_fwd_stats")
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
+    launch()
+    if fold_out:
+        mean, invstd, scsh = bn_finalize_scsh(part, nslab.value, z, gref, bref, rmref,
+                                              rvref, momentum, eps)
+        return z, z, mean, invstd, None, scsh
+    return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
+                         momentum, eps) + (None, None)
 
 
 def stem_ok(x, wref, stride, pad):
@@ -709,25 +582,36 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
     wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
 
     def launch(out=dx):
-        with _WSplit(wref):
-            rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
-                                           cin, kh, kw, stride, pad, _ptr(out), H, W,
-                                           _ptr(addend), _stream())
+        rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
+                                       cin, kh, kw, stride, pad, _ptr(out), H, W,
+                                       _ptr(addend), _stream())
         _check(rc, "cer_conv_dgrad")
     # an in-place accumulation (dx IS the addend) must not be repeated by the
-    # autotune's timing launches: those write a scratch dx instead
+    # autotune's timing launches: they run in place too, on one scratch copy
+    # of the addend made once here (timing the same work as the real launch:
+    # a scratch dx != addend would add a full-tensor copy to every timing)
     inplace = addend is not None and addend.data_ptr() == dx.data_ptr()
-    tune = (lambda: launch(torch.empty_like(dx))) if inplace else launch
+    tune = launch
+    if inplace:
+        scratch = [None]
+
+        def tune():
+            if scratch[0] is None:
+                scratch[0] = addend.clone()
+            _check(_fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
+                                             cin, kh, kw, stride, pad, _ptr(scratch[0]), H, W,
+                                             _ptr(scratch[0]), _stream()), "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
             tune, dy.dtype)
     launch()
 
 
-def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
+def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consume_addend=False):
     """dx of the conv; ``addend`` (same shape and dtype as dx) is added in the
-    GEMM epilogue (the other consumer's gradient of a shared input).  For a
-    strided 1x1 conv the addend is CONSUMED: dx accumulates into its storage
-    (the caller, ops.nn's GradJoin, owns it and uses it nowhere else).
+    GEMM epilogue (the other consumer's gradient of a shared input).
+    ``consume_addend=True`` (only ops.nn's GradJoin passes it: it owns the
+    addend and uses it nowhere else) lets a strided 1x1 conv accumulate dx
+    into the addend's storage; otherwise the addend is never written.
     ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
     output y this conv consumed — the epilogue also computes that BN's
     backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink)."""
@@ -747,8 +631,8 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None):
     # computes, instead of first copying the whole addend into a new dx
     # (a BN link does not change this: conv.hip computes no BN-backward
     # statistics in a strided dgrad with an addend, the BN runs its own pass)
-    if (addend is not None and kh == 1 and kw == 1 and pad == 0 and stride > 1
-            and addend.is_contiguous()):
+    if (consume_addend and addend is not None and kh == 1 and kw == 1 and pad == 0
+            and stride > 1 and addend.is_contiguous()):
         dx = addend
     else:
         dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
@@ -1011,8 +895,7 @@ def linear_bwd(dy, x, y, wref, bref, act, need_dx):
     B = x.shape[0]
     dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _act(dy)
     xb = _act(x)
-    streams.run_side(lambda: _conv_wgrad_launch(xb, B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref),
-                     xb, dz)
+    _conv_wgrad_launch(xb, B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref)
     if not need_dx:
         return None
     dx = torch.empty((B, G * K), dtype=dy.dtype, device=dy.device)

@@ -168,12 +168,13 @@ class PackedConv2d(torch.autograd.Function):
                 if addend is not None:
                     join.pending = None
                     join = None
-                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl)
+                dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl,
+                                    consume_addend=addend is not None)
                 if join is not None:       # first of the two: park dx for the other one
                     dx = join.join(dx)
             # off the critical path: overlaps the dgrad chain below (ops.streams)
             pro = getattr(ctx, "pro", None)
-            streams.run_side(lambda: h.conv2d_wgrad(x, dy, wref, stride, pad, pro=pro), x, dy)
+            h.conv2d_wgrad(x, dy, wref, stride, pad, pro=pro)
         else:
             G = wref.G
             cout, kh, kw, cin = wref.spec.shape
@@ -346,7 +347,7 @@ class PackedConvBNAct(torch.autograd.Function):
             dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
             x4, wref, pad = ctx.x4, ctx.wref, ctx.pad
-            streams.run_side(lambda: _hip().stem_wgrad(x4, dz, wref, pad), x4, dz)
+            _hip().stem_wgrad(x4, dz, wref, pad)
             ctx.x4 = None
             dx = None
         else:

@@ -22,17 +22,10 @@ architecture.
 """
 
 import math
-import os
 
 import numpy as np
 import torch
 
-# CER_W_SPLIT=1: fp32 compute keeps a pre-split (bf16 hi | bf16 lo) image of
-# the trainable params next to them so the 3-pass conv kernels skip the split
-# of the weight operand.  Measured neutral on the headline step (A/B in
-# profiles/r2_ab_presplit_weights.md: -0.4 % at 8 configs, +1.2 % at 1), so
-# off by default (it costs 4 B per param of HBM and of optimizer writes)
-W_SPLIT = os.environ.get("CER_W_SPLIT", "0") == "1"
 ALIGN = 64  # elements: every tensor starts 256-B aligned in fp32, 128-B in bf16
 
 
@@ -223,11 +216,6 @@ def init_row(layout, master_row, seed):
             view.fill_(0.0)
 
 
-def _hip_convs():
-    from ..ops.backend import get_backend
-    return get_backend() == "hip"
-
-
 class Arena(object):
     """State of G packed configurations of one architecture on one device."""
 
@@ -249,13 +237,6 @@ class Arena(object):
             self.work = self.params
         else:
             self.work = torch.zeros(G, L.n_train, dtype=compute_dtype, device=self.device)
-        # split image: per 8 params one 32-B chunk [8 x bf16 hi | 8 x bf16 lo],
-        # so a param's byte offset is the same as in ``params`` (conv.hip
-        # cer_conv_set_wsplit); rewritten by the optimizer and by sync_work
-        self.wsplit = None
-        if (W_SPLIT and compute_dtype == torch.float32 and trainable
-                and self.device.type == "cuda" and _hip_convs()):
-            self.wsplit = torch.zeros(G, L.n_train, dtype=torch.int32, device=self.device)
         self.grad = (torch.zeros(G, L.n_train, dtype=torch.float32, device=self.device)
                      if trainable else None)
         # True: the optimizer clears ``grad`` after consuming it, so every
@@ -288,9 +269,6 @@ class Arena(object):
         self.sync_work(row)
 
     def sync_work(self, row=None):
-        if self.wsplit is not None:
-            from ..ops import _hip
-            _hip.split_image(self, row)
         if self.work is self.params:
             return
         if row is None:

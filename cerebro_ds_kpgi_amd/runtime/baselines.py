@@ -176,6 +176,10 @@ class GradBuckets(object):
             return
         from ..ops import streams
         streams.flush_wgrad()
+        # the all-reduce runs on RCCL's stream, which orders only after the
+        # CURRENT stream: any side-stream weight-gradient work must be joined
+        # first (group.py keeps DDP steps off the side batch; this is the guard)
+        streams.join_side()
         g = self.arena.grad
         for row in range(g.shape[0]):
             self.works.append(dist.all_reduce(g[row, lo:self.hi], group=self.group,

@@ -215,7 +215,6 @@ class _Working(object):
         self.jobs = []
         # called between backward and the optimizer (DDP gradient all-reduce)
         self.grad_hook = None
-        self._split = None
 
     def assign(self, jobs):
         self.jobs = list(jobs)
@@ -248,41 +247,22 @@ class _Working(object):
         # weight gradients are queued during backward and launched as a few
         # multi-layer kernels when the block exits (ops.streams); with >=
         # _SIDE_MIN_G packed configs the first half of them runs on the side
-        # stream during the rest of backward
-        frac = _SIDE_FRAC if self.G >= _SIDE_MIN_G else 0.0
-        hook = self._adam_split() if frac else None
+        # stream during the rest of backward -- not under a gradient
+        # all-reduce hook (DDP): its buckets start mid-backward and must see
+        # final gradients, which a side batch still writing would break
+        frac = (_SIDE_FRAC if self.G >= _SIDE_MIN_G and self.grad_hook is None
+                and getattr(self.net, "grad_buckets", None) is None else 0.0)
         if self.x.device.type == "cuda" and get_backend() == "hip":
             streams.set_batch_rows(_WIDE_ROWS if self.G >= _SIDE_MIN_G else 0)
-        with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self),
-                                    hook=hook):
+        with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self)):
             logits = self.net.forward(self.x, True)
             loss = softmax_ce(logits, self.y, self.acc, self.G)
             loss.sum().backward()
         streams.join()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)
-        if hook is not None and hook.fired:
-            hook.finish()                   # the rest of the update, after the join
-        else:
-            optimizer_step(self.arena, g.optimizer, l2=g.l2)
+        optimizer_step(self.arena, g.optimizer, l2=g.l2)
         self.cursor.add_(1)
-
-    def _adam_split(self):
-        """The optimizer update split across streams (see _AdamSplit), when
-        this working set qualifies: Adam on our fp32 kernels, no shadow /
-        split weight image, no gradient all-reduce between backward and the
-        update (DDP), and a network whose parameter layout puts every BN /
-        bias parameter after its own conv / dense weight (``adam_split_ok``)."""
-        a = self.arena
-        if (not _ADAM_SPLIT or self.grad_hook is not None or self.group.optimizer != "adam"
-                or a.work is not a.params or a.wsplit is not None or get_backend() != "hip"
-                or a.state.device.type != "cuda"
-                or not getattr(self.net, "adam_split_ok", False)):
-            return None
-        if self._split is None:
-            self._split = _AdamSplit(a, self.group.l2)
-        self._split.fired = False
-        return self._split
 
     def train_steps(self, nsteps):
         done = 0
@@ -408,60 +388,6 @@ _SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "4"))
 # wgrad-batch rows per split for those packs (fewer, longer splits: +1 % at
 # 8 configs; one-config packs keep 1024, where 2048 is 1-2.5 % slower)
 _WIDE_ROWS = int(os.environ.get("CER_WGB_ROWS_WIDE", "2048"))
-
-# Optimizer update split across streams with the side wgrad batch (below).
-# Measured neutral-to-slower (profiles/r2_ab_wgrad_chunk.md): off by default.
-_ADAM_SPLIT = os.environ.get("CER_ADAM_SPLIT", "0") == "1"
-
-
-class _AdamSplit(object):
-    """Adam split across streams with the side-stream wgrad batch
-    (ops.streams deferred_wgrad hook).  At the fork, the step counters advance
-    on the compute stream (``pre``); right behind the side batch the update of
-    the arena's parameter suffix [split, n_train) -- the layers that batch
-    covers plus their BN / bias parameters, all of whose gradients are final
-    by then -- runs on the side stream and overlaps the rest of backward
-    (``after``); ``finish`` updates [0, split) after the join.  The suffix is
-    the longest one whose every weight is in the side batch (walking the
-    layout from the end); anything else stays in the main update."""
-
-    def __init__(self, arena, l2):
-        self.a = arena
-        self.l2 = l2
-        L = arena.layout
-        self.specs = sorted(L.train_specs, key=lambda s: s.offset)
-        self.n = L.n_train
-        self.fired = False
-        self.split = self.n
-
-    def pre(self):
-        from ..ops import _hip
-        from ..ops.optim import BETA1, BETA2, EPS
-        _hip.adam_step_range(self.a, 0, 0, BETA1, BETA2, EPS, self.l2, inc_step=True)
-        self.fired = True
-        self.split = self.n
-
-    def after(self, grad_ptrs):
-        from ..ops import _hip
-        from ..ops.optim import BETA1, BETA2, EPS
-        base = self.a.grad.data_ptr()
-        side = {(p - base) // 4 for p in grad_ptrs}
-        split = self.n
-        for s in reversed(self.specs):
-            if s.kind == "weight":
-                if s.offset not in side:
-                    break
-                split = s.offset          # this weight and the BN / bias params after it
-        self.split = split
-        if split < self.n:
-            _hip.adam_step_range(self.a, split, self.n, BETA1, BETA2, EPS, self.l2,
-                                 inc_step=False)
-
-    def finish(self):
-        from ..ops import _hip
-        from ..ops.optim import BETA1, BETA2, EPS
-        _hip.adam_step_range(self.a, 0, self.split, BETA1, BETA2, EPS, self.l2, inc_step=False)
-
 
 # Graph-captured validation (CER_VALID_GRAPH=0 runs it eagerly).  Its round-1
 # failures (invalid eval losses after an epoch boundary) had the same root

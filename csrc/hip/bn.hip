@@ -64,11 +64,9 @@ static void make_grid(int64_t M, int C, const Map& mp, int target, int min_rows,
 }
 
 // ---------------------------------------------------------------------------
-// cross-block hand-off for the cooperative kernels
-// ---------------------------------------------------------------------------
-// A value written by one block and read by a block on another XCD (whose L2
-// is not coherent with ours) inside the same kernel moves by agent-scope
-// atomic stores / loads; SC selects those in the tile functions below.
+// plain / agent-scope element access (SC: a value handed between blocks of
+// one kernel, across the non-coherent per-XCD L2s, moves by agent-scope
+// atomic stores / loads; every launch path here hands off between kernels)
 template <bool SC>
 __device__ __forceinline__ float ldf(const float* p) {
   if (SC) return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -81,50 +79,6 @@ __device__ __forceinline__ void stf(float* p, float v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else
     *p = v;
-}
-
-// Grid-wide barrier for a co-resident grid (the host caps the grid at the
-// occupancy-derived resident-block count).  Same-address atomics from every
-// block serialise at the coherence point (~20 ns each: a 512-block counter
-// barrier costs ~10 us), so arrival is a plain flag store per block instead:
-// block b writes the barrier's epoch into flags[b]; block 0 polls all flags
-// (one per thread, in parallel) and then publishes the epoch in bar[0]; the
-// other blocks spin on bar[0].  The epoch is the bar[0] value every block read
-// at kernel start (before any block can arrive) plus the barrier's ordinal,
-// so barriers never need re-arming.
-struct GridBar {
-  unsigned* rel;     // bar[0]: last published epoch
-  unsigned* flags;   // one arrival word per block
-  unsigned base;     // bar[0] at kernel start
-};
-
-__device__ __forceinline__ GridBar grid_bar_open(unsigned* bar) {
-  __shared__ unsigned base_s;
-  if (threadIdx.x == 0)
-    base_s = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  return GridBar{bar, bar + 64, base_s};
-}
-
-__device__ __forceinline__ void grid_sync(const GridBar& gb, unsigned ordinal) {
-  const unsigned epoch = gb.base + ordinal;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(gb.flags + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x == 0) {
-    for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-      while (__hip_atomic_load(gb.flags + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
-        __builtin_amdgcn_s_sleep(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(gb.rel, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if (threadIdx.x == 0) {
-    while (__hip_atomic_load(gb.rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch)
-      __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -708,75 +662,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
 }
 
 // ---------------------------------------------------------------------------
-// cooperative single-launch BN (one kernel per layer and direction)
-// ---------------------------------------------------------------------------
-// A one-config ResNet-50 step is launch-bound: ~470 kernels at 5-20 us each,
-// a third of them BN stages over a few hundred KB.  These kernels run the
-// stages of one layer in ONE launch on a co-resident grid, separated by
-// grid_sync: forward = finalize -> apply (2 launches -> 1), backward =
-// partials -> finalize -> apply (3 -> 1).  Blocks grid-stride over the same
-// (channel block, row slab) tiles in every stage, so the backward apply
-// re-reads the rows its own block reduced (L2-warm).
-template <typename T>
-__global__ __launch_bounds__(BN_T) void bn_fwd_coop(
-    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
-    float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, float eps,
-    float momentum, const T* __restrict__ x, const T* __restrict__ res,
-    T* __restrict__ y, Strided gamma, Strided beta, int64_t M, int C, int Cper,
-    int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
-  const GridBar gb = grid_bar_open(bar);
-  const int fin_tasks = (C + FIN_C - 1) / FIN_C;
-  for (int t = blockIdx.x; t < fin_tasks; t += gridDim.x)
-    finalize_fwd_task<true>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
-                            C, Cper, eps, momentum, t);
-  grid_sync(gb, 1);
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    apply_fwd_tile<T, 0, true>(x, res, y, ws, nullptr, nullptr, 0, 0.f, gamma, beta, M, C, Cper,
-                            rows_per_slab, act, mp, t % cblocks, t / cblocks);
-}
-
-template <typename T>
-__global__ __launch_bounds__(BN_T) void bn_bwd_coop(
-    const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
-    float* dgamma, float* dbeta, int64_t gstride, T* __restrict__ dx,
-    T* __restrict__ dres, float* __restrict__ ws, float* __restrict__ part, int64_t M, int C,
-    int Cper, int rows_per_slab, int cblocks, int ntiles, int act, Map mp, unsigned* bar) {
-  __shared__ float red[2 * BN_T * VEC];
-  const GridBar gb = grid_bar_open(bar);
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    partials_tile<T, 1, true>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
-                           t % cblocks, t / cblocks, red);
-  grid_sync(gb, 1);
-  const int fin_tasks = (C + FIN_C - 1) / FIN_C;
-  const int slabs = (ntiles + cblocks - 1) / cblocks;
-  for (int t = blockIdx.x; t < fin_tasks; t += gridDim.x)
-    finalize_bwd_task<true>(part, slabs, ws, dgamma, dbeta, gstride, C, Cper, t);
-  grid_sync(gb, 2);
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x)
-    apply_bwd_tile<T, true>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper, rows_per_slab,
-                         act, mp, t % cblocks, t / cblocks);
-}
-
-// ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
 constexpr int RED_TARGET = 512, RED_MIN_ROWS = 64;
 constexpr int APPLY_TARGET = 2048, APPLY_MIN_ROWS = 16;
-
-// cooperative path (bn_fwd_coop / bn_bwd_coop): off unless CER_BN_COOP=1 /
-// cer_bn_set_coop(1); the grid never exceeds the blocks the device can hold
-// at once (occupancy x CUs), which is what makes grid_sync safe.  Measured on
-// MI355X (profiles/r1_ab_bn_coop.md) it is SLOWER than the staged kernels:
-// the cross-XCD barrier round trips (~5 us) cost more than the launches they
-// remove, and a co-resident grid hides less latency than a 2048-block apply.
-static int g_coop = -1;
-constexpr int COOP_SLOTS = 16;               // barrier slots, rotated per launch
-constexpr int COOP_MAX_GRID = 1024;          // arrival flags per slot
-constexpr int COOP_SLOT_WORDS = 64 + COOP_MAX_GRID;
-__device__ unsigned g_coop_bar[COOP_SLOTS * COOP_SLOT_WORDS];
-
-CER_API void cer_bn_set_coop(int on) { g_coop = on; }
 
 // finalize folded into the apply when a layer has at most this many slabs
 // (CER_BN_FOLD, default 64; 0 = always launch the finalize kernel)
@@ -822,53 +711,6 @@ int bn_mask_mode(int act, int has_res) {
   return act == 0 ? YM_NONE : (act == 1 && !has_res && g_zmask) ? YM_Z : YM_Y;
 }
 
-static bool coop_on() {
-  if (g_coop < 0) {
-    const char* e = getenv("CER_BN_COOP");
-    g_coop = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_coop == 1;
-}
-
-// resident-block capacity of `kern` on the current device (cached per device)
-template <typename K>
-static int coop_capacity(K kern, int* cache) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cache[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, BN_T, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      per_cu = cus = 0;
-    cache[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
-  }
-  return cache[dev] > 0 ? cache[dev] : 0;
-}
-
-static unsigned* coop_bar() {
-  static int slot = 0;
-  unsigned* base = nullptr;
-  if (hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_coop_bar)) != hipSuccess) return nullptr;
-  slot = (slot + 1) % COOP_SLOTS;
-  return base + slot * COOP_SLOT_WORDS;
-}
-
-// grid of a cooperative launch: one block per tile up to 4 per CU, never
-// more than the device can keep resident
-static int coop_grid(int ntiles, int capacity, int cus_x2) {
-  int g = ntiles < cus_x2 ? ntiles : cus_x2;
-  if (g > COOP_MAX_GRID) g = COOP_MAX_GRID;
-  return g <= capacity ? g : capacity;
-}
-
-static int device_cus() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cache[dev]) (void)hipDeviceGetAttribute(&cache[dev], hipDeviceAttributeMultiprocessorCount, dev);
-  return cache[dev];
-}
-
 // floats of scratch the partials need (part[slabs][2][C])
 CER_API int64_t cer_bn_part_floats(int64_t M, int C) {
   Map mp = make_map(C);
@@ -906,24 +748,6 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                                                Strided{beta, beta_stride}, M, C, Cper, frows, act,
                                                mp);
     return (int)hipGetLastError();
-  }
-  if (coop_on()) {
-    static int cap_cache[64] = {0};
-    const int cap = coop_capacity(bn_fwd_coop<T>, cap_cache);
-    unsigned* bar = coop_bar();
-    dim3 cg;
-    int crows;
-    make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &cg, &crows);
-    const int ntiles = (int)(cg.x * cg.y);
-    const int grid = coop_grid(ntiles, cap, 4 * device_cus());
-    if (grid > 0 && bar) {
-      bn_fwd_coop<T><<<grid, BN_T, 0, stream>>>(part, nslab, ws, mean_out, invstd_out, rmean, rvar,
-                                             rstat_stride, eps, momentum, x, res, y,
-                                             Strided{gamma, gamma_stride},
-                                             Strided{beta, beta_stride}, M, C, Cper, crows,
-                                             (int)cg.x, ntiles, act, mp, bar);
-      return (int)hipGetLastError();
-    }
   }
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
@@ -1022,20 +846,6 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   int rrows, arows;
   make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  if (pre_nslab <= 0 && coop_on()) {
-    // same (channel block, slab) tiling as bn_partials: part has room for it
-    static int cap_cache[64] = {0};
-    const int cap = coop_capacity(bn_bwd_coop<T>, cap_cache);
-    unsigned* bar = coop_bar();
-    const int ntiles = (int)(rg.x * rg.y);
-    const int grid = coop_grid(ntiles, cap, 4 * device_cus());
-    if (grid > 0 && bar) {
-      bn_bwd_coop<T><<<grid, BN_T, 0, stream>>>(dy, x, y, mean, invstd, Strided{gamma, gamma_stride},
-                                             dgamma, dbeta, grad_stride, dx, dres, ws, part, M, C,
-                                             Cper, rrows, (int)rg.x, ntiles, act, mp, bar);
-      return (int)hipGetLastError();
-    }
-  }
   // mask source: none / y / recomputed from x (see the header); a residual
   // join's mask depends on the residual, so it needs y
   const int ym = bn_mask_mode(act, dres != nullptr);

@@ -84,19 +84,6 @@ struct GatherGeom {
   int64_t cfg_off;    // elements between configs (Cg for the packed layout)
 };
 
-// BN statistics finalize fused into the producing conv (the arithmetic of
-// bn_finalize_fwd in bn.hip); cnt == nullptr: off
-struct BNFinal {
-  unsigned* cnt;          // [G * tiles_n] arrival counters (zero; the last arriver re-zeroes)
-  float* ws;              // [2][C]: mean, invstd (consumed by the BN apply)
-  float* mean_out;        // [C] saved for backward
-  float* invstd_out;      // [C]
-  float* rmean;           // running stats, config stride rstride
-  float* rvar;
-  int64_t rstride;
-  float eps, momentum;
-};
-
 // BN-backward statistics in a dgrad epilogue: the dgrad output is the input
 // gradient dy of a BatchNorm layer (whose output the conv consumed), so the
 // epilogue also produces that BN's per-(M tile, channel) partials
@@ -138,20 +125,6 @@ CER_API void cer_conv_set_prologue(const float* scsh, int ld, int act) {
   g_pro = BNPro{scsh, ld, act};
 }
 
-// Pre-split weights for the NEXT fp32 forward / dgrad call (then cleared by
-// the caller): an image of the same tensor with every 8 consecutive elements
-// stored as [8 x bf16 hi | 8 x bf16 lo] (32 B, the optimizer writes it,
-// optim: cer_adam_step_split), so its byte offsets equal the fp32 tensor's
-// and the B-operand staging skips the hi/lo split.  Used only by the aligned
-// (fast) kernels; fallbacks keep reading the fp32 weights.
-static const void* g_wsplit = nullptr;
-static int64_t g_wsplit_stride = 0;
-
-CER_API void cer_conv_set_wsplit(const void* wsplit, int64_t stride) {
-  g_wsplit = wsplit;
-  g_wsplit_stride = stride;
-}
-
 __device__ __forceinline__ float pro_act(float v, int act) {
   return act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (act ? fmaxf(v, 0.f) : v);
 }
@@ -170,7 +143,6 @@ struct NTParams {
   int o_st, o_H, o_W;     // o_st > 1: GEMM row (b,y,x) stores to output pixel (b, y*o_st, x*o_st)
   float* stats;           // optional BN partials part[slab][2][ldc] (sum, sum^2) of the
                           // bf16 outputs; slab = M tile (fused BN forward)
-  BNFinal fin;            // optional: the last M tile of each N-tile column finalizes BN
   int splits = 1;         // split-K: K-tile ranges per output tile (fwd / dgrad, small grids)
   float* skws = nullptr;  // split-K fp32 partial slots [tile][split][acc regs x threads]
   unsigned* skcnt = nullptr;  // split-K per-tile arrival counters (zero; last arriver re-zeroes)
@@ -702,55 +674,7 @@ __device__ __forceinline__ void stats_finish(const NTParams& p, const bf16_t* ld
   float* dst = p.stats + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
-    if (n < p.N) {
-      const float v = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
-      if (p.fin.cnt)
-        st_sc1(dst + (int64_t)q * p.ldc + n, v);   // read by another CU's finalize
-      else
-        dst[(int64_t)q * p.ldc + n] = v;
-    }
-  }
-  if (!p.fin.cnt) return;
-  // ---- fused finalize: the last M tile of this (config, N tile) column ----
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
-  int* flag = reinterpret_cast<int*>(const_cast<float*>(xch) + 2 * NTHREADS);
-  if (!last_arriver(p.fin.cnt + cfg * tiles_n + n0 / BN, (unsigned)tiles_m, flag)) return;
-  // 256 threads = BN channels x (256 / BN) slab lanes, LDS combine
-  constexpr int LANES = NTHREADS / BN;
-  float* red = const_cast<float*>(xch);   // reuse: [2][LANES][BN]
-  const int nl = tid % BN, ln = tid / BN, n = n0 + nl;
-  float sa = 0.f, sb = 0.f;
-  if (n < p.N) {
-    const float* col = p.stats + (int64_t)cfg * p.N + n;
-    for (int sl = ln; sl < tiles_m; sl += LANES) {
-      sa += ld_sc1(col + (int64_t)sl * 2 * p.ldc);
-      sb += ld_sc1(col + (int64_t)sl * 2 * p.ldc + p.ldc);
-    }
-  }
-  __syncthreads();
-  red[ln * BN + nl] = sa;
-  red[(LANES + ln) * BN + nl] = sb;
-  __syncthreads();
-  if (ln == 0 && n < p.N) {
-    for (int k = 1; k < LANES; ++k) {
-      sa += red[k * BN + nl];
-      sb += red[(LANES + k) * BN + nl];
-    }
-    const BNFinal& f = p.fin;
-    const float inv_m = 1.f / (float)p.M;
-    const float mu = sa * inv_m;
-    const float var = fmaxf(sb * inv_m - mu * mu, 0.f);
-    const float is = rsqrtf(var + f.eps);
-    const int c = cfg * p.N + n;
-    f.ws[c] = mu;
-    f.ws[p.ldc + c] = is;
-    f.mean_out[c] = mu;
-    f.invstd_out[c] = is;
-    float* rm = f.rmean + cfg * f.rstride + n;
-    float* rv = f.rvar + cfg * f.rstride + n;
-    const float unb = p.M > 1 ? var * (float)p.M / (float)(p.M - 1) : var;
-    *rm = (1.f - f.momentum) * *rm + f.momentum * mu;
-    *rv = (1.f - f.momentum) * *rv + f.momentum * unb;
+    if (n < p.N) dst[(int64_t)q * p.ldc + n] = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
   }
 }
 
@@ -2321,7 +2245,7 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
-template <int BM, int BN, int GM, bool PRO = false, bool WS = false, bool WIDE = false>
+template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
@@ -2425,12 +2349,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     for (int i = 0; i < B_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      if constexpr (WS) {            // pre-split weight image: (hi, lo) as loaded
-        h = rb[s][2 * i];
-        l = rb[s][2 * i + 1];
-      } else {
-        split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
-      }
+      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -2579,7 +2498,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WS = false, bool WIDE = false>
+template <int BM, int BN, int GM, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
@@ -2654,12 +2573,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      if constexpr (WS) {            // pre-split weight image: (hi, lo) as loaded
-        h = rb[s][2 * i];
-        l = rb[s][2 * i + 1];
-      } else {
-        split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
-      }
+      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       if constexpr (WIDE) {
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
@@ -3062,10 +2976,10 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
-static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, int kind,
-                          hipStream_t stream, bool wide = false) {
+static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
+                          bool wide = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
-  if (wide) {                      // 32x32x16 MFMA twins (no prologue / pre-split forms)
+  if (wide) {                      // 32x32x16 MFMA twins (no prologue form)
     if (kind == 1) {
       if constexpr (BM * BN <= 128 * 64)
         if (p.K / KS >= 3) {
@@ -3074,9 +2988,9 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, int kind
         }
       pipe_nt32<BM, BN, 2, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else if (!fast) {
-      igemm_nt32<BM, BN, GM_SLOW, false, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+      igemm_nt32<BM, BN, GM_SLOW, false, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else {
-      igemm_nt32<BM, BN, GM_FWD, false, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+      igemm_nt32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
     }
     return;
   }
@@ -3091,12 +3005,7 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, bool ws, int kind
   } else if (!fast)
     igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
   else if (p.pro.scsh)
-    if (ws)
-      igemm_nt32<BM, BN, GM_FWD, true, true><<<grid, NTHREADS, 0, stream>>>(p);
-    else
-      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
-  else if (ws)
-    igemm_nt32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+    igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
 }
@@ -3112,24 +3021,18 @@ static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 // 6-8 register-staged split-K, 9-11 ring split-K (v % 3 = tile shape);
 // 12-23: the same twelve on the 32x32x16 MFMA (wide) kernels
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
-  if (p.fin.cnt) return (int)hipErrorInvalidValue;   // fused finalize: bf16 path only
   const bool fast = nt_fast32(p);
   p.pro = g_pro;
   if (p.pro.scsh && !fast) return (int)hipErrorInvalidValue;
-  const bool ws = fast && g_wsplit != nullptr;
-  if (ws) {
-    p.w = reinterpret_cast<const bf16_t*>(g_wsplit);
-    p.w_gstride = g_wsplit_stride;
-  }
-  // the ring kernel has no prologue / pre-split-weight form
-  const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh && !ws;
+  // the ring kernel has no prologue form
+  const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
   bool wide = false;
   if (v >= 12) {
     v -= 12;
-    // no prologue / pre-split-weight forms; BN-backward statistics (the
-    // unaligned-dgrad fallback) only in the NN kernels' wide epilogue
-    wide = !p.pro.scsh && !ws && p.bb.part == nullptr;
+    // no prologue form; BN-backward statistics (the unaligned-dgrad
+    // fallback) only in the NN kernels' wide epilogue
+    wide = !p.pro.scsh && p.bb.part == nullptr;
     if (((v / 3) & 1) && !ring_ok) v -= 3;
   }
   if (!fast) v = fp32_variant(v);
@@ -3141,9 +3044,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = (int)((p.M + bm - 1) / bm);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, ws, kind, stream, wide); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, ws, kind, stream, wide); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, ws, kind, stream, wide); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide); break;
   }
   return (int)hipGetLastError();
 }
@@ -3151,8 +3054,7 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
 static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, const BNFinal* fin, bool f32,
-                         hipStream_t stream);
+                         int act, float* stats, int* nslab, bool f32, hipStream_t stream);
 
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
@@ -3160,7 +3062,7 @@ CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
                          bf16_t* y, int Ho, int Wo, const bf16_t* bias, int64_t bias_gstride,
                          int act, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
-                       bias_gstride, act, nullptr, nullptr, nullptr, false, stream);
+                       bias_gstride, act, nullptr, nullptr, false, stream);
 }
 
 CER_API int cer_conv_fwd_f32(const float* x, int B, int H, int W, int Cin, int G, const float* w,
@@ -3168,7 +3070,7 @@ CER_API int cer_conv_fwd_f32(const float* x, int B, int H, int W, int Cin, int G
                              float* y, int Ho, int Wo, const float* bias, int64_t bias_gstride,
                              int act, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo, bias,
-                       bias_gstride, act, nullptr, nullptr, nullptr, true, stream);
+                       bias_gstride, act, nullptr, nullptr, true, stream);
 }
 
 // forward + BN statistics partials (bias-free, no activation): part holds
@@ -3179,7 +3081,7 @@ CER_API int cer_conv_fwd_stats(const bf16_t* x, int B, int H, int W, int Cin, in
                                int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
                                int* nslab, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nslab, nullptr, false, stream);
+                       nullptr, 0, 0, part, nslab, false, stream);
 }
 
 CER_API int cer_conv_fwd_stats_f32(const float* x, int B, int H, int W, int Cin, int G,
@@ -3187,20 +3089,7 @@ CER_API int cer_conv_fwd_stats_f32(const float* x, int B, int H, int W, int Cin,
                                    int st, int pad, float* y, int Ho, int Wo, float* part,
                                    int* nslab, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nslab, nullptr, true, stream);
-}
-
-// forward + BN statistics + BN finalize (mean / invstd / running stats) in
-// one launch; cnt: G * ceil(Cout / 64) zeroed unsigned counters, persistent
-CER_API int cer_conv_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, int G,
-                                const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
-                                int st, int pad, bf16_t* y, int Ho, int Wo, float* part,
-                                unsigned* cnt, float* ws, float* mean_out, float* invstd_out,
-                                float* rmean, float* rvar, int64_t rstride, float eps,
-                                float momentum, hipStream_t stream) {
-  BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
-  return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
-                       nullptr, 0, 0, part, nullptr, &f, false, stream);
+                       nullptr, 0, 0, part, nslab, true, stream);
 }
 
 // upper bound over tile choices: one slab per 64-row M tile
@@ -3211,10 +3100,8 @@ CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
 static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, const BNFinal* fin, bool f32,
-                         hipStream_t stream) {
+                         int act, float* stats, int* nslab, bool f32, hipStream_t stream) {
   NTParams p;
-  p.fin = fin ? *fin : BNFinal{};
   p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, f32 ? 4 : 2);
   p.dgrad = 0;
   p.w = reinterpret_cast<const bf16_t*>(w);
@@ -3284,24 +3171,19 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 }
 
 template <int BM, int BN>
-static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, bool ws,
-                          hipStream_t stream, bool wide = false) {
+static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
+                          bool wide = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
-  if (wide) {                      // 32x32x16 MFMA twins (no pre-split-weight form)
+  if (wide) {                      // 32x32x16 MFMA twins
     if (strided)
-      igemm_nn32<BM, BN, GM_DGS, false, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     else
-      igemm_nn32<BM, BN, GM_DG1, false, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      igemm_nn32<BM, BN, GM_DG1, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     return;
   }
   if (strided)
-    if (ws)
-      igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
-    else
-      igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
-  else if (ws)
-    igemm_nn32<BM, BN, GM_DG1, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
   else
     igemm_nn32<BM, BN, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
 }
@@ -3315,7 +3197,6 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
   NTParams p;
   p.addend = reinterpret_cast<const bf16_t*>(addend);  // dx = dgrad + addend (null: dx = dgrad)
   p.stats = nullptr;
-  p.fin = BNFinal{};
   p.bias = nullptr;
   p.bias_gstride = 0;
   p.act = 0;
@@ -3356,7 +3237,7 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     bool wide = false;
     if (v >= 12) {                        // fp32 32x32x16-MFMA twins of 0-11
       v -= 12;
-      wide = f32 && g_wsplit == nullptr;
+      wide = f32;
     }
     if (f32) v = fp32_variant(v);
     set_splits(p, G, v, f32 ? KS : BK);
@@ -3372,15 +3253,10 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
     }
     if (f32) {
-      const bool ws = g_wsplit != nullptr;
-      if (ws) {
-        p.w = reinterpret_cast<const bf16_t*>(g_wsplit);
-        p.w_gstride = g_wsplit_stride;
-      }
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, ws, stream, wide); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, ws, stream, wide); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, ws, stream, wide); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide); break;
       }
       return (int)hipGetLastError();
     }
@@ -3801,7 +3677,7 @@ static GatherGeom stem_geom(const void* x4, int B, int H, int W, int Ho, int Wo,
 static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* x4, void* wpk, void* y, int Ho, int Wo, float* part,
-                         int* nslab, const BNFinal* fin, bool f32, hipStream_t stream) {
+                         int* nslab, bool f32, hipStream_t stream) {
   if (!cer_stem_ok(Cin, W, kw, st, pad)) return (int)hipErrorInvalidValue;
   const int64_t P = (int64_t)B * H * W;
   const int kwp = stem_kwp(kw);
@@ -3839,7 +3715,6 @@ static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
   p.o_H = Ho;
   p.o_W = Wo;
   p.stats = part;
-  p.fin = fin ? *fin : BNFinal{};
   return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
 
@@ -3849,7 +3724,7 @@ CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, c
                          bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
                          int* nslab, hipStream_t stream) {
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nslab, nullptr, false, stream);
+                       Wo, part, nslab, false, stream);
 }
 
 // fp32 twin: x4 / wpk / y fp32 (same element counts)
@@ -3858,19 +3733,7 @@ CER_API int cer_stem_fwd_f32(const float* x, int B, int H, int W, int Cin, int G
                              float* x4, float* wpk, float* y, int Ho, int Wo, float* part,
                              int* nslab, hipStream_t stream) {
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nslab, nullptr, true, stream);
-}
-
-// same with the BN finalize fused (see cer_conv_fwd_bnstat; bf16 only)
-CER_API int cer_stem_fwd_bnstat(const bf16_t* x, int B, int H, int W, int Cin, int G,
-                                const bf16_t* w, int64_t w_gstride, int Cout, int kh, int kw,
-                                int st, int pad, bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho,
-                                int Wo, float* part, unsigned* cnt, float* ws, float* mean_out,
-                                float* invstd_out, float* rmean, float* rvar, int64_t rstride,
-                                float eps, float momentum, hipStream_t stream) {
-  BNFinal f{cnt, ws, mean_out, invstd_out, rmean, rvar, rstride, eps, momentum};
-  return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nullptr, &f, false, stream);
+                       Wo, part, nslab, true, stream);
 }
 
 // dW of the stem from the repacked input; dwp: fp32 scratch of

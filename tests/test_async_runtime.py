@@ -225,7 +225,8 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
     model to the next rank and receives one from the previous.  With a
     forced 0.1 s per transfer a boundary's eight sends overlap (one phase,
     <= 2 x 0.1 s), instead of chaining through the ring (~0.8 s) as they did
-    when every rank walked its transfers one at a time on one communicator."""
+    when every rank walked its transfers one at a time on one communicator.
+    Measured as the mean number of a boundary's transfers in flight."""
     world = 8
     mp.spawn(_ring_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     sends = []
@@ -235,12 +236,15 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
         sends.append(sorted((s[0], s[1]) for s in d["spans"] if s[2] == "send"))
     nb = min(len(s) for s in sends)
     assert nb >= world - 1, [len(s) for s in sends]
-    phases = []
+    conc = []
     for k in range(nb):
-        t0 = min(s[k][0] for s in sends)
-        t1 = max(s[k][1] for s in sends)
-        phases.append(t1 - t0)
-        # spans of different ranks overlap: every send starts before the
-        # first one of the boundary has ended + one transfer
-    print("ring-shift phases (s):", [round(p, 3) for p in phases])
-    assert statistics.median(phases) <= 2 * 0.1, phases
+        spans = [s[k] for s in sends]
+        t0 = min(a for a, _ in spans)
+        t1 = max(b for _, b in spans)
+        # mean number of this boundary's transfers in flight: ~1 when they
+        # chain through the ring, up to 8 when they run as one phase (start
+        # skew between ranks -- the rotation is a data flow, not a barrier --
+        # only lowers it)
+        conc.append(sum(b - a for a, b in spans) / (t1 - t0))
+    print("ring-shift concurrency per boundary:", [round(c, 2) for c in conc])
+    assert statistics.median(conc) >= 3.0, conc

@@ -382,53 +382,6 @@ def test_embbag_matches_oracle(relu):
     assert _rel(h[1], t[1]) < 1e-2
 
 
-@pytest.mark.parametrize("case", [
-    (4, 14, 14, 64, 128, 3, 1, 1, 2, True, False),
-    (2, 56, 56, 3, 64, 7, 2, 3, 2, True, False),
-    (3, 9, 9, 128, 64, 1, 2, 0, 2, 6, True),
-])
-def test_conv_bn_fused_finalize_matches_oracle(case, monkeypatch):
-    """BN finalize by the last-arriving conv tile (CER_BN_FUSED_FINALIZE path)."""
-    from cerebro_ds_kpgi_amd.ops import _hip
-    monkeypatch.setattr(_hip, "_FUSED_FINALIZE", True)
-    test_conv_bn_fused_matches_oracle(case, -1)
-    test_conv_bn_fused_matches_oracle(case, 4)
-
-
-@pytest.mark.parametrize("act,res", [(True, False), (True, True), (6, False)])
-@pytest.mark.parametrize("shape", [(4, 14, 14, 64), (2, 7, 7, 3 * 256), (32, 28, 28, 256),
-                                   (32, 4, 4, 8 * 2048), (3, 5, 7, 48)])
-def test_bn_coop_bitwise_equals_staged(act, res, shape):
-    """Cooperative one-launch BN (grid_sync between stages) == the staged
-    partials / finalize / apply kernels, bit for bit (same reduction tiling)."""
-    from cerebro_ds_kpgi_amd.ops import _hip
-    G = 1 if shape[-1] % 2 else 2
-    C = shape[-1] // G
-    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
-             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
-    torch.manual_seed(7)
-    x = (2 * torch.randn(shape, device="cuda") + 0.3).to(torch.bfloat16)
-    r = torch.randn(shape, device="cuda").to(torch.bfloat16) if res else None
-    gy = torch.randn(shape, device="cuda").to(torch.bfloat16)
-    outs = []
-    try:
-        for coop in (1, 0):
-            _hip.lib().cer_bn_set_coop(coop)
-            a, refs = _make(specs, G, seed=5)
-            xx = x.clone().requires_grad_(True)
-            rr = r.clone().requires_grad_(True) if res else None
-            y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
-            y.backward(gy)
-            torch.cuda.synchronize()
-            outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
-                         a.master.clone()))
-    finally:
-        _hip.lib().cer_bn_set_coop(0)
-    for u, v in zip(*outs):
-        if u is not None:
-            assert torch.equal(u, v)
-
-
 @pytest.mark.parametrize("act,res", [(True, False), (False, False), (True, True)])
 @pytest.mark.parametrize("shape", [(4, 14, 14, 64), (32, 28, 28, 256), (2, 7, 7, 3 * 256)])
 def test_bn_bwd_mask_from_input_equals_mask_from_output(act, res, shape):
@@ -549,10 +502,15 @@ def test_dgrad_addend_equals_dgrad_plus_add(case):
     if k == 1 and p == 0 and s > 1:
         # strided 1x1: the addend is consumed, dx accumulates into its storage
         add2 = add.clone()
-        again = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add2)
+        again = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add2, consume_addend=True)
         torch.cuda.synchronize()
         assert again.data_ptr() == add2.data_ptr()
         assert torch.equal(again, plain)
+    # without the explicit opt-in the addend is never written
+    add3 = add.clone()
+    out = _hip.conv2d_dgrad(dy, refs["w"], xshape, s, p, addend=add3)
+    torch.cuda.synchronize()
+    assert out.data_ptr() != add3.data_ptr() and torch.equal(add3, add)
 
 
 def test_resnet50_gradjoin_on_gpu(monkeypatch):

@@ -194,3 +194,21 @@ def test_loader_refuses_normalised_float_pixels(tmp_path):
     assert stats["stored_bytes"] > 0 and stats["decode_s"] > 0
     with pytest.raises(da.NonIntegralPixels):
         loader(1)
+
+
+def test_loader_reused_for_two_windows(tmp_path):
+    """One loader object serves two prefetch windows (two partition stores):
+    the decode pool drains with the first window and is re-created for the
+    second, and an unconsumed window is cancelled by the next prefetch."""
+    root = str(tmp_path / "gp")
+    da.write_dataset(root, "imagenet", 2, n_train=6, n_valid=3, buffer_size=4)
+    loader = da.da_partition_loader(root, "cpu")
+    for _ in range(2):
+        loader.prefetch([0, 1])
+        out = [loader(p) for p in (0, 1)]
+        assert all(o[0].shape[0] == 6 and o[2].shape[0] == 3 for o in out)
+    loader.prefetch([0, 1])
+    first = loader(0)                      # window left half consumed
+    loader.prefetch([1])
+    tx, ty, vx, vy = loader(1)
+    assert tx.shape[0] == 6 and first[0].shape[0] == 6

@@ -251,68 +251,6 @@ def test_bn_link_dgrad_epilogue_wide_fp32(vd):
         _hip.conv_set_variant(1, -1)
 
 
-def _split_ref(p):
-    """fp32 -> the pre-split image [8 x bf16 hi | 8 x bf16 lo] per 8 values
-    (round-to-nearest-even bf16, as the kernels' cvt), as int32 words."""
-    p = p.contiguous()
-    hi = p.to(torch.bfloat16)
-    lo = (p - hi.float()).to(torch.bfloat16)
-    n = p.shape[-1]
-    img = torch.cat([hi.view(*p.shape[:-1], n // 8, 8), lo.view(*p.shape[:-1], n // 8, 8)], -1)
-    return img.reshape(*p.shape[:-1], 2 * n).view(torch.int32)
-
-
-def test_presplit_weight_image_tracks_params():
-    """Arena.wsplit == split(params) after init, after an Adam step and after
-    a host-side write + sync_work (the image the fp32 conv kernels read)."""
-    from cerebro_ds_kpgi_amd.ops.optim import optimizer_step
-    spec = ParamSpec("w", (64, 3, 3, 64), "weight", fan_in=576)
-    a, refs = _make([spec], 3)
-    if a.wsplit is None:
-        pytest.skip("CER_W_SPLIT=0")
-    assert torch.equal(a.wsplit, _split_ref(a.params))
-    for g in range(3):
-        a.set_hparams(g, 1e-3, 1e-4)
-    a.grad.normal_()
-    optimizer_step(a, "adam")
-    torch.cuda.synchronize()
-    assert torch.equal(a.wsplit, _split_ref(a.params))
-    a.params[1].mul_(0.5)
-    a.sync_work(1)
-    assert torch.equal(a.wsplit, _split_ref(a.params))
-
-
-@pytest.mark.parametrize("case", [CONV_CASES[0], CONV_CASES[2], CONV_CASES[4], CONV_CASES[8]])
-def test_conv_presplit_weights_match_in_kernel_split(case):
-    """The conv fwd / dgrad with the pre-split image give the same result as
-    splitting the fp32 weights in the kernel (same rounding; only split-K
-    accumulation order may differ)."""
-    B, H, W, cin, cout, k, s, p, G = case
-    spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
-    a, refs = _make([spec], G)
-    if a.wsplit is None:
-        pytest.skip("CER_W_SPLIT=0")
-    torch.manual_seed(1)
-    x = torch.randn(B, H, W, G * cin, device="cuda")
-    outs = []
-    for use in (True, False):
-        keep = a.wsplit
-        if not use:
-            a.wsplit = None
-        try:
-            xx = x.clone().requires_grad_(True)
-            y = P.conv2d(xx, refs["w"], s, p)
-            torch.manual_seed(3)
-            y.backward(torch.randn_like(y))
-            torch.cuda.synchronize()
-            outs.append((y.detach(), xx.grad))
-        finally:
-            a.wsplit = keep
-    e = (_rel(outs[0][0], outs[1][0]), _rel(outs[0][1], outs[1][1]))
-    print("presplit", case, "rel diff y/dx = %.2e %.2e" % e)
-    assert max(e) < 1e-6, e
-
-
 @pytest.mark.parametrize("act,res,stem", [(True, False, False), (True, True, False),
                                           (False, False, False), (True, False, True)])
 def test_conv_bn_unit_fp32_vs_fp64(act, res, stem):
@@ -419,6 +357,62 @@ def test_bn_link_dgrad_epilogue_fp32():
             "dW1": _rel(R["w1"].grad(),
                         P64["w1"].grad.view(G, C, C, 3, 3).permute(0, 1, 3, 4, 2))}
     print("bn_link", {k_: "%.1e" % v for k_, v in errs.items()})
+    assert max(errs.values()) < TOL, errs
+
+
+def test_bn_link_strided_gradjoin_inplace_fp32():
+    """A ResNet stage transition: a BN output h feeds two strided 1x1 convs
+    (c1 and the projection shortcut) joined by a GradJoin.  The second dgrad
+    accumulates into the first one's dx IN PLACE (consume_addend) and is
+    BN-linked (it carries h's whole gradient).  dx, dgamma / dbeta of h's BN
+    and both weight gradients against fp64 autograd."""
+    B, H, C, G = 8, 14, 64, 2
+    Co1, Co2 = 32, 128
+    specs = [ParamSpec("w0", (C, 3, 3, C), "weight", fan_in=9 * C),
+             ParamSpec("g0", (C,), "gamma"), ParamSpec("b0", (C,), "beta"),
+             ParamSpec("rm0", (C,), "running_mean"), ParamSpec("rv0", (C,), "running_var")]
+    for i, co in ((1, Co1), (2, Co2)):
+        specs += [ParamSpec("w%d" % i, (co, 1, 1, C), "weight", fan_in=C),
+                  ParamSpec("g%d" % i, (co,), "gamma"), ParamSpec("b%d" % i, (co,), "beta"),
+                  ParamSpec("rm%d" % i, (co,), "running_mean"),
+                  ParamSpec("rv%d" % i, (co,), "running_var")]
+    a, R = _make(specs, G, seed=13)
+    torch.manual_seed(9)
+    x = torch.randn(B, H, H, G * C, device="cuda").requires_grad_(True)
+    h = P.conv_bn_act(x, R["w0"], R["g0"], R["b0"], R["rm0"], R["rv0"], 1, 1, True, None,
+                      0.1, 1e-5, link_out=True)
+    j = P.GradJoin()
+    y1 = P.conv_bn_act(h, R["w1"], R["g1"], R["b1"], R["rm1"], R["rv1"], 2, 0, True, None,
+                       0.1, 1e-5, join=j)
+    y2 = P.conv_bn_act(h, R["w2"], R["g2"], R["b2"], R["rm2"], R["rv2"], 2, 0, False, None,
+                       0.1, 1e-5, join=j)
+    g1, g2 = torch.randn_like(y1), torch.randn_like(y2)
+    (y1 * g1).sum().add_((y2 * g2).sum()).backward()
+    torch.cuda.synchronize()
+
+    def unit(inp, w, g, b, st, pad, mask):
+        z = F.conv2d(inp, w, None, st, pad, 1, G)
+        m = z.mean((0, 2, 3)).view(1, -1, 1, 1)
+        v = z.var((0, 2, 3), unbiased=False).view(1, -1, 1, 1)
+        o = (z - m) / torch.sqrt(v + 1e-5) * g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+        return o if mask is None else o * _nchw((mask > 0).double())
+    x64 = _nchw(x.detach().double()).requires_grad_(True)
+    P64 = {}
+    for i in (0, 1, 2):
+        P64["w%d" % i] = _w64(R["w%d" % i]).requires_grad_(True)
+        P64["g%d" % i] = R["g%d" % i].master().double().reshape(-1).requires_grad_(True)
+        P64["b%d" % i] = R["b%d" % i].master().double().reshape(-1).requires_grad_(True)
+    h64 = unit(x64, P64["w0"], P64["g0"], P64["b0"], 1, 1, h.detach())
+    o1 = unit(h64, P64["w1"], P64["g1"], P64["b1"], 2, 0, y1.detach())
+    o2 = unit(h64, P64["w2"], P64["g2"], P64["b2"], 2, 0, None)
+    ((o1 * _nchw(g1.double())).sum() + (o2 * _nchw(g2.double())).sum()).backward()
+    errs = {"dx": _rel(x.grad, _nhwc(x64.grad)),
+            "dgamma0": _rel(R["g0"].grad().reshape(-1), P64["g0"].grad),
+            "dbeta0": _rel(R["b0"].grad().reshape(-1), P64["b0"].grad),
+            "dW0": _rel(R["w0"].grad(), P64["w0"].grad.view(G, C, C, 3, 3).permute(0, 1, 3, 4, 2)),
+            "dW1": _rel(R["w1"].grad(), P64["w1"].grad.view(G, Co1, C, 1, 1).permute(0, 1, 3, 4, 2)),
+            "dW2": _rel(R["w2"].grad(), P64["w2"].grad.view(G, Co2, C, 1, 1).permute(0, 1, 3, 4, 2))}
+    print("bn_link strided gradjoin", {k_: "%.1e" % v for k_, v in errs.items()})
     assert max(errs.values()) < TOL, errs
 
 

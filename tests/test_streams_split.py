@@ -4,8 +4,7 @@ The GPU tier checks the numerics of the side-stream split
 (tests/test_graph_gpu.py); here the launch pattern itself is pinned with the
 flush replaced by a recorder: the adaptive split (packs of >= 4 configs,
 runtime/group.py) launches ONE side batch of ceil(frac * previous step's
-layer count) layers and the tail on the current stream, with the fork hook
-called around the side batch only.
+layer count) layers and the tail on the current stream.
 """
 
 import pytest
@@ -16,19 +15,16 @@ from cerebro_ds_kpgi_amd.ops import streams as S
 @pytest.fixture
 def recorder(monkeypatch):
     calls = []
+    count = [0]
 
-    def fake_flush(discard=False, side=False, grid=None):
+    def fake_hold_count(*a, **k):
+        pass
+
+    def fake_flush(discard=False, side=False):
         if not S._HELD:
             return
-        hook = S._HOOK if (side and S._DEFER) else None
-        if hook is not None:
-            hook.pre()
-        calls.append(("side" if side else "main", S._NQ, S._CUR[1] if side else 0))
-        if hook is not None:
-            hook.after(list(S._SPANS))
+        calls.append(("side" if side else "main", len(S._HELD), S._SPLIT_GRID if side else 0))
         del S._HELD[:]
-        del S._SPANS[:]
-        S._NQ = 0
 
     monkeypatch.setattr(S, "flush_wgrad", fake_flush)
     monkeypatch.setattr(S.torch.cuda, "is_available", lambda: True)
@@ -36,31 +32,18 @@ def recorder(monkeypatch):
     yield calls
 
 
-class _Hook(object):
-    def __init__(self):
-        self.log = []
-
-    def pre(self):
-        self.log.append("pre")
-
-    def after(self, ptrs):
-        self.log.append(("after", len(ptrs)))
-
-
 @pytest.mark.parametrize("n,frac,want", [(53, 0.5, 27), (54, 0.5, 27), (10, 0.4, 4)])
 def test_adaptive_split_one_side_batch_then_tail(recorder, n, frac, want):
-    hook = _Hook()
     for step in range(3):
         del recorder[:]
-        with S.deferred_wgrad(True, side_frac=frac, key="k", hook=hook):
+        with S.deferred_wgrad(True, side_frac=frac, key="k"):
             for i in range(n):
                 S.hold(object(), grad_ptr=4 * i)
         if step == 0:      # no layer count yet: one batch at the end
             assert recorder == [("main", n, 0)]
         else:
             assert recorder == [("side", want, S._SPLIT_GRID), ("main", n - want, 0)]
-    assert hook.log == ["pre", ("after", want)] * 2
-    assert S._CUR == (0, 0) and S._HOOK is None and not S._DEFER
+    assert S._SPLIT_AT == 0 and not S._DEFER
 
 
 def test_no_split_without_fraction(recorder):
