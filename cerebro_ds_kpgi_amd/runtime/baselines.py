@@ -22,7 +22,9 @@
 * Task parallelism (Hyperopt-Spark, D6) is ``MOPEngine`` with
   ``scheduler="task"``: data replicated on every GPU, whole models per GPU.
 
-All three reuse the pack groups (packed configs, HIP kernels, HIP graphs).
+All three reuse the pack groups (packed configs, HIP kernels, HIP graphs;
+the DDP step is captured as graph segments cut at the bucket boundaries, the
+all-reduces run between segment replays -- ``SegmentedGraph``).
 """
 
 import collections
@@ -61,8 +63,7 @@ class _GroupEngine(object):
         for m in range(len(self.msts)):
             by_key[pack_key(self.msts[m])].append(m)
         self.groups = {k: PackGroup(k, ms, self.msts, self.store, self.device, self.dtype,
-                                    seed_base=opts.seed * 100,
-                                    use_graphs=opts.use_graphs and self.mode != "ddp",
+                                    seed_base=opts.seed * 100, use_graphs=opts.use_graphs,
                                     l2=opts.l2)
                        for k, ms in by_key.items()}
         self.mst_state = {m: {"train_loss": [], "valid_loss": [], "train_top5_error": [],
@@ -159,7 +160,13 @@ class GradBuckets(object):
     (before the optimizer) reduces the rest, makes the compute stream wait
     for every bucket and averages.  Bucket sizes are per-link sized: ring
     all-reduce over xGMI is bound by one link (~50 GB/s per direction), so
-    25-64 MB buckets keep ~1 ms transfers in flight behind the backward."""
+    25-64 MB buckets keep ~1 ms transfers in flight behind the backward.
+
+    HIP graphs (``capture``): the step is captured as a chain of graph
+    SEGMENTS cut at every bucket boundary; the all-reduces stay outside the
+    graphs (launched from the host between two segment replays, so they
+    still overlap the next segment's backward) -- no collective is captured.
+    ``replay()`` runs segment, collective action, segment, ..."""
 
     def __init__(self, arena, world, bucket_bytes=32 << 20, group=None):
         self.arena = arena
@@ -170,6 +177,17 @@ class GradBuckets(object):
         self.works = []
         self.n_buckets = 0
         self.bucket_log = []           # (lo, hi) per bucket of the last step
+        self.seg = None                # SegmentedGraph while capturing
+
+    def _allreduce(self, lo, hi):
+        g = self.arena.grad
+        for row in range(g.shape[0]):
+            self.works.append(dist.all_reduce(g[row, lo:hi], group=self.group, async_op=True))
+
+    def _wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
 
     def ready_from(self, lo, force=False):
         if lo >= self.hi or (not force and self.hi - lo < self.bucket_cols):
@@ -180,24 +198,70 @@ class GradBuckets(object):
         # CURRENT stream: any side-stream weight-gradient work must be joined
         # first (group.py keeps DDP steps off the side batch; this is the guard)
         streams.join_side()
-        g = self.arena.grad
-        for row in range(g.shape[0]):
-            self.works.append(dist.all_reduce(g[row, lo:self.hi], group=self.group,
-                                              async_op=True))
+        if self.seg is not None:
+            self.seg.cut(("ar", lo, self.hi))
+        else:
+            self._allreduce(lo, self.hi)
         self.bucket_log.append((lo, self.hi))
         self.n_buckets += 1
         self.hi = lo
 
     def finish(self, arena=None):
         self.ready_from(0, force=True)
-        for w in self.works:
-            w.wait()
-        self.works = []
+        if self.seg is not None:
+            self.seg.cut(("wait",))
+        else:
+            self._wait()
         self.arena.grad.div_(self.world)
         self.hi = self.arena.layout.n_train
 
+    def run_action(self, act):
+        if act[0] == "ar":
+            self._allreduce(act[1], act[2])
+        else:
+            self._wait()
+
     def reset_log(self):
         self.bucket_log = []
+
+
+class SegmentedGraph(object):
+    """A step captured as several HIP graphs with host actions between them
+    (``cut(action)`` ends the current segment and opens the next one, sharing
+    one memory pool; ``replay(run_action)`` replays them in order).  Used for
+    the DDP step: collectives stay outside every graph."""
+
+    def __init__(self):
+        self.segs = []
+        self.actions = []
+        self._cur = None
+
+    def begin(self):
+        self._open()
+
+    def _open(self):
+        g = torch.cuda.CUDAGraph()
+        pool = self.segs[0].pool() if self.segs else None
+        g.capture_begin(pool=pool, capture_error_mode="relaxed")
+        self._cur = g
+
+    def cut(self, action):
+        self._cur.capture_end()
+        self.segs.append(self._cur)
+        self.actions.append(action)
+        self._open()
+
+    def end(self):
+        self._cur.capture_end()
+        self.segs.append(self._cur)
+        self.actions.append(None)
+        self._cur = None
+
+    def replay(self, run_action):
+        for g, act in zip(self.segs, self.actions):
+            g.replay()
+            if act is not None:
+                run_action(act)
 
 
 class DDPEngine(_GroupEngine):
@@ -217,7 +281,7 @@ class DDPEngine(_GroupEngine):
                 w.prepare(hop_optimizer_state=True)
                 if self.ctx.initialized and world > 1:
                     gb = GradBuckets(w.arena, world,
-                                     int(getattr(self.o, "ddp_bucket_mb", 32)) << 20)
+                                     int(float(getattr(self.o, "ddp_bucket_mb", 32)) * (1 << 20)))
                     w.net.grad_buckets = gb
                     w.grad_hook = gb.finish
                 B = grp.batch_size

@@ -96,6 +96,8 @@ class EngineOptions(object):
         self.sim_job_seconds = kw.get("sim_job_seconds", None)
         self.sim_valid_seconds = kw.get("sim_valid_seconds", 0.0)
         self.sim_hop_seconds = kw.get("sim_hop_seconds", 0.0)     # per hop (slow link)
+        # DDP baseline: gradient bucket size (MB per config row)
+        self.ddp_bucket_mb = kw.get("ddp_bucket_mb", 32)
 
 
 class _StepsPlan(object):

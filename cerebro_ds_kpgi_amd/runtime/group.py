@@ -298,15 +298,43 @@ class _Working(object):
             if done >= nsteps:
                 return done
             streams.join()
-            self.graph = torch.cuda.CUDAGraph()
-            # thread-local capture: the asynchronous runtime's hop thread keeps
-            # issuing RCCL transfers / stream syncs while this thread captures
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-                self._step()
+            gb = getattr(self.net, "grad_buckets", None)
+            if gb is not None:
+                # DDP: graph segments cut at the bucket boundaries, the
+                # all-reduces run between their replays (baselines.GradBuckets)
+                self.graph = self._capture_segmented(gb)
+            else:
+                self.graph = torch.cuda.CUDAGraph()
+                # thread-local capture: the asynchronous runtime's hop thread
+                # keeps issuing RCCL transfers / stream syncs while this
+                # thread captures
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                    self._step()
+        gb = getattr(self.net, "grad_buckets", None)
         while done < nsteps:
-            self.graph.replay()
+            if gb is not None and not isinstance(self.graph, torch.cuda.CUDAGraph):
+                self.graph.replay(gb.run_action)
+            else:
+                self.graph.replay()
             done += 1
         return done
+
+    def _capture_segmented(self, gb):
+        from .baselines import SegmentedGraph
+        sg = SegmentedGraph()
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            sg.begin()
+            gb.seg = sg
+            try:
+                self._step()
+            finally:
+                gb.seg = None
+            sg.end()
+        torch.cuda.current_stream().wait_stream(s)
+        return sg
 
     def _vstep(self):
         g = self.group
