@@ -54,10 +54,15 @@ def main():
                          "reported as a diag_ metric")
     ap.add_argument("--no_graphs", action="store_true")
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--workload", default="headline", choices=["headline", "criteo16", "hetero8"],
+    ap.add_argument("--workload", default="headline",
+                    choices=["headline", "criteo16", "hetero8", "e2e16"],
                     help="headline = BASELINE.json's metric; criteo16 / hetero8 = the other "
                          "BASELINE configs (16-config Criteo confA grid; {ResNet-50, VGG-16} x "
-                         "{lr, batch}), reported as diag_* metrics")
+                         "{lr, batch}); e2e16 = the reference's end-to-end 16-config grid "
+                         "{vgg16, resnet50} x bs{32, 256} x lr x lambda (imagenetcat.py:44-49); "
+                         "all but headline reported as diag_* metrics")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="diagnostic: override the headline grid's batch size")
     ap.add_argument("--da", action="store_true",
                     help="diagnostic: write the synthetic partitions as Greenplum-format DA "
                          "pages first (untimed) and load them through the C++ page / TOAST / "
@@ -88,9 +93,13 @@ def main():
         grid = dict(cat.param_grid_criteo)            # 2 lr x 2 lambda x 4 batch = 16
     elif args.workload == "hetero8":
         grid = dict(cat.param_grid_hetero_rv)         # 2 lr x 2 batch x {resnet50, vgg16}
+    elif args.workload == "e2e16":
+        grid = dict(cat.param_grid)                   # {vgg16, resnet50} x bs{32,256} x lr x l
     else:
         grid = dict(cat.param_grid_scalability)
         grid["model"] = [args.model]
+        if args.batch:
+            grid["batch_size"] = [args.batch]
     msts = get_msts(grid)
     if args.configs:
         msts = msts[:args.configs]
@@ -151,13 +160,14 @@ def main():
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(N)
         headline = (S == 8 and args.workload == "headline" and args.model == "resnet50"
-                    and args.dtype == "fp32")
+                    and args.dtype == "fp32" and args.batch in (0, 32))
         out = {
             "metric": ("agg_train_images_per_sec_8cfg_resnet50_mop" if headline else
                        "diag_train_{}_per_sec_{}cfg_{}_mop_{}".format(
                            "samples" if args.workload == "criteo16" else "images", S,
                            {"headline": args.model, "criteo16": "criteo_confA",
-                            "hetero8": "resnet50_vgg16"}[args.workload], args.dtype)),
+                            "hetero8": "resnet50_vgg16", "e2e16": "e2e_vgg16_resnet50"}[
+                               args.workload], args.dtype)),
             "value": round(value, 2),
             "unit": "samples/s" if args.workload == "criteo16" else "images/s",
             "n_gpus": N,
@@ -178,7 +188,8 @@ def main():
                      if backend == "hip" else "PyTorch-ROCm/MIOpen " + args.dtype),
             "data": "synthetic via DA pages (C++ reader)" if args.da else "synthetic",
             "config": {"model": {"headline": args.model, "criteo16": "confA",
-                                 "hetero8": "resnet50+vgg16"}[args.workload],
+                                 "hetero8": "resnet50+vgg16",
+                                 "e2e16": "vgg16+resnet50"}[args.workload],
                        "global_batch": sum(m["batch_size"] for m in msts), "seq_len": None,
                        "parallelism": "mop{}x{}".format(N, max(1, S // N)),
                        "configs": S,

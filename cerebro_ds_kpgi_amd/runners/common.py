@@ -75,6 +75,16 @@ class _BatchedRun(object):
         self.data_load_time = etl
 
 
+def hyperopt_grid(args):
+    """The reference search space (``run_ctq_hyperopt.py:76-91``), with the
+    model choices replaced by ``--hyperopt_models`` when given."""
+    grid = dict(hh.param_grid_hyperopt)
+    models = [m for m in (getattr(args, "hyperopt_models", "") or "").split(",") if m]
+    if models:
+        grid["model"] = models
+    return grid
+
+
 def run_batched_hyperopt(args, ctx, loader, param_grid=None, engine_kw=None):
     """CTQ-Hyperopt (reference ``run_ctq_hyperopt.py:122-160``): TPE proposes
     ``concurrency`` configs, ONE greedy MOP session trains that batch for
@@ -85,7 +95,7 @@ def run_batched_hyperopt(args, ctx, loader, param_grid=None, engine_kw=None):
     import pickle
     import argparse
     conc = args.concurrency or args.size or ctx.world
-    grid = param_grid or hh.param_grid_hyperopt
+    grid = param_grid or hyperopt_grid(args)
     hp, msts, trials, domain, rand, _ = hh.init_hyperopt(grid, argparse.Namespace(size=conc))
     start, end = 0, len(msts)
     all_state, images, etl = {}, 0, 0.0
@@ -146,7 +156,7 @@ def run_approach(approach, argv=None, shuffle=True):
         eng = run_batched_hyperopt(args, ctx, loader)
     elif args.hyperopt and approach not in ("ma", "ddp"):
         # initial batch proposed by TPE (model ids == trial order)
-        tpe_state = hh.init_hyperopt(args=args)
+        tpe_state = hh.init_hyperopt(hyperopt_grid(args), args=args)
         msts = tpe_state[1]
     if approach == "ctq_hyperopt":
         pass
@@ -168,7 +178,8 @@ def run_approach(approach, argv=None, shuffle=True):
         if tpe_state is not None:
             hp, _, trials, domain, rand, _ = tpe_state
             mst_eval = hh.mst_eval_fn_hyperopt(args.num_epochs, hp, trials, domain,
-                                               args.max_num_config, rand, len(msts))
+                                               args.max_num_config, rand, len(msts),
+                                               param_grid=hyperopt_grid(args))
         else:
             mst_eval = hh.mst_eval_fn(args.num_epochs)
         epochs = 10 ** 6 if args.hyperopt else args.num_epochs

@@ -61,6 +61,9 @@ def get_main_parser():
     p.add_argument("--spark_data_prepared", action="store_true")
     p.add_argument("--hdfs", action="store_true")
     p.add_argument("--max_num_config", type=int, default=32)
+    p.add_argument("--hyperopt_models", type=str, default="",
+                   help="comma list replacing the hyperopt space's model choices (reference: "
+                        "resnet18,resnet34; BASELINE config 5: resnet50)")
     # ---- MI355X engine flags ----
     p.add_argument("--synthetic", type=_bool, default=True,
                    help="generate ImageNet/Criteo-shaped data on the GPUs (no datasets offline)")
