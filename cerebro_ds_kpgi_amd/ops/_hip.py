@@ -695,6 +695,103 @@ def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad
     launch()
 
 
+# ---- grouped convolutions (ResNeXt cardinality; conv.hip cer_conv_grouped_*) ----
+_SIGS.update({
+    "cer_conv_grouped_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i,
+                             c_i, c_p, c_i, c_i, c_p],
+    "cer_conv_grouped_dgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_i,
+                               c_i, c_i, c_i, c_p, c_i, c_i, c_p],
+    "cer_conv_grouped_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i,
+                               c_i, c_i, c_p, c_i64, c_i, c_p],
+    "cer_wgrad_batch_add_grouped": [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i,
+                                    c_i, c_i, c_i, c_p, c_i64],
+})
+
+
+def grouped_ok(wref, groups, stride, pad):
+    cout, kh, kw, cin_g = wref.spec.shape
+    return (groups >= 1 and cout % groups == 0 and
+            not (kh == 1 and kw == 1 and pad == 0 and stride > 1))
+
+
+def grouped_conv_fwd(x, wref, stride, pad, groups):
+    """y of a conv with ``groups`` channel groups inside each packed config;
+    weights per config [cout, kh, kw, cin / groups] (ops.nn.PackedGroupedConv2d)."""
+    x = _act(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    cout, kh, kw, cin_g = wref.spec.shape
+    cin = cin_g * groups
+    assert GC == G * cin, (x.shape, wref.spec.shape, G, groups)
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    y = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
+    wp, ws = wref.work_ptr()
+    _splitk_ready(x.device)
+
+    def launch():
+        _check(_fn("cer_conv_grouped_fwd", x)(_ptr(x), B, H, W, cin, G, groups, c_p(wp), ws, cout,
+                                              kh, kw, stride, pad, _ptr(y), Ho, Wo, _stream()),
+               "cer_conv_grouped_fwd")
+    _select(0, ("grouped", B, H, W, cin, cout, kh, kw, stride, pad, G, groups), launch, x.dtype)
+    launch()
+    return y
+
+
+def grouped_conv_dgrad(dy, wref, xshape, stride, pad, groups):
+    dy = _act(dy)
+    B, Ho, Wo, _ = dy.shape
+    _, H, W, _ = xshape
+    G = wref.G
+    cout, kh, kw, cin_g = wref.spec.shape
+    cin = cin_g * groups
+    dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
+    wp, ws = wref.work_ptr()
+    n_wt = cout * kh * kw * cin_g if ((cout // groups) % 8 or cin_g % 8) else 1
+    wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
+    _splitk_ready(dy.device)
+
+    def launch():
+        _check(_fn("cer_conv_grouped_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, groups, c_p(wp), ws,
+                                                 _ptr(wt), cin, kh, kw, stride, pad, _ptr(dx), H,
+                                                 W, _stream()), "cer_conv_grouped_dgrad")
+    _select(1, ("grouped", B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, groups), launch,
+            dy.dtype)
+    launch()
+    return dx
+
+
+def grouped_conv_wgrad(x, dy, wref, stride, pad, groups):
+    x = _act(x)
+    dy = _act(dy)
+    B, H, W, _ = x.shape
+    _, Ho, Wo, _ = dy.shape
+    G = wref.G
+    cout, kh, kw, cin_g = wref.spec.shape
+    cin = cin_g * groups
+    gp, gs = wref.grad_ptr()
+    if streams.batching():
+        splits = _fn("cer_wgrad_batch_add_grouped", x)(_ptr(x), B, H, W, cin, G, groups, _ptr(dy),
+                                                       Ho, Wo, cout, kh, kw, stride, pad,
+                                                       c_p(gp), gs)
+        if splits > 0:
+            if splits > 1 and not wref.arena.grad_clean:
+                wref.grad().zero_()
+            streams.hold(x, dy, grad_ptr=gp)
+            return
+
+    def launch():
+        splits = lib().cer_wgrad_splits(B * Ho * Wo, cout // groups, kh * kw * cin_g, groups)
+        if splits > 1 and not wref.arena.grad_clean:
+            wref.grad().zero_()
+        _check(_fn("cer_conv_grouped_wgrad", x)(_ptr(x), B, H, W, cin, G, groups, _ptr(dy), Ho,
+                                                Wo, cout, kh, kw, stride, pad, c_p(gp), gs,
+                                                splits, _stream()), "cer_conv_grouped_wgrad")
+    _select(2, ("grouped", B, H, W, cin, cout, kh, kw, stride, pad, G, groups, Ho, Wo), launch,
+            x.dtype, after_tune=lambda: wref.grad().zero_())
+    launch()
+
+
 def conv2d_wgrad(x, dy, wref, stride, pad, pro=None):
     x = _act(x)
     dy = _act(dy)

@@ -691,25 +691,30 @@ def dwconv2d(x, wref, stride=1, pad=1, anchor=None):
 
 
 # ---------------------------------------------------------------------------
-# grouped convolution inside each configuration (ResNeXt cardinality),
-# average pooling and per-config channel concat (DenseNet) — PyTorch path
+# grouped convolution inside each configuration (ResNeXt cardinality; HIP),
+# average pooling and per-config channel concat (DenseNet)
 # ---------------------------------------------------------------------------
 
 class PackedGroupedConv2d(torch.autograd.Function):
     """conv with ``groups`` channel groups per configuration.
 
-    W_g [cout, kh, kw, cin / groups]; all G configs run as one torch grouped
-    conv with G * groups groups.  No HIP kernel: the packed-G implicit GEMM
-    kernels assume dense per-config convs.
+    W_g [cout, kh, kw, cin / groups].  HIP: the packed implicit-GEMM kernels
+    run once per config over its ``groups`` sub-configs (conv.hip
+    ``cer_conv_grouped_*``; weight gradients join the deferred batch).
+    PyTorch oracle: one torch grouped conv with G * groups groups.
     """
 
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad, groups):
         ctx.wref, ctx.stride, ctx.pad, ctx.groups = wref, stride, pad, groups
-        if use_hip("conv", x):
-            note_fallback("grouped_conv")
-        w = _torch_weight(wref)
-        y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * groups))
+        ctx.hip = use_hip("conv", x) and _hip().grouped_ok(wref, groups, stride, pad)
+        if ctx.hip:
+            y = _hip().grouped_conv_fwd(x, wref, stride, pad, groups)
+        else:
+            if use_hip("conv", x):
+                note_fallback("grouped_conv")
+            w = _torch_weight(wref)
+            y = _nhwc(F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G * groups))
         ctx.save_for_backward(x)
         return y
 
@@ -717,11 +722,18 @@ class PackedGroupedConv2d(torch.autograd.Function):
     def backward(ctx, dy):
         x, = ctx.saved_tensors
         wref, stride, pad, groups = ctx.wref, ctx.stride, ctx.pad, ctx.groups
+        dy = dy.contiguous()
+        dx = None
+        if ctx.hip:
+            h = _hip()
+            if ctx.needs_input_grad[0]:
+                dx = h.grouped_conv_dgrad(dy, wref, x.shape, stride, pad, groups)
+            h.grouped_conv_wgrad(x, dy, wref, stride, pad, groups)
+            return dx, None, None, None, None, None
         G = wref.G
         cout, kh, kw, cin_g = wref.spec.shape
         w = _torch_weight(wref)
-        xn, dyn = _nchw(x), _nchw(dy.contiguous())
-        dx = None
+        xn, dyn = _nchw(x), _nchw(dy)
         if ctx.needs_input_grad[0]:
             dx = _nhwc(torch.nn.grad.conv2d_input(xn.shape, w, dyn, stride, pad, 1, G * groups))
         dw = torch.nn.grad.conv2d_weight(xn, w.shape, dyn, stride, pad, 1, G * groups)

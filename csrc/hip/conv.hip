@@ -3054,7 +3054,8 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
 static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, bool f32, hipStream_t stream);
+                         int act, float* stats, int* nslab, bool f32, hipStream_t stream,
+                         int ctot = 0, int ldc = 0, uint32_t shift = 0);
 
 
 CER_API int cer_conv_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
@@ -3100,14 +3101,19 @@ CER_API int64_t cer_conv_stats_floats(int64_t M, int C) {
 static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* y, int Ho, int Wo, const void* bias, int64_t bias_gstride,
-                         int act, float* stats, int* nslab, bool f32, hipStream_t stream) {
+                         int act, float* stats, int* nslab, bool f32, hipStream_t stream,
+                         int ctot, int ldc, uint32_t shift) {
+  // ctot / ldc: channel pitch of x / y when they hold more than these G
+  // packed blocks (grouped convs launch per config on shifted pointers;
+  // ``shift`` = bytes x was advanced by, taken off the buffer-load range)
   NTParams p;
-  p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, f32 ? 4 : 2);
+  p.a = make_geom(x, B, ctot ? ctot : G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, f32 ? 4 : 2);
+  if (p.a.bytes) p.a.bytes -= shift;
   p.dgrad = 0;
   p.w = reinterpret_cast<const bf16_t*>(w);
   p.w_gstride = w_gstride;
   p.out = reinterpret_cast<bf16_t*>(y);
-  p.ldc = G * Cout;
+  p.ldc = ldc ? ldc : G * Cout;
   p.M = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
@@ -3191,9 +3197,13 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
 static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int G, const void* w,
                            int64_t w_gstride, void* wt, int Cin, int kh, int kw, int st, int pad,
                            void* dx, int H, int W, const void* addend, bool f32,
-                           hipStream_t stream) {
+                           hipStream_t stream, int cout_tot = 0, int cin_tot = 0,
+                           uint32_t shift = 0) {
+  // cout_tot / cin_tot: channel pitch of dy / dx (grouped convs, per-config
+  // launches on shifted pointers; ``shift`` = bytes dy was advanced by)
   const int T = kh * kw;
   const int es = f32 ? 4 : 2;
+  const int ctot_dy = cout_tot ? cout_tot : G * Cout;
   NTParams p;
   p.addend = reinterpret_cast<const bf16_t*>(addend);  // dx = dgrad + addend (null: dx = dgrad)
   p.stats = nullptr;
@@ -3204,17 +3214,18 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
   p.o_H = H;
   p.o_W = W;
   p.out = reinterpret_cast<bf16_t*>(dx);
-  p.ldc = G * Cin;
+  p.ldc = cin_tot ? cin_tot : G * Cin;
   p.N = Cin;
   p.K = T * Cout;
   const bool aligned = (Cout % 8 == 0) && (Cin % 8 == 0) &&
-                       (uint64_t)B * Ho * Wo * G * Cout * es < (1ull << 31) &&
+                       (uint64_t)B * Ho * Wo * ctot_dy * es < (1ull << 31) &&
                        (uint64_t)Cout * T * Cin * es < (1ull << 31);
   if (aligned) {
     p.w = reinterpret_cast<const bf16_t*>(w);
     p.w_gstride = w_gstride;
     bool strided = false;
     if (kh == 1 && kw == 1 && pad == 0 && st > 1) {
+      if (cin_tot) return (int)hipErrorInvalidValue;   // grouped: not a strided 1x1
       // rows (b, ho, wo) of dy map to dx pixels (b, ho*st, wo*st); others get 0
       // (or the addend, which the kernel adds on the written pixels)
       const size_t bytes = (size_t)es * B * H * W * G * Cin;
@@ -3228,7 +3239,8 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       p.M = B * Ho * Wo;
       p.o_st = st;
     } else {
-      p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
+      p.a = make_geom(dy, B, ctot_dy, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
+      if (p.a.bytes) p.a.bytes -= shift;
       p.dgrad = 1;
       p.M = B * H * W;
       strided = st > 1;
@@ -3277,7 +3289,8 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     transpose_w_kernel<bf16_t><<<tg, 256, 0, stream>>>(reinterpret_cast<const bf16_t*>(w),
                                                        w_gstride, reinterpret_cast<bf16_t*>(wt),
                                                        Cout, T, Cin);
-  p.a = make_geom(dy, B, G * Cout, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
+  p.a = make_geom(dy, B, ctot_dy, Cout, Ho, Wo, H, W, kh, kw, st, pad, es);
+  if (p.a.bytes) p.a.bytes -= shift;
   p.dgrad = 1;
   p.w = reinterpret_cast<const bf16_t*>(wt);
   p.w_gstride = (int64_t)Cout * T * Cin;
@@ -3421,6 +3434,143 @@ CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int
   return (int)hipGetLastError();
 }
 
+// ---- grouped convolutions (ResNeXt cardinality) ----------------------------
+// A conv with ``groups`` channel groups inside each of the G packed configs
+// is, per config g, a packed conv of ``groups`` sub-configs: input channels
+// [g*Cin + j*Cin/groups, ...), output channels [g*Cout + j*Cout/groups, ...),
+// weights (per config [Cout][kh][kw][Cin/groups]) of group j at
+// w + g*w_gstride + j*(Cout/groups)*kh*kw*(Cin/groups).  The entry points
+// below launch the ordinary kernels once per config on shifted pointers with
+// the full tensors' channel pitch (G launches; ResNeXt packs are small).
+// Strided 1x1 grouped convs are refused (ResNeXt's grouped convs are 3x3).
+static bool grouped_ok(int Cin, int Cout, int groups) {
+  return groups >= 1 && Cin % groups == 0 && Cout % groups == 0;
+}
+
+template <typename E>
+static int grouped_fwd(const E* x, int B, int H, int W, int Cin, int G, int groups, const E* w,
+                       int64_t w_gstride, int Cout, int kh, int kw, int st, int pad, E* y, int Ho,
+                       int Wo, hipStream_t stream) {
+  if (!grouped_ok(Cin, Cout, groups)) return (int)hipErrorInvalidValue;
+  const int ci = Cin / groups, co = Cout / groups;
+  const int64_t wsub = (int64_t)co * kh * kw * ci;
+  const bool f32 = sizeof(E) == 4;
+  for (int g = 0; g < G; ++g) {
+    const int rc = conv_fwd_impl(x + (int64_t)g * Cin, B, H, W, ci, groups, w + g * w_gstride, wsub,
+                                 co, kh, kw, st, pad, y + (int64_t)g * Cout, Ho, Wo, nullptr, 0, 0,
+                                 nullptr, nullptr, f32, stream, G * Cin, G * Cout,
+                                 (uint32_t)((size_t)g * Cin * sizeof(E)));
+    if (rc) return rc;
+  }
+  return (int)hipGetLastError();
+}
+
+template <typename E>
+static int grouped_dgrad(const E* dy, int B, int Ho, int Wo, int Cout, int G, int groups,
+                         const E* w, int64_t w_gstride, E* wt, int Cin, int kh, int kw, int st,
+                         int pad, E* dx, int H, int W, hipStream_t stream) {
+  if (!grouped_ok(Cin, Cout, groups) || (kh == 1 && kw == 1 && pad == 0 && st > 1))
+    return (int)hipErrorInvalidValue;
+  const int ci = Cin / groups, co = Cout / groups;
+  const int64_t wsub = (int64_t)co * kh * kw * ci;
+  const bool f32 = sizeof(E) == 4;
+  for (int g = 0; g < G; ++g) {
+    const int rc = conv_dgrad_impl(dy + (int64_t)g * Cout, B, Ho, Wo, co, groups,
+                                   w + g * w_gstride, wsub, wt, ci, kh, kw, st, pad,
+                                   dx + (int64_t)g * Cin, H, W, nullptr, f32, stream, G * Cout,
+                                   G * Cin, (uint32_t)((size_t)g * Cout * sizeof(E)));
+    if (rc) return rc;
+  }
+  return (int)hipGetLastError();
+}
+
+// WGParams of config g of a grouped conv (sub-configs = its groups)
+template <typename E>
+static WGParams grouped_wg_params(const E* x, int B, int H, int W, int Cin, int G, int groups,
+                                  const E* dy, int Ho, int Wo, int Cout, int kh, int kw, int st,
+                                  int pad, float* dw, int64_t dw_gstride, int g) {
+  const int ci = Cin / groups, co = Cout / groups;
+  WGParams p;
+  p.x = make_geom(x + (int64_t)g * Cin, B, G * Cin, ci, H, W, Ho, Wo, kh, kw, st, pad,
+                  (int)sizeof(E));
+  if (p.x.bytes) p.x.bytes -= (uint32_t)((size_t)g * Cin * sizeof(E));
+  p.dy = reinterpret_cast<const bf16_t*>(dy + (int64_t)g * Cout);
+  p.ldy = G * Cout;
+  p.dw = dw + g * dw_gstride;
+  p.dw_gstride = (int64_t)co * kh * kw * ci;
+  p.Mred = B * Ho * Wo;
+  p.N = co;
+  p.K = kh * kw * ci;
+  p.pro = BNPro{nullptr, 0, 0};
+  return p;
+}
+
+CER_API int cer_conv_grouped_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                 int groups, const bf16_t* w, int64_t w_gstride, int Cout,
+                                 int kh, int kw, int st, int pad, bf16_t* y, int Ho, int Wo,
+                                 hipStream_t stream) {
+  return grouped_fwd(x, B, H, W, Cin, G, groups, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
+                     stream);
+}
+
+CER_API int cer_conv_grouped_fwd_f32(const float* x, int B, int H, int W, int Cin, int G,
+                                     int groups, const float* w, int64_t w_gstride, int Cout,
+                                     int kh, int kw, int st, int pad, float* y, int Ho, int Wo,
+                                     hipStream_t stream) {
+  return grouped_fwd(x, B, H, W, Cin, G, groups, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
+                     stream);
+}
+
+// wt: scratch of G * Cout * kh * kw * Cin / groups elements (unaligned fallback)
+CER_API int cer_conv_grouped_dgrad(const bf16_t* dy, int B, int Ho, int Wo, int Cout, int G,
+                                   int groups, const bf16_t* w, int64_t w_gstride, bf16_t* wt,
+                                   int Cin, int kh, int kw, int st, int pad, bf16_t* dx, int H,
+                                   int W, hipStream_t stream) {
+  return grouped_dgrad(dy, B, Ho, Wo, Cout, G, groups, w, w_gstride, wt, Cin, kh, kw, st, pad, dx,
+                       H, W, stream);
+}
+
+CER_API int cer_conv_grouped_dgrad_f32(const float* dy, int B, int Ho, int Wo, int Cout, int G,
+                                       int groups, const float* w, int64_t w_gstride, float* wt,
+                                       int Cin, int kh, int kw, int st, int pad, float* dx, int H,
+                                       int W, hipStream_t stream) {
+  return grouped_dgrad(dy, B, Ho, Wo, Cout, G, groups, w, w_gstride, wt, Cin, kh, kw, st, pad, dx,
+                       H, W, stream);
+}
+
+// dw must be zeroed by the caller when more than one split is used
+CER_API int cer_conv_grouped_wgrad(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                   int groups, const bf16_t* dy, int Ho, int Wo, int Cout, int kh,
+                                   int kw, int st, int pad, float* dw, int64_t dw_gstride,
+                                   int splits, hipStream_t stream) {
+  if (!grouped_ok(Cin, Cout, groups)) return (int)hipErrorInvalidValue;
+  for (int g = 0; g < G; ++g) {
+    WGParams p = grouped_wg_params(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad,
+                                   dw, dw_gstride, g);
+    const bool fast = wg_fast(Cin / groups, Cout / groups, p);
+    const int v = wg_variant(p.N, p.K, groups, fast);
+    switch (v % 3) {
+      case 0: launch_wg_t<64, 64>(p, groups, v / 3, fast, splits, stream); break;
+      case 1: launch_wg_t<128, 128>(p, groups, v / 3, fast, splits, stream); break;
+      default: launch_wg_t<128, 64>(p, groups, v / 3, fast, splits, stream); break;
+    }
+  }
+  return (int)hipGetLastError();
+}
+
+CER_API int cer_conv_grouped_wgrad_f32(const float* x, int B, int H, int W, int Cin, int G,
+                                       int groups, const float* dy, int Ho, int Wo, int Cout,
+                                       int kh, int kw, int st, int pad, float* dw,
+                                       int64_t dw_gstride, int splits, hipStream_t stream) {
+  if (!grouped_ok(Cin, Cout, groups)) return (int)hipErrorInvalidValue;
+  for (int g = 0; g < G; ++g) {
+    WGParams p = grouped_wg_params(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad,
+                                   dw, dw_gstride, g);
+    run_wg32(p, groups, splits, wg_fast32(Cin / groups, Cout / groups, p), stream);
+  }
+  return (int)hipGetLastError();
+}
+
 // ---- batched (deferred) weight gradients ----------------------------------
 // one queue per dtype; a flush launches both
 static WGParams g_wgq[4096];
@@ -3494,6 +3644,52 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   g_wgq32_G[g_wgq32_n] = G;
   g_wgq32[g_wgq32_n++] = p;
   return p.splits;
+}
+
+// queue a grouped conv's wgrad: one batch entry per config (sub-configs =
+// its groups); returns the split count or 0 (not eligible: launch directly)
+template <typename E>
+static int grouped_batch_add(const E* x, int B, int H, int W, int Cin, int G, int groups,
+                             const E* dy, int Ho, int Wo, int Cout, int kh, int kw, int st,
+                             int pad, float* dw, int64_t dw_gstride) {
+  const bool f32 = sizeof(E) == 4;
+  int& n = f32 ? g_wgq32_n : g_wgq_n;
+  if (!grouped_ok(Cin, Cout, groups) || n + G > 4096) return 0;
+  int splits = 0;
+  for (int g = 0; g < G; ++g) {
+    WGParams p = grouped_wg_params(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad,
+                                   dw, dw_gstride, g);
+    if (!(f32 ? wg_fast32(Cin / groups, Cout / groups, p) : wg_fast(Cin / groups, Cout / groups, p)))
+      return g == 0 ? 0 : -1;               // configs differ only by offsets: all or none
+    const int rows = wgb_rows();
+    p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
+    p.splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
+    splits = p.splits;
+    if (f32) {
+      g_wgq32_G[g_wgq32_n] = groups;
+      g_wgq32[g_wgq32_n++] = p;
+    } else {
+      g_wgq_G[g_wgq_n] = groups;
+      g_wgq[g_wgq_n++] = p;
+    }
+  }
+  return splits;
+}
+
+CER_API int cer_wgrad_batch_add_grouped(const bf16_t* x, int B, int H, int W, int Cin, int G,
+                                        int groups, const bf16_t* dy, int Ho, int Wo, int Cout,
+                                        int kh, int kw, int st, int pad, float* dw,
+                                        int64_t dw_gstride) {
+  return grouped_batch_add(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad, dw,
+                           dw_gstride);
+}
+
+CER_API int cer_wgrad_batch_add_grouped_f32(const float* x, int B, int H, int W, int Cin, int G,
+                                            int groups, const float* dy, int Ho, int Wo, int Cout,
+                                            int kh, int kw, int st, int pad, float* dw,
+                                            int64_t dw_gstride) {
+  return grouped_batch_add(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad, dw,
+                           dw_gstride);
 }
 
 // grid cap of the next fp32 batch flushes (0 = one block per work item)

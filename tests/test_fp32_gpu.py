@@ -647,3 +647,66 @@ def test_bn_apply_folded_into_consumer_fp32_vs_fp64(k2, p2):
         assert db < 1e-4 * refs["g1"].grad().abs().max().item() + 1e-6, db
     print("bn fold", k2, {k_: "%.1e" % v for k_, v in errs.items()})
     assert max(errs.values()) < TOL, errs
+
+
+@pytest.mark.parametrize("B,H,cin,cout,groups,k,s,G", [(4, 14, 128, 128, 32, 3, 1, 2),
+                                                     (2, 28, 256, 256, 32, 3, 2, 2),
+                                                     (3, 7, 64, 96, 8, 3, 1, 3),
+                                                     (2, 9, 48, 48, 4, 1, 1, 2)])
+def test_grouped_conv_fp32_vs_fp64(B, H, cin, cout, groups, k, s, G):
+    """ResNeXt grouped conv on the HIP kernels (per-config launches over the
+    groups, conv.hip cer_conv_grouped_*): y, dx, dW vs fp64 torch grouped conv,
+    inside and outside the deferred weight-gradient batch."""
+    from cerebro_ds_kpgi_amd.ops import _hip, streams
+    from cerebro_ds_kpgi_amd.ops.backend import take_fallbacks
+    p = k // 2
+    spec = ParamSpec("w", (cout, k, k, cin // groups), "weight", fan_in=k * k * cin // groups)
+    for batched in (False, True):
+        a, R = _make([spec], G, seed=21)
+        a.grad_clean = True
+        torch.manual_seed(2)
+        x = torch.randn(B, H, H, G * cin, device="cuda").requires_grad_(True)
+        take_fallbacks()
+        with streams.deferred_wgrad(batched):
+            y = P.grouped_conv2d(x, R["w"], s, p, groups)
+            gy = torch.randn_like(y)
+            y.backward(gy)
+        streams.join()
+        torch.cuda.synchronize()
+        assert not take_fallbacks(), "grouped conv fell back to PyTorch"
+        w64 = _w64(R["w"]).requires_grad_(True)
+        x64 = _nchw(x.detach().double()).requires_grad_(True)
+        y64 = F.conv2d(x64, w64, None, s, p, 1, G * groups)
+        y64.backward(_nchw(gy.double()))
+        errs = {"y": _rel(y, _nhwc(y64.detach())), "dx": _rel(x.grad, _nhwc(x64.grad)),
+                "dW": _rel(R["w"].grad(), w64.grad.view(G, cout, cin // groups, k, k)
+                           .permute(0, 1, 3, 4, 2))}
+        print("grouped", (B, H, cin, cout, groups, k, s, G, batched),
+              {kk: "%.1e" % v for kk, v in errs.items()})
+        assert max(errs.values()) < TOL, errs
+
+
+def test_resnext101_trains_on_hip_under_graph():
+    """Every op of resnext101 (grouped 3x3 convs included) runs on our HIP
+    kernels, so its step is captured as a HIP graph (round-2 VERDICT item 9)."""
+    from cerebro_ds_kpgi_amd.ops.backend import take_fallbacks
+    from cerebro_ds_kpgi_amd.parallel import init_distributed
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    bs = 4
+    msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": bs, "model": "resnext101"}
+            for lr in (1e-4, 1e-5)]
+    take_fallbacks()
+    eng = MOPEngine(msts, init_distributed(), EngineOptions(
+        n_train=16 * bs, n_valid=2 * bs, slots_per_gpu=2, verbose=False, ckpt_every="none",
+        compute_dtype="fp32", shuffle=False))
+    eng.sched.start_epoch(1)
+    eng.store.new_epoch(1)
+    eng._hop_and_load(eng.sched.next_round())
+    w = list(eng.groups.values())[0].current
+    w.prepare(True)
+    w.train_steps(6)
+    torch.cuda.synchronize()
+    assert not w.eager_only, "resnext101 fell back to eager (PyTorch ops)"
+    assert w.graph is not None, "the step was not captured"
+    assert torch.isfinite(w.arena.state).all()
+    eng.close()
