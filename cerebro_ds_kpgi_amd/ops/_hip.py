@@ -29,6 +29,12 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib",
                         os.environ.get("CER_HIP_LIB", "libcerebro_hip.so"))
 
 IMPLEMENTED = {"adam", "loss", "gather"}
+
+# BN partials of a conv epilogue go into STAT_SLABS slabs by fp32 atomics
+# (conv.hip cer_conv_set_stat_slabs), so every BN apply folds its finalize
+# (0: one slab per M tile, plain stores, a separate finalize launch for
+# layers with many tiles).  Buffers come zeroed from the step's stats arena.
+STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "8"))
 _RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
 
 c_p = ctypes.c_void_p
@@ -61,6 +67,9 @@ def lib():
                 fn.argtypes = args
                 fn.restype = c_i64 if name in _RET_I64 else c_i
         _LIB = L
+        if hasattr(L, "cer_conv_set_stat_slabs"):
+            L.cer_conv_set_stat_slabs.argtypes = [c_i]
+            L.cer_conv_set_stat_slabs(STAT_SLABS)
     return _LIB
 
 
@@ -157,6 +166,69 @@ def gather_images(X, Y, perm, part_of_row, cursor, B, x_out, y_out):
                                  _ptr(x_out), _ptr(y_out), n, H * W, G, B,
                                  ctypes.cast(mean, c_p), ctypes.cast(inv, c_p), _stream())
     _check(rc, "cer_gather_images")
+
+
+# ---------------------------------------------------------------------------
+# zeroed BN-statistics buffers (atomic slabs)
+# ---------------------------------------------------------------------------
+class _StatsArena(object):
+    """One zeroed fp32 buffer per training working set, handed out in call
+    order during a step and zeroed ONCE at the step's start (one fill kernel,
+    captured with the step's HIP graph) instead of a fill per layer.  Its
+    size settles in the first (eager) step; a buffer it outgrows is kept
+    alive (earlier graphs may hold it)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = None
+        self.off = 0
+        self.keep = []
+
+    def begin(self):
+        self.off = 0
+        if self.buf is not None:
+            self.buf.zero_()
+
+    def take(self, n):
+        n_al = (n + 63) // 64 * 64
+        if self.buf is None or self.off + n_al > self.buf.numel():
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("BN stats arena grew during graph capture")
+            size = max(self.off + n_al, 2 * (self.buf.numel() if self.buf is not None else 0),
+                       1 << 16)
+            if self.buf is not None:
+                self.keep.append(self.buf)
+            self.buf = torch.zeros(size, dtype=torch.float32, device=self.device)
+        t = self.buf[self.off:self.off + n]
+        self.off += n_al
+        return t
+
+
+_ARENA = [None]
+
+
+def stats_step(arena):
+    """Make ``arena`` (a ``_StatsArena`` or None) the current one and zero it
+    (runtime/group.py, at the start of every training step)."""
+    _ARENA[0] = arena
+    if arena is not None:
+        arena.begin()
+
+
+def new_stats_arena(device):
+    return _StatsArena(torch.device(device))
+
+
+def _stats_buffer(M, C, device):
+    """Zeroed buffer for a conv epilogue's BN partials of an [M, C] output."""
+    if STAT_SLABS > 0:
+        n = min(STAT_SLABS, (M + 63) // 64) * 2 * C
+    else:
+        n = int(lib().cer_conv_stats_floats(M, C))
+    a = _ARENA[0]
+    if a is None or a.device != torch.device(device) or not STAT_SLABS:
+        return torch.zeros(n, dtype=torch.float32, device=device)
+    return a.take(n)
 
 
 # ---------------------------------------------------------------------------
@@ -392,8 +464,7 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     z = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
     C = G * cout
     M = B * Ho * Wo
-    part = torch.empty(int(lib().cer_conv_stats_floats(M, C)), dtype=torch.float32,
-                       device=x.device)
+    part = _stats_buffer(M, C, x.device)
     nslab = ctypes.c_int(0)
     wp, ws = wref.work_ptr()
     _splitk_ready(x.device)
@@ -403,7 +474,9 @@ def conv2d_fwd_stats(x, wref, stride, pad):
                                           stride, pad, _ptr(z), Ho, Wo, _ptr(part),
                                           ctypes.byref(nslab), _stream())
         _check(rc, "cer_conv_fwd_stats")
-    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
+    # the autotune's timing launches accumulate into the (atomic) slabs
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
+            after_tune=part.zero_)
     launch()
     return z, part, nslab.value
 
@@ -489,7 +562,7 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     L = lib()
     _splitk_ready(dev)
     z = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=dev)
-    part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dev)
+    part = _stats_buffer(M, C, dev)
     wp, wstr = wref.work_ptr()
     nslab = ctypes.c_int(0)
     if stem:
@@ -501,7 +574,8 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
             _check(_fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                       stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
                                       _ptr(part), ctypes.byref(nslab), _stream()), "cer_stem_fwd")
-        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype)
+        _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype,
+                after_tune=part.zero_)
         launch()
         return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                              momentum, eps) + (x4, None)
@@ -511,7 +585,8 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
                                           kh, kw, stride, pad, _ptr(z), Ho, Wo,
                                           _ptr(part), ctypes.byref(nslab), _stream())
         _check(rc, "cer_conv_fwd_stats")
-    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
+            after_tune=part.zero_)
     launch()
     if fold_out:
         mean, invstd, scsh = bn_finalize_scsh(part, nslab.value, z, gref, bref, rmref,
@@ -541,8 +616,7 @@ def stem_fwd_stats(x, wref, stride, pad):
     L = lib()
     wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
                       device=x.device)
-    part = torch.empty(int(L.cer_conv_stats_floats(B * Ho * Wo, G * cout)), dtype=torch.float32,
-                       device=x.device)
+    part = _stats_buffer(B * Ho * Wo, G * cout, x.device)
     nslab = ctypes.c_int(0)
     wp, ws = wref.work_ptr()
 
@@ -551,7 +625,8 @@ def stem_fwd_stats(x, wref, stride, pad):
                                 _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
                                 ctypes.byref(nslab), _stream())
         _check(rc, "cer_stem_fwd")
-    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype)
+    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype,
+            after_tune=part.zero_)
     launch()
     return z, part, nslab.value, x4
 
@@ -575,7 +650,7 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend=None, bnstats=False, wref=None):
+                       addend=None, bnstats=False, wref=None, after_tune=None):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -602,7 +677,7 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
                                              cin, kh, kw, stride, pad, _ptr(scratch[0]), H, W,
                                              _ptr(scratch[0]), _stream()), "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
-            tune, dy.dtype)
+            tune, dy.dtype, after_tune=after_tune)
     launch()
 
 
@@ -643,7 +718,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
     link, ybn = bnlink
     L = lib()
     M, C = B * H * W, G * cin
-    part = torch.empty(int(L.cer_conv_stats_floats(M, C)), dtype=torch.float32, device=dy.device)
+    part = _stats_buffer(M, C, dy.device)
     nslab = ctypes.c_int(0)
     gp, gs = link.gref.work_ptr()
     bp, bs = link.bref.work_ptr()
@@ -652,7 +727,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
                            1 if link.has_res else 0, ctypes.byref(nslab))
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend, bnstats=True, wref=wref)
+                           addend, bnstats=True, wref=wref, after_tune=part.zero_)
     finally:
         L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
     if nslab.value > 0:

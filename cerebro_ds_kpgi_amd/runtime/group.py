@@ -215,6 +215,12 @@ class _Working(object):
         self.jobs = []
         # called between backward and the optimizer (DDP gradient all-reduce)
         self.grad_hook = None
+        # zeroed buffers for the conv epilogues' atomic BN partials, zeroed
+        # once per step (ops._hip._StatsArena)
+        self.stats_arena = None
+        if g.device.type == "cuda" and get_backend() == "hip":
+            from ..ops import _hip
+            self.stats_arena = _hip.new_stats_arena(g.device)
 
     def assign(self, jobs):
         self.jobs = list(jobs)
@@ -242,6 +248,16 @@ class _Working(object):
 
     # ------------------------------------------------------------------
     def _step(self):
+        if self.stats_arena is None:
+            return self._step_body()
+        from ..ops import _hip
+        _hip.stats_step(self.stats_arena)
+        try:
+            return self._step_body()
+        finally:
+            _hip.stats_step(None)
+
+    def _step_body(self):
         g = self.group
         gather_batch(g.store, True, self.part_of_row, self.cursor, g.batch_size, self.x, self.y)
         # weight gradients are queued during backward and launched as a few

@@ -152,7 +152,33 @@ struct NTParams {
   BNBwdEpi bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
                          0, 0};
   BNPro pro = BNPro{nullptr, 0, 0};   // fp32 fwd: BN-apply prologue on the gathered A operand
+  int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
+                          // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
 };
+
+// Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
+// with n > 0 every M tile adds its (sum, sum^2) / (sum dz, sum dz*xhat) into
+// slab (tile % n) by fp32 atomics, so the BN apply that consumes them reduces
+// n slabs, not one per tile, and folds the finalize (one BN launch per layer
+// and direction instead of two).  The caller hands zeroed buffers.
+static int g_stat_slabs = 0;
+CER_API void cer_conv_set_stat_slabs(int n) { g_stat_slabs = n > 0 ? n : 0; }
+
+__device__ __forceinline__ void stat_store(float* dst, float v, bool atomic) {
+  if (atomic)
+    atomicAdd(dst, v);
+  else
+    *dst = v;
+}
+
+// slab of M tile ``tile`` (see NTParams::stat_slabs)
+__device__ __forceinline__ int64_t stat_slab(int tile, int slabs) {
+  return slabs ? tile % slabs : tile;
+}
+
+static int stat_nslab(int tiles_m, int slabs) {
+  return slabs && tiles_m > slabs ? slabs : tiles_m;
+}
 
 
 struct WGParams {
@@ -499,13 +525,13 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
     xs[(LANES + lane) * BN + 8 * cc + e] = q8[e];
   }
   __syncthreads();
-  float* dstp = bb.part + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  float* dstp = bb.part + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc + (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
     if (n >= p.N) continue;
     float v = 0.f;
     for (int l = 0; l < LANES; ++l) v += xs[(q * LANES + l) * BN + nl];
-    dstp[(int64_t)q * p.ldc + n] = v;
+    stat_store(dstp + (int64_t)q * p.ldc + n, v, p.stat_slabs != 0);
   }
 }
 
@@ -671,10 +697,12 @@ __device__ __forceinline__ void stats_finish(const NTParams& p, const bf16_t* ld
   if (!p.stats) return;
   constexpr int LDE = BN + 8;
   const float* xch = reinterpret_cast<const float*>(lds + BM * LDE);
-  float* dst = p.stats + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  float* dst = p.stats + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc + (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
-    if (n < p.N) dst[(int64_t)q * p.ldc + n] = xch[q * BN + nl] + xch[(2 + q) * BN + nl];
+    if (n < p.N)
+      stat_store(dst + (int64_t)q * p.ldc + n, xch[q * BN + nl] + xch[(2 + q) * BN + nl],
+                 p.stat_slabs != 0);
   }
 }
 
@@ -1877,10 +1905,13 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       }
     }
   __syncthreads();
-  float* dst = (fstat ? p.stats : bb.part) + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  float* dst = (fstat ? p.stats : bb.part) + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc +
+               (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
-    if (n < p.N) dst[(int64_t)qd * p.ldc + n] = xch[qd * BN + nl] + xch[(2 + qd) * BN + nl];
+    if (n < p.N)
+      stat_store(dst + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                 p.stat_slabs != 0);
   }
 }
 
@@ -2236,10 +2267,13 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
   }
   if (!fstat && !bstat) return;
   __syncthreads();
-  float* dst = (fstat ? p.stats : bb.part) + (int64_t)(m0 / BM) * 2 * p.ldc + (int64_t)cfg * p.N;
+  float* dst = (fstat ? p.stats : bb.part) + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc +
+               (int64_t)cfg * p.N;
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
-    if (n < p.N) dst[(int64_t)qd * p.ldc + n] = xch[qd * BN + nl] + xch[(2 + qd) * BN + nl];
+    if (n < p.N)
+      stat_store(dst + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                 p.stat_slabs != 0);
   }
 }
 
@@ -2953,6 +2987,7 @@ static bool nt_fast(const NTParams& p) {
 }
 
 static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
+  p.stat_slabs = p.stats ? g_stat_slabs : 0;
   const bool fast = nt_fast(p);
   const bool pipe_ok = fast && p.a.Cg % 64 == 0;
   int v = choose(0, p.M, p.N, p.K, G, pipe_ok);
@@ -2963,7 +2998,7 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   if (nslab) {
     int bm, bn;
     tile_dims(v, bm, bn);
-    *nslab = (int)((p.M + bm - 1) / bm);
+    *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
     case 0: launch_nt_t<64, 64>(p, G, kind, fast, stream); break;
@@ -3021,6 +3056,7 @@ static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 // 6-8 register-staged split-K, 9-11 ring split-K (v % 3 = tile shape);
 // 12-23: the same twelve on the 32x32x16 MFMA (wide) kernels
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
+  p.stat_slabs = p.stats ? g_stat_slabs : 0;
   const bool fast = nt_fast32(p);
   p.pro = g_pro;
   if (p.pro.scsh && !fast) return (int)hipErrorInvalidValue;
@@ -3041,7 +3077,7 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   if (nslab) {
     int bm, bn;
     tile_dims(v, bm, bn);
-    *nslab = (int)((p.M + bm - 1) / bm);
+    *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
     case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide); break;
@@ -3258,9 +3294,10 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     // (a strided 1x1 dgrad leaves pixels at zero: fine without an addend)
     if (g_bb.part && (p.o_st == 1 || !addend)) {
       p.bb = g_bb;
+      p.stat_slabs = g_stat_slabs;
       int bm, bn;
       tile_dims(v, bm, bn);
-      if (g_bb_nslab) *g_bb_nslab = (p.M + bm - 1) / bm;
+      if (g_bb_nslab) *g_bb_nslab = stat_nslab((p.M + bm - 1) / bm, g_stat_slabs);
     } else if (g_bb_nslab) {
       *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
     }
