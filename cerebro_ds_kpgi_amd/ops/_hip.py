@@ -30,10 +30,11 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib",
 
 IMPLEMENTED = {"adam", "loss", "gather"}
 
-# BN partials of a conv epilogue go into STAT_SLABS slabs by fp32 atomics
-# (conv.hip cer_conv_set_stat_slabs), so every BN apply folds its finalize
-# (0: one slab per M tile, plain stores, a separate finalize launch for
-# layers with many tiles).  Buffers come zeroed from the step's stats arena.
+# BN partials of a conv epilogue go into STAT_SLABS slabs by exact fp64
+# atomics (conv.hip cer_conv_set_stat_slabs), so every BN apply folds its
+# finalize (0: one fp32 slab per M tile, plain stores, a separate finalize
+# launch for layers with many tiles).  Buffers come zeroed from the step's
+# stats arena.
 STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "8"))
 _RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
 
@@ -221,8 +222,8 @@ def new_stats_arena(device):
 
 def _stats_buffer(M, C, device):
     """Zeroed buffer for a conv epilogue's BN partials of an [M, C] output."""
-    if STAT_SLABS > 0:
-        n = min(STAT_SLABS, (M + 63) // 64) * 2 * C
+    if STAT_SLABS > 0:          # [slabs][2][C] doubles (conv.hip SLAB_F64)
+        n = min(STAT_SLABS, (M + 63) // 64) * 2 * C * 2
     else:
         n = int(lib().cer_conv_stats_floats(M, C))
     a = _ARENA[0]

@@ -329,8 +329,35 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_scsh(
     const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
     float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, int64_t M, int C,
     int Cper, float eps, float momentum, Strided gamma, Strided beta, float* __restrict__ scsh) {
-  finalize_fwd_task<false>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
-                           C, Cper, eps, momentum, blockIdx.x);
+  if (slabs & (1 << 24)) {            // fp64 atomic slabs (conv.hip SLAB_F64)
+    const int n = slabs & ((1 << 24) - 1);
+    const int c = blockIdx.x * FIN_C + threadIdx.x;
+    if (threadIdx.x < FIN_C && c < C) {
+      const double* pd = reinterpret_cast<const double*>(part);
+      double a = 0.0, b = 0.0;
+      for (int sl = 0; sl < n; ++sl) {
+        a += pd[(int64_t)sl * 2 * C + c];
+        b += pd[(int64_t)sl * 2 * C + C + c];
+      }
+      const float inv_m = 1.f / (float)M;
+      const float mu = (float)a * inv_m;
+      const float var = fmaxf((float)b * inv_m - mu * mu, 0.f);
+      const float is = rsqrtf(var + eps);
+      ws[c] = mu;
+      ws[C + c] = is;
+      mean_out[c] = mu;
+      invstd_out[c] = is;
+      const int g = c / Cper, cc = c - g * Cper;
+      float* rm = rmean + g * rstat_stride + cc;
+      float* rv = rvar + g * rstat_stride + cc;
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      *rm = (1.f - momentum) * *rm + momentum * mu;
+      *rv = (1.f - momentum) * *rv + momentum * unb;
+    }
+  } else {
+    finalize_fwd_task<false>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
+                             C, Cper, eps, momentum, blockIdx.x);
+  }
   const int c = blockIdx.x * FIN_C + threadIdx.x;
   if (threadIdx.x >= FIN_C || c >= C) return;
   const int g = c / Cper, cc = c - g * Cper;
@@ -534,6 +561,53 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   }
 }
 
+// fp64 slabs (conv.hip SLAB_F64: a few atomic-accumulated slabs [n][2][C]
+// of doubles, exact sums): every block sums its channels' n slabs in fp64,
+// one lane row per channel vector, and rounds once
+constexpr int SLAB_F64 = 1 << 24;
+
+__device__ __forceinline__ void fold_partials_f64(const double* __restrict__ part, int nslab, int C,
+                                                  const Map& mp, int cbk, float* red, float* a8,
+                                                  float* b8) {
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = cbk * mp.cb + tc * VEC;
+  float* fin = red;                              // [2][cb]
+  if (tr == 0 && c0 < C) {
+    double a[VEC], b[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) a[i] = b[i] = 0.0;
+    for (int sl = 0; sl < nslab; ++sl) {
+      const double* pa = part + (int64_t)sl * 2 * C + c0;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        a[i] += pa[i];
+        b[i] += pa[C + i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      fin[tc * VEC + i] = (float)a[i];
+      fin[mp.cb + tc * VEC + i] = (float)b[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    a8[i] = fin[tc * VEC + i];
+    b8[i] = fin[mp.cb + tc * VEC + i];
+  }
+}
+
+// either slab format (nslab carries SLAB_F64 for the fp64 one)
+__device__ __forceinline__ void fold_any(const float* __restrict__ part, int nslab, int C,
+                                         const Map& mp, int cbk, float* red, float* a8, float* b8) {
+  if (nslab & SLAB_F64)
+    fold_partials_f64(reinterpret_cast<const double*>(part), nslab & (SLAB_F64 - 1), C, mp, cbk,
+                      red, a8, b8);
+  else
+    fold_partials(part, nslab, C, mp, cbk, red, a8, b8);
+}
+
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
 template <typename T>
@@ -544,7 +618,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
-  fold_partials(part, nslab, C, mp, blockIdx.x, red, a, b);
+  fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = blockIdx.x * mp.cb + tc * VEC;
   if (c0 >= C) return;
@@ -606,7 +680,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     int rows_per_slab, int act, Map mp) {
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
-  fold_partials(part, nslab, C, mp, blockIdx.x, red, a, b);
+  fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = blockIdx.x * mp.cb + tc * VEC;
   if (c0 >= C) return;
@@ -738,7 +812,7 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                                             rrows, 0, mp);
     nslab = (int)rg.y;
   }
-  if (nslab <= fold_max()) {
+  if ((nslab & SLAB_F64) || nslab <= fold_max()) {     // fp64 slabs: always few
     dim3 fg;
     int frows;
     make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
@@ -862,7 +936,7 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
       bn_partials<T, 1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                     act, mp, gs, bs, Cper);
   }
-  if (nslab <= fold_max()) {
+  if ((nslab & SLAB_F64) || nslab <= fold_max()) {
     dim3 fg;
     int frows;
     make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);

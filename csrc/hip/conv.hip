@@ -157,27 +157,37 @@ struct NTParams {
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
-// with n > 0 every M tile adds its (sum, sum^2) / (sum dz, sum dz*xhat) into
-// slab (tile % n) by fp32 atomics, so the BN apply that consumes them reduces
-// n slabs, not one per tile, and folds the finalize (one BN launch per layer
-// and direction instead of two).  The caller hands zeroed buffers.
+// with n > 0 every M tile adds its fp32 (sum, sum^2) / (sum dz, sum dz*xhat)
+// into slab (tile % n) of an fp64 buffer [n][2][ldc] by fp64 atomics, so the
+// BN apply that consumes them reduces n slabs, not one per tile, and folds
+// the finalize (one BN launch per layer and direction instead of two).
+// fp64 makes the slab sums EXACT (a few dozen fp32 partials of similar
+// magnitude fit 53 bits), so the result does not depend on the atomics'
+// order: fp32 atomics here made two identical steps differ by 5 % in the
+// gradients of a fresh ResNet-50 (50 BN layers amplify 1e-7 statistic noise;
+// scripts/debug/slab_determinism.py).  The caller hands zeroed buffers; the
+// slab count it gets back carries SLAB_F64 (bn.hip reads the fp64 format).
 static int g_stat_slabs = 0;
 CER_API void cer_conv_set_stat_slabs(int n) { g_stat_slabs = n > 0 ? n : 0; }
+constexpr int SLAB_F64 = 1 << 24;
 
-__device__ __forceinline__ void stat_store(float* dst, float v, bool atomic) {
-  if (atomic)
-    atomicAdd(dst, v);
+// one partial into the statistics buffer: plain fp32 store (one slab per
+// tile) or an fp64 atomic add (``slabs`` > 0; ``dst`` then addresses the
+// float buffer as doubles at the same element index)
+__device__ __forceinline__ void stat_store(float* base, int64_t idx, float v, int slabs) {
+  if (slabs)
+    atomicAdd(reinterpret_cast<double*>(base) + idx, (double)v);
   else
-    *dst = v;
+    base[idx] = v;
 }
 
-// slab of M tile ``tile`` (see NTParams::stat_slabs)
-__device__ __forceinline__ int64_t stat_slab(int tile, int slabs) {
-  return slabs ? tile % slabs : tile;
+// element offset of (slab of M tile ``tile``, config, stat row 0)
+__device__ __forceinline__ int64_t stat_base(int tile, int slabs, int ldc, int cfg, int N) {
+  return (slabs ? tile % slabs : tile) * 2 * (int64_t)ldc + (int64_t)cfg * N;
 }
 
 static int stat_nslab(int tiles_m, int slabs) {
-  return slabs && tiles_m > slabs ? slabs : tiles_m;
+  return slabs ? (tiles_m > slabs ? slabs : tiles_m) | SLAB_F64 : tiles_m;
 }
 
 
@@ -525,13 +535,13 @@ __device__ __forceinline__ void store_tile(const NTParams& p, const bf16_t* lds,
     xs[(LANES + lane) * BN + 8 * cc + e] = q8[e];
   }
   __syncthreads();
-  float* dstp = bb.part + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc + (int64_t)cfg * p.N;
+  const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
     if (n >= p.N) continue;
     float v = 0.f;
     for (int l = 0; l < LANES; ++l) v += xs[(q * LANES + l) * BN + nl];
-    stat_store(dstp + (int64_t)q * p.ldc + n, v, p.stat_slabs != 0);
+    stat_store(bb.part, sb + (int64_t)q * p.ldc + n, v, p.stat_slabs);
   }
 }
 
@@ -697,12 +707,12 @@ __device__ __forceinline__ void stats_finish(const NTParams& p, const bf16_t* ld
   if (!p.stats) return;
   constexpr int LDE = BN + 8;
   const float* xch = reinterpret_cast<const float*>(lds + BM * LDE);
-  float* dst = p.stats + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc + (int64_t)cfg * p.N;
+  const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int q = t / BN, nl = t - q * BN, n = n0 + nl;
     if (n < p.N)
-      stat_store(dst + (int64_t)q * p.ldc + n, xch[q * BN + nl] + xch[(2 + q) * BN + nl],
-                 p.stat_slabs != 0);
+      stat_store(p.stats, sb + (int64_t)q * p.ldc + n, xch[q * BN + nl] + xch[(2 + q) * BN + nl],
+                 p.stat_slabs);
   }
 }
 
@@ -1905,13 +1915,13 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       }
     }
   __syncthreads();
-  float* dst = (fstat ? p.stats : bb.part) + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc +
-               (int64_t)cfg * p.N;
+  float* dst = fstat ? p.stats : bb.part;
+  const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
     if (n < p.N)
-      stat_store(dst + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
-                 p.stat_slabs != 0);
+      stat_store(dst, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                 p.stat_slabs);
   }
 }
 
@@ -2267,13 +2277,13 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
   }
   if (!fstat && !bstat) return;
   __syncthreads();
-  float* dst = (fstat ? p.stats : bb.part) + stat_slab(m0 / BM, p.stat_slabs) * 2 * p.ldc +
-               (int64_t)cfg * p.N;
+  float* dst = fstat ? p.stats : bb.part;
+  const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
     const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
     if (n < p.N)
-      stat_store(dst + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
-                 p.stat_slabs != 0);
+      stat_store(dst, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                 p.stat_slabs);
   }
 }
 
