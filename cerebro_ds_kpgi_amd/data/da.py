@@ -62,6 +62,8 @@ def lib():
                                          ctypes.c_uint32, i64]
         L.cer_da_writer_open.restype = vp
         L.cer_da_writer_add.argtypes = [vp, i32, i32, vp, i64, vp, i64, ctypes.c_int]
+        L.cer_da_writer_add_batch.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, vp, vp,
+                                              ctypes.c_int, ctypes.c_int]
         L.cer_da_writer_close.argtypes = [vp]
         _LIB = L
     return _LIB
@@ -155,28 +157,59 @@ def seg_dir(root, seg, dboid=DBOID):
 
 
 def write_partition(heap_path, toast_path, buffers, dist_key, toastrelid=99999,
-                    first_valueid=1 << 20, seg_bytes=SEG_BYTES, dep_inline=True):
-    """buffers: list of (buffer_id, indep ndarray, dep ndarray)."""
+                    first_valueid=1 << 20, seg_bytes=SEG_BYTES, dep_inline=True, log=None,
+                    threads=None):
+    """buffers: iterable of (buffer_id, indep ndarray, dep ndarray), consumed
+    ``threads`` at a time (the native writer compresses a batch's datums in
+    parallel); ``log``: optional progress callback (buffers, bytes written)."""
     os.makedirs(os.path.dirname(heap_path), exist_ok=True)
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
     w = lib().cer_da_writer_open(heap_path.encode(), toast_path.encode(), toastrelid,
                                  first_valueid, seg_bytes)
     if not w:
         raise IOError("DA writer open failed: {}".format(_err()))
-    for bid, indep, dep in buffers:
-        a = np.ascontiguousarray(indep)
-        b = np.ascontiguousarray(dep)
-        rc = lib().cer_da_writer_add(w, int(dist_key), int(bid), a.ctypes.data, a.nbytes,
-                                     b.ctypes.data, b.nbytes, int(bool(dep_inline)))
+    done = nbytes = 0
+
+    def flush(batch):
+        n = len(batch)
+        arr = lambda t, v: (t * n)(*v)
+        rc = lib().cer_da_writer_add_batch(
+            w, n, arr(ctypes.c_int32, [int(dist_key)] * n), arr(ctypes.c_int32, [b[0] for b in batch]),
+            arr(ctypes.c_void_p, [b[1].ctypes.data for b in batch]),
+            arr(ctypes.c_int64, [b[1].nbytes for b in batch]),
+            arr(ctypes.c_void_p, [b[2].ctypes.data for b in batch]),
+            arr(ctypes.c_int64, [b[2].nbytes for b in batch]), int(bool(dep_inline)), threads)
         if rc != 0:
             lib().cer_da_writer_close(w)
             raise IOError("DA write failed: {}".format(_err()))
+        return sum(b[1].nbytes + b[2].nbytes for b in batch)
+
+    batch = []
+    for bid, indep, dep in buffers:
+        batch.append((int(bid), np.ascontiguousarray(indep), np.ascontiguousarray(dep)))
+        if len(batch) == threads:
+            nbytes += flush(batch)
+            done += len(batch)
+            batch = []
+            if log is not None:
+                log(done, nbytes)
+    if batch:
+        nbytes += flush(batch)
+        done += len(batch)
+        if log is not None:
+            log(done, nbytes)
     if lib().cer_da_writer_close(w) != 0:
         raise IOError("DA writer close failed: {}".format(_err()))
 
 
 def write_dataset(root, dataset, num_partitions, n_train, n_valid, buffer_size=cat.TRAIN_BUFFER_SIZE,
-                  seed=cat.SEED, seg_bytes=SEG_BYTES):
-    """Synthetic packed tables for ``num_partitions`` segments + manifest."""
+                  seed=cat.SEED, seg_bytes=SEG_BYTES, verbose=False):
+    """Synthetic packed tables for ``num_partitions`` segments + manifest.
+    Buffers are converted to the float32 payload one at a time (a full
+    ImageNet partition is 24 GB as float32); ``verbose`` prints progress."""
+    import sys
+    import time
     from . import synthetic
     shapes = {"train": [], "valid": []}
     for p in range(num_partitions):
@@ -185,7 +218,7 @@ def write_dataset(root, dataset, num_partitions, n_train, n_valid, buffer_size=c
             s = seed * 1000 + 2 * p + (split == "valid")
             if dataset == "imagenet":
                 x, y = synthetic.image_partition(n, seed=s)
-                x = x.numpy().astype(np.float32)
+                x = x.numpy()                     # uint8; float32 per buffer below
                 classes = cat.NUM_CLASSES
             elif dataset == "criteo":
                 idx, y = synthetic.criteo_partition(n, seed=s)
@@ -196,16 +229,26 @@ def write_dataset(root, dataset, num_partitions, n_train, n_valid, buffer_size=c
                 raise ValueError(dataset)
             yy = np.zeros((n, classes), dtype=np.int16)
             yy[np.arange(n), y.numpy()] = 1
-            bufs = []
             for bid, s0 in enumerate(range(0, n, buffer_size)):
                 e = min(n, s0 + buffer_size)
-                bufs.append((bid, x[s0:e], yy[s0:e]))
                 shapes[split].append({"dist_key": p, "buffer_id": bid,
                                       "independent_var_shape": list(x[s0:e].shape),
                                       "dependent_var_shape": [e - s0, classes]})
+            bufs = ((bid, x[s0:min(n, s0 + buffer_size)].astype(np.float32),
+                     yy[s0:min(n, s0 + buffer_size)])
+                    for bid, s0 in enumerate(range(0, n, buffer_size)))
+            nbuf = (n + buffer_size - 1) // buffer_size
+            t0 = time.time()
+
+            def log(i, nb, p=p, split=split, nbuf=nbuf, t0=t0):
+                if verbose:
+                    print("  partition {} {}: {}/{} buffers, {:.2f} GB in {:.1f}s".format(
+                        p, split, i, nbuf, nb / 1e9, time.time() - t0), flush=True)
+                    sys.stdout.flush()
             d = seg_dir(root, p)
             write_partition(os.path.join(d, str(rel)), os.path.join(d, str(toast)), bufs, p,
-                            toastrelid=toast, first_valueid=(p + 1) << 20, seg_bytes=seg_bytes)
+                            toastrelid=toast, first_valueid=(p + 1) << 20, seg_bytes=seg_bytes,
+                            log=log)
     man = {"dataset": dataset, "num_partitions": num_partitions, "dboid": DBOID,
            "train": {"relfilenode": TRAIN_RELFILENODE, "toast_relfilenode": TRAIN_TOAST},
            "valid": {"relfilenode": VALID_RELFILENODE, "toast_relfilenode": VALID_TOAST},

@@ -16,6 +16,7 @@ import argparse
 import json
 import os
 import resource
+import sys
 import time
 
 
@@ -39,6 +40,8 @@ def main(argv=None):
     for p in pids:
         tx, ty, vx, vy = loader(p)
         n_img += tx.shape[0] + vx.shape[0]
+        print("partition {} in HBM at {:.1f}s".format(p, time.perf_counter() - t0), file=sys.stderr,
+              flush=True)
         del tx, ty, vx, vy
     if torch.cuda.is_available():
         torch.cuda.synchronize()

@@ -24,7 +24,7 @@ def main(argv=None):
     ap.add_argument("--buffer_size", type=int, default=cat.TRAIN_BUFFER_SIZE)
     a = ap.parse_args(argv)
     t = time.time()
-    da.write_dataset(a.root, a.dataset, a.partitions, a.train, a.valid, a.buffer_size)
+    da.write_dataset(a.root, a.dataset, a.partitions, a.train, a.valid, a.buffer_size, verbose=True)
     print("wrote {} partitions to {} in {:.1f}s".format(a.partitions, a.root, time.time() - t))
 
 

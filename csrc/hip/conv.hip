@@ -2287,15 +2287,73 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
   }
 }
 
+// Intra-block K split (WG = 2 wave groups of 256 threads, 512-thread
+// blocks): group g runs the unchanged 4-wave tile loop over its half of the
+// block's K range in its own LDS region, then group 1 hands its accumulators
+// to group 0 through LDS and exits; group 0 adds them and runs the epilogue
+// (barriers after the exit count the surviving waves only).  Doubles the
+// waves in flight per tile without split-K's workspace round trip: for the
+// latency-bound small-grid GEMMs of a one-config step (4x4 / 7x7 stages)
+// where 1-2 waves per SIMD cannot hide the load latency.  Both groups run the
+// same step count (the last group's surplus steps load zeros: every k at or
+// past ``klim`` is masked), so the block-wide barriers stay matched.
+struct KSplitRange {
+  int kt0, kt1, klim;
+};
+template <int WG>
+__device__ __forceinline__ KSplitRange group_range(const KRange& kr, int grp, int K) {
+  if constexpr (WG == 1) {
+    return KSplitRange{kr.kt0, kr.kt1, K};
+  } else {
+    const int h = (kr.kt1 - kr.kt0 + WG - 1) / WG;
+    const int g0 = kr.kt0 + grp * h;
+    return KSplitRange{g0, g0 + h, min(K, kr.kt1 * KS)};
+  }
+}
+
+// group 1 -> group 0 accumulator hand-off (WG == 2); false in group 1
+template <int WG, int BM, int BN>
+__device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], float* red, int grp,
+                                             int tid) {
+  if constexpr (WG == 1) {
+    return true;
+  } else {
+    constexpr int FI = BM / 32, FJ = BN / 32;
+    __syncthreads();
+    if (grp == 1) {
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[((i * FJ + j) * 4 + e) * NTHREADS + tid] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (grp == 1) return false;
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] += red[((i * FJ + j) * 4 + e) * NTHREADS + tid];
+    return true;
+  }
+}
+
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
-template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
-__global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
+template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false, int WG = 1>
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTParams p) {
+  static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
   constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+  static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
+                "group hand-off must fit one group's LDS region");
+  __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
+  const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
+  bf16_t* const lds = lds_all + grp * LDS_ELEMS;
 #define SA(buf) (lds + (buf) * (BM * BK))
 #define SB(buf) (lds + 2 * BM * BK + (buf) * (BN * BK))
 
@@ -2305,10 +2363,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
   const int split = work % p.splits;
   work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
-  const KRange kr = split_range<KS>(p, split);
+  const KSplitRange kr = group_range<WG>(split_range<KS>(p, split), grp, p.K);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x & (NTHREADS - 1), lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int my_chunk = tid & (CPR - 1);
   const float* wbase = reinterpret_cast<const float*>(p.w) + (int64_t)cfg * p.w_gstride;
@@ -2342,7 +2400,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
     if constexpr (GM != GM_SLOW) {
-      const bool kok = k0 < p.K;
+      const bool kok = k0 < kr.klim;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
@@ -2369,11 +2427,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     } else {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i)
-        gather_chunk_slow32(p.a, cfg, rows[i], k0, p.K, p.dgrad, ra[s][2 * i], ra[s][2 * i + 1]);
+        gather_chunk_slow32(p.a, cfg, rows[i], k0, kr.klim, p.dgrad, ra[s][2 * i], ra[s][2 * i + 1]);
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
         const int n = n0 + (tid + NTHREADS * i) / CPR;
-        load_row8_slow32(wbase + (int64_t)n * p.K + k0, n < p.N ? p.K - k0 : 0, rb[s][2 * i],
+        load_row8_slow32(wbase + (int64_t)n * p.K + k0, n < p.N ? max(kr.klim - k0, 0) : 0, rb[s][2 * i],
                          rb[s][2 * i + 1]);
       }
     }
@@ -2410,6 +2468,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nt32(NTParams p) {
     zero_acc<BM, BN>(acc);
     kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
                   [&](int cur) { mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
+    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all + LDS_ELEMS * (WG - 1)),
+                                  grp, tid))
+      return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
@@ -2542,14 +2603,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WIDE = false>
-__global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, FastDiv dCout) {
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTParams p, int T,
+                                                                         FastDiv dCout) {
+  static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
   constexpr int B_CPR = BN / 8, B_CH = KS * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
   constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
   constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[LDS_ELEMS];
+  static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
+                "group hand-off must fit one group's LDS region");
+  __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
+  const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
+  bf16_t* const lds = lds_all + grp * LDS_ELEMS;
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
@@ -2557,10 +2624,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
   const int split = work % p.splits;
   work /= p.splits;
   const int cfg = work / tiles, tile = work - cfg * tiles;
-  const KRange kr = split_range<KS>(p, split);
+  const KSplitRange kr = group_range<WG>(split_range<KS>(p, split), grp, p.K);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x & (NTHREADS - 1), lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int my_chunk = tid & (CPR - 1);
   const int Cout = p.a.Cg, Cin = p.N;
@@ -2581,7 +2648,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
   auto load_tiles = [&](int kt, auto S) {
     constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
-    const bool kok = k0 < p.K;
+    const bool kok = k0 < kr.klim;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
@@ -2596,7 +2663,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
       const int c = n0 + b_col;
       const int tap = (int)fdiv((uint32_t)k, dCout);
       const int n = k - tap * Cout;
-      const uint32_t o = (k < p.K && c < Cin) ? (uint32_t)((n * T + tap) * Cin + c) * 4u : OOB;
+      const uint32_t o = (k < kr.klim && c < Cin) ? (uint32_t)((n * T + tap) * Cin + c) * 4u : OOB;
       rb[s][2 * i] = bload(rW, o);
       rb[s][2 * i + 1] = bload(rW, o + 16u);
     }
@@ -2643,6 +2710,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void igemm_nn32(NTParams p, int T, Fas
       mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane,
                       acc);
     });
+    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all + LDS_ELEMS * (WG - 1)),
+                                  grp, tid))
+      return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
@@ -2884,6 +2954,9 @@ __global__ __launch_bounds__(256) void transpose_w_kernel(const E* __restrict__ 
 // Kernel variants: (staging kind) x (tile).  kind 0 = register-staged
 // double buffer, 1 = LDS-DMA ring; tile 0 = 64x64, 1 = 128x128, 2 = 128x64
 // (BM x BN; for wgrad BM tiles Cout, BN tiles K).  v = 3 * kind + tile.
+// fp32 only: 12-23 = the 32x32x16-MFMA twins of 0-11; 24-35 = the
+// intra-block K-split (512-thread) twins of the register-staged fwd / dgrad
+// kernels (ring ids map to their register twin; 128x128 has none).
 // cer_conv_set_variant(op, v) pins a variant per op (0 fwd, 1 dgrad, 2 wgrad)
 // for tuning; -1 = the built-in choice.
 static int g_variant[3] = {-1, -1, -1};
@@ -2914,8 +2987,9 @@ static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) 
 static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
   if (g_variant[op] >= 0) {
     int v = g_variant[op];
-    const int wide = v >= 12 ? 12 : 0;              // fp32 32x32x16-MFMA twins: 12-23
+    int wide = v >= 24 ? 24 : v >= 12 ? 12 : 0;        // fp32 twins: 12-23, 24-35
     v -= wide;
+    if (op == 2 && wide == 24) wide = 0;            // wgrad: no K-split twins
     if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
     v += wide;
     if (((v / 3) & 1) && !pipe_ok) v -= 3;
@@ -3001,7 +3075,7 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   const bool fast = nt_fast(p);
   const bool pipe_ok = fast && p.a.Cg % 64 == 0;
   int v = choose(0, p.M, p.N, p.K, G, pipe_ok);
-  if (v >= 12) v -= 12;                             // wide ids: fp32 kernels only
+  v %= 12;                                          // wide / K-split ids: fp32 kernels only
   if (!fast) v = (v >= 6 ? 6 : 0) + v % 3;         // generic gather: register-staged only
   set_splits(p, G, v);
   const int kind = (v / 3) & 1;
@@ -3022,8 +3096,17 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
-                          bool wide = false) {
+                          bool wide = false, bool ks2 = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  if constexpr (BM * BN <= 128 * 64) {
+    if (ks2 && fast && kind == 0 && !wide) {       // intra-block K split, 512 threads
+      if (p.pro.scsh)
+        igemm_nt32<BM, BN, GM_FWD, true, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
+      else
+        igemm_nt32<BM, BN, GM_FWD, false, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
+      return;
+    }
+  }
   if (wide) {                      // 32x32x16 MFMA twins (no prologue form)
     if (kind == 1) {
       if constexpr (BM * BN <= 128 * 64)
@@ -3073,8 +3156,12 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   // the ring kernel has no prologue form
   const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
-  bool wide = false;
-  if (v >= 12) {
+  bool wide = false, ks2 = false;
+  if (v >= 24) {
+    v -= 24;
+    ks2 = fast;
+    if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
+  } else if (v >= 12) {
     v -= 12;
     // no prologue form; BN-backward statistics (the unaligned-dgrad
     // fallback) only in the NN kernels' wide epilogue
@@ -3090,9 +3177,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, ks2); break;
     case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, ks2); break;
   }
   return (int)hipGetLastError();
 }
@@ -3224,9 +3311,18 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
-                          bool wide = false) {
+                          bool wide = false, bool ks2 = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if constexpr (BM * BN <= 128 * 64) {
+    if (ks2 && !wide) {                            // intra-block K split, 512 threads
+      if (strided)
+        igemm_nn32<BM, BN, GM_DGS, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+      else
+        igemm_nn32<BM, BN, GM_DG1, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+      return;
+    }
+  }
   if (wide) {                      // 32x32x16 MFMA twins
     if (strided)
       igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
@@ -3292,8 +3388,11 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       strided = st > 1;
     }
     int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
-    bool wide = false;
-    if (v >= 12) {                        // fp32 32x32x16-MFMA twins of 0-11
+    bool wide = false, ks2 = false;
+    if (v >= 24) {                        // fp32 intra-block K-split twins
+      v -= 24;
+      ks2 = f32;
+    } else if (v >= 12) {                 // fp32 32x32x16-MFMA twins of 0-11
       v -= 12;
       wide = f32;
     }
@@ -3313,9 +3412,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     }
     if (f32) {
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, ks2); break;
         case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, ks2); break;
       }
       return (int)hipGetLastError();
     }
