@@ -219,6 +219,12 @@ def main():
                                                max(st["h2d_s"], 1e-9), 2)}
         print(json.dumps(out))
         sys.stdout.flush()
+        tune_log = os.environ.get("CER_TUNE_LOG")
+        if tune_log and backend == "hip":
+            from cerebro_ds_kpgi_amd.ops import _hip
+            with open(tune_log, "w") as f:
+                json.dump([[op, list(key), v] for (op, key), v in _hip.tuned_variants().items()],
+                          f)
     eng.close()
     if da_root and ctx.rank == 0:
         import shutil

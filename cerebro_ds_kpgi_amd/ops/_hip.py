@@ -367,6 +367,13 @@ _REG32 = (0, 1, 2, 6, 7, 8)
 FP32_VARIANTS = {0: _FWD32, 1: _REG32, 2: (0, 1, 2)}
 if os.environ.get("CER_FP32_WIDE", "1") != "0":
     FP32_VARIANTS = {op: vs + tuple(12 + v for v in vs) for op, vs in FP32_VARIANTS.items()}
+# 24-35: intra-block K-split twins (512-thread blocks, two wave groups on the
+# halves of the K range; conv.hip group_range) of the register-staged 64x64
+# and 128x64 fwd / dgrad kernels, with and without split-K
+# (CER_FP32_KSPLIT=0 leaves them out).
+_KSPLIT32 = (24, 26, 30, 32)
+if os.environ.get("CER_FP32_KSPLIT", "1") != "0":
+    FP32_VARIANTS = {op: vs + (_KSPLIT32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
 
 
 def _select(op, key, launch, dtype, after_tune=None):

@@ -203,6 +203,39 @@ def test_conv_bwd_wide_mfma_fp32_vs_fp64(case, vd, vw):
         _hip.conv_set_variant(2, -1)
 
 
+@pytest.mark.parametrize("v", [24, 26, 30, 32])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_intra_block_ksplit_fp32_vs_fp64(case, v):
+    """The intra-block K-split twins (512-thread igemm_nt32 / igemm_nn32 with
+    WG = 2: two wave groups on the halves of the K range, LDS hand-off of the
+    accumulators), fwd and dgrad pinned, with and without split-K, on every
+    conv case (odd K-tile counts: the last group's surplus step is masked)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(0, v)
+    _hip.conv_set_variant(1, v)
+    try:
+        test_conv_fp32_vs_fp64(case)
+    finally:
+        _hip.conv_set_variant(0, -1)
+        _hip.conv_set_variant(1, -1)
+
+
+@pytest.mark.parametrize("v", [24, 26, 30])
+def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
+    """BN statistics (fwd epilogue), the BN-apply prologue and the BN-link
+    dgrad epilogue from the K-split kernels' surviving wave group."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(0, v)
+    _hip.conv_set_variant(1, v)
+    try:
+        test_conv_bn_unit_fp32_vs_fp64(True, True, False)
+        test_bn_link_dgrad_epilogue_fp32()
+        test_bn_apply_folded_into_consumer_fp32_vs_fp64(3, 1)
+    finally:
+        _hip.conv_set_variant(0, -1)
+        _hip.conv_set_variant(1, -1)
+
+
 @pytest.mark.parametrize("vb", [12, 13, 14])
 def test_wgrad_batch_wide_fp32_vs_fp64(vb):
     """Batched (deferred) fp32 weight gradients on the wide kernels
