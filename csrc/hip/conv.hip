@@ -2311,16 +2311,19 @@ __device__ __forceinline__ KSplitRange group_range(const KRange& kr, int grp, in
   }
 }
 
-// group 1 -> group 0 accumulator hand-off (WG == 2); false in group 1
+// groups 1..WG-1 -> group 0 accumulator hand-off, each through its own LDS
+// region (``regions`` = the block's LDS, ``stride`` floats per group);
+// false in the groups that must exit
 template <int WG, int BM, int BN>
-__device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], float* red, int grp,
-                                             int tid) {
+__device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], float* regions,
+                                             int stride, int grp, int tid) {
   if constexpr (WG == 1) {
     return true;
   } else {
     constexpr int FI = BM / 32, FJ = BN / 32;
     __syncthreads();
-    if (grp == 1) {
+    if (grp > 0) {
+      float* red = regions + grp * stride;
 #pragma unroll
       for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -2329,13 +2332,17 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
           for (int e = 0; e < 4; ++e) red[((i * FJ + j) * 4 + e) * NTHREADS + tid] = acc[i][j][e];
     }
     __syncthreads();
-    if (grp == 1) return false;
+    if (grp > 0) return false;
 #pragma unroll
-    for (int i = 0; i < FI; ++i)
+    for (int g = 1; g < WG; ++g) {
+      const float* red = regions + g * stride;
 #pragma unroll
-      for (int j = 0; j < FJ; ++j)
+      for (int i = 0; i < FI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] += red[((i * FJ + j) * 4 + e) * NTHREADS + tid];
+        for (int j = 0; j < FJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][e] += red[((i * FJ + j) * 4 + e) * NTHREADS + tid];
+    }
     return true;
   }
 }
@@ -2468,8 +2475,8 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
     zero_acc<BM, BN>(acc);
     kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
                   [&](int cur) { mma3_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
-    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all + LDS_ELEMS * (WG - 1)),
-                                  grp, tid))
+    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all), LDS_ELEMS / 2, grp,
+                                  tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
@@ -2710,8 +2717,8 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
       mma3_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane,
                       acc);
     });
-    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all + LDS_ELEMS * (WG - 1)),
-                                  grp, tid))
+    if (!group_reduce<WG, BM, BN>(acc, reinterpret_cast<float*>(lds_all), LDS_ELEMS / 2, grp,
+                                  tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
@@ -2955,8 +2962,10 @@ __global__ __launch_bounds__(256) void transpose_w_kernel(const E* __restrict__ 
 // double buffer, 1 = LDS-DMA ring; tile 0 = 64x64, 1 = 128x128, 2 = 128x64
 // (BM x BN; for wgrad BM tiles Cout, BN tiles K).  v = 3 * kind + tile.
 // fp32 only: 12-23 = the 32x32x16-MFMA twins of 0-11; 24-35 = the
-// intra-block K-split (512-thread) twins of the register-staged fwd / dgrad
-// kernels (ring ids map to their register twin; 128x128 has none).
+// intra-block K-split (512-thread, 2 wave groups) twins of the
+// register-staged fwd / dgrad kernels (ring ids map to their register twin;
+// 128x128 has none).  Four groups (1024 threads, 64x64) measured neutral at
+// G = 1 (profiles/r3_ksplit.md) and are not instantiated.
 // cer_conv_set_variant(op, v) pins a variant per op (0 fwd, 1 dgrad, 2 wgrad)
 // for tuning; -1 = the built-in choice.
 static int g_variant[3] = {-1, -1, -1};
@@ -2989,7 +2998,7 @@ static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
     int v = g_variant[op];
     int wide = v >= 24 ? 24 : v >= 12 ? 12 : 0;        // fp32 twins: 12-23, 24-35
     v -= wide;
-    if (op == 2 && wide == 24) wide = 0;            // wgrad: no K-split twins
+    if (op == 2 && wide >= 24) wide = 0;            // wgrad: no K-split twins
     if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
     v += wide;
     if (((v / 3) & 1) && !pipe_ok) v -= 3;
@@ -3096,10 +3105,10 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
-                          bool wide = false, bool ks2 = false) {
+                          bool wide = false, int wg = 1) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if constexpr (BM * BN <= 128 * 64) {
-    if (ks2 && fast && kind == 0 && !wide) {       // intra-block K split, 512 threads
+    if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
       if (p.pro.scsh)
         igemm_nt32<BM, BN, GM_FWD, true, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
       else
@@ -3156,10 +3165,11 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   // the ring kernel has no prologue form
   const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
-  bool wide = false, ks2 = false;
+  bool wide = false;
+  int wg = 1;
   if (v >= 24) {
+    wg = 2;
     v -= 24;
-    ks2 = fast;
     if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
   } else if (v >= 12) {
     v -= 12;
@@ -3177,9 +3187,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, ks2); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg); break;
     case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, ks2); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg); break;
   }
   return (int)hipGetLastError();
 }
@@ -3311,11 +3321,11 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
-                          bool wide = false, bool ks2 = false) {
+                          bool wide = false, int wg = 1) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
   if constexpr (BM * BN <= 128 * 64) {
-    if (ks2 && !wide) {                            // intra-block K split, 512 threads
+    if (wg > 1 && !wide) {                         // intra-block K split, 512 threads
       if (strided)
         igemm_nn32<BM, BN, GM_DGS, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
       else
@@ -3388,10 +3398,11 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       strided = st > 1;
     }
     int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
-    bool wide = false, ks2 = false;
+    bool wide = false;
+    int wg = 1;
     if (v >= 24) {                        // fp32 intra-block K-split twins
+      wg = f32 ? 2 : 1;
       v -= 24;
-      ks2 = f32;
     } else if (v >= 12) {                 // fp32 32x32x16-MFMA twins of 0-11
       v -= 12;
       wide = f32;
@@ -3412,9 +3423,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     }
     if (f32) {
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, ks2); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg); break;
         case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, ks2); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg); break;
       }
       return (int)hipGetLastError();
     }

@@ -9,6 +9,6 @@ mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_fp32_gpu.py -k "ksplit" -x -q --timeout 300 \
   --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
-CER_TUNE_LOG=$OUT/tune_c1.json timeout -k 10 300 python -u bench.py --configs 1 > $OUT/c1_tuned.json 2> $OUT/c1_tuned.err || exit 1
-cat $OUT/c1_tuned.json
-bash scripts/gpu/ab.sh ksplit "CER_FP32_KSPLIT=0 CER_FP32_KSPLIT=1" "1 8" 2
+CER_TUNE_LOG=$OUT/tune4_c1.json timeout -k 10 300 python -u bench.py --configs 1 > $OUT/c1_tuned4.json 2> $OUT/c1_tuned4.err || exit 1
+cat $OUT/c1_tuned4.json
+bash scripts/gpu/ab.sh ksplit4 "CER_FP32_KSPLIT=2 CER_FP32_KSPLIT=1" "1 8" 2
