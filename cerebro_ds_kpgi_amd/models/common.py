@@ -59,8 +59,6 @@ class PackedNet(object):
         self.bn_eps = 1e-5
         # BN backward partials in consumer dgrad epilogues (ops.nn.BNLink)
         self.bn_links = os.environ.get("CER_BN_LINKS", "1") != "0"
-        # BN apply folded into the sole consumer conv's operand loads (fp32)
-        self.bn_fold = os.environ.get("CER_BN_FOLD_APPLY", "0") == "1"
 
     def spec(self, s):
         self._specs.append(s)
@@ -96,7 +94,7 @@ class PackedNet(object):
                         training, relu, residual, self.bn_momentum, self.bn_eps)
 
     def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False, join=None,
-                res_join=None, link_out=False, fold_out=False):
+                res_join=None, link_out=False):
         """act(BN(conv(x)) + residual); in training the conv epilogue feeds BN
         its batch statistics (ops.nn.PackedConvBNAct).  ``join`` / ``res_join``:
         a ``P.GradJoin`` shared with the other consumer of ``x`` / ``residual``
@@ -106,7 +104,7 @@ class PackedNet(object):
         return P.conv_bn_act(x, self.ref(c.w), self.ref(b.g), self.ref(b.b), self.ref(b.rm),
                              self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
                              self.bn_eps, self.anchor if anchor else None, join, res_join,
-                             link_out and self.bn_links, fold_out and self.bn_fold)
+                             link_out and self.bn_links)
 
     def bucket_mark(self, x, first_spec_above):
         """Gradient-bucket boundary: in backward, once the gradient reaches

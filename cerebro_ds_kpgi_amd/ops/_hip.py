@@ -284,9 +284,6 @@ _SIGS.update({
     "cer_bias_act_bwd": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_softmax_ce_f32": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_conv_dgrad_bnbwd_f32": None,
-    "cer_conv_set_prologue": [c_p, c_i, c_i],
-    "cer_bn_finalize_scsh": [c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_i64,
-                             c_p, c_i64, c_i, c_i, c_f, c_f, c_p],
 })
 _SIGS.pop("cer_conv_dgrad_bnbwd_f32")
 IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
@@ -495,70 +492,18 @@ def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momen
     return y, z, mean, invstd
 
 
-class _Prologue(object):
-    """``with _Prologue(pro):`` the fp32 conv forward / weight-gradient
-    launches inside consume act(x * scale + shift) instead of x (conv.hip
-    BNPro); pro = (scsh [2, C] fp32 tensor, act) or None."""
-    __slots__ = ("pro",)
-
-    def __init__(self, pro):
-        self.pro = pro
-
-    def __enter__(self):
-        if self.pro is not None:
-            scsh, act = self.pro
-            lib().cer_conv_set_prologue(_ptr(scsh), scsh.numel() // 2, _act_code(act))
-
-    def __exit__(self, *a):
-        if self.pro is not None:
-            lib().cer_conv_set_prologue(None, 0, 0)
-        return False
-
-
-def fold_ok(x, gref):
-    """A BN output can stay unmaterialised (its consumer conv applies it):
-    fp32 storage (the register-staged kernels), 8-aligned channels."""
-    return x.dtype == torch.float32 and gref.spec.shape[0] % 8 == 0
-
-
-def bn_finalize_scsh(part, nslab, z, gref, bref, rmref, rvref, momentum, eps):
-    """BN finalize for a folded apply: (mean, invstd, scsh [2, C]); running
-    statistics updated as by the apply path."""
-    C = z.shape[-1]
-    M = z.numel() // C
-    dev = z.device
-    mean = torch.empty(C, dtype=torch.float32, device=dev)
-    invstd = torch.empty(C, dtype=torch.float32, device=dev)
-    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
-    scsh = torch.empty((2, C), dtype=torch.float32, device=dev)
-    gp, gs = gref.work_ptr()
-    bp, bs = bref.work_ptr()
-    rmp, rs = rmref.master_ptr()
-    rvp, _ = rvref.master_ptr()
-    rc = _fn("cer_bn_finalize_scsh", z)(_ptr(part), int(nslab), _ptr(ws), _ptr(mean),
-                                        _ptr(invstd), c_p(rmp), c_p(rvp), rs, c_p(gp), gs,
-                                        c_p(bp), bs, _ptr(scsh), M, C, gref.spec.shape[0], eps,
-                                        momentum, _stream())
-    _check(rc, "cer_bn_finalize_scsh")
-    return mean, invstd, scsh
-
-
 def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                      stride, pad, stem=False, pro=None, fold_out=False):
-    """Fused training unit: conv (+ BN statistics + BN finalize in the GEMM
-    epilogue of the last tile of each channel column) then one BN-apply pass.
-    Returns (y, z, mean, invstd, x4, scsh) — z the conv output (BN input), x4
-    the repacked stem input (stem path) or None.
-    ``pro``: x is itself an unmaterialised BN output (``_Prologue``);
-    ``fold_out``: skip this BN's apply — y IS z, and scsh (the apply's
-    per-channel scale / shift) goes to the consumer conv instead."""
-    with _Prologue(pro):
-        return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
-                                  eps, stride, pad, stem, fold_out)
+                      stride, pad, stem=False):
+    """Fused training unit: conv (+ BN statistics into the fp64 slabs in the
+    GEMM epilogue) then one BN-apply pass that folds the finalize.
+    Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4
+    the repacked stem input (stem path) or None."""
+    return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
+                              eps, stride, pad, stem)
 
 
 def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                       stride, pad, stem, fold_out):
+                       stride, pad, stem):
     x = _act(x)
     B, H, W, GC = x.shape
     G = wref.G
@@ -586,7 +531,7 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
                 after_tune=part.zero_)
         launch()
         return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                             momentum, eps) + (x4, None)
+                             momentum, eps) + (x4,)
 
     def launch():
         rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
@@ -596,12 +541,8 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
             after_tune=part.zero_)
     launch()
-    if fold_out:
-        mean, invstd, scsh = bn_finalize_scsh(part, nslab.value, z, gref, bref, rmref,
-                                              rvref, momentum, eps)
-        return z, z, mean, invstd, None, scsh
     return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                         momentum, eps) + (None, None)
+                         momentum, eps) + (None,)
 
 
 def stem_ok(x, wref, stride, pad):
@@ -875,15 +816,14 @@ def grouped_conv_wgrad(x, dy, wref, stride, pad, groups):
     launch()
 
 
-def conv2d_wgrad(x, dy, wref, stride, pad, pro=None):
+def conv2d_wgrad(x, dy, wref, stride, pad):
     x = _act(x)
     dy = _act(dy)
     B, H, W, _ = x.shape
     _, Ho, Wo, _ = dy.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
-    with _Prologue(pro):
-        _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref)
+    _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref)
 
 
 # ---------------------------------------------------------------------------

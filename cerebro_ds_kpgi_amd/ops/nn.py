@@ -125,26 +125,12 @@ def _bnlink_for(ctx, x, join, addend):
     return link, x
 
 
-def _bnfold(x):
-    """(scsh, act) when x is an unmaterialised BatchNorm output (its apply is
-    folded into this consumer's operand load, see conv_bn_act fold_out)."""
-    return getattr(x, "_cer_bnfold", None)
-
-
-def _materialize(x):
-    """y = act(z * scale + shift) for a consumer that cannot fold the apply."""
-    scsh, act = x._cer_bnfold
-    C = x.shape[-1]
-    return _act(x.reshape(-1, C) * scsh[0] + scsh[1], act).view(x.shape)
-
-
 class PackedConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join = None
         ctx.bnlink = getattr(x, "_cer_bnlink", None)
-        ctx.pro = None
         y = _conv_forward(x, wref, stride, pad)
         ctx.save_for_backward(x)
         return y
@@ -173,8 +159,7 @@ class PackedConv2d(torch.autograd.Function):
                 if join is not None:       # first of the two: park dx for the other one
                     dx = join.join(dx)
             # off the critical path: overlaps the dgrad chain below (ops.streams)
-            pro = getattr(ctx, "pro", None)
-            h.conv2d_wgrad(x, dy, wref, stride, pad, pro=pro)
+            h.conv2d_wgrad(x, dy, wref, stride, pad)
         else:
             G = wref.G
             cout, kh, kw, cin = wref.spec.shape
@@ -189,8 +174,6 @@ class PackedConv2d(torch.autograd.Function):
 
 
 def conv2d(x, wref, stride=1, pad=0, anchor=None):
-    if _bnfold(x) is not None:
-        x = _materialize(x)
     return PackedConv2d.apply(x, anchor, wref, stride, pad)
 
 
@@ -290,7 +273,7 @@ class PackedConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
-                momentum, eps, join=None, res_join=None, link=None, fold=None):
+                momentum, eps, join=None, res_join=None, link=None):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join, ctx.res_join = join, res_join
         ctx.bnlink = getattr(x, "_cer_bnlink", None)     # x is a linked BN's output
@@ -299,29 +282,19 @@ class PackedConvBNAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.x4 = None
-        ctx.pro = _bnfold(x)          # x = z of a BN whose apply this conv folds in
         hip_ok = (use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0
                   and gref.spec.shape[0] % 8 == 0)
-        if ctx.pro is not None and not hip_ok:
-            x = _materialize(x)
-            ctx.pro = None
-        scsh = None
         if hip_ok:
             h = _hip()
             # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
             stem = not x.requires_grad and h.stem_ok(x, wref, stride, pad)
-            fold_out = (fold is not None and not stem and residual is None
-                        and h.fold_ok(x, gref))
-            y, z, mean, invstd, ctx.x4, scsh = h.conv_bn_fwd_train(
+            y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
                 x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride, pad,
-                stem=stem, pro=ctx.pro, fold_out=fold_out)
+                stem=stem)
         else:
             z = _conv_forward(x, wref, stride, pad)
             y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,
                                                 momentum, eps)
-        if fold is not None:
-            # the caller tags the returned tensor (an output can't carry it yet)
-            fold.scsh = scsh
         if link is not None and _bn_hip(z, gref):
             link.z, link.mean, link.invstd = z, mean, invstd
             link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
@@ -353,7 +326,7 @@ class PackedConvBNAct(torch.autograd.Function):
         else:
             dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None, None)
+                None, None)
 
 
 def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
@@ -374,32 +347,19 @@ def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
     return dx, dres
 
 
-class _FoldOut(object):
-    __slots__ = ("scsh",)
-
-    def __init__(self):
-        self.scsh = None
-
-
 def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
-                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False,
-                fold_out=False):
+                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False):
     """``join``: GradJoin shared with the other consumer of ``x``;
     ``res_join``: GradJoin shared with the other consumer of ``residual``;
     ``link_out``: the output's whole gradient comes out of one consumer dgrad
-    (see BNLink) — its BN backward partials are computed there;
-    ``fold_out``: the output's ONLY consumer is another conv_bn_act: where the
-    fp32 HIP kernels allow, the BN apply is skipped and the returned tensor is
-    the BN input z tagged with (scale, shift, act) — the consumer's forward
-    and weight-gradient operand loads apply it (no y in HBM)."""
+    (see BNLink) — its BN backward partials are computed there.  (Folding
+    the BN apply into the consumer conv's operand loads was measured slower
+    at 1, 2 and 8 configs and removed: profiles/r3_resnet50_1cfg_fp32.md.)"""
     link = BNLink() if link_out else None
-    fold = _FoldOut() if fold_out else None
     y = PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
-                              relu, momentum, eps, join, res_join, link, fold)
+                              relu, momentum, eps, join, res_join, link)
     if link is not None:
         y._cer_bnlink = link
-    if fold is not None and fold.scsh is not None:
-        y._cer_bnfold = (fold.scsh, relu)
     return y
 
 

@@ -321,52 +321,6 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
   finalize_bwd_task<false>(part, slabs, ws, dgamma, dbeta, gstride, C, Cper, blockIdx.x);
 }
 
-// finalize + the per-channel (scale, shift) of the apply, for a BatchNorm
-// whose apply is folded into its consumer convolution's operand load
-// (conv.hip BNPro): scsh = [2][C], y = act(z * scale + shift)
-template <typename T>
-__global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_scsh(
-    const float* __restrict__ part, int slabs, float* __restrict__ ws, float* mean_out,
-    float* invstd_out, float* rmean, float* rvar, int64_t rstat_stride, int64_t M, int C,
-    int Cper, float eps, float momentum, Strided gamma, Strided beta, float* __restrict__ scsh) {
-  if (slabs & (1 << 24)) {            // fp64 atomic slabs (conv.hip SLAB_F64)
-    const int n = slabs & ((1 << 24) - 1);
-    const int c = blockIdx.x * FIN_C + threadIdx.x;
-    if (threadIdx.x < FIN_C && c < C) {
-      const double* pd = reinterpret_cast<const double*>(part);
-      double a = 0.0, b = 0.0;
-      for (int sl = 0; sl < n; ++sl) {
-        a += pd[(int64_t)sl * 2 * C + c];
-        b += pd[(int64_t)sl * 2 * C + C + c];
-      }
-      const float inv_m = 1.f / (float)M;
-      const float mu = (float)a * inv_m;
-      const float var = fmaxf((float)b * inv_m - mu * mu, 0.f);
-      const float is = rsqrtf(var + eps);
-      ws[c] = mu;
-      ws[C + c] = is;
-      mean_out[c] = mu;
-      invstd_out[c] = is;
-      const int g = c / Cper, cc = c - g * Cper;
-      float* rm = rmean + g * rstat_stride + cc;
-      float* rv = rvar + g * rstat_stride + cc;
-      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-      *rm = (1.f - momentum) * *rm + momentum * mu;
-      *rv = (1.f - momentum) * *rv + momentum * unb;
-    }
-  } else {
-    finalize_fwd_task<false>(part, slabs, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M,
-                             C, Cper, eps, momentum, blockIdx.x);
-  }
-  const int c = blockIdx.x * FIN_C + threadIdx.x;
-  if (threadIdx.x >= FIN_C || c >= C) return;
-  const int g = c / Cper, cc = c - g * Cper;
-  const float mu = mean_out[c], is = invstd_out[c];          // this thread's own writes
-  const float sc = is * (float)reinterpret_cast<const T*>(gamma.p)[g * gamma.stride + cc];
-  scsh[c] = sc;
-  scsh[C + c] = (float)reinterpret_cast<const T*>(beta.p)[g * beta.stride + cc] - mu * sc;
-}
-
 // ---------------------------------------------------------------------------
 // stage 3: elementwise apply (scale/shift per channel computed once per thread)
 // ---------------------------------------------------------------------------
@@ -1025,16 +979,6 @@ static int cer_bn_bwd_part_t(const T* dy, const T* x, const T* y,
     return cer_bn_fwd_train_part_t<T>(x, res, y, gamma, gs, beta, bs, rmean, rvar, rstride,     \
                                       mean_out, invstd_out, ws, part, nslab, M, C, Cper, eps,    \
                                       momentum, act, stream);                                    \
-  }                                                                                              \
-  CER_API int cer_bn_finalize_scsh##SFX(                                                         \
-      float* part, int nslab, float* ws, float* mean_out, float* invstd_out, float* rmean,       \
-      float* rvar, int64_t rstride, const T* gamma, int64_t gs, const T* beta, int64_t bs,      \
-      float* scsh, int64_t M, int C, int Cper, float eps, float momentum, hipStream_t stream) {   \
-    if (nslab <= 0) return (int)hipErrorInvalidValue;                                            \
-    bn_finalize_scsh<T><<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(                     \
-        part, nslab, ws, mean_out, invstd_out, rmean, rvar, rstride, M, C, Cper, eps, momentum,   \
-        Strided{gamma, gs}, Strided{beta, bs}, scsh);                                            \
-    return (int)hipGetLastError();                                                               \
   }                                                                                              \
   CER_API int cer_bn_apply_fwd##SFX(const T* x, const T* res, T* y, const float* ws,            \
                                     const T* gamma, int64_t gs, const T* beta, int64_t bs,      \

@@ -103,32 +103,6 @@ struct BNBwdEpi {
   int ym, act;                  // mask mode (bn.hip YM_*) and activation code
 };
 
-// BN-apply prologue (fp32 kernels): the gathered activation is the INPUT z of
-// a training-mode BatchNorm whose output y = act(z * scale + shift) is never
-// materialised; the operand load applies it per element (padding taps stay
-// 0, i.e. y's zero padding).  scsh = [2][ld] fp32 (scale | shift) per packed
-// channel (bn.hip cer_bn_finalize_scsh); scsh == nullptr: off.
-struct BNPro {
-  const float* scsh;
-  int ld;       // packed channels of the gathered tensor (G * Cg)
-  int act;      // 0 none, 1 relu, 6 relu6
-};
-
-// BN-apply prologue for the NEXT fp32 forward / weight-gradient calls (until
-// cleared with scsh == nullptr): the activation argument of those calls is a
-// BatchNorm input z, the convolution consumes act(z * scale + shift).  Only
-// the aligned (fast-gather) kernels implement it: a call that would take the
-// generic gather returns hipErrorInvalidValue instead of ignoring it.
-static BNPro g_pro = BNPro{nullptr, 0, 0};
-
-CER_API void cer_conv_set_prologue(const float* scsh, int ld, int act) {
-  g_pro = BNPro{scsh, ld, act};
-}
-
-__device__ __forceinline__ float pro_act(float v, int act) {
-  return act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (act ? fmaxf(v, 0.f) : v);
-}
-
 struct NTParams {
   GatherGeom a;
   int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
@@ -151,7 +125,6 @@ struct NTParams {
                                    // input gradient joins here instead of in an add kernel)
   BNBwdEpi bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
                          0, 0};
-  BNPro pro = BNPro{nullptr, 0, 0};   // fp32 fwd: BN-apply prologue on the gathered A operand
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
 };
@@ -200,7 +173,6 @@ struct WGParams {
   int Mred, N, K;
   int m_per_split;
   int splits;
-  BNPro pro = BNPro{nullptr, 0, 0};   // fp32: BN-apply prologue on the gathered x (BNPro)
 };
 
 // es: element size of the gathered tensor (2 = bf16, 4 = fp32)
@@ -1574,24 +1546,6 @@ __device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint
   lo = make_uint4(l[0], l[1], l[2], l[3]);
 }
 
-// y = valid ? act(z * sc + sh) : 0 on two uint4 of fp32 (8 channels)
-__device__ __forceinline__ void pro_apply(uint4& a, uint4& b, const uint4 (&ss)[4], bool valid,
-                                          int act) {
-  uint32_t* x0 = reinterpret_cast<uint32_t*>(&a);
-  uint32_t* x1 = reinterpret_cast<uint32_t*>(&b);
-  const uint32_t* sc = reinterpret_cast<const uint32_t*>(&ss[0]);
-  const uint32_t* sh = reinterpret_cast<const uint32_t*>(&ss[2]);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float v0 = pro_act(fmaf(__uint_as_float(x0[e]), __uint_as_float(sc[e]),
-                                  __uint_as_float(sh[e])), act);
-    const float v1 = pro_act(fmaf(__uint_as_float(x1[e]), __uint_as_float(sc[4 + e]),
-                                  __uint_as_float(sh[4 + e])), act);
-    x0[e] = valid ? __float_as_uint(v0) : 0u;
-    x1[e] = valid ? __float_as_uint(v1) : 0u;
-  }
-}
-
 __device__ __forceinline__ uint4 f4_bits(const float* e) {
   return make_uint4(__float_as_uint(e[0]), __float_as_uint(e[1]), __float_as_uint(e[2]),
                     __float_as_uint(e[3]));
@@ -2349,7 +2303,7 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
-template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false, int WG = 1>
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
 __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTParams p) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
@@ -2394,14 +2348,6 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
   constexpr int SETS = fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
-  // BN-apply prologue: (scale, shift) of the chunk's 8 channels per set and
-  // the per-chunk "not padding" flags; loaded unconditionally (a null table
-  // has a 0-byte range: zeros, no branch around the loads)
-  constexpr bool pro = PRO && GM != GM_SLOW;     // compile-time: no registers otherwise
-  uint4 rs[pro ? SETS : 1][4];
-  bool av[pro ? SETS : 1][A_CH];
-  __amdgpu_buffer_rsrc_t rP;
-  if constexpr (pro) rP = make_rsrc(p.pro.scsh, (uint32_t)p.pro.ld * 8u);
 
   auto load_tiles = [&](int kt, auto S) {
     constexpr int s = decltype(S)::value;
@@ -2412,16 +2358,8 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
       for (int i = 0; i < A_CH; ++i) {
         const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
         const uint32_t o = kok ? off : OOB;
-        if constexpr (pro) av[s][i] = o != OOB;
         ra[s][2 * i] = bload(rA, o);
         ra[s][2 * i + 1] = bload(rA, o + 16u);
-      }
-      if constexpr (pro) {
-        const uint32_t po = (uint32_t)(cfg * p.a.Cg + kp.c) * 4u;
-        rs[s][0] = bload(rP, po);
-        rs[s][1] = bload(rP, po + 16u);
-        rs[s][2] = bload(rP, po + (uint32_t)p.pro.ld * 4u);
-        rs[s][3] = bload(rP, po + (uint32_t)p.pro.ld * 4u + 16u);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
@@ -2449,7 +2387,6 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      if constexpr (pro) pro_apply(ra[s][2 * i], ra[s][2 * i + 1], rs[s], av[s][i], p.pro.act);
       split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk + 4)) = l;
@@ -2726,7 +2663,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
 }
 
 // wgrad tile body (fp32 operands): dW[n, k] = sum_m dy[m, n] im2col(x)[m, k]
-template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
+template <int BM, int BN, int GM, bool WIDE = false>
 __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf16_t* lds) {
   constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
   constexpr int A_CH = KS * A_CPR / NTHREADS, B_CH = KS * B_CPR / NTHREADS;
@@ -2759,18 +2696,6 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
     rX = make_rsrc(xb, p.x.bytes);
   }
-  // BN-apply prologue on x (see BNPro): a thread's B chunk covers the same 8
-  // channels for the whole reduction, so (scale, shift) load once
-  constexpr bool pro = PRO && GM != GM_SLOW;
-  uint4 rs[4];
-  bool bv[pro ? SETS : 1][B_CH];
-  if constexpr (pro) {
-    const float* ps = p.pro.scsh + cfg * p.x.Cg + bk.c;
-    rs[0] = *reinterpret_cast<const uint4*>(ps);
-    rs[1] = *reinterpret_cast<const uint4*>(ps + 4);
-    rs[2] = *reinterpret_cast<const uint4*>(ps + p.pro.ld);
-    rs[3] = *reinterpret_cast<const uint4*>(ps + p.pro.ld + 4);
-  }
 
   auto load_tiles = [&](int mt, auto S) {
     constexpr int s = decltype(S)::value;
@@ -2788,7 +2713,6 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
         const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
         const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
         const uint32_t o = b_kok ? off : OOB;
-        if constexpr (pro) bv[s][i] = o != OOB;
         rb[s][2 * i] = bload(rX, o);
         rb[s][2 * i + 1] = bload(rX, o + 16u);
       }
@@ -2833,7 +2757,6 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      if constexpr (pro) pro_apply(rb[s][2 * i], rb[s][2 * i + 1], rs, bv[s][i], p.pro.act);
       split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
       if constexpr (WIDE) {
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
@@ -2902,14 +2825,14 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   }
 }
 
-template <int BM, int BN, int GM, bool PRO = false, bool WIDE = false>
+template <int BM, int BN, int GM, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
-  wgrad_reg_body32<BM, BN, GM, PRO, WIDE>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
+  wgrad_reg_body32<BM, BN, GM, WIDE>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
 }
 
 // batched fp32 weight gradients (see wgrad_batch)
-template <int BM, int BN, bool PRO = false, bool WIDE = false>
+template <int BM, int BN, bool WIDE = false>
 // A grid smaller than the batch's work items (cer_wgrad_batch_set_grid: a
 // side-stream batch that should leave most CUs to the dgrad chain) walks the
 // items persistently, block-strided; the full grid takes one item per block
@@ -2923,7 +2846,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
     int i = 0;
     while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     const WGParams p = b.p[i];
-    wgrad_reg_body32<BM, BN, GM_FWD, PRO, WIDE>(p, work - b.start[i], lds);
+    wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
   }
 }
@@ -3109,14 +3032,11 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStre
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
-      if (p.pro.scsh)
-        igemm_nt32<BM, BN, GM_FWD, true, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
-      else
-        igemm_nt32<BM, BN, GM_FWD, false, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
+      igemm_nt32<BM, BN, GM_FWD, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
       return;
     }
   }
-  if (wide) {                      // 32x32x16 MFMA twins (no prologue form)
+  if (wide) {                      // 32x32x16 MFMA twins
     if (kind == 1) {
       if constexpr (BM * BN <= 128 * 64)
         if (p.K / KS >= 3) {
@@ -3125,9 +3045,9 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStre
         }
       pipe_nt32<BM, BN, 2, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else if (!fast) {
-      igemm_nt32<BM, BN, GM_SLOW, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+      igemm_nt32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else {
-      igemm_nt32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
+      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     }
     return;
   }
@@ -3141,8 +3061,6 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStre
     pipe_nt32<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
   } else if (!fast)
     igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
-  else if (p.pro.scsh)
-    igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
 }
@@ -3160,10 +3078,7 @@ static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   p.stat_slabs = p.stats ? g_stat_slabs : 0;
   const bool fast = nt_fast32(p);
-  p.pro = g_pro;
-  if (p.pro.scsh && !fast) return (int)hipErrorInvalidValue;
-  // the ring kernel has no prologue form
-  const bool ring_ok = fast && p.a.Cg % KS == 0 && !p.pro.scsh;
+  const bool ring_ok = fast && p.a.Cg % KS == 0;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
   bool wide = false;
   int wg = 1;
@@ -3173,9 +3088,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
   } else if (v >= 12) {
     v -= 12;
-    // no prologue form; BN-backward statistics (the unaligned-dgrad
-    // fallback) only in the NN kernels' wide epilogue
-    wide = !p.pro.scsh && p.bb.part == nullptr;
+    // BN-backward statistics (the unaligned-dgrad fallback) only in the NN
+    // kernels' wide epilogue
+    wide = p.bb.part == nullptr;
     if (((v / 3) & 1) && !ring_ok) v -= 3;
   }
   if (!fast) v = fp32_variant(v);
@@ -3543,16 +3458,13 @@ static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t 
   splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
   p.splits = splits;
   dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
-  if (wide && !p.pro.scsh)   // 32x32x16-MFMA twins
+  if (wide)   // 32x32x16-MFMA twins
     if (fast)
-      igemm_wgrad32<BM, BN, GM_FWD, false, true><<<grid, NTHREADS, 0, stream>>>(p);
-    else
-      igemm_wgrad32<BM, BN, GM_SLOW, false, true><<<grid, NTHREADS, 0, stream>>>(p);
-  else if (fast)
-    if (p.pro.scsh)
       igemm_wgrad32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     else
-      igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+      igemm_wgrad32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (fast)
+    igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_wgrad32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
 }
@@ -3585,8 +3497,6 @@ CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
-  p.pro = g_pro;
-  if (p.pro.scsh && !wg_fast32(Cin, Cout, p)) return (int)hipErrorInvalidValue;
   run_wg32(p, G, splits, wg_fast32(Cin, Cout, p), stream);
   return (int)hipGetLastError();
 }
@@ -3658,7 +3568,6 @@ static WGParams grouped_wg_params(const E* x, int B, int H, int W, int Cin, int 
   p.Mred = B * Ho * Wo;
   p.N = co;
   p.K = kh * kw * ci;
-  p.pro = BNPro{nullptr, 0, 0};
   return p;
 }
 
@@ -3793,7 +3702,6 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
-  p.pro = g_pro;
   if (!wg_fast32(Cin, Cout, p)) return 0;
   const int rows = wgb_rows();
   p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
@@ -3853,35 +3761,31 @@ CER_API int cer_wgrad_batch_add_grouped_f32(const float* x, int B, int H, int W,
 static int g_wgb_grid = 0;
 CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
 
-template <int BM, int BN, bool PRO, bool WIDE = false>
+template <int BM, int BN, bool WIDE = false>
 static void wgb32_launch_sel(hipStream_t stream) {
-  int idx[4096];
-  int n = 0;
-  for (int k = 0; k < g_wgq32_n; ++k)
-    if ((g_wgq32[k].pro.scsh != nullptr) == PRO) idx[n++] = k;
+  const int n = g_wgq32_n;
   for (int b0 = 0; b0 < n; b0 += WGB_MAX) {
     WGBatch bt;
     bt.n = n - b0 < WGB_MAX ? n - b0 : WGB_MAX;
     int tot = 0;
     for (int i = 0; i < bt.n; ++i) {
-      const int k = idx[b0 + i];
+      const int k = b0 + i;
       bt.p[i] = g_wgq32[k];
       bt.start[i] = tot;
       tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[k]);
     }
     bt.start[bt.n] = tot;
     const int grid = g_wgb_grid > 0 && g_wgb_grid < tot ? g_wgb_grid : tot;
-    if (tot > 0) wgrad_batch32<BM, BN, PRO, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
+    if (tot > 0) wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
   }
 }
 
 template <int BM, int BN>
 static int wgb32_launch(hipStream_t stream, bool wide = false) {
-  if (wide)                  // no prologue form of the wide kernels
-    wgb32_launch_sel<BM, BN, false, true>(stream);
+  if (wide)
+    wgb32_launch_sel<BM, BN, true>(stream);
   else
-    wgb32_launch_sel<BM, BN, false>(stream);
-  wgb32_launch_sel<BM, BN, true>(stream);
+    wgb32_launch_sel<BM, BN>(stream);
   return (int)hipGetLastError();
 }
 

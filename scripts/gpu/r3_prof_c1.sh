@@ -11,7 +11,7 @@ for C in 1 2 8; do
     --steps 20 --warmup 10 > $OUT/c$C.log 2>&1 || { tail -20 $OUT/c$C.log; exit 1; }
   tail -1 $OUT/c$C.log
   python3 -m cerebro_ds_kpgi_amd.tools.prof_summary $OUT/c$C --last-steps 10 > $OUT/c$C.md 2> $OUT/c$C.sum.err || { tail $OUT/c$C.sum.err; exit 1; }
-  find $OUT/c$C -name "*.db" -size +40M -delete
+  find $OUT/c$C -name "*.db" -delete
+  head -30 $OUT/c$C.md
 done
 echo done
-bash scripts/gpu/ab.sh fold "CER_BN_FOLD_APPLY=0 CER_BN_FOLD_APPLY=1" "1 2" 2
