@@ -120,8 +120,10 @@ class DirectAccessReader(object):
         infos = [self.info(i) for i in idx]
         if pinned:
             import torch
-            ind = [torch.empty(ni, dtype=torch.uint8).pin_memory() for _, _, ni, _ in infos]
-            dep = [torch.empty(nd, dtype=torch.uint8).pin_memory() for _, _, _, nd in infos]
+            # allocated pinned (``.pin_memory()`` on a pageable tensor would
+            # allocate twice and copy)
+            ind = [torch.empty(ni, dtype=torch.uint8, pin_memory=True) for _, _, ni, _ in infos]
+            dep = [torch.empty(nd, dtype=torch.uint8, pin_memory=True) for _, _, _, nd in infos]
             ip = [t.data_ptr() for t in ind]
             dp = [t.data_ptr() for t in dep]
         else:
@@ -399,7 +401,10 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
             i = jobs.index(key)
             for k in jobs[i:i + WINDOW]:
                 if k not in futs:
-                    futs[k] = submit(decode, k[0], k[1], max(2, nthreads // WINDOW))
+                    # every decode gets the whole thread budget: the jobs
+                    # are uneven (a train split is ~25x its valid split) and
+                    # a 1/WINDOW share left a lone train decode on 4 threads
+                    futs[k] = submit(decode, k[0], k[1], nthreads)
         fut = futs.pop(key, None)
         return fut.result() if fut is not None else decode(p, split, nthreads)
 

@@ -1532,7 +1532,21 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 }
 
 // 8 fp32 (two 16-B loads) -> 8 bf16 hi + 8 bf16 lo
+// CER_TIMING_NOSPLIT / CER_TIMING_1PASS: timing-only A/B builds (wrong
+// numerics): no hi/lo split VALU, or one MFMA per fragment pair instead of
+// three -- what the split and the extra passes cost (tools.conv_one)
+#ifndef CER_TIMING_NOSPLIT
+#define CER_TIMING_NOSPLIT 0
+#endif
+#ifndef CER_TIMING_1PASS
+#define CER_TIMING_1PASS 0
+#endif
 __device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint4& hi, uint4& lo) {
+  if (CER_TIMING_NOSPLIT) {
+    hi = a;
+    lo = b;
+    return;
+  }
   const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   uint32_t h[4], l[4];
 #pragma unroll
@@ -1585,6 +1599,7 @@ __device__ __forceinline__ void load_row8_slow32(const float* src, int valid, ui
 // three MFMAs per fragment pair: (first operand, second operand) = (x, y)
 __device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const bf16x8& yh,
                                        const bf16x8& yl, f32x4 acc) {
+  if (CER_TIMING_1PASS) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl, yh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yl, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh, yh, acc, 0, 0, 0);

@@ -21,6 +21,7 @@ for T in 16 8; do
   cat gpurun_out/r3da/etl_full_t$T.json
 done
 rm -rf $R/full
+if [ -n "$DA_ONLY_FULL" ]; then rm -rf $R; exit 0; fi
 NT=${1:-16384}
 ( time timeout -k 10 300 python -u -m cerebro_ds_kpgi_amd.tools.make_da_data --root $R/da8 \
     --partitions 8 --dataset imagenet --train $NT --valid 640 ) > gpurun_out/r3da/make8.log 2>&1 || { tail -5 gpurun_out/r3da/make8.log; rm -rf $R; exit 1; }
