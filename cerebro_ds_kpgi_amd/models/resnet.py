@@ -122,9 +122,11 @@ class PackedResNet(PackedNet):
             # block output's two consumers are joined: all link (BNLink), except
             # the last block's output (global average pool)
             link_blk = j is not None and bi + 1 < nb
-            h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j, link_out=True)
+            # b1 / b2 outputs feed only the next conv_bn: HL operand format
+            h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j, link_out=True,
+                             hl_out=True)
             if self.bottleneck:
-                h = self.conv_bn(h, blk["c2"], blk["b2"], training, link_out=True)
+                h = self.conv_bn(h, blk["c2"], blk["b2"], training, link_out=True, hl_out=True)
                 h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc,
                                  res_join=rj, link_out=link_blk)
             else:

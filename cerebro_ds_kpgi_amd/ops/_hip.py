@@ -15,6 +15,7 @@ run as 3-pass split-bf16 MFMA GEMMs with fp32 accumulation, csrc/hip/conv.hip).
 ``_fn(name, t)`` picks the entry point matching tensor ``t``'s dtype.
 """
 
+import contextlib
 import ctypes
 import os
 
@@ -255,6 +256,8 @@ _SIGS.update({
     "cer_wgrad_batch_set_rows": [c_i],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
+    "cer_bn_set_hl_out": [c_i],
+    "cer_conv_set_hl": [c_i, c_i],
     "cer_bn_set_fold": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
     "cer_conv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
@@ -308,10 +311,78 @@ def _act_code(a):
     return 1 if a else 0
 
 
-def _act(t):
-    """Activation operand: bf16 (compute mode) or fp32 (reference precision)."""
+def _act(t, hl_ok=False):
+    """Activation operand: bf16 (compute mode) or fp32 (reference precision).
+    An HL-format tensor (``is_hl``) is only handed as-is to the conv entry
+    points that read HL (``hl_ok``); anything else gets its fp32 value back
+    (hi + lo, what the conv kernels would have used)."""
     assert t.dtype in (torch.bfloat16, torch.float32), t.dtype
+    if not hl_ok and is_hl(t):
+        return hl_to_fp32(t)
     return t.contiguous()
+
+
+# ---------------------------------------------------------------------------
+# HL operand format (csrc/hip/common.h st8_hl, conv.hip take_hi_lo): an fp32
+# tensor whose only consumers are fp32 3-pass conv operand loads is written
+# by its producer (the BN apply forward, the BN backward) as
+# [8 x bf16 hi | 8 x bf16 lo] per 8 channels -- the exact split the conv
+# kernels would compute from the fp32 value, in the same 32 bytes -- so the
+# consumer convs skip the split VALU and see bit-identical operands.
+# CER_HL=0 turns it off.
+# ---------------------------------------------------------------------------
+HL_ENABLED = os.environ.get("CER_HL", "1") != "0"
+
+
+def is_hl(t):
+    return getattr(t, "_cer_hl", False)
+
+
+def hl_to_fp32(t):
+    """fp32 value (hi + lo) of an HL-format tensor."""
+    C = t.shape[-1]
+    u = t.contiguous().view(torch.int32).view(-1, C // 8, 2, 4)
+    hi, lo = u[:, :, 0], u[:, :, 1]
+
+    def unpack(w):                       # 4 words = 8 bf16 -> 8 fp32 (low half first)
+        a = (w << 16).view(torch.float32)
+        b = (w & -65536).view(torch.float32)
+        return torch.stack((a, b), dim=-1).reshape(w.shape[0], w.shape[1], 8)
+    return (unpack(hi) + unpack(lo)).reshape(t.shape)
+
+
+def hl_ok(t, C=None):
+    """``t`` (fp32, channels % 8) may be produced in HL format for conv consumers."""
+    return (HL_ENABLED and t.dtype == torch.float32 and t.is_cuda
+            and (t.shape[-1] if C is None else C) % 8 == 0)
+
+
+@contextlib.contextmanager
+def _hl_operands(x_hl, dy_hl):
+    """The next conv launches read x (fwd A / wgrad B) and/or dy (dgrad /
+    wgrad A) in HL format (conv.hip cer_conv_set_hl)."""
+    x_hl, dy_hl = int(bool(x_hl)), int(bool(dy_hl))
+    if not (x_hl or dy_hl):
+        yield
+        return
+    lib().cer_conv_set_hl(x_hl, dy_hl)
+    try:
+        yield
+    finally:
+        lib().cer_conv_set_hl(0, 0)
+
+
+@contextlib.contextmanager
+def _hl_out(on):
+    """The next BN apply launches write their output (y / dx) in HL format."""
+    if not on:
+        yield
+        return
+    lib().cer_bn_set_hl_out(1)
+    try:
+        yield
+    finally:
+        lib().cer_bn_set_hl_out(0)
 
 
 def _same(t, ref):
@@ -486,25 +557,30 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     return z, part, nslab.value
 
 
-def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps):
+def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps,
+                  hl_out=False):
     y, mean, invstd = bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, act, momentum,
-                                            eps, part, nslab)
+                                            eps, part, nslab, hl_out=hl_out)
     return y, z, mean, invstd
 
 
 def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                      stride, pad, stem=False):
+                      stride, pad, stem=False, hl_out=False):
     """Fused training unit: conv (+ BN statistics into the fp64 slabs in the
     GEMM epilogue) then one BN-apply pass that folds the finalize.
     Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4
-    the repacked stem input (stem path) or None."""
-    return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
-                              eps, stride, pad, stem)
+    the repacked stem input (stem path) or None.  ``x`` may be HL (read as
+    such); ``hl_out``: write y in HL format (its only consumer is a conv;
+    the caller guarantees the BN backward does not read y: no residual)."""
+    x_hl = is_hl(x)
+    with _hl_operands(x_hl, 0):
+        return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
+                                  eps, stride, pad, stem, x_hl, hl_out and residual is None)
 
 
 def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                       stride, pad, stem):
-    x = _act(x)
+                       stride, pad, stem, x_hl=False, hl_out=False):
+    x = _act(x, hl_ok=x_hl)
     B, H, W, GC = x.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
@@ -538,11 +614,11 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
                                           kh, kw, stride, pad, _ptr(z), Ho, Wo,
                                           _ptr(part), ctypes.byref(nslab), _stream())
         _check(rc, "cer_conv_fwd_stats")
-    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
-            after_tune=part.zero_)
+    _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo) + (("hl",) * x_hl),
+            launch, x.dtype, after_tune=part.zero_)
     launch()
     return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                         momentum, eps) + (None,)
+                         momentum, eps, hl_out=hl_out and hl_ok(z)) + (None,)
 
 
 def stem_ok(x, wref, stride, pad):
@@ -599,7 +675,7 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend=None, bnstats=False, wref=None, after_tune=None):
+                       addend=None, bnstats=False, wref=None, after_tune=None, dy_hl=False):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -625,8 +701,8 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
             _check(_fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
                                              cin, kh, kw, stride, pad, _ptr(scratch[0]), H, W,
                                              _ptr(scratch[0]), _stream()), "cer_conv_dgrad")
-    _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats),
-            tune, dy.dtype, after_tune=after_tune)
+    _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats)
+            + (("hl",) * bool(dy_hl)), tune, dy.dtype, after_tune=after_tune)
     launch()
 
 
@@ -638,8 +714,15 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
     into the addend's storage; otherwise the addend is never written.
     ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
     output y this conv consumed — the epilogue also computes that BN's
-    backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink)."""
-    dy = _act(dy)
+    backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink).
+    ``dy`` may be HL (read as such)."""
+    dy_hl = is_hl(dy)
+    with _hl_operands(0, dy_hl):
+        return _conv2d_dgrad(_act(dy, hl_ok=dy_hl), wref, xshape, stride, pad, addend, bnlink,
+                             consume_addend, dy_hl)
+
+
+def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend, dy_hl):
     B, Ho, Wo, _ = dy.shape
     _, H, W, _ = xshape
     G = wref.G
@@ -662,7 +745,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
         dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
     if bnlink is None:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend, wref=wref)
+                           addend, wref=wref, dy_hl=dy_hl)
         return dx
     link, ybn = bnlink
     L = lib()
@@ -676,7 +759,7 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
                            1 if link.has_res else 0, ctypes.byref(nslab))
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend, bnstats=True, wref=wref, after_tune=part.zero_)
+                           addend, bnstats=True, wref=wref, after_tune=part.zero_, dy_hl=dy_hl)
     finally:
         L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
     if nslab.value > 0:
@@ -693,7 +776,8 @@ def conv_set_variant(op, v):
     lib().cer_conv_set_variant(int(op), int(v))
 
 
-def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref):
+def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref,
+                       hl=(False, False)):
     gp, gs = wref.grad_ptr()
     if streams.batching():
         splits = _fn("cer_wgrad_batch_add", x)(_ptr(x), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh,
@@ -714,7 +798,8 @@ def _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad
         _check(rc, "cer_conv_wgrad")
     # timing runs of split-K variants accumulate into the gradient: clear it
     # before the real launch
-    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
+    _select(2, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo)
+            + (("hl", bool(hl[0]), bool(hl[1])),) * any(hl), launch, x.dtype,
             after_tune=lambda: wref.grad().zero_())
     launch()
 
@@ -817,13 +902,18 @@ def grouped_conv_wgrad(x, dy, wref, stride, pad, groups):
 
 
 def conv2d_wgrad(x, dy, wref, stride, pad):
-    x = _act(x)
-    dy = _act(dy)
+    """dW of the conv; ``x`` and / or ``dy`` may be HL (read as such; a
+    batched launch captures the format at queue time)."""
+    x_hl, dy_hl = is_hl(x), is_hl(dy)
+    x = _act(x, hl_ok=x_hl)
+    dy = _act(dy, hl_ok=dy_hl)
     B, H, W, _ = x.shape
     _, Ho, Wo, _ = dy.shape
     G = wref.G
     cout, kh, kw, cin = wref.spec.shape
-    _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref)
+    with _hl_operands(x_hl, dy_hl):
+        _conv_wgrad_launch(x, B, H, W, cin, G, dy, Ho, Wo, cout, kh, kw, stride, pad, wref,
+                           hl=(x_hl, dy_hl))
 
 
 # ---------------------------------------------------------------------------
@@ -856,8 +946,9 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
 
 
 def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, eps, part,
-                          nslab):
-    """BN forward from conv-epilogue partials (cer_conv_fwd_stats)."""
+                          nslab, hl_out=False):
+    """BN forward from conv-epilogue partials (cer_conv_fwd_stats);
+    ``hl_out``: y in HL format (tagged ``_cer_hl``)."""
     x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
@@ -871,11 +962,14 @@ def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, 
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
     res = _same(residual, x) if residual is not None else None
-    rc = _fn("cer_bn_fwd_train_part", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp), bs,
-                                     c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd), _ptr(ws),
-                                     _ptr(part), int(nslab), M, C, Cper, eps, momentum,
-                                     _act_code(act), _stream())
+    with _hl_out(hl_out):
+        rc = _fn("cer_bn_fwd_train_part", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp),
+                                         bs, c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd),
+                                         _ptr(ws), _ptr(part), int(nslab), M, C, Cper, eps,
+                                         momentum, _act_code(act), _stream())
     _check(rc, "cer_bn_fwd_train_part")
+    if hl_out:
+        y._cer_hl = True
     return y, mean, invstd
 
 
@@ -896,10 +990,14 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
     return y
 
 
-def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0):
+def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0,
+               hl_out=False):
     """BN backward; ``part`` / ``nslab``: the (sum dz, sum dz*xhat) partials
-    already computed by the dgrad epilogue that produced dy."""
+    already computed by the dgrad epilogue that produced dy.  ``hl_out``: dx
+    (the conv-output gradient) in HL format for the conv's dgrad / wgrad
+    (tagged ``_cer_hl``); the residual gradient stays fp32."""
     dy = _act(dy)
+    hl_out = hl_out and hl_ok(x)
     C = x.shape[-1]
     M = x.numel() // C
     Cper = gref.spec.shape[0]
@@ -910,17 +1008,20 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
     bp, bs = bref.work_ptr()
     dgp, dgs = gref.grad_ptr()
     dbp, _ = bref.grad_ptr()
-    if part is not None and nslab > 0:
-        rc = _fn("cer_bn_bwd_part", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
-                                   gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx),
-                                   _ptr(dres), _ptr(ws), _ptr(part), int(nslab), M, C, Cper,
-                                   _act_code(act), _stream())
-        _check(rc, "cer_bn_bwd_part")
-        return dx, dres
-    part = _bn_part(M, C, x.device)
-    rc = _fn("cer_bn_bwd", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp), gs,
-                          c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part),
-                          M, C, Cper, _act_code(act), _stream())
+    if hl_out:
+        dx._cer_hl = True
+    with _hl_out(hl_out):
+        if part is not None and nslab > 0:
+            rc = _fn("cer_bn_bwd_part", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd),
+                                       c_p(gp), gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs,
+                                       _ptr(dx), _ptr(dres), _ptr(ws), _ptr(part), int(nslab),
+                                       M, C, Cper, _act_code(act), _stream())
+            _check(rc, "cer_bn_bwd_part")
+            return dx, dres
+        part = _bn_part(M, C, x.device)
+        rc = _fn("cer_bn_bwd", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
+                              gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres),
+                              _ptr(ws), _ptr(part), M, C, Cper, _act_code(act), _stream())
     _check(rc, "cer_bn_bwd")
     return dx, dres
 

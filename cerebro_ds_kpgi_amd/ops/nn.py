@@ -273,7 +273,7 @@ class PackedConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
-                momentum, eps, join=None, res_join=None, link=None):
+                momentum, eps, join=None, res_join=None, link=None, hl_box=None):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join, ctx.res_join = join, res_join
         ctx.bnlink = getattr(x, "_cer_bnlink", None)     # x is a linked BN's output
@@ -284,14 +284,20 @@ class PackedConvBNAct(torch.autograd.Function):
         ctx.x4 = None
         hip_ok = (use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0
                   and gref.spec.shape[0] % 8 == 0)
+        ctx.x_hl = False
         if hip_ok:
             h = _hip()
+            ctx.x_hl = h.is_hl(x)        # an HL-format input (see conv_bn_act hl_out)
             # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
             stem = not x.requires_grad and h.stem_ok(x, wref, stride, pad)
             y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
                 x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride, pad,
-                stem=stem)
+                stem=stem, hl_out=hl_box is not None and not stem and residual is None)
+            if hl_box is not None:
+                hl_box[0] = h.is_hl(y)
         else:
+            if getattr(x, "_cer_hl", False):
+                x = _hip().hl_to_fp32(x)
             z = _conv_forward(x, wref, stride, pad)
             y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,
                                                 momentum, eps)
@@ -306,14 +312,22 @@ class PackedConvBNAct(torch.autograd.Function):
         x, z, y, mean, invstd = ctx.saved_tensors
         gref, bref = ctx.refs
         dy = dy.contiguous()
+        if ctx.x_hl:
+            x._cer_hl = True             # the saved input's format tag
+        # the BN input gradient's only consumers are this conv's dgrad and
+        # wgrad: HL format when both read it (aligned HIP fp32 path, not the stem)
+        wref = ctx.wref
+        hl_bwd = (ctx.x4 is None and use_hip("conv", x) and _bn_hip(z, gref)
+                  and wref.spec.shape[0] % 8 == 0 and wref.spec.shape[3] % 8 == 0)
         link = ctx.link
         if link is not None and link.part is not None:
             # partials from the consumer's dgrad epilogue
             dz, dres = _hip().bn_act_bwd(dy, z, y, mean, invstd, gref, bref, ctx.relu,
-                                         ctx.has_res, part=link.part, nslab=link.nslab)
+                                         ctx.has_res, part=link.part, nslab=link.nslab,
+                                         hl_out=hl_bwd)
             link.part = None
         else:
-            dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref)
+            dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref, hl_out=hl_bwd)
         if link is not None:
             link.z = link.mean = link.invstd = None
         if ctx.res_join is not None and ctx.needs_input_grad[1]:
@@ -326,12 +340,13 @@ class PackedConvBNAct(torch.autograd.Function):
         else:
             dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
-def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
+def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False):
     if _bn_hip(x, gref):
-        return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res)
+        return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res,
+                                 hl_out=hl_out)
     C = x.shape[-1]
     dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
     n = dz.shape[0]
@@ -348,18 +363,25 @@ def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref):
 
 
 def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
-                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False):
+                momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False,
+                hl_out=False):
     """``join``: GradJoin shared with the other consumer of ``x``;
     ``res_join``: GradJoin shared with the other consumer of ``residual``;
     ``link_out``: the output's whole gradient comes out of one consumer dgrad
-    (see BNLink) — its BN backward partials are computed there.  (Folding
-    the BN apply into the consumer conv's operand loads was measured slower
-    at 1, 2 and 8 configs and removed: profiles/r3_resnet50_1cfg_fp32.md.)"""
+    (see BNLink) — its BN backward partials are computed there;
+    ``hl_out``: the output's ONLY consumer is another conv_bn_act (HIP fp32):
+    it is written in HL format (``_hip.is_hl``: the pre-split operand of the
+    consumer's 3-pass kernels, bit-identical operands, no split VALU there).
+    (Folding the BN apply into the consumer conv's operand loads was measured
+    slower at 1, 2 and 8 configs and removed: profiles/r3_resnet50_1cfg_fp32.md.)"""
     link = BNLink() if link_out else None
+    box = [False] if hl_out else None
     y = PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
-                              relu, momentum, eps, join, res_join, link)
+                              relu, momentum, eps, join, res_join, link, box)
     if link is not None:
         y._cer_bnlink = link
+    if box is not None and box[0]:
+        y._cer_hl = True
     return y
 
 

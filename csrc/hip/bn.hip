@@ -332,6 +332,8 @@ __device__ __forceinline__ void apply_fwd_tile(
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, const Strided& gamma,
     const Strided& beta, int64_t M, int C, int Cper, int rows_per_slab, int act, const Map& mp,
     int cbk, int slab) {
+  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
+  act &= 0xff;
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
@@ -368,7 +370,10 @@ __device__ __forceinline__ void apply_fwd_tile(
 #pragma unroll
       for (int i = 0; i < VEC; ++i)
         o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
-      st8(y + rr * C + c0, o);
+      if (hl)
+        st8_hl(y + rr * C + c0, o);
+      else
+        st8(y + rr * C + c0, o);
     }
   }
 }
@@ -390,6 +395,8 @@ __device__ __forceinline__ void apply_bwd_tile(
     const Strided& gamma, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
     int Cper, int rows_per_slab, int act, const Map& mp, int cbk, int slab,
     const Strided& beta = Strided{nullptr, 0}) {
+  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
+  act &= 0xff;
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   if (c0 >= C) return;
@@ -430,7 +437,10 @@ __device__ __forceinline__ void apply_bwd_tile(
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
-      st8(dx + rr * C + c0, o);
+      if (hl)
+        st8_hl(dx + rr * C + c0, o);
+      else
+        st8(dx + rr * C + c0, o);
       if (dres) st8(dres + rr * C + c0, dz);
     }
   }
@@ -570,6 +580,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
     const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
     int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
+  act &= 0xff;
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
@@ -620,7 +632,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
 #pragma unroll
       for (int i = 0; i < VEC; ++i)
         o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
-      st8(y + rr * C + c0, o);
+      if (hl)
+        st8_hl(y + rr * C + c0, o);
+      else
+        st8(y + rr * C + c0, o);
     }
   }
 }
@@ -632,6 +647,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     const float* __restrict__ mean, const float* __restrict__ invstd, Strided gamma,
     Strided beta, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C, int Cper,
     int rows_per_slab, int act, Map mp) {
+  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
+  act &= 0xff;
   __shared__ float red[FOLD_LDS];
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
@@ -683,7 +700,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
-      st8(dx + rr * C + c0, o);
+      if (hl)
+        st8_hl(dx + rr * C + c0, o);
+      else
+        st8(dx + rr * C + c0, o);
       if (dres) st8(dres + rr * C + c0, dz);
     }
   }
@@ -734,6 +754,13 @@ static int apply_au() {
 static int g_zmask = 1;
 CER_API void cer_bn_set_zmask(int on) { g_zmask = on; }
 
+// HL-format output of the NEXT training-mode apply launches (fwd y / bwd dx,
+// fp32 only; st8_hl): the value's only consumers are fp32 3-pass conv
+// operand loads (conv.hip take_hi_lo), which read the pre-split pair instead
+// of splitting the fp32 value -- bit-identical operands, no split VALU
+static int g_bn_hl = 0;
+CER_API void cer_bn_set_hl_out(int on) { g_bn_hl = on ? 1 : 0; }
+
 // mask source of a BN backward (also used by the dgrad-epilogue statistics)
 int bn_mask_mode(int act, int has_res) {
   return act == 0 ? YM_NONE : (act == 1 && !has_res && g_zmask) ? YM_Z : YM_Y;
@@ -755,6 +782,7 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                              float* invstd_out, float* ws, float* part, int nslab, int64_t M,
                              int C, int Cper, float eps, float momentum, int act,
                              hipStream_t stream) {
+  const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 rg, ag;
@@ -773,7 +801,7 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
     bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
                                                rstat_stride, eps, momentum, x, res, y,
                                                Strided{gamma, gamma_stride},
-                                               Strided{beta, beta_stride}, M, C, Cper, frows, act,
+                                               Strided{beta, beta_stride}, M, C, Cper, frows, act_k,
                                                mp);
     return (int)hipGetLastError();
   }
@@ -784,11 +812,11 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
     bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                                 Strided{gamma, gamma_stride},
                                                 Strided{beta, beta_stride}, M, C, Cper, arows,
-                                                act, mp);
+                                                act_k, mp);
   else
     bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                              Strided{gamma, gamma_stride},
-                                             Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                             Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
                                              mp);
   return (int)hipGetLastError();
 }
@@ -826,6 +854,7 @@ static int cer_bn_apply_fwd_t(const T* x, const T* res, T* y, const float* ws,
                              const T* gamma, int64_t gamma_stride, const T* beta,
                              int64_t beta_stride, int64_t M, int C, int Cper, int act,
                              hipStream_t stream) {
+  const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 ag;
@@ -835,11 +864,11 @@ static int cer_bn_apply_fwd_t(const T* x, const T* res, T* y, const float* ws,
     bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                                 Strided{gamma, gamma_stride},
                                                 Strided{beta, beta_stride}, M, C, Cper, arows,
-                                                act, mp);
+                                                act_k, mp);
   else
     bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                              Strided{gamma, gamma_stride},
-                                             Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                             Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
                                              mp);
   return (int)hipGetLastError();
 }
@@ -868,6 +897,7 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
                        const T* beta, int64_t beta_stride, float* dgamma, float* dbeta,
                        int64_t grad_stride, T* dx, T* dres, float* ws, float* part,
                        int pre_nslab, int64_t M, int C, int Cper, int act, hipStream_t stream) {
+  const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
   if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 rg, ag;
@@ -897,16 +927,16 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
     if (ym == YM_NONE)
       bn_apply_bwd_fold<T, YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                           grad_stride, dy, x, y, mean, invstd, gs,
-                                                          bs, dx, dres, M, C, Cper, frows, act,
+                                                          bs, dx, dres, M, C, Cper, frows, act_k,
                                                           mp);
     else if (ym == YM_Z)
       bn_apply_bwd_fold<T, YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
-                                                       dx, dres, M, C, Cper, frows, act, mp);
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
     else
       bn_apply_bwd_fold<T, YM_Y><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
-                                                       dx, dres, M, C, Cper, frows, act, mp);
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
     return (int)hipGetLastError();
   }
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
@@ -914,24 +944,24 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   if (ym == YM_NONE) {
     if (apply_au() == 4)
       bn_apply_bwd<T, YM_NONE, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
-                                                     C, Cper, arows, act, mp, bs);
+                                                     C, Cper, arows, act_k, mp, bs);
     else
       bn_apply_bwd<T, YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
-                                                     C, Cper, arows, act, mp, bs);
+                                                     C, Cper, arows, act_k, mp, bs);
   } else if (ym == YM_Z) {
     if (apply_au() == 4)
       bn_apply_bwd<T, YM_Z, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act, mp, bs);
+                                                  Cper, arows, act_k, mp, bs);
     else
       bn_apply_bwd<T, YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act, mp, bs);
+                                                  Cper, arows, act_k, mp, bs);
   } else {
     if (apply_au() == 4)
       bn_apply_bwd<T, YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act, mp, bs);
+                                                  Cper, arows, act_k, mp, bs);
     else
       bn_apply_bwd<T, YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act, mp, bs);
+                                                  Cper, arows, act_k, mp, bs);
   }
   return (int)hipGetLastError();
 }

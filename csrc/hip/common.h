@@ -66,6 +66,31 @@ __device__ __forceinline__ void st8(float* p, const float* v) {
   reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  // gfx950 v_cvt_pk_bf16_f32 (round to nearest even, NaN preserving)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+
+// 8 fp32 -> HL format: [8 x bf16 hi | 8 x bf16 lo], hi = RNE(x), lo =
+// RNE(x - hi) -- exactly the operand split of the fp32 3-pass conv kernels
+// (conv.hip split_hi_lo / take_hi_lo), in the 32 bytes of the 8 fp32
+__device__ __forceinline__ void st8_hl(float* p, const float* v) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t hp = cvt_pk_bf16(v[2 * i], v[2 * i + 1]);
+    h[i] = hp;
+    l[i] = cvt_pk_bf16(v[2 * i] - __uint_as_float(hp << 16),
+                       v[2 * i + 1] - __uint_as_float(hp & 0xffff0000u));
+  }
+  reinterpret_cast<uint4*>(p)[0] = make_uint4(h[0], h[1], h[2], h[3]);
+  reinterpret_cast<uint4*>(p)[1] = make_uint4(l[0], l[1], l[2], l[3]);
+}
+__device__ __forceinline__ void st8_hl(bf16_t* p, const float* v) { st8(p, v); }  // bf16: unused
+
 __device__ __forceinline__ float ld1(const bf16_t* p) { return bf2f(*p); }
 __device__ __forceinline__ float ld1(const float* p) { return *p; }
 __device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f2bf(v); }

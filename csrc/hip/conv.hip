@@ -127,6 +127,7 @@ struct NTParams {
                          0, 0};
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
+  int a_hl = 0;           // fp32 kernels: the A operand is in HL format (take_hi_lo)
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
@@ -142,6 +143,17 @@ struct NTParams {
 // slab count it gets back carries SLAB_F64 (bn.hip reads the fp64 format).
 static int g_stat_slabs = 0;
 CER_API void cer_conv_set_stat_slabs(int n) { g_stat_slabs = n > 0 ? n : 0; }
+
+// HL operand format (take_hi_lo) of the NEXT fp32 launches until reset:
+// x_hl -- the activation (fwd A operand, wgrad B operand) is HL; dy_hl -- the
+// output gradient (dgrad / wgrad A operand) is HL.  Only the aligned gathers
+// read HL: a launch that would take a generic (per-element) gather or a
+// grouped per-config launch returns hipErrorInvalidValue instead.
+static int g_hl_x = 0, g_hl_dy = 0;
+CER_API void cer_conv_set_hl(int x_hl, int dy_hl) {
+  g_hl_x = x_hl ? 1 : 0;
+  g_hl_dy = dy_hl ? 1 : 0;
+}
 constexpr int SLAB_F64 = 1 << 24;
 
 // one partial into the statistics buffer: plain fp32 store (one slab per
@@ -173,6 +185,7 @@ struct WGParams {
   int Mred, N, K;
   int m_per_split;
   int splits;
+  int x_hl = 0, dy_hl = 0;  // HL-format operands (take_hi_lo)
 };
 
 // es: element size of the gathered tensor (2 = bf16, 4 = fp32)
@@ -1523,14 +1536,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch(WGBatch b) {
 // consecutive output channels of one row: one 16-B store).
 constexpr int KS = 32;
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
-  // gfx950 v_cvt_pk_bf16_f32 (round to nearest even, NaN preserving)
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2));
-}
-
 // 8 fp32 (two 16-B loads) -> 8 bf16 hi + 8 bf16 lo
 // CER_TIMING_NOSPLIT / CER_TIMING_1PASS: timing-only A/B builds (wrong
 // numerics): no hi/lo split VALU, or one MFMA per fragment pair instead of
@@ -1558,6 +1563,21 @@ __device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint
   }
   hi = make_uint4(h[0], h[1], h[2], h[3]);
   lo = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
+// HL operand format (conv-only activations and BN-backward gradients, see
+// cer_conv_set_hl): every 8 channels are stored as [8 x bf16 hi | 8 x bf16
+// lo] of the fp32 values, split exactly as split_hi_lo does -- the same 32
+// bytes at the same offsets as 8 fp32, so the gathers are unchanged and the
+// 3-pass MFMAs see bit-identical operands.  An HL chunk IS the (hi, lo) pair.
+__device__ __forceinline__ void take_hi_lo(bool hl, const uint4& a, const uint4& b, uint4& hi,
+                                           uint4& lo) {
+  if (hl) {
+    hi = a;
+    lo = b;
+  } else {
+    split_hi_lo(a, b, hi, lo);
+  }
 }
 
 __device__ __forceinline__ uint4 f4_bits(const float* e) {
@@ -1965,7 +1985,8 @@ __device__ __forceinline__ void mma3w_nt(const bf16_t* sa, const bf16_t* sb, int
 // substep s, half h are fp32 16s + 8h .. +7 = chunks 4s + 2h, 4s + 2h + 1
 template <int BM, int BN>
 __device__ __forceinline__ void mma3w_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
-                                              int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+                                              int lane, f32x16 (&acc)[BM / 64][BN / 64],
+                                              bool ahl) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -1987,7 +2008,7 @@ __device__ __forceinline__ void mma3w_ring_nt(const bf16_t* sa, const bf16_t* sb
       const uint4 x0 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 4 * s + 2 * h));
       const uint4 x1 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 4 * s + 2 * h + 1));
       uint4 hh, ll;
-      split_hi_lo(x0, x1, hh, ll);
+      take_hi_lo(ahl, x0, x1, hh, ll);
       ah[i] = __builtin_bit_cast(bf16x8, hh);
       al[i] = __builtin_bit_cast(bf16x8, ll);
     }
@@ -2402,7 +2423,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
+      take_hi_lo(p.a_hl != 0, ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -2448,7 +2469,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
 // costs 2.5x a read per byte on the VGPR -> LDS path.  Requires Cg % 32 == 0.
 template <int BM, int BN>
 __device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
-                                             int lane, f32x4 (&acc)[BM / 32][BN / 32]) {
+                                             int lane, f32x4 (&acc)[BM / 32][BN / 32], bool ahl) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   const int fr = lane & 15, fc = lane >> 4;
   bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
@@ -2468,7 +2489,7 @@ __device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb,
     const uint4 x0 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 2 * fc));
     const uint4 x1 = *reinterpret_cast<const uint4*>(sa + nt_off(row, 2 * fc + 1));
     uint4 h, l;
-    split_hi_lo(x0, x1, h, l);
+    take_hi_lo(ahl, x0, x1, h, l);
     ah[i] = __builtin_bit_cast(bf16x8, h);
     al[i] = __builtin_bit_cast(bf16x8, l);
   }
@@ -2546,14 +2567,16 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
   if constexpr (WIDE) {
     zero_accw<BM, BN>(acc);
     ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
-      mma3w_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+      mma3w_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc,
+                            p.a_hl != 0);
     });
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   } else {
     zero_acc<BM, BN>(acc);
     ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
-      mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc);
+      mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc,
+                           p.a_hl != 0);
     });
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
@@ -2635,7 +2658,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
+      take_hi_lo(p.a_hl != 0, ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk + 4)) = l;
     }
@@ -2759,7 +2782,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     for (int i = 0; i < A_CH; ++i) {
       const int row = a_row0 + A_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(ra[s][2 * i], ra[s][2 * i + 1], h, l);
+      take_hi_lo(p.dy_hl != 0, ra[s][2 * i], ra[s][2 * i + 1], h, l);
       if constexpr (WIDE) {
         *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row, a_col)) = h;
         *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row + KS, a_col)) = l;
@@ -2772,7 +2795,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      take_hi_lo(p.x_hl != 0, rb[s][2 * i], rb[s][2 * i + 1], h, l);
       if constexpr (WIDE) {
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
@@ -3093,6 +3116,7 @@ static int fp32_variant(int v) { return (v >= 6 ? 6 : 0) + v % 3; }
 static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   p.stat_slabs = p.stats ? g_stat_slabs : 0;
   const bool fast = nt_fast32(p);
+  if (p.a_hl && !fast) return (int)hipErrorInvalidValue;
   const bool ring_ok = fast && p.a.Cg % KS == 0;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
   bool wide = false;
@@ -3197,6 +3221,10 @@ static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
   p.o_H = Ho;
   p.o_W = Wo;
   p.stats = stats;
+  if (f32) {
+    p.a_hl = g_hl_x;
+    if (p.a_hl && (ctot || ldc)) return (int)hipErrorInvalidValue;   // grouped: no HL
+  }
   return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
 
@@ -3302,6 +3330,10 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
   const bool aligned = (Cout % 8 == 0) && (Cin % 8 == 0) &&
                        (uint64_t)B * Ho * Wo * ctot_dy * es < (1ull << 31) &&
                        (uint64_t)Cout * T * Cin * es < (1ull << 31);
+  if (f32) {
+    p.a_hl = g_hl_dy;
+    if (p.a_hl && (cout_tot || cin_tot)) return (int)hipErrorInvalidValue;   // grouped: no HL
+  }
   if (aligned) {
     p.w = reinterpret_cast<const bf16_t*>(w);
     p.w_gstride = w_gstride;
@@ -3512,6 +3544,9 @@ CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
+  p.x_hl = g_hl_x;
+  p.dy_hl = g_hl_dy;
+  if ((p.x_hl || p.dy_hl) && !wg_fast32(Cin, Cout, p)) return (int)hipErrorInvalidValue;
   run_wg32(p, G, splits, wg_fast32(Cin, Cout, p), stream);
   return (int)hipGetLastError();
 }
@@ -3643,7 +3678,7 @@ CER_API int cer_conv_grouped_wgrad_f32(const float* x, int B, int H, int W, int 
                                        int groups, const float* dy, int Ho, int Wo, int Cout,
                                        int kh, int kw, int st, int pad, float* dw,
                                        int64_t dw_gstride, int splits, hipStream_t stream) {
-  if (!grouped_ok(Cin, Cout, groups)) return (int)hipErrorInvalidValue;
+  if (!grouped_ok(Cin, Cout, groups) || g_hl_x || g_hl_dy) return (int)hipErrorInvalidValue;
   for (int g = 0; g < G; ++g) {
     WGParams p = grouped_wg_params(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad,
                                    dw, dw_gstride, g);
@@ -3717,7 +3752,9 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   p.Mred = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kw * Cin;
-  if (!wg_fast32(Cin, Cout, p)) return 0;
+  p.x_hl = g_hl_x;
+  p.dy_hl = g_hl_dy;
+  if (!wg_fast32(Cin, Cout, p)) return 0;     // HL operands: the direct launch refuses
   const int rows = wgb_rows();
   p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
   p.splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
@@ -3734,7 +3771,7 @@ static int grouped_batch_add(const E* x, int B, int H, int W, int Cin, int G, in
                              int pad, float* dw, int64_t dw_gstride) {
   const bool f32 = sizeof(E) == 4;
   int& n = f32 ? g_wgq32_n : g_wgq_n;
-  if (!grouped_ok(Cin, Cout, groups) || n + G > 4096) return 0;
+  if (!grouped_ok(Cin, Cout, groups) || n + G > 4096 || g_hl_x || g_hl_dy) return 0;
   int splits = 0;
   for (int g = 0; g < G; ++g) {
     WGParams p = grouped_wg_params(x, B, H, W, Cin, G, groups, dy, Ho, Wo, Cout, kh, kw, st, pad,
