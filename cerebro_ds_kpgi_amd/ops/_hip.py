@@ -332,6 +332,7 @@ def _act(t, hl_ok=False):
 # CER_HL=0 turns it off.
 # ---------------------------------------------------------------------------
 HL_ENABLED = os.environ.get("CER_HL", "1") != "0"
+HL_COUNTS = {"x": 0, "dy": 0, "out": 0}     # launches that read / wrote HL (tests, logs)
 
 
 def is_hl(t):
@@ -365,6 +366,8 @@ def _hl_operands(x_hl, dy_hl):
     if not (x_hl or dy_hl):
         yield
         return
+    HL_COUNTS["x"] += x_hl
+    HL_COUNTS["dy"] += dy_hl
     lib().cer_conv_set_hl(x_hl, dy_hl)
     try:
         yield
@@ -378,6 +381,7 @@ def _hl_out(on):
     if not on:
         yield
         return
+    HL_COUNTS["out"] += 1
     lib().cer_bn_set_hl_out(1)
     try:
         yield

@@ -144,10 +144,12 @@ def test_hl_chain_bitwise_equals_fp32_chain(G, B, H):
     assert _hip.HL_ENABLED
 
 
-def test_resnet50_training_bitwise_with_and_without_hl():
-    """Packed ResNet-50 (2 configs, bs 4, fp32, HIP graphs): six training
-    steps through the engine give bit-identical parameters with the HL
-    format on and off, and the HL run did use HL conv launches."""
+def test_resnet50_training_with_and_without_hl():
+    """Packed ResNet-50 (2 configs, bs 4, fp32, HIP graphs, conv variants
+    pinned): six engine training steps with the HL format land as close to
+    the fp32-format run as two fp32-format runs land to each other (their
+    only difference: the order of the split-K fp32 atomics, which Adam
+    amplifies element-wise), and the HL run used HL conv launches."""
     from cerebro_ds_kpgi_amd.ops import _hip
     from cerebro_ds_kpgi_amd.parallel import init_distributed
     from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
@@ -155,8 +157,12 @@ def test_resnet50_training_bitwise_with_and_without_hl():
     msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": bs, "model": "resnet50"}
             for lr in (1e-3, 1e-4)]
     states = []
-    for on in (False, True):
+    for k in _hip.HL_COUNTS:
+        _hip.HL_COUNTS[k] = 0
+    for on in (False, False, True):
         _hl(on)
+        _hip.conv_set_variant(0, 0)
+        _hip.conv_set_variant(1, 0)
         try:
             eng = MOPEngine(msts, init_distributed(), EngineOptions(
                 n_train=16 * bs, n_valid=2 * bs, slots_per_gpu=2, verbose=False,
@@ -173,12 +179,14 @@ def test_resnet50_training_bitwise_with_and_without_hl():
             eng.close()
         finally:
             _hl(True)
-    assert torch.isfinite(states[0]).all() and torch.isfinite(states[1]).all()
-    # per-config parameter norms: the same training up to the split-K fp32
-    # atomics' order noise (which Adam amplifies element-wise)
-    n0, n1 = states[0].double().norm(dim=1), states[1].double().norm(dim=1)
-    rel = ((n0 - n1).abs() / n0).max().item()
-    assert rel < 2e-3, rel
-    keys = [k for k in _hip.tuned_variants() if "hl" in str(k[1])]
-    assert keys, "no HL conv launch ran"
-    assert {0, 1} <= {k[0] for k in keys}, "HL reached only ops {}".format({k[0] for k in keys})
+            _hip.conv_set_variant(0, -1)
+            _hip.conv_set_variant(1, -1)
+    assert all(torch.isfinite(s).all() for s in states)
+
+    def dist(a, b):
+        na, nb = a.double().norm(dim=1), b.double().norm(dim=1)
+        return ((na - nb).abs() / na).max().item()
+    noise, hl = dist(states[0], states[1]), dist(states[0], states[2])
+    print("per-config norm rel diff: fp32 vs fp32 %.2e, fp32 vs HL %.2e" % (noise, hl))
+    assert hl <= max(4 * noise, 1e-5), (hl, noise)
+    assert min(_hip.HL_COUNTS.values()) > 0, _hip.HL_COUNTS
