@@ -26,8 +26,20 @@ basic blocks with the same stem; 101/152 bottleneck depths [3,4,23,3] /
 [3,8,36,3] (model-size drill-down).
 """
 
+import os
+
+import torch
+
 from .common import BN, Conv, Dense, PackedNet
 from ..ops import nn as P
+from ..ops import streams
+from ..ops.backend import get_backend
+
+# projection shortcuts on the branch stream (CER_SC_BRANCH=1): the shortcut
+# conv + BN of a stage's first block runs concurrently with the main path's
+# c1 / c2 in forward and, being created after c1, its backward runs ahead of
+# c1's (autograd's order) on the branch stream, beside c2 / c1's backward
+_SC_BRANCH = os.environ.get("CER_SC_BRANCH", "0") == "1"
 
 _BOTTLENECK = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 _BASIC = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}
@@ -113,11 +125,17 @@ class PackedResNet(PackedNet):
             # x has two consumers (c1 and the shortcut): their input gradients
             # meet in a GradJoin instead of an autograd add kernel
             j = P.GradJoin() if training else None
-            if "cs" in blk:
+            branch = ("cs" in blk and training and _SC_BRANCH and x.is_cuda
+                      and get_backend() == "hip")
+            if branch:
+                cur = torch.cuda.current_stream(x.device)
+                fork = torch.cuda.Event()
+                fork.record(cur)
+            elif "cs" in blk:
                 sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j)
-                rj = None
-            else:
-                sc, rj = x, j
+            rj = None if "cs" in blk else j
+            if "cs" not in blk:
+                sc = x
             # every BN output inside the block has one conv consumer, and the
             # block output's two consumers are joined: all link (BNLink), except
             # the last block's output (global average pool)
@@ -125,8 +143,18 @@ class PackedResNet(PackedNet):
             # b1 / b2 outputs feed only the next conv_bn: HL operand format
             h = self.conv_bn(x, blk["c1"], blk["b1"], training, join=j, link_out=True,
                              hl_out=True)
+            if branch:
+                bs = streams.branch_stream(x.device.index)
+                bs.wait_event(fork)
+                x.record_stream(bs)
+                with torch.cuda.stream(bs):
+                    sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j)
             if self.bottleneck:
                 h = self.conv_bn(h, blk["c2"], blk["b2"], training, link_out=True, hl_out=True)
+            if branch:
+                cur.wait_stream(bs)
+                sc.record_stream(cur)
+            if self.bottleneck:
                 h = self.conv_bn(h, blk["c3"], blk["b3"], training, relu=True, residual=sc,
                                  res_join=rj, link_out=link_blk)
             else:

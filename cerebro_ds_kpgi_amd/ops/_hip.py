@@ -47,9 +47,6 @@ c_f = ctypes.c_float
 _SIGS = {
     "cer_adam_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p,
                       c_p, c_i, c_f, c_f, c_f, c_i, c_p],
-    "cer_adam_step_ex": [c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64,
-                         c_p, c_p, c_i, c_f, c_f, c_f, c_i, c_p, c_i64, c_i64, c_i, c_p],
-    "cer_set_flag": [c_p, c_i, c_p],
     "cer_sgd_step": [c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i, c_p, c_i64, c_p, c_p, c_i,
                      c_f, c_i, c_p],
     "cer_softmax_ce": [c_p, c_i, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
@@ -100,25 +97,16 @@ def _check(rc, name):
 
 
 # ---------------------------------------------------------------------------
-def adam_step(arena, beta1, beta2, eps, l2, flag=None, i0=0, i1=None, inc=True):
-    """Fused Adam over arena parameters [i0, i1) (default: all), advancing
-    the step counters first when ``inc``; ``flag`` (device int32 tensor): the
-    launch is a no-op while it holds 0 (runtime/group.py lagged update)."""
+def adam_step(arena, beta1, beta2, eps, l2):
     L = arena.layout
     st = arena.state
     work = arena.work if arena.work is not arena.params else None
-    rc = lib().cer_adam_step_ex(
+    rc = lib().cer_adam_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
         _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
         _ptr(work), work.stride(0) if work is not None else 0,
-        _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)),
-        _ptr(flag), int(i0), int(L.n_train if i1 is None else i1), int(bool(inc)), _stream())
-    _check(rc, "cer_adam_step_ex")
-
-
-def set_flag(flag, v):
-    """flag[0] = v on the current stream (a kernel: capture safe)."""
-    _check(lib().cer_set_flag(_ptr(flag), int(v), _stream()), "cer_set_flag")
+        _ptr(arena.lr), _ptr(arena.wd), arena.G, beta1, beta2, eps, int(bool(l2)), _stream())
+    _check(rc, "cer_adam_step")
 
 
 def sgd_step(arena, momentum, l2):
@@ -426,11 +414,13 @@ def _tune_enabled():
 
 
 def _splitk_ready(device):
-    """Register this device's persistent split-K workspace with the library
-    (once per device switch; the pointers are baked into captured graphs)."""
-    key = str(device)
-    cur = _SPLITK.get("_current")
-    if cur == key:
+    """Register the persistent split-K workspace of this device with the
+    library: one for a model's branch stream (ops.streams.branch_stream),
+    one for everything else -- kernels of the two may run at once, so each
+    has its own partial slots and arrival counters (the pointers are baked
+    into captured graphs)."""
+    key = (str(device), streams.on_branch(device))
+    if _SPLITK.get("_current") == key:
         return
     ws = _SPLITK.get(key)
     if ws is None:

@@ -77,19 +77,40 @@ class GradJoin(object):
     gradients in a separate elementwise kernel; instead the consumer whose
     backward runs first parks its gradient here (and returns None to
     autograd), and the second adds it — inside its dgrad GEMM epilogue when it
-    is a HIP conv (``conv2d_dgrad(addend=...)``).  Correct in either order."""
-    __slots__ = ("pending",)
+    is a HIP conv (``conv2d_dgrad(addend=...)``).  Correct in either order,
+    and across streams: the two consumers' backwards may run on different
+    streams (a ResNet shortcut on the branch stream, ops.streams), so parking
+    records an event that the taking stream waits on (``take``)."""
+    __slots__ = ("pending", "_ev")
 
     def __init__(self):
         self.pending = None
+        self._ev = None
+
+    def _park(self, g):
+        self.pending = g
+        self._ev = None
+        if g is not None and g.is_cuda:
+            self._ev = torch.cuda.Event()
+            self._ev.record()
+
+    def take(self):
+        """The parked gradient (or None), ordered before the current stream's
+        next work; the join is empty afterwards."""
+        g, ev = self.pending, self._ev
+        self.pending, self._ev = None, None
+        if g is not None and ev is not None:
+            cur = torch.cuda.current_stream(g.device)
+            cur.wait_event(ev)
+            g.record_stream(cur)
+        return g
 
     def join(self, g):
         """First arrival: park g, return None.  Second: return the other one."""
         if self.pending is None:
-            self.pending = g
+            self._park(g)
             return None
-        other, self.pending = self.pending, None
-        return other
+        return self.take()
 
 
 def _join_after(join, g):
@@ -149,10 +170,9 @@ class PackedConv2d(torch.autograd.Function):
             h = _hip()
             if need_dx:
                 # the other consumer's gradient, if it already ran, joins in the epilogue
-                addend = join.pending if join is not None else None
+                addend = join.take() if join is not None else None
                 bnl = _bnlink_for(ctx, x, join, addend)
                 if addend is not None:
-                    join.pending = None
                     join = None
                 dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl,
                                     consume_addend=addend is not None)

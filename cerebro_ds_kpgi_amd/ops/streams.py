@@ -131,9 +131,32 @@ def flush_wgrad(discard=False, side=False):
             t.record_stream(st)
         _PENDING.add(dev)
     else:
+        cur = torch.cuda.current_stream()
+        for t in _HELD:                  # operands made on a branch stream
+            t.record_stream(cur)
         rc = _hip.lib().cer_wgrad_batch_flush(_BATCH_VARIANT, 1 if discard else 0, _hip._stream())
     del _HELD[:]
     _hip._check(rc, "cer_wgrad_batch_flush")
+
+
+_BRANCH = {}
+
+
+def branch_stream(dev):
+    """Per-device stream for a model's parallel branch (ResNet projection
+    shortcuts, models/resnet.py); autograd runs the branch's backward there."""
+    s = _BRANCH.get(dev)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _BRANCH[dev] = s
+    return s
+
+
+def on_branch(device):
+    """True while the current stream of ``device`` is its branch stream."""
+    dev = torch.device(device).index
+    s = _BRANCH.get(dev)
+    return s is not None and torch.cuda.current_stream(dev) == s
 
 
 def _side(dev):

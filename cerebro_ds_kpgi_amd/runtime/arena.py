@@ -246,34 +246,6 @@ class Arena(object):
         self.lr = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.wd = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.model_ids = [None] * G
-        # lagged optimizer update (runtime/group.py): [(i0, i1, event)] of the
-        # chunks of an Adam update still running on a side stream, in offset
-        # order; an op that reads a parameter first makes the current stream
-        # wait for the chunk holding it (ParamRef accessors -> lag_wait)
-        self.lag = None
-        self._lag_next = 0
-
-    def lag_begin(self, chunks):
-        self.lag, self._lag_next = list(chunks), 0
-
-    def lag_wait(self, offset):
-        """Current stream waits for every pending chunk up to the one holding
-        parameter element ``offset`` (buffers past n_train: no Adam, no wait)."""
-        lag = self.lag
-        if lag is None or offset >= self.layout.n_train:
-            return
-        cur = torch.cuda.current_stream(self.device)
-        while self._lag_next < len(lag) and lag[self._lag_next][0] <= offset:
-            cur.wait_event(lag[self._lag_next][2])
-            self._lag_next += 1
-
-    def lag_wait_all(self):
-        if self.lag is None:
-            return
-        cur = torch.cuda.current_stream(self.device)
-        for _, _, ev in self.lag[self._lag_next:]:
-            cur.wait_event(ev)
-        self.lag, self._lag_next = None, 0
 
     # ---- views -----------------------------------------------------------
     def _view(self, base, spec):
@@ -342,35 +314,23 @@ class ParamRef(object):
         return self.arena.G
 
     def work(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         return self.arena.work_view(self.spec)
 
     def grad(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         return self.arena.grad_view(self.spec)
 
     def master(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         return self.arena.master_view(self.spec)
 
     # raw addressing for HIP kernels: base pointer + per-config stride (elements)
     def work_ptr(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         w = self.arena.work
         return w.data_ptr() + self.spec.offset * w.element_size(), w.stride(0)
 
     def grad_ptr(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         g = self.arena.grad
         return g.data_ptr() + self.spec.offset * g.element_size(), g.stride(0)
 
     def master_ptr(self):
-        if self.arena.lag is not None:
-            self.arena.lag_wait(self.spec.offset)
         m = self.arena.master
         return m.data_ptr() + self.spec.offset * m.element_size(), m.stride(0)

@@ -203,7 +203,7 @@ class MOPEngine(object):
             write_manifest(os.path.join(opts.logs_root, "manifest.json"),
                            make_data_catalog(self.dataset, self.P, ctx.world),
                            {"msts": self.msts, "partitions": self.P, "gpus": ctx.world,
-                            "slots_per_gpu": V, "n_train": self.n_train, "n_valid": self.n_valid})
+                            "slots_per_gpu": self.V, "n_train": self.n_train, "n_valid": self.n_valid})
 
     # ------------------------------------------------------------------
     def _build_groups(self, model_ids):

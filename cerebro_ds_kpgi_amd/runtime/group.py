@@ -221,11 +221,6 @@ class _Working(object):
         if g.device.type == "cuda" and get_backend() == "hip":
             from ..ops import _hip
             self.stats_arena = _hip.new_stats_arena(g.device)
-        # lagged Adam (see _lag_issue): device flag "an update is pending",
-        # side stream, chunk boundaries
-        self.lag_flag = None
-        self._lag_stream = None
-        self._lag_bounds = None
 
     def assign(self, jobs):
         self.jobs = list(jobs)
@@ -262,64 +257,9 @@ class _Working(object):
         finally:
             _hip.stats_step(None)
 
-    # -- lagged optimizer update -------------------------------------------
-    # The Adam update of step t's gradient runs at the START of step t+1, on a
-    # side stream, in chunks of the arena in forward (offset) order; each op
-    # of step t+1's forward waits only for the chunk holding its parameters
-    # (Arena.lag_wait), so the bandwidth-bound update runs under the forward
-    # of the earlier layers instead of after backward.  Numerics are those of
-    # the plain update: every parameter is updated exactly once, before its
-    # first read, and every chunk has finished before backward starts (it
-    # also clears the gradients backward accumulates into).  A device flag
-    # makes the update a no-op on the first step of a train_steps call;
-    # train_steps applies the last pending update itself before it returns,
-    # so nothing outside (validation, hops, checkpoints, metrics) ever sees a
-    # lagging state.  Adam only, no gradient hook (DDP), HIP backend.
-    def _lag_on(self):
-        g = self.group
-        return (_LAG and g.optimizer == "adam" and self.grad_hook is None
-                and getattr(self.net, "grad_buckets", None) is None
-                and self.x.device.type == "cuda" and get_backend() == "hip")
-
-    def _lag_setup(self):
-        if self.lag_flag is None:
-            self.lag_flag = torch.zeros(1, dtype=torch.int32, device=self.group.device)
-            self._lag_stream = torch.cuda.Stream(self.group.device)
-            self._lag_bounds = lag_bounds(self.group.layout)
-
-    def _lag_issue(self):
-        from ..ops import _hip
-        from ..ops.optim import BETA1, BETA2, EPS
-        self._lag_setup()
-        cur = torch.cuda.current_stream(self.group.device)
-        side = self._lag_stream
-        side.wait_stream(cur)
-        chunks = []
-        b = self._lag_bounds
-        with torch.cuda.stream(side):
-            for k in range(len(b) - 1):
-                _hip.adam_step(self.arena, BETA1, BETA2, EPS, self.group.l2, flag=self.lag_flag,
-                               i0=b[k], i1=b[k + 1], inc=(k == 0))
-                ev = torch.cuda.Event()
-                ev.record(side)
-                chunks.append((b[k], b[k + 1], ev))
-        self.arena.lag_begin(chunks)
-
-    def _lag_flush(self):
-        """Apply the pending update (if any) now and clear the flag."""
-        if self.lag_flag is None:
-            return
-        from ..ops import _hip
-        from ..ops.optim import BETA1, BETA2, EPS
-        _hip.adam_step(self.arena, BETA1, BETA2, EPS, self.group.l2, flag=self.lag_flag)
-        _hip.set_flag(self.lag_flag, 0)
-
     def _step_body(self):
         g = self.group
         gather_batch(g.store, True, self.part_of_row, self.cursor, g.batch_size, self.x, self.y)
-        lag = self._lag_on()
-        if lag:
-            self._lag_issue()
         # weight gradients are queued during backward and launched as a few
         # multi-layer kernels when the block exits (ops.streams); with >=
         # _SIDE_MIN_G packed configs the first half of them runs on the side
@@ -332,52 +272,15 @@ class _Working(object):
             streams.set_batch_rows(_WIDE_ROWS if self.G >= _SIDE_MIN_G else 0)
         with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self)):
             logits = self.net.forward(self.x, True)
-            self.arena.lag_wait_all()
             loss = softmax_ce(logits, self.y, self.acc, self.G)
             loss.sum().backward()
         streams.join()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)
-        if lag:
-            from ..ops import _hip
-            _hip.set_flag(self.lag_flag, 1)      # applied by the next step or the flush
-        else:
-            optimizer_step(self.arena, g.optimizer, l2=g.l2)
+        optimizer_step(self.arena, g.optimizer, l2=g.l2)
         self.cursor.add_(1)
 
     def train_steps(self, nsteps):
-        if self._lag_on():
-            self._lag_setup()            # outside any capture
-        main = self._main_stream()
-        if main is None:
-            try:
-                return self._train_steps(nsteps)
-            finally:
-                self._lag_flush()
-        cur = torch.cuda.current_stream(self.group.device)
-        main.wait_stream(cur)
-        try:
-            with torch.cuda.stream(main):
-                try:
-                    return self._train_steps(nsteps)
-                finally:
-                    self._lag_flush()
-        finally:
-            cur.wait_stream(main)
-
-    def _main_stream(self):
-        """CER_PRIO=1: the training step (eager, captured and replayed) runs on
-        a highest-priority stream, so the dispatcher serves its critical-path
-        kernels before the side streams' (batched wgrads, lagged Adam) when
-        CUs free up."""
-        if not _PRIO or self.group.device.type != "cuda":
-            return None
-        if getattr(self, "_prio_stream", None) is None:
-            lo, hi = torch.cuda.Stream.priority_range()
-            self._prio_stream = torch.cuda.Stream(self.group.device, priority=hi)
-        return self._prio_stream
-
-    def _train_steps(self, nsteps):
         done = 0
         streams.join()
         if not self.group.use_graphs or self.eager_only:
@@ -421,8 +324,7 @@ class _Working(object):
                 # thread-local capture: the asynchronous runtime's hop thread
                 # keeps issuing RCCL transfers / stream syncs while this
                 # thread captures
-                with torch.cuda.graph(self.graph, stream=self._main_stream(),
-                                      capture_error_mode="thread_local"):
+                with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                     self._step()
         gb = getattr(self.net, "grad_buckets", None)
         while done < nsteps:
@@ -530,28 +432,6 @@ _SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "4"))
 # wgrad-batch rows per split for those packs (fewer, longer splits: +1 % at
 # 8 configs; one-config packs keep 1024, where 2048 is 1-2.5 % slower)
 _WIDE_ROWS = int(os.environ.get("CER_WGB_ROWS_WIDE", "2048"))
-# lagged Adam under the next step's forward (_Working._lag_issue; CER_LAG=0
-# runs the update at the end of every step) and its chunk boundaries as
-# fractions of the arena (snapped to parameter starts): small chunks first,
-# since the first layers wait for them
-_LAG = os.environ.get("CER_LAG", "1") != "0"
-_LAG_FRACS = (1 / 64, 1 / 32, 1 / 16, 1 / 8, 1 / 4, 1 / 2)
-_PRIO = os.environ.get("CER_PRIO", "0") == "1"
-
-
-def lag_bounds(layout, fracs=_LAG_FRACS):
-    """Chunk boundaries [0, ..., n_train] of the lagged update: the first
-    parameter start at or past each fraction of the trainable arena."""
-    n = layout.n_train
-    starts = sorted(s.offset for s in layout.train_specs)
-    bounds = [0]
-    for frac in fracs:
-        b = next((o for o in starts if o >= frac * n), n)
-        if b > bounds[-1]:
-            bounds.append(b)
-    if bounds[-1] != n:
-        bounds.append(n)
-    return bounds
 
 # Graph-captured validation (CER_VALID_GRAPH=0 runs it eagerly).  Its round-1
 # failures (invalid eval losses after an epoch boundary) had the same root

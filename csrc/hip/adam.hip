@@ -13,18 +13,9 @@
 // without a memset per layer.
 #include "common.h"
 
-// ``flag`` (optional, device int): the update runs only while *flag != 0 --
-// the lagged update of the previous step's gradient issued at the start of
-// a captured step (cer_adam_step_ex) is a no-op on the first step of a run
-__global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G,
-                              const int* flag) {
+__global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (flag && *flag == 0) return;
   if (g < G) state[g * row_stride + off_step] += 1.0f;
-}
-
-__global__ void set_flag_kernel(int* flag, int v) {
-  if (threadIdx.x == 0) *flag = v;
 }
 
 // WRITE_BF16: also write the bf16 compute shadow of the params (bf16 mode);
@@ -34,12 +25,10 @@ __global__ __launch_bounds__(256) void adam_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
-    const float* __restrict__ wd, float b1, float b2, float eps, int l2, const int* flag,
-    int64_t i0) {
+    const float* __restrict__ wd, float b1, float b2, float eps, int l2) {
   const int g = blockIdx.y;
-  const int64_t i = i0 + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (i >= n_train) return;
-  if (flag && *flag == 0) return;
   float* row = state + g * row_stride;
   const float t = row[off_step];
   const float bc1 = 1.f - __powf(b1, t);
@@ -83,46 +72,22 @@ __global__ __launch_bounds__(256) void adam_kernel(
   }
 }
 
-// Adam over parameters [i0, i1) of every row (i1 <= n_train, both % 8 == 0);
-// ``inc``: advance the step counters first (once per update: the chunked
-// launches of one update pass inc only on the first); ``flag``: see
-// adam_inc_step (nullptr = always)
-CER_API int cer_adam_step_ex(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
-                             int64_t off_v, int64_t off_step, float* grad, int64_t grad_stride,
-                             int zero_grad, bf16_t* work, int64_t work_stride, const float* lr,
-                             const float* wd, int G, float b1, float b2, float eps, int l2,
-                             const int* flag, int64_t i0, int64_t i1, int inc,
-                             hipStream_t stream) {
-  if (n_train % 8 != 0 || i0 % 8 != 0 || i1 % 8 != 0 || i0 < 0 || i1 > n_train || i1 < i0)
-    return (int)hipErrorInvalidValue;
-  if (inc) adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G, flag);
-  if (i1 == i0) return (int)hipGetLastError();
-  dim3 grid(cer_blocks((i1 - i0) / 8, 256), G);
-  if (work)
-    adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, i1, off_m, off_v, off_step,
-                                                 grad, grad_stride, zero_grad, work, work_stride,
-                                                 lr, wd, b1, b2, eps, l2, flag, i0);
-  else
-    adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, i1, off_m, off_v, off_step,
-                                                  grad, grad_stride, zero_grad, nullptr, 0, lr, wd,
-                                                  b1, b2, eps, l2, flag, i0);
-  return (int)hipGetLastError();
-}
-
 CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int64_t off_m,
                           int64_t off_v, int64_t off_step, float* grad, int64_t grad_stride,
                           int zero_grad, bf16_t* work, int64_t work_stride, const float* lr,
                           const float* wd, int G, float b1, float b2, float eps, int l2,
                           hipStream_t stream) {
-  return cer_adam_step_ex(state, row_stride, n_train, off_m, off_v, off_step, grad, grad_stride,
-                          zero_grad, work, work_stride, lr, wd, G, b1, b2, eps, l2, nullptr, 0,
-                          n_train, 1, stream);
-}
-
-// *flag = v on the stream (a kernel, not a memset: captured memset nodes
-// misbehave on replay, runtime/group.py)
-CER_API int cer_set_flag(int* flag, int v, hipStream_t stream) {
-  set_flag_kernel<<<1, 64, 0, stream>>>(flag, v);
+  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  dim3 grid(cer_blocks(n_train / 8, 256), G);
+  if (work)
+    adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
+                                                 off_step, grad, grad_stride, zero_grad, work,
+                                                 work_stride, lr, wd, b1, b2, eps, l2);
+  else
+    adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
+                                                  off_step, grad, grad_stride, zero_grad, nullptr,
+                                                  0, lr, wd, b1, b2, eps, l2);
   return (int)hipGetLastError();
 }
 
@@ -179,7 +144,7 @@ CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int6
                          bf16_t* work, int64_t work_stride, const float* lr, const float* wd,
                          int G, float momentum, int l2, hipStream_t stream) {
   if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
-  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G, nullptr);
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
   if (work)
     sgd_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step, grad,

@@ -1,0 +1,78 @@
+"""ResNet projection shortcuts on the branch stream (models/resnet.py
+``CER_SC_BRANCH``): forward fork / join around the shortcut conv + BN, its
+backward on the branch stream, the GradJoin hand-off between the streams
+(event-ordered), and a per-stream split-K workspace.  A packed ResNet-50
+trained through the engine (HIP graphs) with the branch lands as close to
+the single-stream run as two single-stream runs land to each other."""
+
+import pytest
+import torch
+
+from cerebro_ds_kpgi_amd.models import resnet as resnet_mod
+from cerebro_ds_kpgi_amd.ops import backend
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _hip_backend():
+    backend.set_backend("hip")
+    backend.force_torch_ops([])
+    backend.take_fallbacks()
+    yield
+    assert not backend.take_fallbacks(), "an op fell back to the PyTorch path"
+
+
+def test_gradjoin_orders_the_parked_gradient_across_streams():
+    from cerebro_ds_kpgi_amd.ops import nn as P
+    j = P.GradJoin()
+    s = torch.cuda.Stream()
+    a = torch.zeros(1 << 20, device="cuda")
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(2_000_000)          # the parking stream is slow
+        g = a + 1.0
+        assert j.join(g) is None
+    got = j.join(torch.ones_like(a))          # second arrival on the main stream
+    out = got * 2.0
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.full_like(a, 2.0))
+
+
+@pytest.mark.parametrize("configs", [1, 2])
+def test_resnet50_training_with_and_without_branch(monkeypatch, configs):
+    from cerebro_ds_kpgi_amd.ops import _hip
+    from cerebro_ds_kpgi_amd.parallel import init_distributed
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    bs, steps = 4, 6
+    msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": bs, "model": "resnet50"}
+            for lr in (1e-3, 1e-4)][:configs]
+    states = []
+    for on in (False, False, True):
+        monkeypatch.setattr(resnet_mod, "_SC_BRANCH", on)
+        _hip.conv_set_variant(0, 0)
+        _hip.conv_set_variant(1, 0)
+        try:
+            eng = MOPEngine(msts, init_distributed(), EngineOptions(
+                n_train=16 * bs, n_valid=2 * bs, slots_per_gpu=configs, verbose=False,
+                ckpt_every="none", compute_dtype="fp32", shuffle=False))
+            eng.sched.start_epoch(1)
+            eng.store.new_epoch(1)
+            eng._hop_and_load(eng.sched.next_round())
+            w = list(eng.groups.values())[0].current
+            w.prepare(True)
+            w.train_steps(steps)
+            torch.cuda.synchronize()
+            assert w.graph is not None
+            states.append(w.arena.state.clone())
+            eng.close()
+        finally:
+            _hip.conv_set_variant(0, -1)
+            _hip.conv_set_variant(1, -1)
+    assert all(torch.isfinite(s).all() for s in states)
+
+    def dist(a, b):
+        na, nb = a.double().norm(dim=1), b.double().norm(dim=1)
+        return ((na - nb).abs() / na).max().item()
+    noise, br = dist(states[0], states[1]), dist(states[0], states[2])
+    print("per-config norm rel diff: plain vs plain %.2e, plain vs branch %.2e" % (noise, br))
+    assert br <= max(4 * noise, 1e-5), (br, noise)

@@ -117,12 +117,13 @@ def test_ctq_hyperopt_batches(tmp_path):
 
 
 @pytest.mark.parametrize("engine", ["ma", "ddp", "task"])
-def test_baseline_engines_train(engine):
+def test_baseline_engines_train(engine, tmp_path):
     from cerebro_ds_kpgi_amd.runtime.baselines import DDPEngine, MAEngine
     from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    # logs_root: the run manifest is written too (task parallel once failed there)
     o = EngineOptions(n_train=64, n_valid=16, compute_dtype="fp32", verbose=False,
                       ckpt_every="none", scheduler="task" if engine == "task" else "rotation",
-                      partitions=2)
+                      partitions=2, logs_root=str(tmp_path))
     cls = {"ma": MAEngine, "ddp": DDPEngine, "task": MOPEngine}[engine]
     eng = cls(_tiny(2), _ctx(), o)
     eng.run(3)
