@@ -39,7 +39,7 @@ from ..ops.backend import get_backend
 # conv + BN of a stage's first block runs concurrently with the main path's
 # c1 / c2 in forward and, being created after c1, its backward runs ahead of
 # c1's (autograd's order) on the branch stream, beside c2 / c1's backward
-_SC_BRANCH = os.environ.get("CER_SC_BRANCH", "0") == "1"
+_SC_BRANCH = os.environ.get("CER_SC_BRANCH", "1") == "1"
 
 _BOTTLENECK = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 _BASIC = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}
