@@ -574,77 +574,43 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ part, int nsl
 
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
-// CER_BNF_V (A/B twins, tools.build --variant): 1 = the loads that do not
-// depend on the statistics (gamma, beta, the running statistics) are issued
-// before the fold's barrier; 0 = after it; 2 = as 1 without the statistic
-// writes (timing only: wrong running statistics)
-#ifndef CER_BNF_V
-#define CER_BNF_V 1
-#endif
-
 template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
-    const float* __restrict__ part, int nslab, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ rmean, float* __restrict__ rvar,
-    int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
+    const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
+    float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
     const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
     int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  const int cs = c0 < C ? c0 : 0;          // in-range channel for the early loads
-  const int g = cs / Cper, cc = cs - g * Cper;
-  const bool wst = blockIdx.y == 0 && tr == 0 && c0 < C;   // one writer per channel
-  float ga[VEC], be[VEC], rm0[VEC], rv0[VEC];
-#if CER_BNF_V >= 1
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
-  ld8((const T*)beta.p + g * beta.stride + cc, be);
-  if (wst) {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      rm0[i] = rmean[g * rstat_stride + cc + i];
-      rv0[i] = rvar[g * rstat_stride + cc + i];
-    }
-  }
-#endif
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
   if (c0 >= C) return;
-#if CER_BNF_V == 0
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
-  ld8((const T*)beta.p + g * beta.stride + cc, be);
-  if (wst) {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      rm0[i] = rmean[g * rstat_stride + cc + i];
-      rv0[i] = rvar[g * rstat_stride + cc + i];
-    }
-  }
-#endif
   const float inv_m = 1.f / (float)M;
-  float mu[VEC], is[VEC], var[VEC], sc[VEC], sh[VEC];
+  float mu[VEC], is[VEC], var[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     mu[i] = a[i] * inv_m;
     var[i] = fmaxf(b[i] * inv_m - mu[i] * mu[i], 0.f);
     is[i] = rsqrtf(var[i] + eps);
-    sc[i] = is[i] * ga[i];                 // bitwise bn_scale_shift
-    sh[i] = be[i] - mu[i] * sc[i];
   }
-#if CER_BNF_V != 2
-  if (wst) {
+  const int g = c0 / Cper, cc = c0 - g * Cper;
+  if (blockIdx.y == 0 && tr == 0) {          // one writer per channel
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       mean_out[c0 + i] = mu[i];
       invstd_out[c0 + i] = is[i];
+      float* rm = rmean + g * rstat_stride + cc + i;
+      float* rv = rvar + g * rstat_stride + cc + i;
       const float unb = M > 1 ? var[i] * (float)M / (float)(M - 1) : var[i];
-      rmean[g * rstat_stride + cc + i] = (1.f - momentum) * rm0[i] + momentum * mu[i];
-      rvar[g * rstat_stride + cc + i] = (1.f - momentum) * rv0[i] + momentum * unb;
+      *rm = (1.f - momentum) * *rm + momentum * mu[i];
+      *rv = (1.f - momentum) * *rv + momentum * unb;
     }
   }
-#endif
+  float sc[VEC], sh[VEC];
+  bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;
