@@ -231,8 +231,15 @@ def conv2d_bias_act(x, wref, bref, stride=1, pad=0, act=1, anchor=None):
 # ---------------------------------------------------------------------------
 
 def _bn_hip(x, gref):
-    """HIP BN kernels move 8 channels per thread: per-config channels % 8 == 0."""
-    return hip_gate("bn", gref.spec.shape[0] % 8 == 0, x)
+    """HIP BN kernels: 8 channels per thread when every config's channel count
+    is a multiple of 8, one otherwise (ragged widths: NASNet-Mobile's 11 / 22
+    / 44 filters) -- every width runs on HIP."""
+    return hip_gate("bn", True, x)
+
+
+def _bn_aligned(gref):
+    """8-aligned widths: the conv-epilogue BN statistics and BN links apply."""
+    return gref.spec.shape[0] % 8 == 0
 
 
 def _flat_param(ref):
@@ -321,7 +328,7 @@ class PackedConvBNAct(torch.autograd.Function):
             z = _conv_forward(x, wref, stride, pad)
             y, mean, invstd = _bn_forward_train(z, residual, gref, bref, rmref, rvref, relu,
                                                 momentum, eps)
-        if link is not None and _bn_hip(z, gref):
+        if link is not None and _bn_hip(z, gref) and _bn_aligned(gref):
             link.z, link.mean, link.invstd = z, mean, invstd
             link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
         ctx.save_for_backward(x, z, y, mean, invstd)
@@ -486,7 +493,7 @@ class MaxPoolHip(torch.autograd.Function):
 
 
 def maxpool2d(x, k, s, p=0):
-    if hip_gate("pool", x.shape[-1] % 8 == 0, x):
+    if hip_gate("pool", True, x):
         return MaxPoolHip.apply(x, k, s, p)
     return _nhwc(F.max_pool2d(_nchw(x), k, s, p))
 
@@ -504,7 +511,7 @@ class GlobalAvgPoolHip(torch.autograd.Function):
 
 def global_avgpool(x):
     """[B, H, W, C] -> [B, C]."""
-    if hip_gate("pool", x.shape[-1] % 8 == 0, x):
+    if hip_gate("pool", True, x):
         return GlobalAvgPoolHip.apply(x)
     return x.float().mean(dim=(1, 2)).to(x.dtype)
 
@@ -654,7 +661,7 @@ class PackedDWConv2d(torch.autograd.Function):
     def forward(ctx, x, anchor, wref, stride, pad):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         C, kh, kw = wref.spec.shape
-        ctx.hip = hip_gate("dwconv", C % 8 == 0 and kh == kw and kh in (3, 5, 7)
+        ctx.hip = hip_gate("dwconv", kh == kw and kh in (3, 5, 7)
                            and stride in (1, 2) and max(_pad4(pad)) < kh, x)
         if ctx.hip:
             y = _hip().dwconv_fwd(x, wref, stride, pad)
@@ -765,7 +772,7 @@ class AvgPoolHip(torch.autograd.Function):
 def avgpool2d(x, k, s, p=0, count_include_pad=False):
     """Per-channel k x k / s average pooling with symmetric zero padding ``p``;
     count_include_pad=False divides by the in-bounds taps (Keras/TF 'same')."""
-    if hip_gate("pool", x.shape[-1] % 8 == 0 and p < k, x):
+    if hip_gate("pool", p < k, x):
         return AvgPoolHip.apply(x, k, s, p, count_include_pad)
     # contiguous NCHW: PyTorch-ROCm's avg_pool2d backward on a channels-last
     # view with padding and count_include_pad=False returns wrong gradients

@@ -46,10 +46,14 @@ struct Map {
   int tc_n, tr_n, cb;  // threads along channels, row lanes, channels per block
 };
 
-static Map make_map(int C) {
-  int tc = (C / VEC) < 32 ? (C / VEC) : 32;
+// V channels per thread (VEC, or 1 for ragged channel counts).  tc_n need
+// not divide BN_T: the BN_T % tc_n surplus threads (tr == tr_n) are idle in
+// every kernel
+static Map make_map(int C, int V = VEC) {
+  const int cap = V == 1 ? 64 : 32;
+  int tc = (C / V) < cap ? (C / V) : cap;
   if (tc < 1) tc = 1;
-  return Map{tc, BN_T / tc, tc * VEC};
+  return Map{tc, BN_T / tc, tc * V};
 }
 
 // grid (channel blocks, row slabs) with ~`target` blocks and >= min_rows rows per slab
@@ -87,15 +91,15 @@ __device__ __forceinline__ void stf(float* p, float v) {
 constexpr int YM_NONE = 0, YM_Y = 1, YM_Z = 2;
 
 // forward scale / shift of 8 channels (bitwise the apply_fwd_tile values)
-template <typename T>
+template <typename T, int V = VEC>
 __device__ __forceinline__ void bn_scale_shift(const Strided& gamma, const Strided& beta, int g,
                                                int cc, const float* mu, const float* is,
                                                float* sc, float* sh) {
   float ga[VEC], be[VEC];
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
-  ld8((const T*)beta.p + g * beta.stride + cc, be);
+  ldv<V>((const T*)gamma.p + g * gamma.stride + cc, ga);
+  ldv<V>((const T*)beta.p + g * beta.stride + cc, be);
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
+  for (int i = 0; i < V; ++i) {
     sc[i] = is[i] * ga[i];
     sh[i] = be[i] - mu[i] * sc[i];
   }
@@ -110,7 +114,7 @@ __device__ __forceinline__ float dz_of(float d, float yv, float xv, float sc, fl
 }
 
 // one (channel block cbk, row slab) tile; `red` = 2*BN_T*VEC floats of LDS
-template <typename T, int MODE, bool SC, int YM = YM_Y>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
+template <typename T, int MODE, bool SC, int YM = YM_Y, int V = VEC>  // MODE 0: (sum x, sum x^2)   1: (sum dz, sum dz*xhat)
 __device__ __forceinline__ void partials_tile(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
@@ -118,19 +122,19 @@ __device__ __forceinline__ void partials_tile(
     const Strided& gamma = Strided{nullptr, 0}, const Strided& beta = Strided{nullptr, 0},
     int Cper = 1) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = cbk * mp.cb + tc * VEC;
-  const bool cok = c0 < C;
+  const int c0 = cbk * mp.cb + tc * V;
+  const bool cok = c0 < C && tr < mp.tr_n;
   float s[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, q[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
   float mu[VEC], is[VEC], sc[VEC], sh[VEC];
   if (MODE == 1 && cok) {
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) {
+    for (int i = 0; i < V; ++i) {
       mu[i] = mean[c0 + i];
       is[i] = invstd[c0 + i];
     }
     if (YM == YM_Z) {
       const int g = c0 / Cper;
-      bn_scale_shift<T>(gamma, beta, g, c0 - g * Cper, mu, is, sc, sh);
+      bn_scale_shift<T, V>(gamma, beta, g, c0 - g * Cper, mu, is, sc, sh);
     }
   }
   const int64_t r0 = (int64_t)slab * rows_per_slab;
@@ -147,10 +151,10 @@ __device__ __forceinline__ void partials_tile(
         const int64_t rr = r + (int64_t)u * mp.tr_n;
         ok[u] = rr < r1;
         if (ok[u]) {
-          ld8(x + rr * C + c0, v[u]);
+          ldv<V>(x + rr * C + c0, v[u]);
           if (MODE == 1) {
-            ld8(dy + rr * C + c0, d[u]);
-            if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
+            ldv<V>(dy + rr * C + c0, d[u]);
+            if (YM == YM_Y) ldv<V>(y + rr * C + c0, yv[u]);
           }
         }
       }
@@ -159,13 +163,13 @@ __device__ __forceinline__ void partials_tile(
         if (!ok[u]) continue;
         if (MODE == 0) {
 #pragma unroll
-          for (int i = 0; i < VEC; ++i) {
+          for (int i = 0; i < V; ++i) {
             s[i] += v[u][i];
             q[i] += v[u][i] * v[u][i];
           }
         } else {
 #pragma unroll
-          for (int i = 0; i < VEC; ++i) {
+          for (int i = 0; i < V; ++i) {
             const float dz = dz_of<YM>(d[u][i], yv[u][i], v[u][i], sc[i], sh[i], act);
             s[i] += dz;
             q[i] += dz * (v[u][i] - mu[i]) * is[i];
@@ -176,10 +180,12 @@ __device__ __forceinline__ void partials_tile(
   }
   float* rs = red;
   float* rq = red + BN_T * VEC;
+  if (tr < mp.tr_n) {
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    rs[tr * mp.cb + tc * VEC + i] = s[i];
-    rq[tr * mp.cb + tc * VEC + i] = q[i];
+    for (int i = 0; i < V; ++i) {
+      rs[tr * mp.cb + tc * V + i] = s[i];
+      rq[tr * mp.cb + tc * V + i] = q[i];
+    }
   }
   __syncthreads();
   for (int cl = threadIdx.x; cl < mp.cb; cl += BN_T) {
@@ -197,14 +203,14 @@ __device__ __forceinline__ void partials_tile(
   __syncthreads();  // `red` is reused by the next tile of a cooperative block
 }
 
-template <typename T, int MODE, int YM = YM_Y>
+template <typename T, int MODE, int YM = YM_Y, int V = VEC>
 __global__ __launch_bounds__(BN_T) void bn_partials(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
     int64_t M, int C, int rows_per_slab, int act, Map mp, Strided gamma = Strided{nullptr, 0},
     Strided beta = Strided{nullptr, 0}, int Cper = 1) {
   __shared__ float red[2 * BN_T * VEC];
-  partials_tile<T, MODE, false, YM>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
+  partials_tile<T, MODE, false, YM, V>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
                                  blockIdx.x, blockIdx.y, red, gamma, beta, Cper);
 }
 
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(FIN_C * FIN_L) void bn_finalize_bwd(
 // stage 3: elementwise apply (scale/shift per channel computed once per thread)
 // ---------------------------------------------------------------------------
 // MODE 0: train fwd, ws = (mean, invstd); MODE 1: eval fwd from running stats
-template <typename T, int MODE, bool SC, int AU = 2>   // AU: rows in flight per thread
+template <typename T, int MODE, bool SC, int AU = 2, int V = VEC>   // AU: rows in flight per thread
 __device__ __forceinline__ void apply_fwd_tile(
     const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
@@ -335,12 +341,12 @@ __device__ __forceinline__ void apply_fwd_tile(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = cbk * mp.cb + tc * VEC;
-  if (c0 >= C) return;
+  const int c0 = cbk * mp.cb + tc * V;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   float mu[VEC], is[VEC], sc[VEC], sh[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
+  for (int i = 0; i < V; ++i) {
     if (MODE == 0) {
       mu[i] = ldf<SC>(ws + c0 + i);
       is[i] = ldf<SC>(ws + C + c0 + i);
@@ -349,7 +355,7 @@ __device__ __forceinline__ void apply_fwd_tile(
       is[i] = rsqrtf(rvar[g * rstat_stride + cc + i] + eps);
     }
   }
-  bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
+  bn_scale_shift<T, V>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -358,8 +364,8 @@ __device__ __forceinline__ void apply_fwd_tile(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        ld8(x + rr * C + c0, v[u]);
-        if (res) ld8(res + rr * C + c0, rv[u]);
+        ldv<V>(x + rr * C + c0, v[u]);
+        if (res) ldv<V>(res + rr * C + c0, rv[u]);
       }
     }
 #pragma unroll
@@ -368,27 +374,31 @@ __device__ __forceinline__ void apply_fwd_tile(
       if (rr >= r1) continue;
       float o[VEC];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i)
+      for (int i = 0; i < V; ++i)
         o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
-      if (hl)
-        st8_hl(y + rr * C + c0, o);
-      else
-        st8(y + rr * C + c0, o);
+      if constexpr (V == VEC) {
+        if (hl)
+          st8_hl(y + rr * C + c0, o);
+        else
+          st8(y + rr * C + c0, o);
+      } else {
+        stv<V>(y + rr * C + c0, o);       // ragged widths: never HL (host-gated)
+      }
     }
   }
 }
 
-template <typename T, int MODE, int AU = 2>
+template <typename T, int MODE, int AU = 2, int V = VEC>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
     const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
     Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
-  apply_fwd_tile<T, MODE, false, AU>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
+  apply_fwd_tile<T, MODE, false, AU, V>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
                               Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
 }
 
-template <typename T, bool SC, int YM = YM_Y, int AU = 2>
+template <typename T, bool SC, int YM = YM_Y, int AU = 2, int V = VEC>
 __device__ __forceinline__ void apply_bwd_tile(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
@@ -398,21 +408,21 @@ __device__ __forceinline__ void apply_bwd_tile(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = cbk * mp.cb + tc * VEC;
-  if (c0 >= C) return;
+  const int c0 = cbk * mp.cb + tc * V;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
+  ldv<V>((const T*)gamma.p + g * gamma.stride + cc, ga);
   const float inv_m = 1.f / (float)M;
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
+  for (int i = 0; i < V; ++i) {
     mu[i] = mean[c0 + i];
     is[i] = invstd[c0 + i];
     k1[i] = ga[i] * is[i];
     k2[i] = ldf<SC>(ws + C + c0 + i) * inv_m;
     sdz[i] = ldf<SC>(ws + c0 + i) * inv_m;
   }
-  if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
+  if (YM == YM_Z) bn_scale_shift<T, V>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)slab * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
@@ -421,9 +431,9 @@ __device__ __forceinline__ void apply_bwd_tile(
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
       if (rr < r1) {
-        ld8(dy + rr * C + c0, d[u]);
-        ld8(x + rr * C + c0, xv[u]);
-        if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
+        ldv<V>(dy + rr * C + c0, d[u]);
+        ldv<V>(x + rr * C + c0, xv[u]);
+        if (YM == YM_Y) ldv<V>(y + rr * C + c0, yv[u]);
       }
     }
 #pragma unroll
@@ -432,27 +442,31 @@ __device__ __forceinline__ void apply_bwd_tile(
       if (rr >= r1) continue;
       float o[VEC], dz[VEC];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
+      for (int i = 0; i < V; ++i) {
         dz[i] = dz_of<YM>(d[u][i], yv[u][i], xv[u][i], sc[i], sh[i], act);
         const float xh = (xv[u][i] - mu[i]) * is[i];
         o[i] = k1[i] * (dz[i] - sdz[i] - xh * k2[i]);
       }
-      if (hl)
-        st8_hl(dx + rr * C + c0, o);
-      else
-        st8(dx + rr * C + c0, o);
-      if (dres) st8(dres + rr * C + c0, dz);
+      if constexpr (V == VEC) {
+        if (hl)
+          st8_hl(dx + rr * C + c0, o);
+        else
+          st8(dx + rr * C + c0, o);
+      } else {
+        stv<V>(dx + rr * C + c0, o);      // ragged widths: never HL (host-gated)
+      }
+      if (dres) stv<V>(dres + rr * C + c0, dz);
     }
   }
 }
 
-template <typename T, int YM, int AU = 2>
+template <typename T, int YM, int AU = 2, int V = VEC>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ ws,
     Strided gamma, T* __restrict__ dx, T* __restrict__ dres, int64_t M, int C,
     int Cper, int rows_per_slab, int act, Map mp, Strided beta) {
-  apply_bwd_tile<T, false, YM, AU>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
+  apply_bwd_tile<T, false, YM, AU, V>(dy, x, y, mean, invstd, ws, gamma, dx, dres, M, C, Cper,
                             rows_per_slab, act, mp, blockIdx.x, blockIdx.y, beta);
 }
 
@@ -473,7 +487,7 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   float a[VEC] = {0, 0, 0, 0, 0, 0, 0, 0}, b[VEC] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (c0 < C) {
+  if (c0 < C && tr < mp.tr_n) {
     // FU slabs' loads issued before any add (the partials were just written
     // by other CUs: each load is an L2/MALL round trip)
     constexpr int FU = 4;
@@ -501,10 +515,12 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   }
   float* rs = red;
   float* rq = red + BN_T * VEC;
+  if (tr < mp.tr_n) {
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    rs[tr * mp.cb + tc * VEC + i] = a[i];
-    rq[tr * mp.cb + tc * VEC + i] = b[i];
+    for (int i = 0; i < VEC; ++i) {
+      rs[tr * mp.cb + tc * VEC + i] = a[i];
+      rq[tr * mp.cb + tc * VEC + i] = b[i];
+    }
   }
   __syncthreads();
   float* fin = red + 2 * BN_T * VEC;          // [2][cb]
@@ -587,7 +603,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  if (c0 >= C) return;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const float inv_m = 1.f / (float)M;
   float mu[VEC], is[VEC], var[VEC];
 #pragma unroll
@@ -654,7 +670,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  if (c0 >= C) return;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   if (blockIdx.y == 0 && tr == 0) {
 #pragma unroll
@@ -768,11 +784,80 @@ int bn_mask_mode(int act, int has_res) {
 
 // floats of scratch the partials need (part[slabs][2][C])
 CER_API int64_t cer_bn_part_floats(int64_t M, int C) {
-  Map mp = make_map(C);
-  dim3 g;
-  int rows;
-  make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &g, &rows);
-  return (int64_t)g.y * 2 * C;
+  int64_t n = 0;
+  for (int V : {VEC, 1}) {            // aligned and ragged (V = 1) grids
+    const Map mp = make_map(C, V);
+    dim3 g;
+    int rows;
+    make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &g, &rows);
+    n = n > (int64_t)g.y * 2 * C ? n : (int64_t)g.y * 2 * C;
+  }
+  return n;
+}
+
+// ---- ragged channel counts (C or Cper not a multiple of 8): one channel per
+// thread (V = 1), statistics by partials -> finalize -> apply, no fold, no
+// HL output (NASNet-Mobile's 11 / 22 / 44-filter layers; ops.nn gates HL on
+// 8-aligned widths only)
+template <typename T>
+static int bn_fwd_train_ragged(const T* x, const T* res, T* y, const T* gamma,
+                               int64_t gamma_stride, const T* beta, int64_t beta_stride,
+                               float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
+                               float* invstd_out, float* ws, float* part, int64_t M, int C,
+                               int Cper, float eps, float momentum, int act, hipStream_t stream) {
+  if (act >> 8) return (int)hipErrorInvalidValue;         // HL output needs 8-aligned widths
+  const Map mp = make_map(C, 1);
+  dim3 rg, ag;
+  int rrows, arows;
+  make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
+  make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
+  bn_partials<T, 0, YM_Y, 1><<<rg, BN_T, 0, stream>>>(x, nullptr, nullptr, nullptr, nullptr,
+                                                      part, M, C, rrows, 0, mp);
+  bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(
+      part, (int)rg.y, ws, mean_out, invstd_out, rmean, rvar, rstat_stride, M, C, Cper, eps,
+      momentum);
+  bn_apply_fwd<T, 0, 2, 1><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                                    Strided{gamma, gamma_stride},
+                                                    Strided{beta, beta_stride}, M, C, Cper,
+                                                    arows, act, mp);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static int bn_bwd_ragged(const T* dy, const T* x, const T* y, const float* mean,
+                         const float* invstd, const T* gamma, int64_t gamma_stride,
+                         const T* beta, int64_t beta_stride, float* dgamma, float* dbeta,
+                         int64_t grad_stride, T* dx, T* dres, float* ws, float* part, int64_t M,
+                         int C, int Cper, int act, hipStream_t stream) {
+  if (act >> 8) return (int)hipErrorInvalidValue;
+  const Map mp = make_map(C, 1);
+  dim3 rg, ag;
+  int rrows, arows;
+  make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
+  make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
+  const int ym = bn_mask_mode(act, dres != nullptr);
+  const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
+  if (ym == YM_NONE)
+    bn_partials<T, 1, YM_NONE, 1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
+                                                          rrows, act, mp, gs, bs, Cper);
+  else if (ym == YM_Z)
+    bn_partials<T, 1, YM_Z, 1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
+                                                       rrows, act, mp, gs, bs, Cper);
+  else
+    bn_partials<T, 1, YM_Y, 1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
+                                                       rrows, act, mp, gs, bs, Cper);
+  bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, (int)rg.y, ws, dgamma,
+                                                                    dbeta, grad_stride, C, Cper);
+  if (ym == YM_NONE)
+    bn_apply_bwd<T, YM_NONE, 2, 1><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx,
+                                                           dres, M, C, Cper, arows, act, mp, bs);
+  else if (ym == YM_Z)
+    bn_apply_bwd<T, YM_Z, 2, 1><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres,
+                                                        M, C, Cper, arows, act, mp, bs);
+  else
+    bn_apply_bwd<T, YM_Y, 2, 1><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres,
+                                                        M, C, Cper, arows, act, mp, bs);
+  return (int)hipGetLastError();
 }
 
 template <typename T>
@@ -783,7 +868,12 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                              int C, int Cper, float eps, float momentum, int act,
                              hipStream_t stream) {
   const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
-  if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
+  if (C % VEC || Cper % VEC) {
+    if (nslab > 0) return (int)hipErrorInvalidValue;    // conv-epilogue partials: aligned only
+    return bn_fwd_train_ragged(x, res, y, gamma, gamma_stride, beta, beta_stride, rmean, rvar,
+                               rstat_stride, mean_out, invstd_out, ws, part, M, C, Cper, eps,
+                               momentum, act_k, stream);
+  }
   const Map mp = make_map(C);
   dim3 rg, ag;
   int rrows, arows;
@@ -878,14 +968,22 @@ static int cer_bn_fwd_eval_t(const T* x, const T* res, T* y, const T* gamma,
                             int64_t gamma_stride, const T* beta, int64_t beta_stride,
                             const float* rmean, const float* rvar, int64_t rstat_stride,
                             int64_t M, int C, int Cper, float eps, int act, hipStream_t stream) {
-  if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
-  const Map mp = make_map(C);
+  const bool rag = (C % VEC) || (Cper % VEC);
+  const Map mp = make_map(C, rag ? 1 : VEC);
   dim3 ag;
   int arows;
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  bn_apply_fwd<T, 1><<<ag, BN_T, 0, stream>>>(x, res, y, nullptr, rmean, rvar, rstat_stride, eps,
-                                           Strided{gamma, gamma_stride},
-                                           Strided{beta, beta_stride}, M, C, Cper, arows, act, mp);
+  if (rag)
+    bn_apply_fwd<T, 1, 2, 1><<<ag, BN_T, 0, stream>>>(x, res, y, nullptr, rmean, rvar,
+                                                      rstat_stride, eps,
+                                                      Strided{gamma, gamma_stride},
+                                                      Strided{beta, beta_stride}, M, C, Cper,
+                                                      arows, act, mp);
+  else
+    bn_apply_fwd<T, 1><<<ag, BN_T, 0, stream>>>(x, res, y, nullptr, rmean, rvar, rstat_stride,
+                                             eps, Strided{gamma, gamma_stride},
+                                             Strided{beta, beta_stride}, M, C, Cper, arows, act,
+                                             mp);
   return (int)hipGetLastError();
 }
 
@@ -898,7 +996,11 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
                        int64_t grad_stride, T* dx, T* dres, float* ws, float* part,
                        int pre_nslab, int64_t M, int C, int Cper, int act, hipStream_t stream) {
   const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
-  if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
+  if (C % VEC || Cper % VEC) {
+    if (pre_nslab > 0) return (int)hipErrorInvalidValue;  // dgrad-epilogue partials: aligned only
+    return bn_bwd_ragged(dy, x, y, mean, invstd, gamma, gamma_stride, beta, beta_stride, dgamma,
+                         dbeta, grad_stride, dx, dres, ws, part, M, C, Cper, act_k, stream);
+  }
   const Map mp = make_map(C);
   dim3 rg, ag;
   int rrows, arows;

@@ -96,6 +96,30 @@ __device__ __forceinline__ float ld1(const float* p) { return *p; }
 __device__ __forceinline__ void st1(bf16_t* p, float v) { *p = f2bf(v); }
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 
+// V consecutive elements (V = 8: ld8 / st8; V = 1: one element) -- the
+// vector width of the per-channel kernels (BN, pooling, depthwise conv):
+// 8 when every config's channel count is a multiple of 8, else 1 (ragged
+// widths such as NASNet-Mobile's 11 / 22 / 44 filters)
+template <int V, typename T>
+__device__ __forceinline__ void ldv(const T* p, float* v) {
+  if constexpr (V == 8) {
+    ld8(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = ld1(p + i);
+  }
+}
+
+template <int V, typename T>
+__device__ __forceinline__ void stv(T* p, const float* v) {
+  if constexpr (V == 8) {
+    st8(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) st1(p + i, v[i]);
+  }
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1,6 +1,7 @@
 // Pooling + bias/activation elementwise kernels on packed NHWC (SURVEY.md
-// K10, K15).  All kernels move 8 channels per thread (16 B in bf16, 32 B in fp32);
-// every op has a bf16 and an _f32 entry point.
+// K10, K15).  All kernels move 8 channels per thread (16 B in bf16, 32 B in fp32),
+// or 1 when the channel count is not a multiple of 8 (ragged widths, e.g.
+// NASNet-Mobile's); every op has a bf16 and an _f32 entry point.
 //
 // maxpool fwd stores the argmax window offset (uint8) per output element;
 // maxpool bwd is a deterministic *gather* (each input pixel sums the
@@ -9,26 +10,26 @@
 
 constexpr int PT = 256;
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x,
                                                          T* __restrict__ y,
                                                          uint8_t* __restrict__ arg, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   const int64_t total = (int64_t)B * Ho * Wo * cv;
   if (t >= total) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   int64_t pix = t / cv;
   const int wo = (int)(pix % Wo);
   pix /= Wo;
   const int ho = (int)(pix % Ho);
   const int b = (int)(pix / Ho);
-  float best[8];
-  uint8_t bi[8];
+  float best[V];
+  uint8_t bi[V];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < V; ++i) {
     best[i] = -INFINITY;
     bi[i] = 0;
   }
@@ -38,10 +39,10 @@ __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x
     for (int q = 0; q < k; ++q) {
       const int w = wo * s - pad + q;
       if (w < 0 || w >= W) continue;
-      float v[8];
-      ld8(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
+      float v[V];
+      ldv<V>(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < V; ++i)
         if (v[i] > best[i]) {
           best[i] = v[i];
           bi[i] = (uint8_t)(r * k + q);
@@ -49,30 +50,35 @@ __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x
     }
   }
   const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
-  st8(y + o, best);
-  uint2 packed;
-  packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
-  packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-  *reinterpret_cast<uint2*>(arg + o) = packed;
+  stv<V>(y + o, best);
+  if constexpr (V == 8) {
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(arg + o) = packed;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) arg[o + i] = bi[i];
+  }
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                          const uint8_t* __restrict__ arg,
                                                          T* __restrict__ dx, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   const int64_t total = (int64_t)B * H * W * cv;
   if (t >= total) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   int64_t pix = t / cv;
   const int w = (int)(pix % W);
   pix /= W;
   const int h = (int)(pix % H);
   const int b = (int)(pix / H);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[V] = {};
   // windows containing h: ho*s - pad <= h <= ho*s - pad + k - 1
   int ho0 = (h + pad - k + 1 + s - 1) / s;
   if (h + pad - k + 1 < 0) ho0 = 0;
@@ -84,60 +90,66 @@ __global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const T* __restrict__ d
     for (int wo = wo0; wo <= wo1; ++wo) {
       const uint8_t want = (uint8_t)((h + pad - ho * s) * k + (w + pad - wo * s));
       const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
-      uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
-      float g[8];
-      ld8(dy + o, g);
+      float g[V];
+      ldv<V>(dy + o, g);
+      if constexpr (V == 8) {
+        uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        uint32_t word = i < 4 ? packed.x : packed.y;
-        uint8_t a = (uint8_t)(word >> (8 * (i & 3)));
-        if (a == want) acc[i] += g[i];
+        for (int i = 0; i < V; ++i) {
+          uint32_t word = i < 4 ? packed.x : packed.y;
+          uint8_t a = (uint8_t)(word >> (8 * (i & 3)));
+          if (a == want) acc[i] += g[i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+          if (arg[o + i] == want) acc[i] += g[i];
       }
     }
   }
-  st8(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
+  stv<V>(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
 }
 
 // global average pool: x [B, HW, C] -> y [B, C]
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void gavg_fwd_kernel(const T* __restrict__ x,
                                                       T* __restrict__ y, int B, int HW,
                                                       int C) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   if (t >= (int64_t)B * cv) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   const int b = (int)(t / cv);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[V] = {};
   for (int i = 0; i < HW; ++i) {
-    float v[8];
-    ld8(x + ((int64_t)b * HW + i) * C + c0, v);
+    float v[V];
+    ldv<V>(x + ((int64_t)b * HW + i) * C + c0, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    for (int j = 0; j < V; ++j) acc[j] += v[j];
   }
   const float inv = 1.f / (float)HW;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] *= inv;
-  st8(y + (int64_t)b * C + c0, acc);
+  for (int j = 0; j < V; ++j) acc[j] *= inv;
+  stv<V>(y + (int64_t)b * C + c0, acc);
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void gavg_bwd_kernel(const T* __restrict__ dy,
                                                       T* __restrict__ dx, int B, int HW,
                                                       int C) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   const int64_t total = (int64_t)B * HW * cv;
   if (t >= total) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   const int64_t pix = t / cv;
   const int b = (int)(pix / HW);
-  float g[8];
-  ld8(dy + (int64_t)b * C + c0, g);
+  float g[V];
+  ldv<V>(dy + (int64_t)b * C + c0, g);
   const float inv = 1.f / (float)HW;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] *= inv;
-  st8(dx + pix * C + c0, g);
+  for (int j = 0; j < V; ++j) g[j] *= inv;
+  stv<V>(dx + pix * C + c0, g);
 }
 
 // bias + activation: y = act(x + bias[g][c]) over [M, C] packed channels
@@ -235,10 +247,14 @@ __global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const T* __restrict__ 
 template <typename T>
 static int cer_maxpool_fwd_t(const T* x, T* y, uint8_t* arg, int B, int H, int W, int C,
                             int Ho, int Wo, int k, int s, int pad, hipStream_t stream) {
-  if (C % 8 || k * k > 255) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)B * Ho * Wo * (C / 8);
-  maxpool_fwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, arg, B, H, W, C, Ho, Wo,
-                                                               k, s, pad);
+  if (k * k > 255) return (int)hipErrorInvalidValue;
+  // 8 channels per thread when C % 8 == 0, else 1 (ragged widths)
+  if (C % 8 == 0)
+    maxpool_fwd_kernel<T, 8><<<cer_blocks((int64_t)B * Ho * Wo * (C / 8), PT), PT, 0, stream>>>(
+        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad);
+  else
+    maxpool_fwd_kernel<T, 1><<<cer_blocks((int64_t)B * Ho * Wo * C, PT), PT, 0, stream>>>(
+        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad);
   return (int)hipGetLastError();
 }
 
@@ -246,27 +262,33 @@ template <typename T>
 static int cer_maxpool_bwd_t(const T* dy, const uint8_t* arg, T* dx, int B, int H,
                             int W, int C, int Ho, int Wo, int k, int s, int pad,
                             hipStream_t stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)B * H * W * (C / 8);
-  maxpool_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, arg, dx, B, H, W, C, Ho, Wo,
-                                                               k, s, pad);
+  if (C % 8 == 0)
+    maxpool_bwd_kernel<T, 8><<<cer_blocks((int64_t)B * H * W * (C / 8), PT), PT, 0, stream>>>(
+        dy, arg, dx, B, H, W, C, Ho, Wo, k, s, pad);
+  else
+    maxpool_bwd_kernel<T, 1><<<cer_blocks((int64_t)B * H * W * C, PT), PT, 0, stream>>>(
+        dy, arg, dx, B, H, W, C, Ho, Wo, k, s, pad);
   return (int)hipGetLastError();
 }
 
 template <typename T>
 static int cer_gavgpool_fwd_t(const T* x, T* y, int B, int HW, int C,
                              hipStream_t stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  gavg_fwd_kernel<T><<<cer_blocks((int64_t)B * (C / 8), PT), PT, 0, stream>>>(x, y, B, HW, C);
+  if (C % 8 == 0)
+    gavg_fwd_kernel<T, 8><<<cer_blocks((int64_t)B * (C / 8), PT), PT, 0, stream>>>(x, y, B, HW, C);
+  else
+    gavg_fwd_kernel<T, 1><<<cer_blocks((int64_t)B * C, PT), PT, 0, stream>>>(x, y, B, HW, C);
   return (int)hipGetLastError();
 }
 
 template <typename T>
 static int cer_gavgpool_bwd_t(const T* dy, T* dx, int B, int HW, int C,
                              hipStream_t stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  int64_t total = (int64_t)B * HW * (C / 8);
-  gavg_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, HW, C);
+  if (C % 8 == 0)
+    gavg_bwd_kernel<T, 8><<<cer_blocks((int64_t)B * HW * (C / 8), PT), PT, 0, stream>>>(dy, dx, B,
+                                                                                      HW, C);
+  else
+    gavg_bwd_kernel<T, 1><<<cer_blocks((int64_t)B * HW * C, PT), PT, 0, stream>>>(dy, dx, B, HW, C);
   return (int)hipGetLastError();
 }
 
@@ -324,51 +346,51 @@ __device__ __forceinline__ float avg_div(int ho, int wo, int H, int W, int k, in
   return n > 0 ? 1.f / (float)n : 0.f;
 }
 
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void avgpool_fwd_kernel(const T* __restrict__ x,
                                                          T* __restrict__ y, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pt, int pl, int count_pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   const int64_t total = (int64_t)B * Ho * Wo * cv;
   if (t >= total) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   int64_t pix = t / cv;
   const int wo = (int)(pix % Wo);
   pix /= Wo;
   const int ho = (int)(pix % Ho);
   const int b = (int)(pix / Ho);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[V] = {};
   for (int r = 0; r < k; ++r) {
     const int h = ho * s - pt + r;
     if (h < 0 || h >= H) continue;
     for (int q = 0; q < k; ++q) {
       const int w = wo * s - pl + q;
       if (w < 0 || w >= W) continue;
-      float v[8];
-      ld8(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
+      float v[V];
+      ldv<V>(x + (((int64_t)b * H + h) * W + w) * C + c0, v);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
+      for (int i = 0; i < V; ++i) acc[i] += v[i];
     }
   }
   const float inv = avg_div(ho, wo, H, W, k, s, pt, pl, count_pad);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] *= inv;
-  st8(y + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, acc);
+  for (int i = 0; i < V; ++i) acc[i] *= inv;
+  stv<V>(y + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, acc);
 }
 
 // deterministic gather: each input pixel sums dy / divisor over the windows covering it
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const T* __restrict__ dy,
                                                          T* __restrict__ dx, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
                                                          int s, int pt, int pl, int count_pad) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
-  const int cv = C / 8;
+  const int cv = C / V;
   const int64_t total = (int64_t)B * H * W * cv;
   if (t >= total) return;
-  const int c0 = (int)(t % cv) * 8;
+  const int c0 = (int)(t % cv) * V;
   int64_t pix = t / cv;
   const int w = (int)(pix % W);
   pix /= W;
@@ -380,28 +402,31 @@ __global__ __launch_bounds__(PT) void avgpool_bwd_kernel(const T* __restrict__ d
   const int wo0 = wl <= 0 ? 0 : (wl + s - 1) / s;
   const int ho1 = min(Ho - 1, (h + pt) / s);
   const int wo1 = min(Wo - 1, (w + pl) / s);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float acc[V] = {};
   for (int ho = ho0; ho <= ho1; ++ho) {
     for (int wo = wo0; wo <= wo1; ++wo) {
-      float g[8];
-      ld8(dy + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, g);
+      float g[V];
+      ldv<V>(dy + (((int64_t)b * Ho + ho) * Wo + wo) * C + c0, g);
       const float inv = avg_div(ho, wo, H, W, k, s, pt, pl, count_pad);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += g[i] * inv;
+      for (int i = 0; i < V; ++i) acc[i] += g[i] * inv;
     }
   }
-  st8(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
+  stv<V>(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
 }
 
 template <typename T>
 static int cer_avgpool_fwd_t(const T* x, T* y, int B, int H, int W, int C, int Ho,
                             int Wo, int k, int s, int pt, int pl, int count_pad,
                             hipStream_t stream) {
-  if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
+  if (k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
     return (int)hipErrorInvalidValue;
-  const int64_t total = (int64_t)B * Ho * Wo * (C / 8);
-  avgpool_fwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(x, y, B, H, W, C, Ho, Wo, k, s,
-                                                               pt, pl, count_pad);
+  if (C % 8 == 0)
+    avgpool_fwd_kernel<T, 8><<<cer_blocks((int64_t)B * Ho * Wo * (C / 8), PT), PT, 0, stream>>>(
+        x, y, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad);
+  else
+    avgpool_fwd_kernel<T, 1><<<cer_blocks((int64_t)B * Ho * Wo * C, PT), PT, 0, stream>>>(
+        x, y, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad);
   return (int)hipGetLastError();
 }
 
@@ -409,11 +434,14 @@ template <typename T>
 static int cer_avgpool_bwd_t(const T* dy, T* dx, int B, int H, int W, int C, int Ho,
                             int Wo, int k, int s, int pt, int pl, int count_pad,
                             hipStream_t stream) {
-  if (C % 8 || k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
+  if (k < 1 || s < 1 || pt < 0 || pl < 0 || pt >= k || pl >= k)
     return (int)hipErrorInvalidValue;
-  const int64_t total = (int64_t)B * H * W * (C / 8);
-  avgpool_bwd_kernel<T><<<cer_blocks(total, PT), PT, 0, stream>>>(dy, dx, B, H, W, C, Ho, Wo, k, s,
-                                                               pt, pl, count_pad);
+  if (C % 8 == 0)
+    avgpool_bwd_kernel<T, 8><<<cer_blocks((int64_t)B * H * W * (C / 8), PT), PT, 0, stream>>>(
+        dy, dx, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad);
+  else
+    avgpool_bwd_kernel<T, 1><<<cer_blocks((int64_t)B * H * W * C, PT), PT, 0, stream>>>(
+        dy, dx, B, H, W, C, Ho, Wo, k, s, pt, pl, count_pad);
   return (int)hipGetLastError();
 }
 

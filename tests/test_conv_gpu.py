@@ -28,9 +28,9 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _make(specs, G, seed=0):
+def _make(specs, G, seed=0, dtype=torch.bfloat16):
     lay = ModelLayout(specs)
-    a = Arena(lay, G, "cuda", torch.bfloat16)
+    a = Arena(lay, G, "cuda", dtype)
     torch.manual_seed(1000 + seed)   # identical parameters for the HIP and oracle runs
     for g in range(G):
         a.init_model(g, seed + g)
@@ -592,3 +592,102 @@ def test_resnet50_bn_links_train_finite():
         grads.append(a.grad.clone())
     assert torch.isfinite(grads[0]).all()
     assert _rel(grads[0], grads[1]) < 0.1
+
+
+# ---- ragged channel widths (NASNet-Mobile's 11 / 22 / 44 filters; 88 and 176
+# are 8-aligned but leave BN_T % (C / 8) surplus threads in the BN map) ----
+@pytest.mark.parametrize("act,res", [(True, False), (True, True), (False, False)])
+@pytest.mark.parametrize("G,C", [(1, 11), (2, 11), (3, 44), (1, 88), (1, 176), (2, 22)])
+def test_bn_act_ragged_fp32_matches_oracle(act, res, G, C):
+    """fp32 BN train fwd / bwd / eval on HIP vs the PyTorch path of the same
+    op, for channel counts that are not multiples of 8 (one channel per
+    thread) and for 8-aligned counts whose map leaves idle surplus threads."""
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    shape = (4, 9, 7, G * C)
+    torch.manual_seed(2)
+    x = 2 * torch.randn(shape, device="cuda") + 0.3
+    r = torch.randn(shape, device="cuda") if res else None
+    outs = []
+    for force in ([], ["bn"]):
+        backend.force_torch_ops(force)
+        backend.take_fallbacks()
+        a, refs = _make(specs, G, seed=5, dtype=torch.float32)
+        xx = x.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True) if res else None
+        y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y))
+        ye = P.bn_act(x, refs["g"], refs["b"], refs["rm"], refs["rv"], False, act, r)
+        torch.cuda.synchronize()
+        if not force:
+            assert not backend.take_fallbacks()
+        outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone(),
+                     a.master.clone(), ye))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert _rel(h[0], t[0]) < 1e-5
+    assert _rel(h[1], t[1]) < 1e-4
+    if res:
+        assert _rel(h[2], t[2]) < 1e-5
+    assert _rel(h[3], t[3]) < 1e-4          # dgamma / dbeta
+    assert _rel(h[4], t[4]) < 1e-5          # running stats
+    assert _rel(h[5], t[5]) < 1e-5          # eval path
+
+
+@pytest.mark.parametrize("C", [11, 22])
+def test_pools_ragged_fp32_match_oracle(C):
+    torch.manual_seed(4)
+    shape = (2, 15, 15, C)
+    x = torch.randperm(int(torch.tensor(shape).prod()), device="cuda").float().view(shape)
+    x = x / x.numel()
+    for name, fn in (("max", lambda t: P.maxpool2d(t, 3, 2, 1)),
+                     ("avg_same", lambda t: P.avgpool2d(t, 3, 1, 1, count_include_pad=False)),
+                     ("avg_valid", lambda t: P.avgpool2d(t, 3, 2, 0)),
+                     ("gavg", P.global_avgpool)):
+        res = []
+        for force in ([], ["pool"]):
+            backend.force_torch_ops(force)
+            backend.take_fallbacks()
+            xx = x.clone().requires_grad_(True)
+            y = fn(xx)
+            torch.manual_seed(3)
+            y.backward(torch.randn_like(y))
+            torch.cuda.synchronize()
+            if not force:
+                assert not backend.take_fallbacks(), name
+            res.append((y.detach(), xx.grad))
+        backend.force_torch_ops([])
+        assert _rel(res[0][0], res[1][0]) < 1e-6, name
+        assert _rel(res[0][1], res[1][1]) < 1e-5, name
+
+
+@pytest.mark.parametrize("case", [
+    (2, 14, 14, 11, 1, 1, 3, 1), (2, 15, 15, 11, 2, 2, 5, (1, 2, 1, 2)),
+    (2, 28, 28, 22, 2, 1, 7, (2, 3, 2, 3)), (2, 14, 14, 44, 1, 2, 3, 1)])
+def test_dwconv_ragged_fp32_matches_oracle(case):
+    """Depthwise conv with per-config channel counts that are not multiples
+    of 8 (one channel per thread), NASNet-Mobile shapes."""
+    B, H, W, C, s, G, k, pad = case
+    spec = ParamSpec("dw", (C, k, k), "weight", fan_in=k * k)
+    torch.manual_seed(5)
+    x = torch.randn(B, H, W, G * C, device="cuda")
+    outs = []
+    for force in ([], ["dwconv"]):
+        backend.force_torch_ops(force)
+        backend.take_fallbacks()
+        a, refs = _make([spec], G, dtype=torch.float32)
+        xx = x.clone().requires_grad_(True)
+        y = P.dwconv2d(xx, refs["dw"], s, pad)
+        torch.manual_seed(3)
+        y.backward(torch.randn_like(y))
+        torch.cuda.synchronize()
+        if not force:
+            assert not backend.take_fallbacks()
+        outs.append((y.detach(), xx.grad, a.grad.clone()))
+    backend.force_torch_ops([])
+    h, t = outs
+    assert h[0].shape == t[0].shape
+    assert _rel(h[0], t[0]) < 1e-5
+    assert _rel(h[1], t[1]) < 1e-5
+    assert _rel(h[2], t[2]) < 1e-5
