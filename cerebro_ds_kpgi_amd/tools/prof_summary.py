@@ -20,6 +20,7 @@ FAMILIES = [
     ("conv dgrad (MFMA, NN)", r"igemm_nn_dgrad|igemm_nn32|pipe_nn"),
     ("conv/linear wgrad (MFMA, TN; batched)", r"igemm_wgrad|pipe_wg|wgrad_batch"),
     ("weight transpose (dgrad)", r"transpose_w"),
+    ("depthwise conv (fwd / dgrad / wgrad)", r"dw_fwd|dw_dgrad|dw_wgrad"),
     ("batchnorm", r"^bn_|bn_partials|bn_apply|bn_finalize"),
     ("pooling", r"maxpool|gavg|avgpool"),
     ("stem repack / fold", r"stem_"),
