@@ -125,8 +125,10 @@ class PackedResNet(PackedNet):
             # x has two consumers (c1 and the shortcut): their input gradients
             # meet in a GradJoin instead of an autograd add kernel
             j = P.GradJoin() if training else None
+            # (not under DDP's gradient buckets: a graph segment may end
+            # between the branch's backward and its join)
             branch = ("cs" in blk and training and _SC_BRANCH and x.is_cuda
-                      and get_backend() == "hip")
+                      and get_backend() == "hip" and self.grad_buckets is None)
             if branch:
                 cur = torch.cuda.current_stream(x.device)
                 fork = torch.cuda.Event()
