@@ -257,6 +257,8 @@ _SIGS.update({
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_set_hl_out": [c_i],
+    "cer_bn_set_mask_out": [c_p],
+    "cer_bn_set_mask_in": [c_i],
     "cer_conv_set_hl": [c_i, c_i],
     "cer_bn_set_fold": [c_i],
     "cer_bn_part_floats": [c_i64, c_i],
@@ -387,6 +389,50 @@ def _hl_out(on):
         yield
     finally:
         lib().cer_bn_set_hl_out(0)
+
+
+# Residual-join activation masks as bits (bn.hip YM_M): the forward apply of
+# a BN with a residual writes its ReLU mask as [M][C / 8] bytes next to y,
+# and the backward -- the BN apply / partials and the BN-link statistics in
+# the consumer's dgrad epilogue -- reads 1 bit instead of the fp32 y per
+# element (fp32, 8-aligned widths).  CER_BN_BITMASK=0 reads y.
+BITMASK_ENABLED = os.environ.get("CER_BN_BITMASK", "1") != "0"
+
+
+def mask_ok(t, act, residual):
+    return (BITMASK_ENABLED and residual is not None and act in (1, 6)
+            and t.dtype == torch.float32 and t.is_cuda and t.shape[-1] % 8 == 0)
+
+
+def new_mask(t):
+    C = t.shape[-1]
+    return torch.empty((t.numel() // C, C // 8), dtype=torch.uint8, device=t.device)
+
+
+@contextlib.contextmanager
+def _mask_out(mask):
+    if mask is None:
+        yield
+        return
+    lib().cer_bn_set_mask_out(_ptr(mask))
+    try:
+        yield
+    finally:
+        lib().cer_bn_set_mask_out(None)
+
+
+@contextlib.contextmanager
+def mask_in(on):
+    """Backward launches inside read residual-join masks as bits (their y
+    argument is the mask)."""
+    if not on:
+        yield
+        return
+    lib().cer_bn_set_mask_in(1)
+    try:
+        yield
+    finally:
+        lib().cer_bn_set_mask_in(0)
 
 
 def _same(t, ref):
@@ -565,8 +611,11 @@ def conv2d_fwd_stats(x, wref, stride, pad):
 
 def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps,
                   hl_out=False):
+    mask = new_mask(z) if mask_ok(z, _act_code(act), residual) else None
     y, mean, invstd = bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, act, momentum,
-                                            eps, part, nslab, hl_out=hl_out)
+                                            eps, part, nslab, hl_out=hl_out, mask=mask)
+    if mask is not None:
+        y._cer_mask = mask
     return y, z, mean, invstd
 
 
@@ -760,9 +809,13 @@ def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend,
     nslab = ctypes.c_int(0)
     gp, gs = link.gref.work_ptr()
     bp, bs = link.bref.work_ptr()
-    L.cer_conv_dgrad_bnbwd(_ptr(part), _ptr(link.z), _ptr(_same(ybn, dy)), _ptr(link.mean),
-                           _ptr(link.invstd), c_p(gp), gs, c_p(bp), bs, _act_code(link.act),
-                           1 if link.has_res else 0, ctypes.byref(nslab))
+    lmask = getattr(link, "mask", None)
+    use_mask = lmask is not None and link.has_res and _act_code(link.act) in (1, 6)
+    with mask_in(use_mask):          # the epilogue's mask mode is fixed here
+        L.cer_conv_dgrad_bnbwd(_ptr(part), _ptr(link.z),
+                               _ptr(lmask) if use_mask else _ptr(_same(ybn, dy)),
+                               _ptr(link.mean), _ptr(link.invstd), c_p(gp), gs, c_p(bp), bs,
+                               _act_code(link.act), 1 if link.has_res else 0, ctypes.byref(nslab))
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
                            addend, bnstats=True, wref=wref, after_tune=part.zero_, dy_hl=dy_hl)
@@ -952,9 +1005,10 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
 
 
 def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, eps, part,
-                          nslab, hl_out=False):
+                          nslab, hl_out=False, mask=None):
     """BN forward from conv-epilogue partials (cer_conv_fwd_stats);
-    ``hl_out``: y in HL format (tagged ``_cer_hl``)."""
+    ``hl_out``: y in HL format (tagged ``_cer_hl``); ``mask``: also write
+    the activation mask as bits (``mask_ok`` / ``new_mask``)."""
     x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
@@ -968,7 +1022,7 @@ def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, 
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
     res = _same(residual, x) if residual is not None else None
-    with _hl_out(hl_out):
+    with _hl_out(hl_out), _mask_out(mask):
         rc = _fn("cer_bn_fwd_train_part", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp),
                                          bs, c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd),
                                          _ptr(ws), _ptr(part), int(nslab), M, C, Cper, eps,
@@ -997,11 +1051,15 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
 
 
 def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0,
-               hl_out=False):
+               hl_out=False, mask=None):
     """BN backward; ``part`` / ``nslab``: the (sum dz, sum dz*xhat) partials
     already computed by the dgrad epilogue that produced dy.  ``hl_out``: dx
     (the conv-output gradient) in HL format for the conv's dgrad / wgrad
-    (tagged ``_cer_hl``); the residual gradient stays fp32."""
+    (tagged ``_cer_hl``); the residual gradient stays fp32.  ``mask``: the
+    forward's activation bits of a residual join, read instead of y."""
+    use_mask = mask is not None and has_res and _act_code(act) in (1, 6)
+    if use_mask:
+        y = mask
     dy = _act(dy)
     hl_out = hl_out and hl_ok(x)
     C = x.shape[-1]
@@ -1016,7 +1074,7 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
     dbp, _ = bref.grad_ptr()
     if hl_out:
         dx._cer_hl = True
-    with _hl_out(hl_out):
+    with _hl_out(hl_out), mask_in(use_mask):
         if part is not None and nslab > 0:
             rc = _fn("cer_bn_bwd_part", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd),
                                        c_p(gp), gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs,

@@ -129,10 +129,11 @@ class BNLink(object):
     its own pass over (dy, z[, y]).  Only set by models on outputs whose whole
     gradient comes out of one dgrad — a sole conv consumer, or two consumers
     joined by a GradJoin (the second arrival holds the full gradient)."""
-    __slots__ = ("z", "mean", "invstd", "gref", "bref", "act", "has_res", "part", "nslab")
+    __slots__ = ("z", "mean", "invstd", "gref", "bref", "act", "has_res", "part", "nslab",
+                 "mask")
 
     def __init__(self):
-        self.z = self.mean = self.invstd = self.gref = self.bref = None
+        self.z = self.mean = self.invstd = self.gref = self.bref = self.mask = None
         self.act, self.has_res, self.part, self.nslab = 0, False, None, 0
 
 
@@ -312,6 +313,7 @@ class PackedConvBNAct(torch.autograd.Function):
         hip_ok = (use_hip("conv", x) and use_hip("bn", x) and wref.spec.shape[0] % 8 == 0
                   and gref.spec.shape[0] % 8 == 0)
         ctx.x_hl = False
+        ctx.mask = None
         if hip_ok:
             h = _hip()
             ctx.x_hl = h.is_hl(x)        # an HL-format input (see conv_bn_act hl_out)
@@ -320,6 +322,8 @@ class PackedConvBNAct(torch.autograd.Function):
             y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
                 x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride, pad,
                 stem=stem, hl_out=hl_box is not None and not stem and residual is None)
+            # a residual join's activation mask as bits (ops._hip mask_ok)
+            ctx.mask = getattr(y, "_cer_mask", None)
             if hl_box is not None:
                 hl_box[0] = h.is_hl(y)
         else:
@@ -331,6 +335,7 @@ class PackedConvBNAct(torch.autograd.Function):
         if link is not None and _bn_hip(z, gref) and _bn_aligned(gref):
             link.z, link.mean, link.invstd = z, mean, invstd
             link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
+            link.mask = ctx.mask
         ctx.save_for_backward(x, z, y, mean, invstd)
         return y
 
@@ -351,12 +356,14 @@ class PackedConvBNAct(torch.autograd.Function):
             # partials from the consumer's dgrad epilogue
             dz, dres = _hip().bn_act_bwd(dy, z, y, mean, invstd, gref, bref, ctx.relu,
                                          ctx.has_res, part=link.part, nslab=link.nslab,
-                                         hl_out=hl_bwd)
+                                         hl_out=hl_bwd, mask=ctx.mask)
             link.part = None
         else:
-            dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref, hl_out=hl_bwd)
+            dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref, hl_out=hl_bwd,
+                                    mask=ctx.mask)
         if link is not None:
-            link.z = link.mean = link.invstd = None
+            link.z = link.mean = link.invstd = link.mask = None
+        ctx.mask = None
         if ctx.res_join is not None and ctx.needs_input_grad[1]:
             dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
@@ -370,10 +377,10 @@ class PackedConvBNAct(torch.autograd.Function):
                 None, None, None)
 
 
-def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False):
+def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False, mask=None):
     if _bn_hip(x, gref):
         return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res,
-                                 hl_out=hl_out)
+                                 hl_out=hl_out, mask=mask)
     C = x.shape[-1]
     dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
     n = dz.shape[0]

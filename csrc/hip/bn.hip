@@ -88,7 +88,26 @@ __device__ __forceinline__ void stf(float* p, float v) {
 // ---------------------------------------------------------------------------
 // stage 1: per-slab partial sums -> part[slab][2][C]
 // ---------------------------------------------------------------------------
-constexpr int YM_NONE = 0, YM_Y = 1, YM_Z = 2;
+constexpr int YM_NONE = 0, YM_Y = 1, YM_Z = 2, YM_M = 3;
+
+// YM_M: the activation mask of a residual join as one bit per element,
+// written by the forward apply (mask_out [M][C / 8] bytes, bit i = channel
+// 8j + i active: act_bwd(1, y) != 0) and read in backward instead of the
+// fp32 output y -- 1/32 of y's bytes, bit-identical decisions (8-aligned
+// widths only).  The backward kernels take the mask through their y pointer.
+__device__ __forceinline__ uint32_t act_bits8(const float* o, int act) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m |= (o[i] > 0.f && (act != 6 || o[i] < 6.f)) ? (1u << i) : 0u;
+  return m;
+}
+
+// 8 mask bits -> y-like values (1 active / 0 not) for the YM_Y arithmetic
+__device__ __forceinline__ void mask_to_y8(const uint8_t* mrow, int c0, float* yv) {
+  const uint32_t m = mrow[c0 >> 3];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) yv[i] = (m >> i) & 1u ? 1.f : 0.f;
+}
 
 // forward scale / shift of 8 channels (bitwise the apply_fwd_tile values)
 template <typename T, int V = VEC>
@@ -110,6 +129,7 @@ template <int YM>
 __device__ __forceinline__ float dz_of(float d, float yv, float xv, float sc, float sh, int act) {
   if (YM == YM_NONE) return d;
   if (YM == YM_Z) return (xv * sc + sh + 0.f) > 0.f ? d : 0.f;
+  if (YM == YM_M) return yv > 0.f ? d : 0.f;
   return act_bwd(d, yv, act);
 }
 
@@ -155,6 +175,8 @@ __device__ __forceinline__ void partials_tile(
           if (MODE == 1) {
             ldv<V>(dy + rr * C + c0, d[u]);
             if (YM == YM_Y) ldv<V>(y + rr * C + c0, yv[u]);
+            if constexpr (YM == YM_M)
+              mask_to_y8(reinterpret_cast<const uint8_t*>(y) + rr * (C / 8), c0, yv[u]);
           }
         }
       }
@@ -337,7 +359,7 @@ __device__ __forceinline__ void apply_fwd_tile(
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, const Strided& gamma,
     const Strided& beta, int64_t M, int C, int Cper, int rows_per_slab, int act, const Map& mp,
-    int cbk, int slab) {
+    int cbk, int slab, uint8_t* __restrict__ mask_out = nullptr) {
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
@@ -381,8 +403,9 @@ __device__ __forceinline__ void apply_fwd_tile(
           st8_hl(y + rr * C + c0, o);
         else
           st8(y + rr * C + c0, o);
+        if (mask_out) mask_out[rr * (C / VEC) + (c0 >> 3)] = (uint8_t)act_bits8(o, act);
       } else {
-        stv<V>(y + rr * C + c0, o);       // ragged widths: never HL (host-gated)
+        stv<V>(y + rr * C + c0, o);       // ragged widths: never HL / mask (host-gated)
       }
     }
   }
@@ -393,9 +416,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd(
     const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
     const float* __restrict__ ws, const float* __restrict__ rmean,
     const float* __restrict__ rvar, int64_t rstat_stride, float eps, Strided gamma,
-    Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+    Strided beta, int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp,
+    uint8_t* __restrict__ mask_out = nullptr) {
   apply_fwd_tile<T, MODE, false, AU, V>(x, res, y, ws, rmean, rvar, rstat_stride, eps, gamma, beta, M, C,
-                              Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y);
+                              Cper, rows_per_slab, act, mp, blockIdx.x, blockIdx.y, mask_out);
 }
 
 template <typename T, bool SC, int YM = YM_Y, int AU = 2, int V = VEC>
@@ -434,6 +458,8 @@ __device__ __forceinline__ void apply_bwd_tile(
         ldv<V>(dy + rr * C + c0, d[u]);
         ldv<V>(x + rr * C + c0, xv[u]);
         if (YM == YM_Y) ldv<V>(y + rr * C + c0, yv[u]);
+        if constexpr (YM == YM_M)
+          mask_to_y8(reinterpret_cast<const uint8_t*>(y) + rr * (C / 8), c0, yv[u]);
       }
     }
 #pragma unroll
@@ -595,7 +621,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
     float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
     const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
-    int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp) {
+    int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp,
+    uint8_t* __restrict__ mask_out) {
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
@@ -652,6 +679,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
         st8_hl(y + rr * C + c0, o);
       else
         st8(y + rr * C + c0, o);
+      if (mask_out) mask_out[rr * (C / VEC) + (c0 >> 3)] = (uint8_t)act_bits8(o, act);
     }
   }
 }
@@ -703,6 +731,8 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
         ld8(dy + rr * C + c0, d[u]);
         ld8(x + rr * C + c0, xv[u]);
         if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
+        if constexpr (YM == YM_M)
+          mask_to_y8(reinterpret_cast<const uint8_t*>(y) + rr * (C / 8), c0, yv[u]);
       }
     }
 #pragma unroll
@@ -778,8 +808,19 @@ static int g_bn_hl = 0;
 CER_API void cer_bn_set_hl_out(int on) { g_bn_hl = on ? 1 : 0; }
 
 // mask source of a BN backward (also used by the dgrad-epilogue statistics)
+// residual-join activation masks as bits (YM_M): the NEXT training-mode
+// forward apply also writes its mask to ``mask`` ([M][C / 8] bytes; null
+// = off); cer_bn_set_mask_in(1): backward launches whose mode would be YM_Y
+// read such a mask through their y argument instead
+static uint8_t* g_mask_out = nullptr;
+static int g_mask_in = 0;
+CER_API void cer_bn_set_mask_out(void* mask) { g_mask_out = reinterpret_cast<uint8_t*>(mask); }
+CER_API void cer_bn_set_mask_in(int on) { g_mask_in = on ? 1 : 0; }
+
 int bn_mask_mode(int act, int has_res) {
-  return act == 0 ? YM_NONE : (act == 1 && !has_res && g_zmask) ? YM_Z : YM_Y;
+  if (act == 0) return YM_NONE;
+  if (act == 1 && !has_res && g_zmask) return YM_Z;
+  return g_mask_in ? YM_M : YM_Y;
 }
 
 // floats of scratch the partials need (part[slabs][2][C])
@@ -805,7 +846,7 @@ static int bn_fwd_train_ragged(const T* x, const T* res, T* y, const T* gamma,
                                float* rmean, float* rvar, int64_t rstat_stride, float* mean_out,
                                float* invstd_out, float* ws, float* part, int64_t M, int C,
                                int Cper, float eps, float momentum, int act, hipStream_t stream) {
-  if (act >> 8) return (int)hipErrorInvalidValue;         // HL output needs 8-aligned widths
+  if ((act >> 8) || g_mask_out) return (int)hipErrorInvalidValue;  // HL / bit masks: aligned only
   const Map mp = make_map(C, 1);
   dim3 rg, ag;
   int rrows, arows;
@@ -836,6 +877,7 @@ static int bn_bwd_ragged(const T* dy, const T* x, const T* y, const float* mean,
   make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   const int ym = bn_mask_mode(act, dres != nullptr);
+  if (ym == YM_M) return (int)hipErrorInvalidValue;     // bit masks: 8-aligned widths only
   const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
   if (ym == YM_NONE)
     bn_partials<T, 1, YM_NONE, 1><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
@@ -892,7 +934,7 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                                                rstat_stride, eps, momentum, x, res, y,
                                                Strided{gamma, gamma_stride},
                                                Strided{beta, beta_stride}, M, C, Cper, frows, act_k,
-                                               mp);
+                                               mp, g_mask_out);
     return (int)hipGetLastError();
   }
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
@@ -902,12 +944,12 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
     bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                                 Strided{gamma, gamma_stride},
                                                 Strided{beta, beta_stride}, M, C, Cper, arows,
-                                                act_k, mp);
+                                                act_k, mp, g_mask_out);
   else
     bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
                                              Strided{gamma, gamma_stride},
                                              Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
-                                             mp);
+                                             mp, g_mask_out);
   return (int)hipGetLastError();
 }
 
@@ -1018,6 +1060,9 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
     else if (ym == YM_Z)
       bn_partials<T, 1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                     act, mp, gs, bs, Cper);
+    else if (ym == YM_M)
+      bn_partials<T, 1, YM_M><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
+                                                    act, mp, gs, bs, Cper);
     else
       bn_partials<T, 1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
                                                     act, mp, gs, bs, Cper);
@@ -1033,6 +1078,10 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
                                                           mp);
     else if (ym == YM_Z)
       bn_apply_bwd_fold<T, YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
+    else if (ym == YM_M)
+      bn_apply_bwd_fold<T, YM_M><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                        grad_stride, dy, x, y, mean, invstd, gs, bs,
                                                        dx, dres, M, C, Cper, frows, act_k, mp);
     else
@@ -1057,6 +1106,9 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
     else
       bn_apply_bwd<T, YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                   Cper, arows, act_k, mp, bs);
+  } else if (ym == YM_M) {
+    bn_apply_bwd<T, YM_M><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                Cper, arows, act_k, mp, bs);
   } else {
     if (apply_au() == 4)
       bn_apply_bwd<T, YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,

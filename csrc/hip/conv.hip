@@ -1804,6 +1804,8 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   const float* zb = bstat ? reinterpret_cast<const float*>(bb.z) + (int64_t)cfg * p.N : nullptr;
   const float* yb = bstat && bb.ym == 1 ? reinterpret_cast<const float*>(bb.y) + (int64_t)cfg * p.N
                                        : nullptr;
+  // ym 3 (bn.hip YM_M): the activation mask as bits, [M][ldc / 8] bytes
+  const uint8_t* mb = bstat && bb.ym == 3 ? reinterpret_cast<const uint8_t*>(bb.y) : nullptr;
   float bc[FN][4], mu[FN][4], is[FN][4], sc[FN][4], sh[FN][4], s[FN][4], q[FN][4];
 #pragma unroll
   for (int j = 0; j < FN; ++j)
@@ -1874,13 +1876,18 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         if (yb) {
           const float4 y4 = *reinterpret_cast<const float4*>(yb + go);
           yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+        } else if (mb) {
+          const int64_t bi = go + (int64_t)cfg * p.N;     // element index in [M][ldc]
+          const uint32_t m = (uint32_t)mb[bi >> 3] >> (bi & 7);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) yv[e] = (m >> e) & 1u ? 1.f : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float dz = v[e];
           if (bb.ym == 2)
             dz = (zv[e] * sc[j][e] + sh[j][e] + 0.f) > 0.f ? dz : 0.f;
-          else if (bb.ym == 1)
+          else if (bb.ym == 1 || bb.ym == 3)
             dz = bb.act == 6 ? ((yv[e] > 0.f && yv[e] < 6.f) ? dz : 0.f) : (yv[e] > 0.f ? dz : 0.f);
           s[j][e] += dz;
           q[j][e] += dz * (zv[e] - mu[j][e]) * is[j][e];
@@ -2153,6 +2160,8 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
   const float* zb = bstat ? reinterpret_cast<const float*>(bb.z) + (int64_t)cfg * p.N : nullptr;
   const float* yb = bstat && bb.ym == 1 ? reinterpret_cast<const float*>(bb.y) + (int64_t)cfg * p.N
                                        : nullptr;
+  // ym 3 (bn.hip YM_M): the activation mask as bits, [M][ldc / 8] bytes
+  const uint8_t* mb = bstat && bb.ym == 3 ? reinterpret_cast<const uint8_t*>(bb.y) : nullptr;
   int64_t orow[FM];
   bool rok[FM];
 #pragma unroll
@@ -2233,13 +2242,18 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
           if (yb) {
             const float4 y4 = *reinterpret_cast<const float4*>(yb + go);
             yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+          } else if (mb) {
+            const int64_t bi = go + (int64_t)cfg * p.N;     // element index in [M][ldc]
+            const uint32_t m = (uint32_t)mb[bi >> 3] >> (bi & 7);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) yv[e] = (m >> e) & 1u ? 1.f : 0.f;
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float dz = v[e];
             if (bb.ym == 2)
               dz = (zv[e] * sc[g][e] + sh[g][e] + 0.f) > 0.f ? dz : 0.f;
-            else if (bb.ym == 1)
+            else if (bb.ym == 1 || bb.ym == 3)
               dz = bb.act == 6 ? ((yv[e] > 0.f && yv[e] < 6.f) ? dz : 0.f) : (yv[e] > 0.f ? dz : 0.f);
             s[g][e] += dz;
             q[g][e] += dz * (zv[e] - mu[g][e]) * is[g][e];
