@@ -177,10 +177,13 @@ class PackedConv2d(torch.autograd.Function):
                     join = None
                 dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl,
                                     consume_addend=addend is not None)
-                if join is not None:       # first of the two: park dx for the other one
-                    dx = join.join(dx)
-            # off the critical path: overlaps the dgrad chain below (ops.streams)
+            # off the critical path: overlaps the dgrad chain below (ops.streams);
+            # issued before a park, so the event the other consumer waits on
+            # also orders this stream's wgrad (a branch-stream backward launched
+            # without batching would otherwise race the optimizer)
             h.conv2d_wgrad(x, dy, wref, stride, pad)
+            if need_dx and join is not None:   # first of the two: park dx for the other one
+                dx = join.join(dx)
         else:
             G = wref.G
             cout, kh, kw, cin = wref.spec.shape
