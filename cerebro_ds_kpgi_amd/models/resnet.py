@@ -149,8 +149,13 @@ class PackedResNet(PackedNet):
                 bs = streams.branch_stream(x.device.index)
                 bs.wait_event(fork)
                 x.record_stream(bs)
-                with torch.cuda.stream(bs):
-                    sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j)
+                streams.set_branch_parent(x.device.index, cur)
+                try:
+                    with torch.cuda.stream(bs):
+                        sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False,
+                                          join=j)
+                finally:
+                    streams.set_branch_parent(x.device.index, None)
             if self.bottleneck:
                 h = self.conv_bn(h, blk["c2"], blk["b2"], training, link_out=True, hl_out=True)
             if branch:

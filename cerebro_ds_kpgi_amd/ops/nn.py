@@ -317,6 +317,9 @@ class PackedConvBNAct(torch.autograd.Function):
                   and gref.spec.shape[0] % 8 == 0)
         ctx.x_hl = False
         ctx.mask = None
+        # a branch-stream unit (models/resnet.py shortcut): the stream its
+        # block forked from, which consumes its input gradient in backward
+        ctx.parent = streams.branch_parent(x.device) if x.is_cuda else None
         if hip_ok:
             h = _hip()
             ctx.x_hl = h.is_hl(x)        # an HL-format input (see conv_bn_act hl_out)
@@ -347,6 +350,10 @@ class PackedConvBNAct(torch.autograd.Function):
         x, z, y, mean, invstd = ctx.saved_tensors
         gref, bref = ctx.refs
         dy = dy.contiguous()
+        if ctx.parent is not None:
+            # dy was made on the parent stream: keep its memory from being
+            # reused there while this stream still reads it
+            dy.record_stream(torch.cuda.current_stream(dy.device))
         if ctx.x_hl:
             x._cer_hl = True             # the saved input's format tag
         # the BN input gradient's only consumers are this conv's dgrad and
@@ -376,6 +383,8 @@ class PackedConvBNAct(torch.autograd.Function):
             dx = None
         else:
             dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
+        if ctx.parent is not None and dx is not None:
+            dx.record_stream(ctx.parent)      # consumed on the parent stream
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
                 None, None, None)
 

@@ -152,6 +152,20 @@ def branch_stream(dev):
     return s
 
 
+_PARENT = {}
+
+
+def set_branch_parent(dev, stream):
+    """The stream a model's branch forked from (None: no branch open)."""
+    _PARENT[dev] = stream
+
+
+def branch_parent(device):
+    """Parent stream while the current stream is the branch, else None."""
+    dev = torch.device(device).index
+    return _PARENT.get(dev) if on_branch(device) else None
+
+
 def on_branch(device):
     """True while the current stream of ``device`` is its branch stream."""
     dev = torch.device(device).index
