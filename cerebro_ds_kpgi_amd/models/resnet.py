@@ -127,8 +127,11 @@ class PackedResNet(PackedNet):
             j = P.GradJoin() if training else None
             # (not under DDP's gradient buckets: a graph segment may end
             # between the branch's backward and its join; fp32 only: in the
-            # bf16 diagnostic mode graph replays drift from eager by 1e-3 -
-            # 8e-3 with the branch, tests/test_graph_gpu.py, not root-caused)
+            # bf16 diagnostic mode replays drift from eager by 1e-3 - 8e-3
+            # with the branch (tests/test_graph_gpu.py) -- most likely the
+            # split-K fp32 atomics' order, which overlapping kernels vary,
+            # flipping bf16 roundings of activations; fp32 replays stay at
+            # the 1e-4 noise floor)
             branch = ("cs" in blk and training and _SC_BRANCH and x.is_cuda
                       and x.dtype == torch.float32 and get_backend() == "hip"
                       and self.grad_buckets is None)
