@@ -75,4 +75,8 @@ def test_resnet50_training_with_and_without_branch(monkeypatch, configs):
         return ((na - nb).abs() / na).max().item()
     noise, br = dist(states[0], states[1]), dist(states[0], states[2])
     print("per-config norm rel diff: plain vs plain %.2e, plain vs branch %.2e" % (noise, br))
-    assert br <= max(4 * noise, 1e-5), (br, noise)
+    # the plain-vs-plain floor itself varies 5e-5 .. 1.5e-3 between boxes
+    # (split-K fp32 atomics' order, amplified by Adam): bound by the larger
+    # of 4x this run's floor and 2e-3; a lost or doubled gradient
+    # contribution moves the norms by orders of magnitude more
+    assert br <= max(4 * noise, 2e-3), (br, noise)
