@@ -7,10 +7,10 @@ context and before the optimizer — launches the queue as a few multi-layer
 kernels (``wgrad_batch`` in csrc/hip/conv.hip).  The operands stay referenced
 here until the flush.
 
-Split batch (packs of >= 4 configs, ``deferred_wgrad(side_frac=0.5)`` from
+Split batch (packs of >= 4 configs, ``deferred_wgrad(side_frac=0.4)`` from
 runtime/group.py): in backward a layer's input gradient (dgrad) is on the
 critical path while its weight gradient is only needed by the optimizer.
-Once half of the previous step's layer count is queued, that batch -- the
+Once 40 % of the previous step's layer count is queued, that batch -- the
 upper stages' wgrads -- launches ONCE on a per-device side stream (forked
 from the current stream at that point) on a capped, persistent grid
 (``CER_WGB_SPLIT_GRID`` = 96 blocks), so it runs on a slice of the CUs while
