@@ -16,9 +16,10 @@
 //          window) instead of 4k times
 //  dgrad : one thread = 8 channels x 1 input pixel (gathers the dy taps that
 //          reach it; stride 2 handled by divisibility)
-//  wgrad : block = 8 channels x 256 row lanes x a band of filter rows; each
-//          lane accumulates the band's taps over its pixels, wave reduction,
-//          LDS across waves, fp32 atomics into the gradient arena (which the
+//  wgrad : block = up to 64 channel groups x 256/CB position lanes x a band
+//          of filter rows; channel-contiguous lanes (coalesced), 4 output
+//          columns per position with a sliding input window, shuffle + LDS
+//          reduction, fp32 atomics into the gradient arena (which the
 //          optimizer keeps zeroed)
 #include "common.h"
 
@@ -138,64 +139,110 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
   stv<V>(dx + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, acc);
 }
 
-// grid (GC / 8, row slabs, K / RB filter-row bands); 256 lanes stride over the
-// slab's output pixels, each accumulating RB x K taps x 8 channels
-template <int K, int RB, int V, typename T>
+// grid (ceil(CV / CB), position slabs, K / RB filter-row bands), CV = GC / V
+// channel groups.  Thread t = (position lane t >> lcb, channel group t & (CB-1)):
+// adjacent lanes read adjacent channel groups of ONE pixel, so a wave's load
+// covers 64 / CB pixels with CB * V contiguous channels each (the earlier
+// lane-per-pixel layout touched 64 cache lines per load and was bound by the
+// vector-cache line rate).  A position is X consecutive output columns of one
+// row: dy is loaded once per position, and per filter row the (X-1)*ST + K
+// input pixels once (sliding window), instead of X * (1 + RB * K) loads.
+// Position lanes of a channel group reduce by shuffles, the 4 waves by LDS
+// atomics, then one fp32 atomic per (channel, tap) into the gradient arena.
+template <int K, int RB, int ST, int X, int V, typename T>
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ dw,
-                                                       int64_t dw_gstride, DWGeom d, int st,
-                                                       int64_t pix_per_slab) {
+                                                       int64_t dw_gstride, DWGeom d, int lcb,
+                                                       int64_t pos_per_slab) {
   constexpr int NT = RB * K;
-  __shared__ float red[NT * V][4];
-  const int GC = d.G * d.C;
-  const int gc0 = blockIdx.x * V;
+  constexpr int NWIN = (X - 1) * ST + K;
+  __shared__ float red[64 * NT * V];
+  const int CB = 1 << lcb;
+  const int GC = d.G * d.C, CV = GC / V;
+  const int c = threadIdx.x & (CB - 1), pr = threadIdx.x >> lcb, PR = 256 >> lcb;
+  const int cv = blockIdx.x * CB + c;
+  const bool active = cv < CV;
+  const int gc0 = cv * V;
   const int r0 = blockIdx.z * RB;
-  const int64_t P = (int64_t)d.B * d.Ho * d.Wo;
-  const int64_t p0 = (int64_t)blockIdx.y * pix_per_slab;
-  const int64_t p1 = min(P, p0 + pix_per_slab);
+  const int xgroups = (d.Wo + X - 1) / X;
+  const int64_t Pn = (int64_t)d.B * d.Ho * xgroups;
+  const int64_t q0 = (int64_t)blockIdx.y * pos_per_slab;
+  const int64_t q1 = min(Pn, q0 + pos_per_slab);
   float acc[NT][V];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[t][i] = 0.f;
-  for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
-    const int wo = (int)(p % d.Wo);
-    const int64_t q = p / d.Wo;
-    const int ho = (int)(q % d.Ho);
-    const int b = (int)(q / d.Ho);
-    float g[V];
-    ldv<V>(dy + p * GC + gc0, g);
+  if (active) {
+    for (int64_t q = q0 + pr; q < q1; q += PR) {
+      const int xg = (int)(q % xgroups);
+      const int64_t u = q / xgroups;
+      const int ho = (int)(u % d.Ho);
+      const int b = (int)(u / d.Ho);
+      const int wo0 = xg * X;
+      float g[X][V];
 #pragma unroll
-    for (int rr = 0; rr < RB; ++rr) {
-      const int hi = ho * st - d.pt + r0 + rr;
-      if (hi < 0 || hi >= d.H) continue;
+      for (int xi = 0; xi < X; ++xi) {
+        if (wo0 + xi < d.Wo) {
+          ldv<V>(dy + (((int64_t)b * d.Ho + ho) * d.Wo + wo0 + xi) * GC + gc0, g[xi]);
+        } else {
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const int wi = wo * st - d.pl + s;
-        if (wi < 0 || wi >= d.W) continue;
-        float v[V];
-        ldv<V>(x + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, v);
+          for (int i = 0; i < V; ++i) g[xi][i] = 0.f;
+        }
+      }
+      const int wi0 = wo0 * ST - d.pl;
 #pragma unroll
-        for (int i = 0; i < V; ++i) acc[rr * K + s][i] += v[i] * g[i];
+      for (int rr = 0; rr < RB; ++rr) {
+        const int hi = ho * ST - d.pt + r0 + rr;
+        if (hi < 0 || hi >= d.H) continue;
+        const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
+        float win[NWIN][V];
+#pragma unroll
+        for (int j = 0; j < NWIN; ++j) {
+          const int wi = wi0 + j;
+          if (wi >= 0 && wi < d.W) {
+            ldv<V>(xrow + (int64_t)wi * GC, win[j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+          for (int s = 0; s < K; ++s)
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[rr * K + s][i] += win[xi * ST + s][i] * g[xi][i];
       }
     }
   }
-  // wave reduction, then 4 waves -> LDS -> one atomic per (tap, channel)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // position lanes of a wave (lane ^ CB, ^ 2CB, ...) -> lanes 0..CB-1
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < V; ++i) {
-      const float v = warp_sum(acc[t][i]);
-      if (lane == 0) red[t * V + i][wid] = v;
+      float v = acc[t][i];
+      for (int o = CB; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      acc[t][i] = v;
     }
+  const int n = CB * NT * V;
+  for (int e = threadIdx.x; e < n; e += 256) red[e] = 0.f;
   __syncthreads();
-  for (int e = threadIdx.x; e < NT * V; e += 256) {
-    const float v = red[e][0] + red[e][1] + red[e][2] + red[e][3];
-    const int t = e / V, i = e - t * V;
-    const int gc = gc0 + i, g = gc / d.C, c = gc - g * d.C;
-    atomicAdd(dw + g * dw_gstride + (int64_t)c * K * K + r0 * K + t, v);
+  if ((threadIdx.x & 63) < CB && active) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < V; ++i) atomicAdd(&red[(c * NT + t) * V + i], acc[t][i]);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const int ce = e / (NT * V), rem = e - ce * (NT * V);
+    const int t = rem / V, i = rem - t * V;
+    const int cve = blockIdx.x * CB + ce;
+    if (cve >= CV) continue;
+    const int gc = cve * V + i, g = gc / d.C, ch = gc - g * d.C;
+    atomicAdd(dw + g * dw_gstride + (int64_t)ch * K * K + r0 * K + t, red[e]);
   }
 }
 
@@ -257,23 +304,53 @@ void launch_dgrad(const T* dy, const T* w, T* dx, const DWGeom& d, int st, hipSt
     launch_dgrad_v<K, 1, T>(dy, w, dx, d, st, stream);
 }
 
+// channel groups per block: the widest power of two <= 64 that leaves at most
+// 1/8 of the block's channel lanes idle
+inline int wgrad_lcb(int CV) {
+  int l = 6;
+  while (l > 0) {
+    const int cb = 1 << l;
+    const int64_t n = (int64_t)(CV + cb - 1) / cb * cb;
+    if ((n - CV) * 8 <= CV) break;
+    --l;
+  }
+  return l;
+}
+
+template <int K, int RB, int V, typename T>
+void launch_wgrad_k(const T* x, const T* dy, float* dw, int64_t dw_gstride, const DWGeom& d,
+                    int st, hipStream_t stream) {
+  constexpr int X = 4;
+  const int CV = d.G * d.C / V;
+  const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
+  const int cblocks = (CV + CB - 1) / CB;
+  constexpr int bands = K / RB;
+  const int64_t Pn = (int64_t)d.B * d.Ho * ((d.Wo + X - 1) / X);
+  // ~1024 blocks; every position lane at least 2 positions (bounds the atomics)
+  int64_t slabs = (1024 + (int64_t)cblocks * bands - 1) / ((int64_t)cblocks * bands);
+  int64_t per = (Pn + slabs - 1) / slabs;
+  if (per < 2 * PR) per = 2 * PR;
+  slabs = (Pn + per - 1) / per;
+  dim3 grid(cblocks, (unsigned)slabs, bands);
+  if (st == 1)
+    dw_wgrad_kernel<K, RB, 1, X, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, lcb,
+                                                                 per);
+  else
+    dw_wgrad_kernel<K, RB, 2, X, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, lcb,
+                                                                 per);
+}
+
 template <int V, typename T>
 void launch_wgrad(const T* x, const T* dy, float* dw, int64_t dw_gstride, const DWGeom& d, int k,
                   int st, hipStream_t stream) {
-  const int64_t P = (int64_t)d.B * d.Ho * d.Wo;
-  const int cblocks = d.G * d.C / V;
-  const int bands = (k == 7) ? 7 : 1;      // k = 7: one filter row per block (56 accumulators)
-  int64_t slabs = (2048 + (int64_t)cblocks * bands - 1) / ((int64_t)cblocks * bands);
-  int64_t per = (P + slabs - 1) / slabs;
-  if (per < 256) per = 256;
-  slabs = (P + per - 1) / per;
-  dim3 grid(cblocks, (unsigned)slabs, bands);
+  // k = 3: the whole filter per block (72 accumulators at V = 8); k = 5 / 7:
+  // one filter row per block
   if (k == 3)
-    dw_wgrad_kernel<3, 3, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    launch_wgrad_k<3, 3, V, T>(x, dy, dw, dw_gstride, d, st, stream);
   else if (k == 5)
-    dw_wgrad_kernel<5, 5, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    launch_wgrad_k<5, 1, V, T>(x, dy, dw, dw_gstride, d, st, stream);
   else
-    dw_wgrad_kernel<7, 1, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, st, per);
+    launch_wgrad_k<7, 1, V, T>(x, dy, dw, dw_gstride, d, st, stream);
 }
 
 }  // namespace

@@ -309,7 +309,9 @@ def test_conv_bn_fused_matches_oracle(case, variant):
     (2, 14, 14, 32, 1, 2, 3, 1), (2, 15, 13, 48, 2, 3, 3, 1), (3, 7, 7, 16, 1, 1, 3, 1),
     (2, 14, 14, 16, 1, 2, 5, 2), (2, 14, 14, 24, 2, 2, 5, (1, 2, 1, 2)),     # NASNet 5x5
     (2, 28, 28, 16, 2, 2, 7, (2, 3, 2, 3)), (2, 7, 7, 8, 1, 3, 7, 3),          # NASNet 7x7
-    (2, 15, 15, 8, 2, 2, 7, (3, 3, 3, 3)), (1, 9, 10, 8, 2, 2, 3, (0, 1, 0, 1))])
+    (2, 15, 15, 8, 2, 2, 7, (3, 3, 3, 3)), (1, 9, 10, 8, 2, 2, 3, (0, 1, 0, 1)),
+    # wide packs: wgrad channel blocks of 32 / 64 groups, and idle lanes (144 / 8 = 18)
+    (2, 14, 14, 96, 1, 8, 3, 1), (1, 8, 9, 512, 2, 2, 3, 1), (2, 9, 11, 144, 2, 1, 3, 1)])
 def test_dwconv_matches_oracle(case):
     """Depthwise k in {3,5,7}, stride 1/2, symmetric and Keras-asymmetric padding."""
     B, H, W, C, s, G, k, pad = case
