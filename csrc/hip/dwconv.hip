@@ -14,8 +14,9 @@
 //  fwd   : one thread = 8 channels x 4 consecutive output columns; per filter
 //          row the (4-1)*stride + k input pixels are loaded once (sliding
 //          window) instead of 4k times
-//  dgrad : one thread = 8 channels x 1 input pixel (gathers the dy taps that
-//          reach it; stride 2 handled by divisibility)
+//  dgrad : one thread = 8 channels x 4 consecutive input columns (gathers
+//          the dy taps that reach them; a sliding dy window at stride 1,
+//          divisibility checks at stride 2)
 //  wgrad : block = up to 64 channel groups x 256/CB position lanes x a band
 //          of filter rows; channel-contiguous lanes (coalesced), 4 output
 //          columns per position with a sliding input window, shuffle + LDS
@@ -101,22 +102,31 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x,
   }
 }
 
+// one thread = V channels x DW_X consecutive input columns: each filter row's
+// weights are loaded once per 4 pixels, and at stride 1 the row's
+// DW_X + K - 1 dy pixels once (sliding window) instead of 4K times
 template <int K, int ST, int V, typename T>
 __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
                                                        const T* __restrict__ w,
                                                        T* __restrict__ dx, DWGeom d) {
   const int GC = d.G * d.C, CV = GC / V;
+  const int xgroups = (d.W + DW_X - 1) / DW_X;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)d.B * d.H * d.W * CV;
+  const int64_t total = (int64_t)d.B * d.H * xgroups * CV;
   if (idx >= total) return;
   const int cv = (int)(idx % CV);
   int64_t t = idx / CV;
-  const int wi = (int)(t % d.W);
-  t /= d.W;
+  const int xg = (int)(t % xgroups);
+  t /= xgroups;
   const int hi = (int)(t % d.H);
   const int b = (int)(t / d.H);
   const int gc0 = cv * V;
-  float acc[V] = {};
+  const int wi0 = xg * DW_X;
+  float acc[DW_X][V];
+#pragma unroll
+  for (int xi = 0; xi < DW_X; ++xi)
+#pragma unroll
+    for (int i = 0; i < V; ++i) acc[xi][i] = 0.f;
   for (int r = 0; r < K; ++r) {
     const int hn = hi + d.pt - r;
     if (hn < 0 || hn % ST) continue;
@@ -124,19 +134,49 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
     if (ho >= d.Ho) continue;
     float wr[K][V];
     load_wrow<K, V, T>(w, d, gc0, r, wr);
+    const T* dyrow = dy + ((int64_t)b * d.Ho + ho) * d.Wo * GC + gc0;
+    if constexpr (ST == 1) {
+      // window j <-> output column wi0 + pl - (K - 1) + j
+      constexpr int NWIN = DW_X + K - 1;
+      const int wo_lo = wi0 + d.pl - (K - 1);
+      float win[NWIN][V];
 #pragma unroll
-    for (int s = 0; s < K; ++s) {
-      const int wn = wi + d.pl - s;
-      if (wn < 0 || wn % ST) continue;
-      const int wo = wn / ST;
-      if (wo >= d.Wo) continue;
-      float v[V];
-      ldv<V>(dy + (((int64_t)b * d.Ho + ho) * d.Wo + wo) * GC + gc0, v);
+      for (int j = 0; j < NWIN; ++j) {
+        const int wo = wo_lo + j;
+        if (wo >= 0 && wo < d.Wo) {
+          ldv<V>(dyrow + (int64_t)wo * GC, win[j]);
+        } else {
 #pragma unroll
-      for (int i = 0; i < V; ++i) acc[i] += v[i] * wr[s][i];
+          for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int xi = 0; xi < DW_X; ++xi)
+#pragma unroll
+        for (int s = 0; s < K; ++s)
+#pragma unroll
+          for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wr[s][i];
+    } else {
+#pragma unroll
+      for (int xi = 0; xi < DW_X; ++xi)
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+          const int wn = wi0 + xi + d.pl - s;
+          if (wn < 0 || wn % ST) continue;
+          const int wo = wn / ST;
+          if (wo >= d.Wo) continue;
+          float v[V];
+          ldv<V>(dyrow + (int64_t)wo * GC, v);
+#pragma unroll
+          for (int i = 0; i < V; ++i) acc[xi][i] += v[i] * wr[s][i];
+        }
     }
   }
-  stv<V>(dx + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, acc);
+#pragma unroll
+  for (int xi = 0; xi < DW_X; ++xi) {
+    const int wi = wi0 + xi;
+    if (wi < d.W) stv<V>(dx + (((int64_t)b * d.H + hi) * d.W + wi) * GC + gc0, acc[xi]);
+  }
 }
 
 // grid (ceil(CV / CB), position slabs, K / RB filter-row bands), CV = GC / V
@@ -289,7 +329,7 @@ void launch_fwd(const T* x, const T* w, T* y, const DWGeom& d, int st, hipStream
 template <int K, int V, typename T>
 void launch_dgrad_v(const T* dy, const T* w, T* dx, const DWGeom& d, int st,
                     hipStream_t stream) {
-  const int64_t n = (int64_t)d.B * d.H * d.W * (d.G * d.C / V);
+  const int64_t n = (int64_t)d.B * d.H * ((d.W + DW_X - 1) / DW_X) * (d.G * d.C / V);
   if (st == 1)
     dw_dgrad_kernel<K, 1, V, T><<<cer_blocks(n, 256), 256, 0, stream>>>(dy, w, dx, d);
   else
