@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ dw,
                                                        int64_t dw_gstride, DWGeom d, int lcb,
-                                                       int64_t pos_per_slab) {
+                                                       int pos_per_slab) {
   constexpr int NT = RB * K;
   constexpr int NWIN = (X - 1) * ST + K;
   __shared__ float red[64 * NT * V];
@@ -206,20 +206,22 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
   const int gc0 = cv * V;
   const int r0 = blockIdx.z * RB;
   const int xgroups = (d.Wo + X - 1) / X;
-  const int64_t Pn = (int64_t)d.B * d.Ho * xgroups;
-  const int64_t q0 = (int64_t)blockIdx.y * pos_per_slab;
-  const int64_t q1 = min(Pn, q0 + pos_per_slab);
+  // positions fit in 32 bits (checked on the host): 32-bit division per step
+  const int Pn = d.B * d.Ho * xgroups;
+  const int q0 = blockIdx.y * pos_per_slab;
+  const int q1 = min(Pn, q0 + pos_per_slab);
   float acc[NT][V];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[t][i] = 0.f;
   if (active) {
-    for (int64_t q = q0 + pr; q < q1; q += PR) {
-      const int xg = (int)(q % xgroups);
-      const int64_t u = q / xgroups;
-      const int ho = (int)(u % d.Ho);
-      const int b = (int)(u / d.Ho);
+    for (int q = q0 + pr; q < q1; q += PR) {
+      const unsigned u = (unsigned)q / (unsigned)xgroups;
+      const int xg = q - (int)u * xgroups;
+      const unsigned bq = u / (unsigned)d.Ho;
+      const int ho = (int)u - (int)bq * d.Ho;
+      const int b = (int)bq;
       const int wo0 = xg * X;
       float g[X][V];
 #pragma unroll
@@ -357,10 +359,14 @@ inline int wgrad_lcb(int CV) {
   return l;
 }
 
+#ifndef CER_DWW_X
+#define CER_DWW_X 4   // output columns per wgrad position (A/B twins: -DCER_DWW_X=2)
+#endif
+
 template <int K, int RB, int V, typename T>
 void launch_wgrad_k(const T* x, const T* dy, float* dw, int64_t dw_gstride, const DWGeom& d,
                     int st, hipStream_t stream) {
-  constexpr int X = 4;
+  constexpr int X = CER_DWW_X;
   const int CV = d.G * d.C / V;
   const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
   const int cblocks = (CV + CB - 1) / CB;
@@ -374,10 +380,10 @@ void launch_wgrad_k(const T* x, const T* dy, float* dw, int64_t dw_gstride, cons
   dim3 grid(cblocks, (unsigned)slabs, bands);
   if (st == 1)
     dw_wgrad_kernel<K, RB, 1, X, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, lcb,
-                                                                 per);
+                                                                 (int)per);
   else
     dw_wgrad_kernel<K, RB, 2, X, V, T><<<grid, 256, 0, stream>>>(x, dy, dw, dw_gstride, d, lcb,
-                                                                 per);
+                                                                 (int)per);
 }
 
 template <int V, typename T>
@@ -418,6 +424,7 @@ static int dwconv_bwd_t(const T* dy, const T* x, int B, int H, int W, int C, int
                            int k, int st, int pt, int pl, int Ho, int Wo, T* dx,
                            hipStream_t stream) {
   if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo)) return (int)hipErrorInvalidValue;
+  if ((int64_t)B * Ho * Wo > INT32_MAX) return (int)hipErrorInvalidValue;
   const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
   if (dx) {
     if (k == 3)

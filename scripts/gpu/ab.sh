@@ -7,7 +7,8 @@
 #           commas, e.g. "CER_NONE=0 CER_BN_FOLD=256 CER_HIP_LIB=libcerebro_hip_pf34.so"
 #           or "CER_WGB_SIDE_FRAC=0.5,CER_WGB_SPLIT_GRID=64" (A/B twins of the
 #           kernel library are built beforehand with tools.build --variant)
-# CONFIGS:  bench.py --configs values (default "8 1")
+# CONFIGS:  bench.py --configs values (default "8 1"); AB_ARGS (env) adds
+#           bench.py arguments, e.g. AB_ARGS="--model mobilenetv2"
 # ROUNDS:   back-to-back rounds over all variants (default 2)
 # TESTS:    optional pytest selection run once per variant first (e.g.
 #           "tests/test_fp32_gpu.py -k conv"); a failure stops the script
@@ -32,7 +33,7 @@ for R in $(seq 1 "$ROUNDS"); do
   for V in $VARIANTS; do
     for C in $CFGS; do
       F="$OUT/b_${V//[,\/]/_}_c${C}_$R"
-      env ${V//,/ } timeout -k 10 300 python -u bench.py --configs "$C" > "$F.json" 2> "$F.err" || exit $?
+      env ${V//,/ } timeout -k 10 300 python -u bench.py --configs "$C" ${AB_ARGS:-} > "$F.json" 2> "$F.err" || exit $?
       echo "$V c$C r$R $(python3 -c "import json;d=json.load(open('$F.json'));print(d['value'],d['ms_per_step'])")"
     done
   done
