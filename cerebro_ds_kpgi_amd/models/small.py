@@ -76,7 +76,7 @@ class PackedMobileNetV2(PackedNet):
             h = x
             if "exp" in blk:
                 h = self.conv_bn(h, blk["exp"], blk["exp_bn"], training, relu=6)
-            h = P.dwconv2d(h, self.ref(blk["dw"]), blk["stride"], 1)
+            h = P.dwconv2d(h, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
             h = self.bn(h, blk["dw_bn"], training, relu=6)
             h = self.conv_bn(h, blk["proj"], blk["proj_bn"], training, relu=False,
                              residual=x if blk["res"] else None)

@@ -50,7 +50,7 @@ class PackedMobileNetV1(PackedNet):
     def forward(self, x, training):
         x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True)
         for blk in self.blocks:
-            x = P.dwconv2d(x, self.ref(blk["dw"]), blk["stride"], 1)
+            x = P.dwconv2d(x, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
             x = self.bn(x, blk["dw_bn"], training, relu=6)
             x = self.conv_bn(x, blk["pw"], blk["pw_bn"], training, relu=6)
         x = P.global_avgpool(x)

@@ -37,6 +37,7 @@ IMPLEMENTED = {"adam", "loss", "gather"}
 # launch for layers with many tiles).  Buffers come zeroed from the step's
 # stats arena.
 STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "8"))
+SLAB_F64 = 1 << 24     # conv.hip: a returned slab count with this flag is fp64 slabs
 _RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
 
 c_p = ctypes.c_void_p
@@ -298,6 +299,8 @@ _SIGS2 = {
                        c_p, c_p],
     "cer_dwconv_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i,
                        c_i, c_i, c_i, c_p, c_p],
+    "cer_dwconv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
+                             c_i, c_p, c_p, c_i, c_p],
     "cer_avgpool_fwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_avgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_embbag_fwd": [c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p, c_p],
@@ -1218,6 +1221,42 @@ def dwconv_fwd(x, wref, stride, pad):
                               _ptr(y), _stream())
     _check(rc, "cer_dwconv_fwd")
     return y
+
+
+# smallest output (elements) that takes the fused depthwise forward + BN
+# statistics.  A sweep (0 / 4M / 16M, profiles/r3_secondary_published.md)
+# showed no size at which the plain forward + BN statistics pass wins, so 0.
+DW_STATS_MIN = int(os.environ.get("CER_DW_STATS_MIN", "0"))
+
+
+def dwconv_stats_ok(x, wref, stride, pad):
+    """The fused 3x3 forward + BN statistics (cer_dwconv_fwd_stats) applies."""
+    C, kh, kw = wref.spec.shape
+    if not (STAT_SLABS > 0 and kh == 3 and C % 8 == 0 and x.shape[-1] % 8 == 0):
+        return False
+    Ho, Wo = dw_out_hw(x.shape[1], x.shape[2], kh, stride, pad)
+    return x.shape[0] * Ho * Wo * x.shape[-1] >= DW_STATS_MIN
+
+
+def dwconv_fwd_stats(x, wref, stride, pad):
+    """y = dwconv(x) plus the BN (sum, sum^2) partials of y in the conv
+    epilogue's fp64 slab format; returns (y, part, nslab) for
+    ``bn_act_fwd_train_part`` (the BN then skips its statistics pass)."""
+    x = _act(x)
+    B, H, W, GC = x.shape
+    G = wref.G
+    C, kh, kw = wref.spec.shape
+    Ho, Wo = dw_out_hw(H, W, kh, stride, pad)
+    pt, _, pl, _ = _pad4(pad)
+    M = B * Ho * Wo
+    y = torch.empty((B, Ho, Wo, GC), dtype=x.dtype, device=x.device)
+    part = _stats_buffer(M, GC, x.device)
+    nsl = min(STAT_SLABS, (M + 63) // 64)
+    wp, ws = wref.work_ptr()
+    rc = _fn("cer_dwconv_fwd_stats", x)(_ptr(x), B, H, W, C, G, c_p(wp), ws, kh, stride, pt, pl,
+                                    Ho, Wo, _ptr(y), _ptr(part), nsl, _stream())
+    _check(rc, "cer_dwconv_fwd_stats")
+    return y, part, nsl | SLAB_F64
 
 
 def dwconv_bwd(dy, x, wref, stride, pad, need_dx):

@@ -17,6 +17,8 @@ Each op dispatches to our HIP kernel (``ops._hip``) or to the PyTorch oracle
 implementation in this file (``ops.backend``).
 """
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -252,7 +254,13 @@ def _flat_param(ref):
 
 def _bn_forward_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
     C = x.shape[-1]
+    part = getattr(x, "_cer_part", None)      # statistics from the producer (dwconv2d stats)
+    if part is not None:
+        del x._cer_part
     if _bn_hip(x, gref):
+        if part is not None and _bn_aligned(gref):
+            return _hip().bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, relu,
+                                                momentum, eps, part[0], part[1])
         return _hip().bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, relu, momentum, eps)
     x2 = x.reshape(-1, C).float()
     n = x2.shape[0]
@@ -672,17 +680,26 @@ def _zero_pad(x, pad):
     return F.pad(x, (0, 0, pl, pr, pt, pb))
 
 
+# CER_DW_STATS=0: the BN after a depthwise conv computes its own statistics
+_DW_STATS = os.environ.get("CER_DW_STATS", "1") != "0"
+
+
 class PackedDWConv2d(torch.autograd.Function):
     """Depthwise k x k conv (k in {3, 5, 7}), stride 1/2; ``pad`` is an int or
     (top, bottom, left, right) — Keras stride-2 ``correct_pad`` is asymmetric."""
 
     @staticmethod
-    def forward(ctx, x, anchor, wref, stride, pad):
+    def forward(ctx, x, anchor, wref, stride, pad, stats=False):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         C, kh, kw = wref.spec.shape
         ctx.hip = hip_gate("dwconv", kh == kw and kh in (3, 5, 7)
                            and stride in (1, 2) and max(_pad4(pad)) < kh, x)
-        if ctx.hip:
+        if ctx.hip and stats and _DW_STATS and _hip().dwconv_stats_ok(x, wref, stride, pad):
+            # BN (sum, sum^2) partials of y for the BN that consumes it
+            # (_bn_forward_train takes them instead of a statistics pass)
+            y, part, nslab = _hip().dwconv_fwd_stats(x, wref, stride, pad)
+            y._cer_part = (part, nslab)
+        elif ctx.hip:
             y = _hip().dwconv_fwd(x, wref, stride, pad)
         else:
             w = wref.work().reshape(wref.G * C, 1, kh, kw)
@@ -698,7 +715,7 @@ class PackedDWConv2d(torch.autograd.Function):
         dy = dy.contiguous()
         if ctx.hip:
             dx = _hip().dwconv_bwd(dy, x, wref, stride, pad, ctx.needs_input_grad[0])
-            return dx, None, None, None, None
+            return dx, None, None, None, None, None
         C, kh, kw = wref.spec.shape
         GC = wref.G * C
         w = wref.work().reshape(GC, 1, kh, kw)
@@ -711,11 +728,13 @@ class PackedDWConv2d(torch.autograd.Function):
             dx = _nhwc(dxp[:, :, pt:pt + x.shape[1], pl:pl + x.shape[2]])
         dw = torch.nn.grad.conv2d_weight(xp, w.shape, dyn, stride, 0, 1, GC)
         wref.grad().copy_(dw.view(wref.G, C, kh, kw))
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
-def dwconv2d(x, wref, stride=1, pad=1, anchor=None):
-    return PackedDWConv2d.apply(x, anchor, wref, stride, pad)
+def dwconv2d(x, wref, stride=1, pad=1, anchor=None, stats=False):
+    """``stats``: the output's consumer is a training-mode BN (``bn_act``);
+    the HIP 3x3 path then also emits its batch statistics."""
+    return PackedDWConv2d.apply(x, anchor, wref, stride, pad, stats)
 
 
 # ---------------------------------------------------------------------------

@@ -288,6 +288,119 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
   }
 }
 
+// 3x3 forward + the BN (sum, sum^2) partials of its output for the BN that
+// consumes it (ops.nn.dwconv2d stats=True), so that BN skips its statistics
+// pass.  Layout as dw_wgrad_kernel: grid (ceil(CV / CB), position slabs),
+// thread = (position lane, channel group of 8); the whole 3x3 x 8 filter stays
+// in registers for the slab; per position the fwd sliding window.  Position
+// lanes reduce by shuffles, the 4 waves through LDS in a fixed order, then
+// fp64 atomics into slab (blockIdx.y % nsl) of the [nsl][2][GC] buffer in the
+// conv epilogue's SLAB_F64 format (conv.hip stat_store), which bn.hip's
+// fold-finalize apply reads.
+template <int ST, typename T>
+__global__ __launch_bounds__(256) void dw_fwd_stats_kernel(const T* __restrict__ x,
+                                                           const T* __restrict__ w,
+                                                           T* __restrict__ y, DWGeom d, int lcb,
+                                                           int pos_per_slab,
+                                                           float* __restrict__ part, int nsl) {
+  constexpr int K = 3, V = DW_V, X = DW_X;
+  constexpr int NWIN = (X - 1) * ST + K;
+  __shared__ float red[4][64][2 * V];
+  const int CB = 1 << lcb;
+  const int GC = d.G * d.C, CV = GC / V;
+  const int c = threadIdx.x & (CB - 1), pr = threadIdx.x >> lcb, PR = 256 >> lcb;
+  const int cv = blockIdx.x * CB + c;
+  const bool active = cv < CV;
+  const int gc0 = cv * V;
+  const int xgroups = (d.Wo + X - 1) / X;
+  const int Pn = d.B * d.Ho * xgroups;
+  const int q0 = blockIdx.y * pos_per_slab;
+  const int q1 = min(Pn, q0 + pos_per_slab);
+  float sm[V], sq[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) sm[i] = sq[i] = 0.f;
+  if (active) {
+    float wk[K][K][V];
+#pragma unroll
+    for (int r = 0; r < K; ++r) load_wrow<K, V, T>(w, d, gc0, r, wk[r]);
+    for (int q = q0 + pr; q < q1; q += PR) {
+      const unsigned u = (unsigned)q / (unsigned)xgroups;
+      const int xg = q - (int)u * xgroups;
+      const unsigned bq = u / (unsigned)d.Ho;
+      const int ho = (int)u - (int)bq * d.Ho;
+      const int b = (int)bq;
+      const int wo0 = xg * X;
+      const int wi0 = wo0 * ST - d.pl;
+      float acc[X][V];
+#pragma unroll
+      for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[xi][i] = 0.f;
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int hi = ho * ST - d.pt + r;
+        if (hi < 0 || hi >= d.H) continue;
+        const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
+        float win[NWIN][V];
+#pragma unroll
+        for (int j = 0; j < NWIN; ++j) {
+          const int wi = wi0 + j;
+          if (wi >= 0 && wi < d.W) {
+            ldv<V>(xrow + (int64_t)wi * GC, win[j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+          for (int s = 0; s < K; ++s)
+#pragma unroll
+            for (int i = 0; i < V; ++i) acc[xi][i] += win[xi * ST + s][i] * wk[r][s][i];
+      }
+#pragma unroll
+      for (int xi = 0; xi < X; ++xi) {
+        if (wo0 + xi >= d.Wo) continue;
+        T* yp = y + (((int64_t)b * d.Ho + ho) * d.Wo + wo0 + xi) * GC + gc0;
+        stv<V>(yp, acc[xi]);
+        // statistics of the STORED values (bf16 output: rounded as BN reads them)
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          float v = acc[xi][i];
+          if constexpr (!std::is_same<T, float>::value) v = bf2f(f2bf(v));
+          sm[i] += v;
+          sq[i] += v * v;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    for (int o = CB; o < 64; o <<= 1) {
+      sm[i] += __shfl_xor(sm[i], o, 64);
+      sq[i] += __shfl_xor(sq[i], o, 64);
+    }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < CB) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      red[wid][lane][i] = sm[i];
+      red[wid][lane][V + i] = sq[i];
+    }
+  }
+  __syncthreads();
+  double* slab = reinterpret_cast<double*>(part) + (int64_t)(blockIdx.y % nsl) * 2 * GC;
+  for (int e = threadIdx.x; e < CB * 2 * V; e += 256) {
+    const int ce = e / (2 * V), rem = e - ce * (2 * V);
+    const int cve = blockIdx.x * CB + ce;
+    if (cve >= CV) continue;
+    const float v = red[0][ce][rem] + red[1][ce][rem] + red[2][ce][rem] + red[3][ce][rem];
+    const int row = rem / V, i = rem - row * V;
+    atomicAdd(slab + (int64_t)row * GC + cve * V + i, (double)v);
+  }
+}
+
 DWGeom make_dw(int B, int H, int W, int C, int G, int pt, int pl, int Ho, int Wo, int64_t ws) {
   DWGeom d;
   d.B = B;
@@ -441,6 +554,31 @@ static int dwconv_bwd_t(const T* dy, const T* x, int B, int H, int W, int C, int
   return (int)hipGetLastError();
 }
 
+// 3x3, every config's C % 8 == 0; ``part`` zeroed [nsl][2][G*C] doubles
+template <typename T>
+static int dwconv_fwd_stats_t(const T* x, int B, int H, int W, int C, int G, const T* w,
+                              int64_t w_gstride, int k, int st, int pt, int pl, int Ho, int Wo,
+                              T* y, float* part, int nsl, hipStream_t stream) {
+  if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo) || k != 3 || C % DW_V || nsl <= 0)
+    return (int)hipErrorInvalidValue;
+  if ((int64_t)B * Ho * Wo > INT32_MAX) return (int)hipErrorInvalidValue;
+  const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
+  const int CV = G * C / DW_V;
+  const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
+  const int cblocks = (CV + CB - 1) / CB;
+  const int64_t Pn = (int64_t)B * Ho * ((Wo + DW_X - 1) / DW_X);
+  int64_t slabs = (1024 + cblocks - 1) / cblocks;
+  int64_t per = (Pn + slabs - 1) / slabs;
+  if (per < 2 * PR) per = 2 * PR;
+  slabs = (Pn + per - 1) / per;
+  dim3 grid(cblocks, (unsigned)slabs);
+  if (st == 1)
+    dw_fwd_stats_kernel<1, T><<<grid, 256, 0, stream>>>(x, w, y, d, lcb, (int)per, part, nsl);
+  else
+    dw_fwd_stats_kernel<2, T><<<grid, 256, 0, stream>>>(x, w, y, d, lcb, (int)per, part, nsl);
+  return (int)hipGetLastError();
+}
+
 #define CER_DW_ENTRY_POINTS(T, SFX)                                                              \
   CER_API int cer_dwconv_fwd##SFX(const T* x, int B, int H, int W, int C, int G, const T* w,    \
                                   int64_t w_gstride, int k, int st, int pt, int pl, int Ho,     \
@@ -453,6 +591,13 @@ static int dwconv_bwd_t(const T* dy, const T* x, int B, int H, int W, int C, int
                                   hipStream_t stream) {                                         \
     return dwconv_bwd_t<T>(dy, x, B, H, W, C, G, w, w_gstride, dw, dw_gstride, k, st, pt, pl,   \
                            Ho, Wo, dx, stream);                                                 \
+  }                                                                                              \
+  CER_API int cer_dwconv_fwd_stats##SFX(const T* x, int B, int H, int W, int C, int G,          \
+                                        const T* w, int64_t w_gstride, int k, int st, int pt,   \
+                                        int pl, int Ho, int Wo, T* y, float* part, int nsl,     \
+                                        hipStream_t stream) {                                   \
+    return dwconv_fwd_stats_t<T>(x, B, H, W, C, G, w, w_gstride, k, st, pt, pl, Ho, Wo, y,     \
+                                 part, nsl, stream);                                            \
   }
 
 CER_DW_ENTRY_POINTS(bf16_t, )

@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r3tier
-bash scripts/gpu/gpu_tier.sh r3a || exit $?
+bash scripts/gpu/gpu_tier.sh ${1:-r3a} || exit $?
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3tier/smoke.log 2>&1 || exit $?
 tail -1 gpurun_out/r3tier/smoke.log
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r3tier/driver.json 2> gpurun_out/r3tier/driver.err || exit $?
