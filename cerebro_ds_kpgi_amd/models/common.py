@@ -89,9 +89,12 @@ class PackedNet(object):
     def conv(self, x, c, anchor=False):
         return P.conv2d(x, self.ref(c.w), c.stride, c.pad, self.anchor if anchor else None)
 
-    def bn(self, x, b, training, relu=True, residual=None):
+    def bn(self, x, b, training, relu=True, residual=None, link_out=False):
+        """``link_out``: the output's only consumer is the next ``conv_bn``,
+        whose dgrad epilogue then computes this BN's backward partials."""
         return P.bn_act(x, self.ref(b.g), self.ref(b.b), self.ref(b.rm), self.ref(b.rv),
-                        training, relu, residual, self.bn_momentum, self.bn_eps)
+                        training, relu, residual, self.bn_momentum, self.bn_eps,
+                        link_out and self.bn_links)
 
     def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False, join=None,
                 res_join=None, link_out=False, hl_out=False):

@@ -77,7 +77,7 @@ class PackedMobileNetV2(PackedNet):
             if "exp" in blk:
                 h = self.conv_bn(h, blk["exp"], blk["exp_bn"], training, relu=6)
             h = P.dwconv2d(h, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
-            h = self.bn(h, blk["dw_bn"], training, relu=6)
+            h = self.bn(h, blk["dw_bn"], training, relu=6, link_out=True)
             h = self.conv_bn(h, blk["proj"], blk["proj_bn"], training, relu=False,
                              residual=x if blk["res"] else None)
             x = h

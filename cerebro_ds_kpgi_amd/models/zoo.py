@@ -51,7 +51,7 @@ class PackedMobileNetV1(PackedNet):
         x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True)
         for blk in self.blocks:
             x = P.dwconv2d(x, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
-            x = self.bn(x, blk["dw_bn"], training, relu=6)
+            x = self.bn(x, blk["dw_bn"], training, relu=6, link_out=True)
             x = self.conv_bn(x, blk["pw"], blk["pw_bn"], training, relu=6)
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)

@@ -284,12 +284,19 @@ class PackedBNAct(torch.autograd.Function):
     """y = act(BN(x) + residual);  BN statistics per packed channel."""
 
     @staticmethod
-    def forward(ctx, x, residual, gref, bref, rmref, rvref, relu, momentum, eps):
+    def forward(ctx, x, residual, gref, bref, rmref, rvref, relu, momentum, eps, link=None):
         ctx.refs = (gref, bref)
         ctx.relu = relu
         ctx.has_res = residual is not None
         y, mean, invstd = _bn_forward_train(x, residual, gref, bref, rmref, rvref, relu, momentum,
                                             eps)
+        ctx.link = None
+        if link is not None and _bn_hip(x, gref) and _bn_aligned(gref):
+            # the consumer conv's dgrad epilogue computes this BN's backward
+            # partials (BNLink; e.g. MobileNetV2's depthwise BN -> projection)
+            link.z, link.mean, link.invstd = x, mean, invstd
+            link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
+            ctx.link = link
         ctx.save_for_backward(x, y, mean, invstd)
         return y
 
@@ -297,8 +304,15 @@ class PackedBNAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, mean, invstd = ctx.saved_tensors
         gref, bref = ctx.refs
-        dx, dres = _bn_backward(ctx, dy.contiguous(), x, y, mean, invstd, gref, bref)
-        return dx, dres, None, None, None, None, None, None, None
+        link = ctx.link
+        if link is not None and link.part is not None:
+            dx, dres = _hip().bn_act_bwd(dy.contiguous(), x, y, mean, invstd, gref, bref,
+                                         ctx.relu, ctx.has_res, part=link.part, nslab=link.nslab)
+        else:
+            dx, dres = _bn_backward(ctx, dy.contiguous(), x, y, mean, invstd, gref, bref)
+        if link is not None:
+            link.z = link.mean = link.invstd = link.part = None
+        return dx, dres, None, None, None, None, None, None, None, None
 
 
 class PackedConvBNAct(torch.autograd.Function):
@@ -454,9 +468,15 @@ def bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps):
 
 
 def bn_act(x, gref, bref, rmref, rvref, training, relu=True, residual=None,
-           momentum=0.1, eps=1e-5):
+           momentum=0.1, eps=1e-5, link_out=False):
+    """``link_out`` (training): the output's whole gradient comes out of one
+    consumer conv's dgrad (see BNLink), which computes the BN backward partials."""
     if training:
-        return PackedBNAct.apply(x, residual, gref, bref, rmref, rvref, relu, momentum, eps)
+        link = BNLink() if link_out else None
+        y = PackedBNAct.apply(x, residual, gref, bref, rmref, rvref, relu, momentum, eps, link)
+        if link is not None:
+            y._cer_bnlink = link
+        return y
     return bn_act_eval(x, residual, gref, bref, rmref, rvref, relu, eps)
 
 

@@ -81,3 +81,62 @@ def test_dwconv_stats_matches_bn_pass(G, C, B, H, s, dtype):
     assert _rel(st1, st0) < 1e-5
     assert _rel(dx1, dx0) < tol
     assert _rel(g1, g0) < tol
+
+
+@pytest.mark.parametrize("G,C,B,H,dtype", [(8, 96, 4, 14, torch.float32), (1, 144, 3, 11, torch.float32),
+                                           (4, 96, 4, 14, torch.bfloat16)])
+def test_standalone_bn_link_matches_own_pass(G, C, B, H, dtype, monkeypatch):
+    """dwconv -> BN (link_out) -> 1x1 conv_bn (MobileNetV2's depthwise BN and
+    projection): the projection's dgrad epilogue computes the BN backward
+    partials; against the BN's own backward pass."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    Co = 64
+    specs = [ParamSpec("dw", (C, 3, 3), "weight", fan_in=9)]
+    for i, c in ((1, C), (2, Co)):
+        specs += [ParamSpec("g%d" % i, (c,), "gamma"), ParamSpec("b%d" % i, (c,), "beta"),
+                  ParamSpec("rm%d" % i, (c,), "running_mean"),
+                  ParamSpec("rv%d" % i, (c,), "running_var")]
+    specs.insert(5, ParamSpec("w2", (Co, 1, 1, C), "weight", fan_in=C))
+    used = []
+    real = _hip.bn_act_bwd
+
+    def spy(*a, **k):
+        used.append(k.get("part") is not None)
+        return real(*a, **k)
+    monkeypatch.setattr(_hip, "bn_act_bwd", spy)
+    torch.manual_seed(12)
+    x0 = torch.randn(B, H, H, G * C, device="cuda").to(dtype)
+    go = torch.randn(B, H, H, G * Co, device="cuda").to(dtype)
+    res = []
+    for link in (False, True):
+        used.clear()
+        torch.manual_seed(1000)
+        a = Arena(ModelLayout(specs), G, "cuda", dtype)
+        for g in range(G):
+            a.init_model(g, 5 + g)
+        for sp in specs:
+            if sp.kind in ("gamma", "beta"):
+                a.master_view(sp).uniform_(0.5, 1.5)
+        a.sync_work()
+        r = {sp.name: ParamRef(a, sp) for sp in specs}
+        _hip.conv_set_variant(0, 0)
+        _hip.conv_set_variant(1, 0)
+        try:
+            x = x0.clone().requires_grad_(True)
+            h = P.dwconv2d(x, r["dw"], 1, 1, stats=True)
+            h = P.bn_act(h, r["g1"], r["b1"], r["rm1"], r["rv1"], True, relu=6, link_out=link)
+            o = P.conv_bn_act(h, r["w2"], r["g2"], r["b2"], r["rm2"], r["rv2"], 1, 0, 6)
+            o.backward(go)
+            torch.cuda.synchronize()
+        finally:
+            _hip.conv_set_variant(0, -1)
+            _hip.conv_set_variant(1, -1)
+        # the depthwise BN is the last BN backward to run
+        assert used[-1] == link, used
+        res.append((o.detach(), x.grad, a.state.clone(), a.grad.clone()))
+    (o0, dx0, st0, g0), (o1, dx1, st1, g1) = res
+    assert torch.equal(o0, o1)
+    assert torch.equal(st0, st1)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(dx1, dx0) < tol
+    assert _rel(g1, g0) < tol
