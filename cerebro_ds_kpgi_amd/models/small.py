@@ -75,7 +75,8 @@ class PackedMobileNetV2(PackedNet):
         for blk in self.blocks:
             h = x
             if "exp" in blk:
-                h = self.conv_bn(h, blk["exp"], blk["exp_bn"], training, relu=6)
+                h = self.conv_bn(h, blk["exp"], blk["exp_bn"], training, relu=6,
+                                 link_out=True)     # its sole consumer: the depthwise dgrad
             h = P.dwconv2d(h, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
             h = self.bn(h, blk["dw_bn"], training, relu=6, link_out=True)
             h = self.conv_bn(h, blk["proj"], blk["proj_bn"], training, relu=False,

@@ -301,6 +301,8 @@ _SIGS2 = {
                        c_i, c_i, c_i, c_p, c_p],
     "cer_dwconv_fwd_stats": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
                              c_i, c_p, c_p, c_i, c_p],
+    "cer_dwconv_bwd_bn": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_p,
+                          c_i64, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_i, c_p],
     "cer_avgpool_fwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_avgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_embbag_fwd": [c_p, c_i, c_i, c_i, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p, c_p],
@@ -1259,7 +1261,9 @@ def dwconv_fwd_stats(x, wref, stride, pad):
     return y, part, nsl | SLAB_F64
 
 
-def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
+def dwconv_bwd(dy, x, wref, stride, pad, need_dx, bnlink=None):
+    """``bnlink``: the BNLink of the BN that produced ``x`` (its output); when
+    usable, dx also yields that BN's backward partials (``link.part``)."""
     dy = _act(dy)
     x = _act(x)
     B, H, W, GC = x.shape
@@ -1272,6 +1276,21 @@ def dwconv_bwd(dy, x, wref, stride, pad, need_dx):
     dx = torch.empty_like(x) if need_dx else None
     wp, ws = wref.work_ptr()
     gp, gs = wref.grad_ptr()
+    link = bnlink
+    if (link is not None and need_dx and link.z is not None and link.part is None
+            and not link.has_res and _act_code(link.act) in (0, 1, 6) and STAT_SLABS > 0
+            and kh == 3 and C % 8 == 0 and link.z.shape == x.shape
+            and link.z.dtype == x.dtype):
+        M = B * H * W
+        part = _stats_buffer(M, GC, x.device)
+        nsl = min(STAT_SLABS, (M + 63) // 64)
+        rc = _fn("cer_dwconv_bwd_bn", dy)(_ptr(dy), _ptr(x), _ptr(link.z), _ptr(link.mean),
+                                      _ptr(link.invstd), _act_code(link.act), B, H, W, C, G,
+                                      c_p(wp), ws, c_p(gp), gs, kh, stride, pt, pl, Ho, Wo,
+                                      _ptr(dx), _ptr(part), nsl, _stream())
+        _check(rc, "cer_dwconv_bwd_bn")
+        link.part, link.nslab = part, nsl | SLAB_F64
+        return dx
     rc = _fn("cer_dwconv_bwd", dy)(_ptr(dy), _ptr(x), B, H, W, C, G, c_p(wp), ws, c_p(gp), gs, kh,
                               stride, pt, pl, Ho, Wo, _ptr(dx), _stream())
     _check(rc, "cer_dwconv_bwd")

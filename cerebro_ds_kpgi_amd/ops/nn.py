@@ -702,6 +702,8 @@ def _zero_pad(x, pad):
 
 # CER_DW_STATS=0: the BN after a depthwise conv computes its own statistics
 _DW_STATS = os.environ.get("CER_DW_STATS", "1") != "0"
+# CER_DW_BNLINK=0: the BN before a depthwise conv runs its own backward pass
+_DW_BNLINK = os.environ.get("CER_DW_BNLINK", "1") != "0"
 
 
 class PackedDWConv2d(torch.autograd.Function):
@@ -711,6 +713,8 @@ class PackedDWConv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, stride, pad, stats=False):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
+        # x is a linked BN's output: dgrad computes that BN's backward partials
+        ctx.bnlink = getattr(x, "_cer_bnlink", None) if _DW_BNLINK else None
         C, kh, kw = wref.spec.shape
         ctx.hip = hip_gate("dwconv", kh == kw and kh in (3, 5, 7)
                            and stride in (1, 2) and max(_pad4(pad)) < kh, x)
@@ -734,7 +738,8 @@ class PackedDWConv2d(torch.autograd.Function):
         wref, stride, pad = ctx.wref, ctx.stride, ctx.pad
         dy = dy.contiguous()
         if ctx.hip:
-            dx = _hip().dwconv_bwd(dy, x, wref, stride, pad, ctx.needs_input_grad[0])
+            dx = _hip().dwconv_bwd(dy, x, wref, stride, pad, ctx.needs_input_grad[0],
+                                   bnlink=ctx.bnlink)
             return dx, None, None, None, None, None
         C, kh, kw = wref.spec.shape
         GC = wref.G * C

@@ -401,6 +401,145 @@ __global__ __launch_bounds__(256) void dw_fwd_stats_kernel(const T* __restrict__
   }
 }
 
+// 3x3 input gradient + the backward partials of the BN that PRODUCED the
+// depthwise input (BN link, ops.nn.BNLink: MobileNetV2's expansion BN), so
+// that BN skips its own pass over (dy, z, y).  dx is that BN's output
+// gradient d; with its output y (= this conv's input) and input z:
+//   dz = act'(y) d,  partials (sum dz, sum dz (z - mean) invstd)
+// -- the conv dgrad epilogue's YM_Y arithmetic (conv.hip epi32 bnbwd), over
+// the STORED d.  Layout and reduction as dw_fwd_stats_kernel (positions are
+// 4 input columns); fp64 atomics into slab (blockIdx.y % nsl).
+template <int ST, typename T>
+__global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
+    const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx, DWGeom d, int lcb,
+    int pos_per_slab, const T* __restrict__ ybn, const T* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int act,
+    float* __restrict__ part, int nsl) {
+  constexpr int K = 3, V = DW_V, X = DW_X;
+  __shared__ float red[4][64][2 * V];
+  const int CB = 1 << lcb;
+  const int GC = d.G * d.C, CV = GC / V;
+  const int c = threadIdx.x & (CB - 1), pr = threadIdx.x >> lcb, PR = 256 >> lcb;
+  const int cv = blockIdx.x * CB + c;
+  const bool active = cv < CV;
+  const int gc0 = cv * V;
+  const int xgroups = (d.W + X - 1) / X;
+  const int Pn = d.B * d.H * xgroups;
+  const int q0 = blockIdx.y * pos_per_slab;
+  const int q1 = min(Pn, q0 + pos_per_slab);
+  float sm[V], sq[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) sm[i] = sq[i] = 0.f;
+  if (active) {
+    float wk[K][K][V], mu[V], is[V];
+#pragma unroll
+    for (int r = 0; r < K; ++r) load_wrow<K, V, T>(w, d, gc0, r, wk[r]);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      mu[i] = mean[gc0 + i];
+      is[i] = invstd[gc0 + i];
+    }
+    for (int q = q0 + pr; q < q1; q += PR) {
+      const unsigned u = (unsigned)q / (unsigned)xgroups;
+      const int xg = q - (int)u * xgroups;
+      const unsigned bq = u / (unsigned)d.H;
+      const int hi = (int)u - (int)bq * d.H;
+      const int b = (int)bq;
+      const int wi0 = xg * X;
+      float acc[X][V];
+#pragma unroll
+      for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[xi][i] = 0.f;
+#pragma unroll
+      for (int r = 0; r < K; ++r) {
+        const int hn = hi + d.pt - r;
+        if (hn < 0 || hn % ST) continue;
+        const int ho = hn / ST;
+        if (ho >= d.Ho) continue;
+        const T* dyrow = dy + ((int64_t)b * d.Ho + ho) * d.Wo * GC + gc0;
+        if constexpr (ST == 1) {
+          constexpr int NWIN = X + K - 1;
+          const int wo_lo = wi0 + d.pl - (K - 1);
+          float win[NWIN][V];
+#pragma unroll
+          for (int j = 0; j < NWIN; ++j) {
+            const int wo = wo_lo + j;
+            if (wo >= 0 && wo < d.Wo) {
+              ldv<V>(dyrow + (int64_t)wo * GC, win[j]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+            }
+          }
+#pragma unroll
+          for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+            for (int s = 0; s < K; ++s)
+#pragma unroll
+              for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wk[r][s][i];
+        } else {
+#pragma unroll
+          for (int xi = 0; xi < X; ++xi)
+#pragma unroll
+            for (int s = 0; s < K; ++s) {
+              const int wn = wi0 + xi + d.pl - s;
+              if (wn < 0 || wn % ST) continue;
+              const int wo = wn / ST;
+              if (wo >= d.Wo) continue;
+              float v[V];
+              ldv<V>(dyrow + (int64_t)wo * GC, v);
+#pragma unroll
+              for (int i = 0; i < V; ++i) acc[xi][i] += v[i] * wk[r][s][i];
+            }
+        }
+      }
+#pragma unroll
+      for (int xi = 0; xi < X; ++xi) {
+        if (wi0 + xi >= d.W) continue;
+        const int64_t off = (((int64_t)b * d.H + hi) * d.W + wi0 + xi) * GC + gc0;
+        stv<V>(dx + off, acc[xi]);
+        float yv[V], zv[V];
+        ldv<V>(ybn + off, yv);
+        ldv<V>(z + off, zv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          float dd = acc[xi][i];
+          if constexpr (!std::is_same<T, float>::value) dd = bf2f(f2bf(dd));
+          const bool pass = act == 6 ? (yv[i] > 0.f && yv[i] < 6.f) : act == 1 ? yv[i] > 0.f : true;
+          const float dz = pass ? dd : 0.f;
+          sm[i] += dz;
+          sq[i] += dz * (zv[i] - mu[i]) * is[i];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i)
+    for (int o = CB; o < 64; o <<= 1) {
+      sm[i] += __shfl_xor(sm[i], o, 64);
+      sq[i] += __shfl_xor(sq[i], o, 64);
+    }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < CB) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      red[wid][lane][i] = sm[i];
+      red[wid][lane][V + i] = sq[i];
+    }
+  }
+  __syncthreads();
+  double* slab = reinterpret_cast<double*>(part) + (int64_t)(blockIdx.y % nsl) * 2 * GC;
+  for (int e = threadIdx.x; e < CB * 2 * V; e += 256) {
+    const int ce = e / (2 * V), rem = e - ce * (2 * V);
+    const int cve = blockIdx.x * CB + ce;
+    if (cve >= CV) continue;
+    const float v = red[0][ce][rem] + red[1][ce][rem] + red[2][ce][rem] + red[3][ce][rem];
+    const int row = rem / V, i = rem - row * V;
+    atomicAdd(slab + (int64_t)row * GC + cve * V + i, (double)v);
+  }
+}
+
 DWGeom make_dw(int B, int H, int W, int C, int G, int pt, int pl, int Ho, int Wo, int64_t ws) {
   DWGeom d;
   d.B = B;
@@ -579,6 +718,40 @@ static int dwconv_fwd_stats_t(const T* x, int B, int H, int W, int C, int G, con
   return (int)hipGetLastError();
 }
 
+// backward with the producing BN's backward partials (dw_dgrad_bn_kernel):
+// 3x3, C % 8 == 0, act in {0, 1 (ReLU), 6 (ReLU6)}; ``part`` zeroed
+// [nsl][2][G*C] doubles; dw zero on entry
+template <typename T>
+static int dwconv_bwd_bn_t(const T* dy, const T* x, const T* z, const float* mean,
+                           const float* invstd, int act, int B, int H, int W, int C, int G,
+                           const T* w, int64_t w_gstride, float* dw, int64_t dw_gstride, int k,
+                           int st, int pt, int pl, int Ho, int Wo, T* dx, float* part, int nsl,
+                           hipStream_t stream) {
+  if (!dw_shape_ok(C, k, st, pt, pl, Ho, Wo) || k != 3 || C % DW_V || nsl <= 0 || !dx ||
+      (act != 0 && act != 1 && act != 6))
+    return (int)hipErrorInvalidValue;
+  if ((int64_t)B * H * W > INT32_MAX || (int64_t)B * Ho * Wo > INT32_MAX)
+    return (int)hipErrorInvalidValue;
+  const DWGeom d = make_dw(B, H, W, C, G, pt, pl, Ho, Wo, w_gstride);
+  const int CV = G * C / DW_V;
+  const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
+  const int cblocks = (CV + CB - 1) / CB;
+  const int64_t Pn = (int64_t)B * H * ((W + DW_X - 1) / DW_X);
+  int64_t slabs = (1024 + cblocks - 1) / cblocks;
+  int64_t per = (Pn + slabs - 1) / slabs;
+  if (per < 2 * PR) per = 2 * PR;
+  slabs = (Pn + per - 1) / per;
+  dim3 grid(cblocks, (unsigned)slabs);
+  if (st == 1)
+    dw_dgrad_bn_kernel<1, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z, mean,
+                                                       invstd, act, part, nsl);
+  else
+    dw_dgrad_bn_kernel<2, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z, mean,
+                                                       invstd, act, part, nsl);
+  launch_wgrad<DW_V, T>(x, dy, dw, dw_gstride, d, k, st, stream);
+  return (int)hipGetLastError();
+}
+
 #define CER_DW_ENTRY_POINTS(T, SFX)                                                              \
   CER_API int cer_dwconv_fwd##SFX(const T* x, int B, int H, int W, int C, int G, const T* w,    \
                                   int64_t w_gstride, int k, int st, int pt, int pl, int Ho,     \
@@ -598,6 +771,14 @@ static int dwconv_fwd_stats_t(const T* x, int B, int H, int W, int C, int G, con
                                         hipStream_t stream) {                                   \
     return dwconv_fwd_stats_t<T>(x, B, H, W, C, G, w, w_gstride, k, st, pt, pl, Ho, Wo, y,     \
                                  part, nsl, stream);                                            \
+  }                                                                                              \
+  CER_API int cer_dwconv_bwd_bn##SFX(const T* dy, const T* x, const T* z, const float* mean,    \
+                                     const float* invstd, int act, int B, int H, int W, int C,  \
+                                     int G, const T* w, int64_t w_gstride, float* dw,           \
+                                     int64_t dw_gstride, int k, int st, int pt, int pl, int Ho, \
+                                     int Wo, T* dx, float* part, int nsl, hipStream_t stream) { \
+    return dwconv_bwd_bn_t<T>(dy, x, z, mean, invstd, act, B, H, W, C, G, w, w_gstride, dw,    \
+                              dw_gstride, k, st, pt, pl, Ho, Wo, dx, part, nsl, stream);        \
   }
 
 CER_DW_ENTRY_POINTS(bf16_t, )

@@ -140,3 +140,64 @@ def test_standalone_bn_link_matches_own_pass(G, C, B, H, dtype, monkeypatch):
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     assert _rel(dx1, dx0) < tol
     assert _rel(g1, g0) < tol
+
+
+@pytest.mark.parametrize("G,C,B,H,s,dtype", [(8, 96, 4, 14, 1, torch.float32),
+                                             (2, 144, 3, 11, 2, torch.float32),
+                                             (4, 96, 4, 14, 2, torch.bfloat16)])
+def test_dwconv_dgrad_bn_link_matches_own_pass(G, C, B, H, s, dtype, monkeypatch):
+    """1x1 conv_bn (ReLU6, link_out) -> dwconv -> BN (MobileNetV2's expansion
+    unit and depthwise conv): the depthwise dgrad computes the expansion BN's
+    backward partials; against that BN's own backward pass."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    Ci = 32
+    specs = [ParamSpec("w1", (C, 1, 1, Ci), "weight", fan_in=Ci)]
+    for i in (1, 2):
+        specs += [ParamSpec("g%d" % i, (C,), "gamma"), ParamSpec("b%d" % i, (C,), "beta"),
+                  ParamSpec("rm%d" % i, (C,), "running_mean"),
+                  ParamSpec("rv%d" % i, (C,), "running_var")]
+        if i == 1:
+            specs.append(ParamSpec("dw", (C, 3, 3), "weight", fan_in=9))
+    used = []
+    real = _hip.bn_act_bwd
+
+    def spy(*a, **k):
+        used.append(k.get("part") is not None)
+        return real(*a, **k)
+    monkeypatch.setattr(_hip, "bn_act_bwd", spy)
+    torch.manual_seed(13)
+    x0 = torch.randn(B, H, H, G * Ci, device="cuda").to(dtype)
+    res = []
+    for link in (False, True):
+        used.clear()
+        torch.manual_seed(1000)
+        a = Arena(ModelLayout(specs), G, "cuda", dtype)
+        for g in range(G):
+            a.init_model(g, 9 + g)
+        for sp in specs:
+            if sp.kind in ("gamma", "beta"):
+                a.master_view(sp).uniform_(0.5, 1.5)
+        a.sync_work()
+        r = {sp.name: ParamRef(a, sp) for sp in specs}
+        _hip.conv_set_variant(0, 0)
+        _hip.conv_set_variant(1, 0)
+        try:
+            x = x0.clone().requires_grad_(True)
+            h = P.conv_bn_act(x, r["w1"], r["g1"], r["b1"], r["rm1"], r["rv1"], 1, 0, 6,
+                              link_out=link)
+            h = P.dwconv2d(h, r["dw"], s, 1, stats=True)
+            o = P.bn_act(h, r["g2"], r["b2"], r["rm2"], r["rv2"], True, relu=6)
+            torch.manual_seed(3)
+            o.backward(torch.randn_like(o.float()).to(dtype))
+            torch.cuda.synchronize()
+        finally:
+            _hip.conv_set_variant(0, -1)
+            _hip.conv_set_variant(1, -1)
+        assert used[-1] == link, used       # the expansion BN's backward runs last
+        res.append((o.detach(), x.grad, a.state.clone(), a.grad.clone()))
+    (o0, dx0, st0, g0), (o1, dx1, st1, g1) = res
+    assert torch.equal(o0, o1)
+    assert torch.equal(st0, st1)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert _rel(dx1, dx0) < tol
+    assert _rel(g1, g0) < tol
