@@ -1231,6 +1231,10 @@ def dwconv_fwd(x, wref, stride, pad):
 DW_STATS_MIN = int(os.environ.get("CER_DW_STATS_MIN", "0"))
 
 
+# stride-2 depthwise dgrads also compute the producing BN's backward partials
+DW_BNLINK_S2 = os.environ.get("CER_DW_BNLINK_S2", "1") != "0"
+
+
 def dwconv_stats_ok(x, wref, stride, pad):
     """The fused 3x3 forward + BN statistics (cer_dwconv_fwd_stats) applies."""
     C, kh, kw = wref.spec.shape
@@ -1277,7 +1281,8 @@ def dwconv_bwd(dy, x, wref, stride, pad, need_dx, bnlink=None):
     wp, ws = wref.work_ptr()
     gp, gs = wref.grad_ptr()
     link = bnlink
-    if (link is not None and need_dx and link.z is not None and link.part is None
+    if (link is not None and need_dx and (stride == 1 or DW_BNLINK_S2)
+            and link.z is not None and link.part is None
             and not link.has_res and _act_code(link.act) in (0, 1, 6) and STAT_SLABS > 0
             and kh == 3 and C % 8 == 0 and link.z.shape == x.shape
             and link.z.dtype == x.dtype):
