@@ -71,7 +71,11 @@ class PackedMobileNetV2(PackedNet):
         self.build_layout()
 
     def forward(self, x, training):
-        x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True)
+        # the first block has no expansion: its depthwise dgrad then computes
+        # the stem BN's backward partials (BN link)
+        b0 = self.blocks[0]
+        x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True,
+                         link_out="exp" not in b0 and not b0["res"])
         for blk in self.blocks:
             h = x
             if "exp" in blk:

@@ -48,11 +48,15 @@ class PackedMobileNetV1(PackedNet):
         self.build_layout()
 
     def forward(self, x, training):
-        x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True)
-        for blk in self.blocks:
+        # every pointwise BN output but the last feeds only the next depthwise
+        # conv, whose dgrad computes its backward partials (BN link)
+        x = self.conv_bn(x, self.stem, self.stem_bn, training, relu=6, anchor=True,
+                         link_out=True)
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
             x = P.dwconv2d(x, self.ref(blk["dw"]), blk["stride"], 1, stats=training)
             x = self.bn(x, blk["dw_bn"], training, relu=6, link_out=True)
-            x = self.conv_bn(x, blk["pw"], blk["pw_bn"], training, relu=6)
+            x = self.conv_bn(x, blk["pw"], blk["pw_bn"], training, relu=6, link_out=i < last)
         x = P.global_avgpool(x)
         return self.dense(x, self.fc)
 
