@@ -611,6 +611,24 @@ inline int wgrad_lcb(int CV) {
   return l;
 }
 
+// target block counts of the slab-loop grids: wgrad (CER_DWW_BLOCKS) and the
+// fwd / dgrad kernels with BN statistics (CER_DW_BN_BLOCKS).  Fewer, longer
+// slabs won on MobileNetV2 at 8 configs (wgrad 1024 -> 256 blocks: +3.3 %,
+// one config neutral; profiles/r3_secondary_published.md)
+inline int64_t env_blocks(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? (int64_t)v : dflt;
+}
+inline int64_t dww_blocks() {
+  static const int64_t n = env_blocks("CER_DWW_BLOCKS", 256);
+  return n;
+}
+inline int64_t dwbn_blocks() {
+  static const int64_t n = env_blocks("CER_DW_BN_BLOCKS", 1024);
+  return n;
+}
+
 #ifndef CER_DWW_X
 #define CER_DWW_X 4   // output columns per wgrad position (A/B twins: -DCER_DWW_X=2)
 #endif
@@ -624,8 +642,9 @@ void launch_wgrad_k(const T* x, const T* dy, float* dw, int64_t dw_gstride, cons
   const int cblocks = (CV + CB - 1) / CB;
   constexpr int bands = K / RB;
   const int64_t Pn = (int64_t)d.B * d.Ho * ((d.Wo + X - 1) / X);
-  // ~1024 blocks; every position lane at least 2 positions (bounds the atomics)
-  int64_t slabs = (1024 + (int64_t)cblocks * bands - 1) / ((int64_t)cblocks * bands);
+  // ~dww_blocks() blocks; every position lane at least 2 positions (bounds the atomics)
+  const int64_t target = dww_blocks();
+  int64_t slabs = (target + (int64_t)cblocks * bands - 1) / ((int64_t)cblocks * bands);
   int64_t per = (Pn + slabs - 1) / slabs;
   if (per < 2 * PR) per = 2 * PR;
   slabs = (Pn + per - 1) / per;
@@ -706,7 +725,7 @@ static int dwconv_fwd_stats_t(const T* x, int B, int H, int W, int C, int G, con
   const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
   const int cblocks = (CV + CB - 1) / CB;
   const int64_t Pn = (int64_t)B * Ho * ((Wo + DW_X - 1) / DW_X);
-  int64_t slabs = (1024 + cblocks - 1) / cblocks;
+  int64_t slabs = (dwbn_blocks() + cblocks - 1) / cblocks;
   int64_t per = (Pn + slabs - 1) / slabs;
   if (per < 2 * PR) per = 2 * PR;
   slabs = (Pn + per - 1) / per;
@@ -737,7 +756,7 @@ static int dwconv_bwd_bn_t(const T* dy, const T* x, const T* z, const float* mea
   const int lcb = wgrad_lcb(CV), CB = 1 << lcb, PR = 256 >> lcb;
   const int cblocks = (CV + CB - 1) / CB;
   const int64_t Pn = (int64_t)B * H * ((W + DW_X - 1) / DW_X);
-  int64_t slabs = (1024 + cblocks - 1) / cblocks;
+  int64_t slabs = (dwbn_blocks() + cblocks - 1) / cblocks;
   int64_t per = (Pn + slabs - 1) / slabs;
   if (per < 2 * PR) per = 2 * PR;
   slabs = (Pn + per - 1) / per;
