@@ -135,12 +135,10 @@ def main():
     # and is reported separately as prime_steps
     prime = PRIME_STEPS
     eng.run_steps(prime, prime)
-    # warm-up, untimed; then open every RCCL peer connection a hop may use,
-    # so no connection setup lands in the first timed hop
+    # warm-up, untimed (every RCCL peer connection a hop may use was opened
+    # when the engine created its hop communicator, parallel.hop.hop_group)
     if args.warmup > 0:
         eng.run_steps(args.warmup, args.steps_per_round)
-    from cerebro_ds_kpgi_amd.parallel.hop import warm_p2p
-    warm_p2p(ctx.world, ctx.rank, ctx.device)
     sync()
     ctx.barrier()
     sync()

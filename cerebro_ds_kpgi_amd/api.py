@@ -11,9 +11,13 @@ reference drives (``cerebro_gpdb/run_da_cerebro_standalone.py:84-120``,
 On MI355X the data plane, the model and the train step are the framework's
 own (HBM partition store, packed HIP models, fused step), so:
 
-* ``input_fn`` selects the data source: ``data.da.input_fn`` (or a catalog
-  whose ``data_root`` holds a DA manifest) -> Direct-Access pages; anything
-  else / ``None`` -> synthetic partitions of the dataset's shape;
+* ``input_fn`` + ``data_catalog`` select the data source
+  (``_data_source``): ``data.da.input_fn`` (or a catalog whose ``data_root``
+  holds a DA manifest) -> Direct-Access pages; ``data.fs.input_fn`` /
+  ``input_fn_criteo`` (or a catalog ``data_root`` with ``train/`` partitions)
+  -> the filesystem partitions; no ``input_fn`` and no ``data_root`` ->
+  synthetic partitions of the dataset's shape (logged); any other
+  ``input_fn`` raises ``ValueError``;
 * ``model_fn``: ``None`` / ``native_model_fn`` build each MST's ``model``
   from ``models.registry``.  A custom ``model_fn(mst)`` must return either an
   architecture name or a ``models.common.PackedNet`` (our packed-model API:
@@ -53,12 +57,67 @@ def _catalog_root(data_catalog):
     return inner.get("data_root", "")
 
 
-def _is_da(input_fn, data_catalog):
-    from .data.da import MANIFEST
-    if input_fn is not None and getattr(input_fn, "__module__", "").endswith("data.da"):
-        return True
+def _fn_module(fn):
+    return getattr(fn, "__module__", "") or ""
+
+
+def _data_source(input_fn, data_catalog, data_set_name):
+    """Resolve the reference's data arguments to (kind, root, dataset).
+
+    kind: ``"da"`` (Greenplum-format pages through the C++ reader),
+    ``"fs"`` (``.npy`` partitions in the reference's filesystem layout) or
+    ``"synthetic"`` (no ``input_fn`` and no catalog ``data_root``: synthetic
+    partitions of the dataset's shape, said so in the log).  The reference
+    passes ``input_fn`` / ``input_fn_criteo`` with a ``DATA_CATALOG``
+    (``run_filesystem_cerebro_standalone.py:24-51,85-98``) or the DA
+    ``input_fn`` (``run_da_cerebro_standalone.py:84-120``); any other
+    ``input_fn`` is refused rather than silently replaced by synthetic data.
+    """
+    from .data import da, fs
     root = _catalog_root(data_catalog)
-    return bool(root) and os.path.exists(os.path.join(root, MANIFEST))
+    mod = _fn_module(input_fn)
+    name = getattr(input_fn, "__name__", "")
+    dataset = data_set_name
+    if input_fn is not None:
+        if mod.endswith("data.da"):
+            kind = "da"
+        elif mod.endswith("data.fs") and name in ("input_fn", "input_fn_criteo"):
+            kind = "fs"
+            if name == "input_fn_criteo":
+                dataset = dataset or "criteo"
+        else:
+            raise ValueError(
+                "schedule(): unsupported input_fn {}.{}; pass data.fs.input_fn / "
+                "data.fs.input_fn_criteo (filesystem partitions) or data.da.input_fn "
+                "(Direct-Access pages) with a data_catalog whose data_root holds them, or "
+                "input_fn=None for synthetic data".format(mod, name))
+        if not root:
+            raise ValueError("schedule(): input_fn {} needs a data_catalog with a data_root"
+                             .format(name))
+    elif root:
+        if os.path.exists(os.path.join(root, da.MANIFEST)):
+            kind = "da"
+        elif fs.is_fs_root(root):
+            kind = "fs"
+        else:
+            raise ValueError("schedule(): data_catalog data_root {} holds neither a DA "
+                             "manifest nor filesystem partitions".format(root))
+    else:
+        return "synthetic", "", dataset
+    if kind == "da" and not os.path.exists(os.path.join(root, da.MANIFEST)):
+        raise ValueError("schedule(): data_root {} holds no DA manifest ({})"
+                         .format(root, da.MANIFEST))
+    if kind == "fs":
+        if not fs.is_fs_root(root):
+            raise ValueError("schedule(): data_root {} holds no train/ partitions".format(root))
+        if dataset is None:
+            dataset = fs.fs_dataset_of(root)
+    return kind, root, dataset
+
+
+def _da_input_fn():
+    from .data.da import input_fn
+    return input_fn
 
 
 def native_model_fn(mst):
@@ -125,11 +184,29 @@ def schedule(data_set_name=None, input_fn=None, model_fn=None, train_fn=None,
         msts = _adopt_model_fn(model_fn, msts)
         logs("schedule(): model_fn -> architectures {}".format(sorted({m["model"] for m in msts})))
     ctx = ctx or init_distributed()
+    if engine_kw.get("da_root"):
+        data_catalog = {"data_root": engine_kw.pop("da_root")}
+        input_fn = input_fn if input_fn is not None else _da_input_fn()
+    kind, root, dataset = _data_source(input_fn, data_catalog, data_set_name)
     loader = None
-    if _is_da(input_fn, data_catalog):
+    if kind == "da":
         from .data.da import da_partition_loader
-        root = engine_kw.pop("da_root", None) or _catalog_root(data_catalog)
         loader = da_partition_loader(root, ctx.device)
+    elif kind == "fs":
+        from .data import fs
+        loader = fs.fs_partition_loader(root, dataset, ctx.device)
+        nparts = fs.count_partitions(root)
+        engine_kw.setdefault("dataset", dataset)
+        if engine_kw.get("slots_per_gpu") is None:
+            engine_kw["slots_per_gpu"] = max(1, nparts // ctx.world)
+        if engine_kw["slots_per_gpu"] * ctx.world > nparts:
+            raise ValueError("schedule(): {} GPUs x {} slots need {} partitions; {} holds {}"
+                             .format(ctx.world, engine_kw["slots_per_gpu"],
+                                     engine_kw["slots_per_gpu"] * ctx.world, root, nparts))
+    else:
+        logs("schedule(): no input_fn / data_root -> synthetic {} partitions"
+             .format(dataset or "dataset-shaped"))
+    logs("schedule(): data source {}{}".format(kind, " " + root if root else ""))
     opts = EngineOptions(models_root=ckpt_root, logs_root=log_files_root, store_loader=loader,
                          ckpt_every="subepoch" if save_every else engine_kw.pop("ckpt_every", "epoch"),
                          **engine_kw)

@@ -146,3 +146,33 @@ def fs_partition_loader(root, dataset, device):
 
 def is_fs_root(root):
     return bool(root) and os.path.isdir(os.path.join(root, "train"))
+
+
+def _train_indices(root):
+    import re
+    idx = set()
+    for f in os.listdir(os.path.join(root, "train")):
+        m = re.match(r"train_(\d+)\.(images\.npy|ids\.npy|npy)$", f)
+        if m:
+            idx.add(int(m.group(1)))
+    return idx
+
+
+def count_partitions(root):
+    """Number of consecutive training partitions train_0 .. train_{n-1}."""
+    idx = _train_indices(root)
+    n = 0
+    while n in idx:
+        n += 1
+    return n
+
+
+def fs_dataset_of(root):
+    """"imagenet" (``train_{i}.images.npy``) or "criteo" (``train_{i}.npy`` /
+    compact ``train_{i}.ids.npy``) from the files a filesystem root holds."""
+    if os.path.exists(os.path.join(root, "train", "train_0.images.npy")):
+        return "imagenet"
+    if (os.path.exists(os.path.join(root, "train", "train_0.npy"))
+            or os.path.exists(os.path.join(root, "train", "train_0.ids.npy"))):
+        return "criteo"
+    raise ValueError("{} holds no train_0 partition".format(root))

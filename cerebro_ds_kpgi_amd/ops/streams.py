@@ -47,6 +47,7 @@ _HELD = []          # operands of queued wgrads (alive until the flush)
 _NSTEP = 0          # layers queued in the current deferred block
 _LAST = {}          # ... in the previous block of the same key
 _SPLIT_AT = 0       # layers after which the side batch launches (0: no split)
+_FORCE_SPLIT = [0]  # test hook: split after exactly this many layers (0: off)
 
 
 def batching():
@@ -97,8 +98,11 @@ def deferred_wgrad(enabled=True, side_frac=0.0, key=None):
     if on:
         if _DEFER == 0:
             _SPLIT_AT = 0
+            _FORKED.clear()
             if side_frac > 0 and _LAST.get(key, 0) > 1:
                 _SPLIT_AT = -(-int(round(side_frac * 1000)) * _LAST[key] // 1000)
+                if _FORCE_SPLIT[0]:
+                    _SPLIT_AT = _FORCE_SPLIT[0]
             _NSTEP = 0
         _DEFER += 1
     try:
@@ -121,6 +125,13 @@ def flush_wgrad(discard=False, side=False):
         dev = cur.device.index
         st = _side(dev)
         st.wait_stream(cur)              # the fork: every queued dy is issued by now
+        # the queued layers' operands may come from BOTH streams of a block
+        # with a branch (ResNet projection shortcut): when the split fires
+        # on the branch, the main stream's earlier work (e.g. c2's dz) is
+        # not ordered before it, and vice versa -- wait on the other one too
+        other = _other_stream(dev, cur)
+        if other is not None:
+            st.wait_stream(other)
         L = _hip.lib()
         L.cer_wgrad_batch_set_grid(_SPLIT_GRID)
         try:
@@ -153,11 +164,29 @@ def branch_stream(dev):
 
 
 _PARENT = {}
+_FORKED = {}        # device -> parent stream of a branch forked in this deferred block
 
 
 def set_branch_parent(dev, stream):
     """The stream a model's branch forked from (None: no branch open)."""
     _PARENT[dev] = stream
+    if stream is not None and _DEFER:
+        _FORKED[dev] = stream
+
+
+def _other_stream(dev, cur):
+    """The stream besides ``cur`` that produced operands of this deferred
+    block: the parent when ``cur`` is the branch, the branch when a branch
+    was forked in the block and ``cur`` is its parent; else None.  (A
+    branch forked in the block is part of the same capture, so the wait is
+    legal inside a HIP graph capture.)"""
+    parent = _FORKED.get(dev)
+    if parent is None:
+        return None
+    br = _BRANCH.get(dev)
+    if cur == br:
+        return parent
+    return br
 
 
 def branch_parent(device):

@@ -9,8 +9,8 @@ the replicated scheduler state, so every send has its matching recv by
 construction; ``validate_plan`` checks the pairing.
 
 All of a boundary's transfers are issued as one batched group
-(``batch_isend_irecv`` -> ``ncclGroupStart/Send/Recv/GroupEnd``) so
-independent links run concurrently.
+(``batch_isend_irecv`` -> ``ncclGroupStart/Send/Recv/GroupEnd``) on the
+one hop communicator (``hop_group``), so independent links run concurrently.
 """
 
 import torch
@@ -138,38 +138,21 @@ def warm_p2p(world, rank, device, group=None):
     return len(bufs)
 
 
+def hop_group(world, rank, device, backend=None):
+    """The hop data plane: ONE process group over all ranks (one RCCL
+    communicator), created collectively and warmed -- every rank exchanges a
+    tiny buffer with every other rank in one group, which initialises the
+    communicator with all ranks taking part (a first call by a subset is
+    undefined behaviour) and opens every peer connection a hop may use.
 
-def pair_groups(world, rank, backend, device):
-    """One process group per unordered rank pair, created collectively (every
-    rank calls ``new_group`` for every pair, in the same order), each warmed
-    by a tiny exchange so no RCCL connection setup lands in a real hop.
-    Returns {peer: group} for this rank.
+    Only the hop service uses it (the asynchronous runtime's hop thread, or
+    the lock-step runtime's main thread): no other thread issues work on
+    this communicator, so its operations are posted in the same global order
+    on every rank (``async_mop.HopService``).  Replaces round 3's C(N, 2)
+    two-rank communicators driven from one thread per peer."""
+    if world <= 1:
+        return None
+    g = dist.new_group(ranks=list(range(world)), backend=backend)
+    warm_p2p(world, rank, device, group=g)
+    return g
 
-    Two-rank communicators are what lets the asynchronous hop service run
-    transfers of different pairs concurrently: on one shared communicator
-    RCCL executes point-to-point operations in issue order, so a rank's
-    receive from r-1 and send to r+1 would serialise (and the ring's sends
-    would chain through every rank).  With xGMI every pair of the 8 GPUs has
-    its own link, so concurrent pairs do not share bandwidth either."""
-    links = {}
-    for i in range(world):
-        for j in range(i + 1, world):
-            g = dist.new_group(ranks=[i, j], backend=backend)
-            if rank in (i, j):
-                links[j if rank == i else i] = g
-    # warm every link, pairs in one global order (deadlock-free)
-    for i in range(world):
-        for j in range(i + 1, world):
-            if rank not in (i, j):
-                continue
-            peer = j if rank == i else i
-            s = torch.full((16,), float(rank), device=device)
-            r = torch.empty(16, device=device)
-            ops = [dist.P2POp(dist.isend, s, peer, links[peer], tag=910000 + rank),
-                   dist.P2POp(dist.irecv, r, peer, links[peer], tag=910000 + peer)]
-            for q in dist.batch_isend_irecv(ops):
-                q.wait()
-            if float(r[0]) != float(peer):
-                raise RuntimeError("hop link warm-up: rank {} got {} from {}".format(
-                    rank, float(r[0]), peer))
-    return links

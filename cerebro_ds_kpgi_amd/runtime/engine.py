@@ -180,18 +180,18 @@ class MOPEngine(object):
         self.hop_bytes = 0
         self.hop_time = 0.0          # exposed: time a rank waited for a hop
         self.hop_busy_time = 0.0     # transfers themselves (async runtime)
+        self.hop_groups = 0          # batch_isend_irecv groups posted (async runtime)
         self.hop_spans = []
         self.coord_msts = None
         self._asched = {}
         self._chan = None
         self._nsession = 0
-        self._hop_links = {}
+        self._hop_group = None
         if ctx.initialized and not self.task_parallel:
-            # async hops: one communicator per rank pair (and a stream and a
-            # thread per peer, async_mop.HopService), so transfers between
-            # different pairs run concurrently
-            from ..parallel.hop import pair_groups
-            self._hop_links = pair_groups(ctx.world, ctx.rank, ctx.backend, self.device)
+            # the hop data plane: one communicator, used only by the hop
+            # service (async_mop.HopService / _hop_and_load), warmed here
+            from ..parallel.hop import hop_group
+            self._hop_group = hop_group(ctx.world, ctx.rank, self.device, ctx.backend)
         self.epoch = 0
         self.failures = []
         self._fired = set()
@@ -267,7 +267,8 @@ class MOPEngine(object):
             def recv_buf(m):
                 w, row = row_of[m]
                 return w.recv_buffer(row, hopt)
-            n = execute_moves(moves, rank, send_buf, recv_buf, check=self.o.hop_check)
+            n = execute_moves(moves, rank, send_buf, recv_buf, group=self._hop_group,
+                              check=self.o.hop_check)
             if n:
                 for mv in moves:
                     if mv.src == rank:
@@ -635,9 +636,9 @@ class MOPEngine(object):
             self._chan = (tcp_client(addr, self.o.ctrl_timeout), addr)
         return Channel(self._chan[0], pfx, self.o.ctrl_timeout, self._chan[1])
 
-    def hop_links(self):
-        """{peer rank: process group of (this rank, peer)} for the hops."""
-        return self._hop_links
+    def hop_group(self):
+        """The process group (one communicator) every hop of this engine uses."""
+        return self._hop_group
 
     def coord_begin(self):
         self.coord_msts = [dict(m) for m in self.msts]

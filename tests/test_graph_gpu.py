@@ -177,3 +177,67 @@ def test_captured_validation_matches_eager(model):
     finally:
         grp_mod._VALID_GRAPH = saved
         eng.close()
+
+
+def test_side_split_at_every_layer_matches_one_batch():
+    """the side wgrad batch must be ordered after BOTH streams of
+    a block with a projection-shortcut branch.  Force the split after every
+    possible layer count (so it fires on the branch stream for the shortcut
+    layers, and on the main stream while a branch is open) and compare each
+    step's gradient arena with the one-batch-at-the-end step, eagerly and
+    replayed from a captured graph."""
+    from cerebro_ds_kpgi_amd.models import create_model_from_mst
+    from cerebro_ds_kpgi_amd.ops.loss import softmax_ce
+    from cerebro_ds_kpgi_amd.runtime import Arena
+    G, B = 4, 8
+    net = create_model_from_mst({"model": "resnet50"})
+    a = Arena(net.layout, G, "cuda", torch.float32)
+    for g in range(G):
+        a.init_model(g, 2018 + g)
+    net.bind(a)
+    a.grad_clean = True
+    torch.manual_seed(0)
+    x = torch.randn(B, 112, 112, 3 * G, device="cuda")
+    y = torch.randint(0, 1000, (G, B), device="cuda", dtype=torch.int32)
+    acc = torch.zeros(G, 4, device="cuda")
+    frac = [0.0]
+
+    def step():
+        a.grad.zero_()
+        with streams.deferred_wgrad(True, side_frac=frac[0], key="split_sweep"):
+            softmax_ce(net.forward(x, True), y, acc, G).sum().backward()
+        streams.join()
+
+    m0 = a.master.clone()
+    for _ in range(2):
+        a.master.copy_(m0)
+        step()
+    torch.cuda.synchronize()
+    ref = a.grad.double().clone()
+    nlayers = streams._LAST["split_sweep"]
+    assert nlayers > 40, nlayers
+    frac[0] = 0.5
+    try:
+        for k in range(1, nlayers):
+            streams._FORCE_SPLIT[0] = k
+            a.master.copy_(m0)
+            step()
+            torch.cuda.synchronize()
+            rel = ((a.grad.double() - ref).norm() / ref.norm()).item()
+            assert rel < 1e-3, (k, rel)     # split-K fp32 atomics: not bitwise
+        for k in range(1, nlayers, 5):
+            streams._FORCE_SPLIT[0] = k
+            a.master.copy_(m0)
+            step()                           # the layer count of this split's key
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            for _ in range(2):
+                a.master.copy_(m0)
+                graph.replay()
+                torch.cuda.synchronize()
+                rel = ((a.grad.double() - ref).norm() / ref.norm()).item()
+                assert rel < 1e-3, ("graph", k, rel)
+            graph.reset()
+    finally:
+        streams._FORCE_SPLIT[0] = 0

@@ -151,3 +151,62 @@ def test_log_analyzer_breakdown(tmp_path):
     assert {"train", "valid"} <= names and names & {"hop", "wait_arrival"}
     assert res["best"]["epochs"] == [1, 2]
     assert list(res["system"].values())[0]["seconds"] >= 0
+
+
+def _store_digest(t):
+    import hashlib
+    return hashlib.sha1(t.contiguous().cpu().numpy().tobytes()).hexdigest()
+
+
+def test_schedule_filesystem_input_fn_trains_on_those_partitions(tmp_path, monkeypatch):
+    """the reference's filesystem entry point passes
+    ``input_fn`` / ``input_fn_criteo`` with a ``DATA_CATALOG``
+    (``run_filesystem_cerebro_standalone.py:24-51,85-98``); schedule() must
+    load exactly those partitions (store bytes == the files' bytes), and an
+    unknown input_fn must raise instead of training on synthetic data."""
+    import numpy as np
+    from cerebro_ds_kpgi_amd.api import schedule
+    from cerebro_ds_kpgi_amd.data import fs
+    from cerebro_ds_kpgi_amd.runtime import engine as engine_mod
+    from cerebro_ds_kpgi_amd.selection.hyperopt_helper import mst_eval_fn
+    root = str(tmp_path / "criteo")
+    cat = fs.write_fs_dataset(root, "criteo", 2, 48, 16)
+    seen = {}
+    orig_close = engine_mod.MOPEngine.close
+
+    def spy_close(self):
+        seen["train_x"] = _store_digest(self.store.train_x)
+        seen["train_y"] = _store_digest(self.store.train_y)
+        seen["P"] = self.P
+        orig_close(self)
+    monkeypatch.setattr(engine_mod.MOPEngine, "close", spy_close)
+    msts = [{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": 16, "model": "confA"}
+            for lr in (1e-3, 1e-4)]
+    state = schedule(data_set_name="criteo", input_fn=fs.input_fn_criteo,
+                     initial_msts=msts, mst_eval_fn=mst_eval_fn(1),
+                     data_catalog={"criteo": cat}, ctx=_ctx(), compute_dtype="fp32",
+                     verbose=False, ckpt_every="none")
+    assert all(len(s["train_loss"]) == 1 for s in state.values())
+    # what the files hold, through the reference's own input_fn contract
+    want_x, want_y = [], []
+    for i in range(2):
+        ref = fs.input_fn_criteo(os.path.join(root, cat["train"][i]))
+        want_x.append(fs._criteo_ids(ref["images"]))
+        want_y.append(ref["labels"].argmax(1).astype(np.int32))
+    import torch
+    assert seen["P"] == 2
+    assert seen["train_x"] == _store_digest(torch.from_numpy(np.stack(want_x)))
+    assert seen["train_y"] == _store_digest(torch.from_numpy(np.stack(want_y)))
+    # a catalog data_root alone selects the same source
+    schedule(initial_msts=msts[:1], mst_eval_fn=mst_eval_fn(1), data_catalog=cat,
+             ctx=_ctx(), compute_dtype="fp32", verbose=False, ckpt_every="none")
+    assert seen["train_x"] == _store_digest(torch.from_numpy(np.stack(want_x)))
+
+    def my_input_fn(path):
+        return None
+    with pytest.raises(ValueError, match="unsupported input_fn"):
+        schedule(input_fn=my_input_fn, initial_msts=msts, data_catalog=cat, ctx=_ctx())
+    with pytest.raises(ValueError, match="data_root"):
+        schedule(input_fn=fs.input_fn, initial_msts=msts, ctx=_ctx())
+    with pytest.raises(ValueError, match="neither"):
+        schedule(initial_msts=msts, data_catalog={"data_root": str(tmp_path)}, ctx=_ctx())
