@@ -130,21 +130,26 @@ class MAEngine(_GroupEngine):
     def _average(self, w, count):
         """w <- sum_r count_r * w_r / sum_r count_r over ranks (params + BN
         stats): the reference's count-weighted merge (``madlib_keras_wrapper.py:
-        63-116``) as two RCCL all-reduces."""
+        63-116``, the image count travels with the weights as in
+        ``serialize_state_with_nd_weights``) as ONE RCCL all-reduce per merge:
+        every config row's ``count * w`` and the count packed into one
+        contiguous buffer (the master section of the arena is a strided
+        ``[G, n]`` view, which collectives reject)."""
         if not self.ctx.initialized:
             return
         master = w.arena.master
         if getattr(self, "keep_pre_average", False):
             self.pre_average = master.detach().clone()
-        cnt = torch.tensor([float(count)], device=master.device)
-        master.mul_(float(count))
-        # one contiguous state row per config ([G, R] rows; the master section
-        # of the whole arena is a strided view, which collectives reject)
-        works = [dist.all_reduce(master[g], async_op=True) for g in range(master.shape[0])]
-        dist.all_reduce(cnt)
-        for wk in works:
-            wk.wait()
-        master.div_(cnt)
+        G, n = master.shape
+        buf = torch.empty(G * n + 1, device=master.device, dtype=torch.float32)
+        body = buf[:G * n].view(G, n)
+        body.copy_(master)
+        body.mul_(float(count))
+        buf[G * n] = float(count)
+        dist.all_reduce(buf)
+        self.n_collectives = getattr(self, "n_collectives", 0) + 1
+        body.div_(buf[G * n])
+        master.copy_(body)
         w.arena.sync_work()
 
 
@@ -175,19 +180,39 @@ class GradBuckets(object):
         self.group = group
         self.hi = arena.layout.n_train
         self.works = []
+        self.pending = []              # (lo, hi, staging view) awaiting copy-back
+        self.stage = None              # contiguous staging: one slice per bucket
+        self.stage_off = 0
         self.n_buckets = 0
+        self.n_collectives = 0
         self.bucket_log = []           # (lo, hi) per bucket of the last step
         self.seg = None                # SegmentedGraph while capturing
 
     def _allreduce(self, lo, hi):
+        """ONE all-reduce per bucket over all G config rows: the bucket's
+        columns of every row (a strided [G, hi-lo] view) are packed into a
+        contiguous slice of the staging buffer, reduced, and copied back
+        (divided by the world size) in ``_wait``."""
         g = self.arena.grad
-        for row in range(g.shape[0]):
-            self.works.append(dist.all_reduce(g[row, lo:hi], group=self.group, async_op=True))
+        G, n = g.shape[0], hi - lo
+        if self.stage is None:
+            self.stage = torch.empty(G * self.arena.layout.n_train, device=g.device,
+                                     dtype=g.dtype)
+        buf = self.stage[self.stage_off:self.stage_off + G * n].view(G, n)
+        self.stage_off += G * n
+        buf.copy_(g[:, lo:hi])
+        self.works.append(dist.all_reduce(buf, group=self.group, async_op=True))
+        self.pending.append((lo, hi, buf))
+        self.n_collectives += 1
 
     def _wait(self):
         for w in self.works:
             w.wait()
-        self.works = []
+        g = self.arena.grad
+        for lo, hi, buf in self.pending:
+            buf.mul_(1.0 / self.world)
+            g[:, lo:hi].copy_(buf)
+        self.works, self.pending, self.stage_off = [], [], 0
 
     def ready_from(self, lo, force=False):
         if lo >= self.hi or (not force and self.hi - lo < self.bucket_cols):
@@ -212,7 +237,6 @@ class GradBuckets(object):
             self.seg.cut(("wait",))
         else:
             self._wait()
-        self.arena.grad.div_(self.world)
         self.hi = self.arena.layout.n_train
 
     def run_action(self, act):

@@ -3,6 +3,8 @@
 * MA: after every epoch all ranks hold the image-count-weighted mean of the
   per-rank weights (reference merge ``madlib_keras_wrapper.py:63-116``),
   including with unequal counts;
+* MA and DDP coalesce their collectives: one all-reduce per merge and one
+  per gradient bucket, over all G packed config rows;
 * DDP: the gradient after the bucketed, backward-overlapped all-reduce equals
   the single-process gradient of the concatenated batch (BN-free model: the
   reference's DDP keeps BatchNorm statistics per rank), with one bucket per
@@ -24,6 +26,19 @@ def _env(rank, world, port):
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
                        "CEREBRO_BACKEND": "torch", "CEREBRO_QUIET": "1"})
     torch.set_num_threads(1)
+
+
+def _count_all_reduce():
+    """Count torch.distributed.all_reduce calls from here on (this process)."""
+    import torch.distributed as dist
+    calls = [0]
+    orig = dist.all_reduce
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return orig(*a, **k)
+    dist.all_reduce = counted
+    return calls
 
 
 def _tiny_msts(n):
@@ -48,7 +63,9 @@ def _ma_worker(rank, world, port, outdir):
     g = torch.Generator().manual_seed(100 + rank)
     w.arena.master.copy_(torch.randn(w.arena.master.shape, generator=g))
     out["x"] = w.arena.master.detach().clone()
+    calls = _count_all_reduce()
     eng._average(w, rank + 1)
+    out["collectives"] = torch.tensor(calls[0])
     out["avg"] = w.arena.master.detach().clone()
     torch.save(out, os.path.join(outdir, "ma_{}.pt".format(rank)))
     shutdown(ctx)
@@ -66,6 +83,7 @@ def test_ma_weighted_average_three_ranks(tmp_path):
     want = sum((i + 1) * res[i]["x"] for i in range(world)) / sum(range(1, world + 1))
     for r in res:
         torch.testing.assert_close(r["avg"], want, rtol=1e-5, atol=1e-6)
+        assert int(r["collectives"]) == 1          # one all-reduce per merge (G rows + count)
 
 
 def _ddp_grad_worker(rank, world, port, outdir):
@@ -94,12 +112,14 @@ def _ddp_grad_worker(rank, world, port, outdir):
     # DDP: this rank's slice, bucketed all-reduce during backward
     gb = GradBuckets(arena, world, bucket_bytes=4)
     net.grad_buckets = gb
+    calls = _count_all_reduce()
     loss = softmax_ce(net.forward(xs[rank], True), ys[rank], acc, G)
     loss.sum().backward()
     in_backward = gb.n_buckets
     gb.finish()
     torch.save({"want": want, "got": arena.grad.clone(), "buckets": in_backward,
-                "log": gb.bucket_log}, os.path.join(outdir, "ddp_{}.pt".format(rank)))
+                "log": gb.bucket_log, "collectives": torch.tensor(calls[0])},
+               os.path.join(outdir, "ddp_{}.pt".format(rank)))
     shutdown(ctx)
 
 
@@ -114,6 +134,8 @@ def test_ddp_bucketed_gradient_equals_large_batch(tmp_path):
         lo_hi = res["log"]
         assert len(lo_hi) == 3 and lo_hi[-1][0] == 0  # + the tail bucket at finish()
         assert all(a[0] == b[1] for a, b in zip(lo_hi, lo_hi[1:]))   # contiguous, top-down
+        # ONE all-reduce per bucket over both config rows (coalesced)
+        assert int(res["collectives"]) == len(lo_hi)
 
 
 def _ddp_engine_worker(rank, world, port, outdir):
