@@ -82,6 +82,9 @@ def hyperopt_grid(args):
     models = [m for m in (getattr(args, "hyperopt_models", "") or "").split(",") if m]
     if models:
         grid["model"] = models
+    buckets = getattr(args, "hyperopt_batch_buckets", "none") or "none"
+    if buckets != "none":
+        grid["batch_size_buckets"] = [int(b) for b in buckets.split(",") if b]
     return grid
 
 

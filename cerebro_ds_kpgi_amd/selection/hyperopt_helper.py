@@ -25,16 +25,33 @@ from ..config.catalog import SEED, param_grid_hyperopt
 from . import tpe
 
 
+def batch_choices(param_grid=param_grid_hyperopt):
+    """Batch sizes TPE chooses from: every integer in the reference range
+    [lo, hi] (run_ctq_hyperopt.py:76-91), or -- ``batch_size_buckets`` in the
+    grid -- only those values (all inside the range).  Bucketing is what lets
+    a TPE batch pack: configs of one (architecture, batch size) train as ONE
+    launch stream on a GPU, while 8 distinct batch sizes are 8 single-config
+    pack groups (profiles/r3_hyperopt.md)."""
+    lo, hi = param_grid["batch_size"][0], param_grid["batch_size"][1]
+    b = param_grid.get("batch_size_buckets")
+    if not b:
+        return list(range(lo, hi + 1))
+    bad = [x for x in b if not lo <= x <= hi]
+    if bad:
+        raise ValueError("batch_size_buckets {} outside the search range [{}, {}]"
+                         .format(bad, lo, hi))
+    return sorted(set(int(x) for x in b))
+
+
 def build_search_space(param_grid=param_grid_hyperopt):
     """Reference space (run_ctq_hyperopt.py:76-91): model/lambda choices,
-    log-uniform lr, batch size a choice over every integer in [lo, hi]."""
+    log-uniform lr, batch size a choice over ``batch_choices``."""
     return {
         "model": tpe.choice("model", param_grid["model"]),
         "lambda_value": tpe.choice("lambda_value", param_grid["lambda_value"]),
         "learning_rate": tpe.loguniform("learning_rate", param_grid["learning_rate"][0],
                                         param_grid["learning_rate"][1]),
-        "batch_size": tpe.choice("batch_size", list(range(param_grid["batch_size"][0],
-                                                           param_grid["batch_size"][1] + 1))),
+        "batch_size": tpe.choice("batch_size", batch_choices(param_grid)),
     }
 
 

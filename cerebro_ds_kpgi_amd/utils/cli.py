@@ -64,6 +64,10 @@ def get_main_parser():
     p.add_argument("--hyperopt_models", type=str, default="",
                    help="comma list replacing the hyperopt space's model choices (reference: "
                         "resnet18,resnet34; BASELINE config 5: resnet50)")
+    p.add_argument("--hyperopt_batch_buckets", type=str, default="16,32,64,128,256",
+                   help="batch sizes TPE chooses from (comma list inside the reference range "
+                        "[16, 256]); configs with equal (model, batch) train as one packed "
+                        "launch stream. 'none' = every integer in the range (reference space)")
     # ---- MI355X engine flags ----
     p.add_argument("--synthetic", type=_bool, default=True,
                    help="generate ImageNet/Criteo-shaped data on the GPUs (no datasets offline)")

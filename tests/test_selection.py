@@ -2,6 +2,7 @@
 ``utils.py:58-86``) and the own-TPE search."""
 
 import numpy as np
+import pytest
 
 from cerebro_ds_kpgi_amd.config import catalog as cat
 from cerebro_ds_kpgi_amd.selection import get_exp_specific_msts, get_msts
@@ -151,3 +152,28 @@ def test_weight_blob_formats_roundtrip():
     assert S.serialize_state_with_1d_weights(96.0, flat) == st
     S.nd_weights_to_arena(a, 0, back)
     assert torch.equal(a.state[0, :net.layout.n_master], a.state[1, :net.layout.n_master])
+
+
+def test_hyperopt_batch_buckets_pack_configs():
+    """with batch-size buckets TPE proposes only bucket values
+    (inside the reference's [16, 256]), so a batch of 8 proposals falls into
+    a few (model, batch) pack groups; 'none' keeps the full integer range."""
+    import argparse
+    from cerebro_ds_kpgi_amd.runners.common import hyperopt_grid
+    from cerebro_ds_kpgi_amd.selection import hyperopt_helper as hh
+    from cerebro_ds_kpgi_amd.utils.cli import get_main_parser
+    args = get_main_parser().parse_args(["--hyperopt_models", "resnet50"])
+    grid = hyperopt_grid(args)
+    assert grid["batch_size_buckets"] == [16, 32, 64, 128, 256]
+    hp, msts, trials, domain, rand, _ = hh.init_hyperopt(grid, argparse.Namespace(size=8))
+    for i, m in enumerate(msts):
+        trials.report(hp[i]["tid"], float(i))
+    hp, msts, s, e = hh.hyperopt_add_one_batch_configs(None, hp, msts, domain, trials, 8,
+                                                       rand=rand)
+    assert all(m["batch_size"] in (16, 32, 64, 128, 256) for m in msts)
+    assert len({(m["model"], m["batch_size"]) for m in msts[:8]}) <= 5
+    args = get_main_parser().parse_args(["--hyperopt_batch_buckets", "none"])
+    assert "batch_size_buckets" not in hyperopt_grid(args)
+    assert len(hh.batch_choices(hyperopt_grid(args))) == 241
+    with pytest.raises(ValueError):
+        hh.batch_choices({"batch_size": [16, 256], "batch_size_buckets": [8]})
