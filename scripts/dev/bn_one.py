@@ -1,6 +1,6 @@
 """Time the BatchNorm apply kernels of one packed layer shape (fp32, HIP).
 
-    python -m cerebro_ds_kpgi_amd.tools.bn_one --rows 1568 --C 256 --G 1 --iters 200
+    python scripts/dev/bn_one.py --rows 1568 --C 256 --G 1 --iters 200
 
 Times, per launch (CUDA events around ``iters`` back-to-back launches; and
 the same launches replayed from a HIP graph, the training step's form):
@@ -14,13 +14,18 @@ the same launches replayed from a HIP graph, the training step's form):
 Prints one JSON line per case: us per launch eager / graph and GB/s.
 """
 
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
 import argparse
 import json
 
 import torch
 
-from ..ops import _hip, backend
-from ..runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
+from cerebro_ds_kpgi_amd.ops import _hip, backend
+from cerebro_ds_kpgi_amd.runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
 
 SLAB_F64 = 1 << 24
 

@@ -1,14 +1,19 @@
 """Run one packed conv shape's fwd / dgrad / wgrad a few times (profiling target).
 
-    python -m cerebro_ds_kpgi_amd.tools.conv_one --shape 32,7,7,256,256,3,1,1 --G 8 --iters 20
+    python scripts/dev/conv_one.py --shape 32,7,7,256,256,3,1,1 --G 8 --iters 20
 """
+
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 
 import argparse
 
 import torch
 
-from ..ops import backend
-from .bench_conv import bench_shape
+from cerebro_ds_kpgi_amd.ops import backend
+from cerebro_ds_kpgi_amd.tools.bench_conv import bench_shape
 
 
 def main(argv=None):

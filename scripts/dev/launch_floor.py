@@ -1,6 +1,6 @@
 """Measure the per-kernel floor of a HIP-graph replay on this GPU.
 
-    python -m cerebro_ds_kpgi_amd.tools.launch_floor [--n 300]
+    python scripts/dev/launch_floor.py [--n 300]
 
 Captures ``n`` dependent tiny kernels (one-block in-place adds, and
 256-block ones) in a graph and reports replay wall time per kernel; then
@@ -8,6 +8,11 @@ the same ``n`` kernels split over two streams (fork/join inside the graph)
 to see how much of the floor two independent chains overlap.  This is the
 question behind the one-config ResNet-50 step (~300 kernels per step).
 """
+
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 
 import argparse
 import json

@@ -1,6 +1,6 @@
 """Isolated timing of the batched fp32 weight gradients of one ResNet-50 step.
 
-    python -m cerebro_ds_kpgi_amd.tools.wgrad_batch_bench --G 8 [--variants 0,1,2,12,13,14]
+    python scripts/dev/wgrad_batch_bench.py --G 8 [--variants 0,1,2,12,13,14]
 
 Queues the weight gradient of every aligned ResNet-50 conv (bs 32, 112x112,
 ``resnet50_shapes``) inside one ``streams.deferred_wgrad`` block and times the
@@ -12,15 +12,20 @@ configuration: ms per flush and the fp32-equivalent TFLOP/s over the
 step's wgrad FLOPs.  The stem (Cin = 3) takes its own path and is left out.
 """
 
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+
 import argparse
 import json
 import statistics
 
 import torch
 
-from ..ops import _hip, backend, streams
-from ..runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
-from .bench_conv import resnet50_shapes
+from cerebro_ds_kpgi_amd.ops import _hip, backend, streams
+from cerebro_ds_kpgi_amd.runtime.arena import Arena, ModelLayout, ParamRef, ParamSpec
+from cerebro_ds_kpgi_amd.tools.bench_conv import resnet50_shapes
 
 
 def _layers(G, B, dtype=torch.float32):

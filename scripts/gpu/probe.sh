@@ -4,7 +4,7 @@
 # round-3 build as this round's starting point.
 set -o pipefail
 cd "$(dirname "$0")/../.."
-out=gpurun_out/r4_probe
+out=gpurun_out/probe
 mkdir -p $out
 for n in 2 4; do
   timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
