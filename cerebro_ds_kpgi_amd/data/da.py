@@ -53,6 +53,9 @@ def lib():
         L.cer_da_last_error.restype = ctypes.c_char_p
         L.cer_da_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         L.cer_da_open.restype = vp
+        L.cer_da_open2.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+        L.cer_da_open2.restype = vp
+        L.cer_da_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.cer_da_count.argtypes = [vp]
         L.cer_da_info.argtypes = [vp, ctypes.c_int, ctypes.POINTER(i32), ctypes.POINTER(i32),
                                   ctypes.POINTER(i64), ctypes.POINTER(i64)]
@@ -97,11 +100,26 @@ def pglz_decompress(comp, rawsize):
 # ---------------------------------------------------------------------------
 # reader
 # ---------------------------------------------------------------------------
+STAT_KEYS = ("map_s", "heap_s", "index_s", "read_wall_s", "read_busy_s", "read_copy_s",
+             "read_pglz_s", "read_threads", "index_threads")
+
+
 class DirectAccessReader(object):
-    def __init__(self, heap_path, toast_path):
-        self.h = lib().cer_da_open(heap_path.encode(), toast_path.encode())
+    """``nthreads``: threads of the TOAST index scan at open (the read takes
+    its own count)."""
+
+    def __init__(self, heap_path, toast_path, nthreads=16):
+        self.h = lib().cer_da_open2(heap_path.encode(), toast_path.encode(), int(nthreads))
         if not self.h:
             raise IOError("DA open failed: {}".format(_err()))
+
+    def stats(self):
+        """Phase timings of this reader (s): mmap of the segment files, heap
+        parse, TOAST index (open); wall, summed worker busy / TOAST-chunk copy
+        / pglz time of the last ``read``; thread counts."""
+        out = (ctypes.c_double * 9)()
+        lib().cer_da_stats(self.h, out)
+        return dict(zip(STAT_KEYS, list(out)))
 
     def __len__(self):
         return lib().cer_da_count(self.h)
@@ -329,7 +347,10 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     (partition, split) decodes run ahead on a thread pool.
     ``stats`` (a dict) accumulates ETL timings: ``decode_s`` (wall time the
     consumer waited for the C++ reader), ``h2d_s`` (copies + conversion,
-    wall), ``payload_bytes``
+    wall), the reader's phases summed over decodes (``DirectAccessReader.stats``:
+    ``map_s``, ``heap_s``, ``index_s``, ``read_wall_s``, ``read_busy_s``,
+    ``read_copy_s``, ``read_pglz_s``, plus ``open_s`` and ``alloc_read_s`` as
+    seen from Python), ``payload_bytes``
     (decompressed), ``stored_bytes`` (on disk, heap + TOAST) and ``buffers``."""
     import time
     import torch
@@ -381,10 +402,16 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
                 stored += os.path.getsize(f)
                 seg += 1
                 f = "{}.{}".format(path, seg)
-        r = DirectAccessReader(heap, toast)
+        t0 = time.perf_counter()
+        r = DirectAccessReader(heap, toast, threads)
+        t1 = time.perf_counter()
         recs = sorted(r.read(threads, pinned=cuda), key=lambda t: t[1])
+        t2 = time.perf_counter()
+        ph = r.stats()
         r.close()
-        return recs, stored
+        ph["open_s"] = t1 - t0
+        ph["alloc_read_s"] = t2 - t1          # pinned staging allocation + read
+        return recs, stored, ph
 
     def prefetch(pids):
         """The store's partitions, in load order: start decoding ahead."""
@@ -411,8 +438,13 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     def load_split(p, split):
         shapes = {(s["dist_key"], s["buffer_id"]): s for s in man["shapes"][split]}
         t0 = time.perf_counter()
-        recs, stored = fetch(p, split)
+        recs, stored, ph = fetch(p, split)
         st["stored_bytes"] += stored
+        for k, v in ph.items():
+            if k.endswith("_s"):
+                st[k] = st.get(k, 0.0) + v
+            else:
+                st[k] = max(st.get(k, 0), v)
         t1 = time.perf_counter()
         st["decode_s"] += t1 - t0
         xs, ys, bads = [], [], []

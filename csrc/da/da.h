@@ -24,6 +24,8 @@
 extern "C" {
 int64_t cer_pglz_compress(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap);
 int64_t cer_pglz_decompress(const uint8_t* src, int64_t srclen, uint8_t* dst, int64_t rawsize);
+int64_t cer_pglz_decompress_pieces(const uint8_t* const* ptrs, const int64_t* lens, int n,
+                                   int64_t skip, uint8_t* dst, int64_t rawsize);
 }
 
 namespace da {

@@ -1,20 +1,29 @@
 // Direct-Access page reader / writer.  See da.h for
 // the on-disk format.
 //
-// Reader: all heap pages of a relation (every 1-GB segment file) are parsed
-// into tuples; the TOAST relation is scanned once into a chunk index keyed by
-// value id (hash map, only ids referenced by the heap); buffers are then
-// detoasted + pglz-decompressed in parallel on a thread pool, straight into
-// caller-provided (pinned) host memory.  Integrity checks follow the
+// Reader: every segment file of the heap and TOAST relations is mmap-ed (no
+// read into a private copy: round 3 fread the whole relation -- 13 GB for a
+// full ImageNet-112 partition -- on one thread into a zero-filled vector,
+// which is where the decode wall time went, profiles/r4_da_etl.md); heap
+// pages are parsed into tuples; the TOAST pages are scanned into a chunk
+// index keyed by value id on a thread pool (page ranges per thread, only ids
+// referenced by the heap, merged once); buffers are then detoasted +
+// pglz-decompressed in parallel, straight into caller-provided (pinned) host
+// memory.  Each phase is timed (cer_da_stats).  Integrity checks follow the
 // reference: line-pointer area multiple of 4, no special space on TOAST
 // pages, chunk counts / sizes, final size, pglz end-of-stream.
 //
 // Writer: builds the same format from raw buffers (compressing with pglz),
 // for tests and for generating synthetic DA partitions.
 #include <arpa/inet.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -52,18 +61,57 @@ std::vector<std::string> segment_files(const std::string& base) {
   return out;
 }
 
-bool read_file(const std::string& path, std::vector<uint8_t>* buf) {
-  FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) return set_err("cannot open " + path);
-  std::fseek(f, 0, SEEK_END);
-  long n = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  size_t old = buf->size();
-  buf->resize(old + (size_t)n);
-  size_t got = n ? std::fread(buf->data() + old, 1, (size_t)n, f) : 0;
-  std::fclose(f);
-  if ((long)got != n) return set_err("short read " + path);
-  if (n % kBlck) return set_err("segment size not a multiple of BLCKSZ: " + path);
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// One relation (heap or TOAST): its segment files mapped read-only, and the
+// address of every page in relation order.
+struct Relation {
+  struct Seg {
+    void* base = nullptr;
+    size_t len = 0;
+  };
+  std::vector<Seg> segs;
+  std::vector<const uint8_t*> pages;
+  ~Relation() {
+    for (auto& g : segs)
+      if (g.base && g.len) munmap(g.base, g.len);
+  }
+};
+
+bool map_relation(const std::string& base, Relation* rel, bool required) {
+  auto files = segment_files(base);
+  if (files.empty()) return required ? set_err("no segment files at " + base) : true;
+  for (auto& path : files) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return set_err("cannot open " + path);
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) {
+      close(fd);
+      return set_err("cannot stat " + path);
+    }
+    const size_t n = (size_t)sb.st_size;
+    if (n % kBlck) {
+      close(fd);
+      return set_err("segment size not a multiple of BLCKSZ: " + path);
+    }
+    Relation::Seg g;
+    if (n) {
+      g.base = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (g.base == MAP_FAILED) {
+        close(fd);
+        return set_err("cannot mmap " + path);
+      }
+      g.len = n;
+      madvise(g.base, n, MADV_WILLNEED);     // start the page-cache reads now
+    }
+    close(fd);
+    rel->segs.push_back(g);
+    for (size_t o = 0; o < n; o += kBlck)
+      rel->pages.push_back(static_cast<const uint8_t*>(g.base) + o);
+  }
   return true;
 }
 
@@ -140,15 +188,19 @@ bool parse_datum(const uint8_t* p, const uint8_t* end, Datum* d, int64_t* consum
 // reader
 // ---------------------------------------------------------------------------
 struct DAReader {
-  std::vector<uint8_t> heap, toast;
+  Relation heap, toast;
   std::vector<Tuple> tuples;
   std::unordered_map<uint32_t, std::vector<Chunk>> chunks;
+  int nthreads = 8;
+  // phase timings (seconds): open = map + heap parse + TOAST index; read =
+  // the last cer_da_read (wall) and its workers' busy / copy / pglz sums
+  double map_s = 0, heap_s = 0, index_s = 0;
+  double read_wall_s = 0, read_busy_s = 0, read_copy_s = 0, read_pglz_s = 0;
+  int read_threads = 0;
 };
 
 static bool parse_heap(DAReader* r) {
-  const int64_t npages = (int64_t)r->heap.size() / kBlck;
-  for (int64_t pg = 0; pg < npages; ++pg) {
-    const uint8_t* page = r->heap.data() + pg * kBlck;
+  for (const uint8_t* page : r->heap.pages) {
     PageHdr h = page_header(page);
     if (h.lower < kPageHeader || h.lower > kBlck) return set_err("bad pd_lower");
     if ((h.lower - kPageHeader) % kItemId) return set_err("line pointer area not a multiple of 4");
@@ -177,15 +229,12 @@ static bool parse_heap(DAReader* r) {
   return true;
 }
 
-static bool index_toast(DAReader* r) {
-  std::unordered_set<uint32_t> want;
-  for (auto& t : r->tuples) {
-    if (t.indep.external) want.insert(t.indep.ptr.valueid);
-    if (t.dep.external) want.insert(t.dep.ptr.valueid);
-  }
-  const int64_t npages = (int64_t)r->toast.size() / kBlck;
-  for (int64_t pg = 0; pg < npages; ++pg) {
-    const uint8_t* page = r->toast.data() + pg * kBlck;
+// scan TOAST pages [p0, p1): chunks of wanted value ids, in page order
+static bool index_toast_range(const DAReader* r, const std::unordered_set<uint32_t>& want,
+                              size_t p0, size_t p1,
+                              std::vector<std::pair<uint32_t, Chunk>>* out) {
+  for (size_t pg = p0; pg < p1; ++pg) {
+    const uint8_t* page = r->toast.pages[pg];
     PageHdr h = page_header(page);
     if (h.special != kBlck) return set_err("THERE SHALL NOT BE INDICES (special space on TOAST page)");
     if (h.lower < kPageHeader || h.lower > kBlck || (h.lower - kPageHeader) % kItemId)
@@ -206,23 +255,57 @@ static bool index_toast(DAReader* r) {
       if (csize < 4) return set_err("TOAST chunk shorter than its header");
       if (off + t_hoff + 8 + csize > (uint32_t)kBlck) return set_err("TOAST chunk beyond page");
       if (want.count(chunk_id))
-        r->chunks[chunk_id].push_back(Chunk{(int32_t)chunk_seq, cv + 4, csize - 4});
+        out->emplace_back(chunk_id, Chunk{(int32_t)chunk_seq, cv + 4, csize - 4});
       off += t_hoff + 8 + csize;
     }
   }
   return true;
 }
 
+static bool index_toast(DAReader* r) {
+  std::unordered_set<uint32_t> want;
+  for (auto& t : r->tuples) {
+    if (t.indep.external) want.insert(t.indep.ptr.valueid);
+    if (t.dep.external) want.insert(t.dep.ptr.valueid);
+  }
+  const size_t np = r->toast.pages.size();
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)r->nthreads, np / 64 + 1));
+  std::vector<std::vector<std::pair<uint32_t, Chunk>>> part((size_t)nt);
+  std::vector<std::string> errs((size_t)nt);
+  std::vector<char> ok((size_t)nt, 1);
+  auto work = [&](int t) {
+    const size_t p0 = np * (size_t)t / (size_t)nt, p1 = np * (size_t)(t + 1) / (size_t)nt;
+    part[(size_t)t].reserve((p1 - p0) * 4);
+    if (!index_toast_range(r, want, p0, p1, &part[(size_t)t])) {
+      ok[(size_t)t] = 0;
+      errs[(size_t)t] = g_err;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  for (int t = 0; t < nt; ++t)
+    if (!ok[(size_t)t]) return set_err(errs[(size_t)t]);
+  r->chunks.reserve(want.size());
+  for (auto& v : part)
+    for (auto& kv : v) r->chunks[kv.first].push_back(kv.second);
+  return true;
+}
+
 static bool detoast(const DAReader* r, const Datum& d, uint8_t* out, int64_t out_size,
-                    std::vector<uint8_t>* scratch) {
+                    std::vector<uint8_t>* scratch, double* copy_s, double* pglz_s) {
   if (!d.external) {
     const uint8_t* p = d.inl;
     const uint32_t vs = varsize_4b(p);
     const uint32_t raw = rd32(p + 4);
     if ((int64_t)raw != out_size) return set_err("inline raw size does not match");
+    const double t0 = now_s();
     if (cer_pglz_decompress(p + 8, vs - 8, out, raw) < 0) return set_err("compressed data is corrupt");
+    *pglz_s += now_s() - t0;
     return true;
   }
+  const double tc = now_s();
   auto it = r->chunks.find(d.ptr.valueid);
   if (it == r->chunks.end()) return set_err("missing TOAST value " + std::to_string(d.ptr.valueid));
   std::vector<Chunk> cs = it->second;
@@ -230,28 +313,49 @@ static bool detoast(const DAReader* r, const Datum& d, uint8_t* out, int64_t out
   const int64_t ext = d.ptr.extsize;
   const int64_t nchunks = (ext - 1) / kToastMaxChunk + 1;
   if ((int64_t)cs.size() != nchunks) return set_err("TOAST chunk count mismatch");
-  scratch->resize((size_t)ext);
-  int64_t pos = 0;
   for (int64_t i = 0; i < nchunks; ++i) {
     const Chunk& c = cs[(size_t)i];
     if (c.seq != i) return set_err("TOAST chunk sequence gap");
     if (i < nchunks - 1 && c.size != (uint32_t)kToastMaxChunk) return set_err("unexpected chunk size");
     if (i == nchunks - 1 && i * kToastMaxChunk + (int64_t)c.size != ext)
       return set_err("unexpected last chunk size");
-    std::memcpy(scratch->data() + pos, c.data, c.size);
-    pos += c.size;
   }
   const bool compressed = ext < (int64_t)d.ptr.rawsize - 4;
   if (!compressed) {
     if (ext != out_size) return set_err("external raw size mismatch");
-    std::memcpy(out, scratch->data(), (size_t)ext);
+    int64_t pos = 0;
+    for (const Chunk& c : cs) {
+      std::memcpy(out + pos, c.data, c.size);
+      pos += c.size;
+    }
+    *copy_s += now_s() - tc;
     return true;
   }
   if (ext < 4) return set_err("external compressed datum shorter than its header");
-  const uint32_t raw = rd32(scratch->data());
+  // the stream is read in place from the chunks (pglz_decompress_pieces): no
+  // copy of the compressed value into a scratch buffer first
+  std::vector<const uint8_t*> ptrs(cs.size());
+  std::vector<int64_t> lens(cs.size());
+  for (size_t i = 0; i < cs.size(); ++i) {
+    ptrs[i] = cs[i].data;
+    lens[i] = cs[i].size;
+  }
+  uint8_t hdr[4];
+  for (int64_t k = 0, i = 0, o = 0; k < 4; ++k) {     // rawsize u32 (may straddle chunks)
+    while (o >= lens[(size_t)i]) {
+      ++i;
+      o = 0;
+    }
+    hdr[k] = ptrs[(size_t)i][o++];
+  }
+  const uint32_t raw = rd32(hdr);
   if ((int64_t)raw != out_size) return set_err("external raw size does not match");
-  if (cer_pglz_decompress(scratch->data() + 4, ext - 4, out, raw) < 0)
+  const double tp = now_s();
+  *copy_s += tp - tc;
+  if (cer_pglz_decompress_pieces(ptrs.data(), lens.data(), (int)cs.size(), 4, out, raw) < 0)
     return set_err("compressed data is corrupt");
+  *pglz_s += now_s() - tp;
+  (void)scratch;
   return true;
 }
 
@@ -264,23 +368,45 @@ extern "C" {
 
 const char* cer_da_last_error() { return g_err.c_str(); }
 
-void* cer_da_open(const char* heap_base, const char* toast_base) {
+// nthreads: TOAST-index threads (0: 16)
+void* cer_da_open2(const char* heap_base, const char* toast_base, int nthreads) {
   auto* r = new DAReader();
-  auto hs = segment_files(heap_base);
-  if (hs.empty()) {
-    set_err(std::string("no heap segment files at ") + heap_base);
+  r->nthreads = nthreads > 0 ? nthreads : 16;
+  double t0 = now_s();
+  if (!map_relation(heap_base, &r->heap, true) || !map_relation(toast_base, &r->toast, false)) {
     delete r;
     return nullptr;
   }
-  for (auto& p : hs)
-    if (!read_file(p, &r->heap)) { delete r; return nullptr; }
-  for (auto& p : segment_files(toast_base))
-    if (!read_file(p, &r->toast)) { delete r; return nullptr; }
-  if (!parse_heap(r) || !index_toast(r)) {
+  double t1 = now_s();
+  r->map_s = t1 - t0;
+  if (!parse_heap(r)) {
     delete r;
     return nullptr;
   }
+  double t2 = now_s();
+  r->heap_s = t2 - t1;
+  if (!index_toast(r)) {
+    delete r;
+    return nullptr;
+  }
+  r->index_s = now_s() - t2;
   return r;
+}
+
+void* cer_da_open(const char* heap_base, const char* toast_base) {
+  return cer_da_open2(heap_base, toast_base, 0);
+}
+
+// phase timings: out[0..8] = map, heap parse, TOAST index (open), read wall,
+// read busy (sum over workers), read TOAST copy (sum), read pglz (sum),
+// read threads, TOAST-index threads
+int cer_da_stats(void* h, double* out) {
+  auto* r = static_cast<DAReader*>(h);
+  const double v[9] = {r->map_s, r->heap_s, r->index_s, r->read_wall_s, r->read_busy_s,
+                       r->read_copy_s, r->read_pglz_s, (double)r->read_threads,
+                       (double)r->nthreads};
+  for (int i = 0; i < 9; ++i) out[i] = v[i];
+  return 9;
 }
 
 int cer_da_count(void* h) { return (int)static_cast<DAReader*>(h)->tuples.size(); }
@@ -305,14 +431,32 @@ int cer_da_read(void* h, int n, const int* idx, uint8_t** indep_out, uint8_t** d
   std::atomic<int> next(0), failed(0);
   std::string first_err;
   std::atomic<bool> have_err(false);
-  auto work = [&]() {
+  nthreads = std::max(1, std::min(nthreads, n));
+  std::vector<double> busy((size_t)nthreads, 0.0), copy((size_t)nthreads, 0.0),
+      pglz((size_t)nthreads, 0.0);
+  // largest values first: a partition's buffers are few and large (a
+  // pglz stream is serial), so the last round of a size-blind order leaves
+  // most threads idle
+  std::vector<int> order(idx, idx + n);
+  std::vector<int> slot((size_t)n);
+  for (int j = 0; j < n; ++j) slot[(size_t)j] = j;
+  std::stable_sort(slot.begin(), slot.end(), [&](int a, int b) {
+    return raw_size(r->tuples[(size_t)order[(size_t)a]].indep) >
+           raw_size(r->tuples[(size_t)order[(size_t)b]].indep);
+  });
+  auto work = [&](int w) {
     std::vector<uint8_t> scratch;
     for (;;) {
-      int j = next.fetch_add(1);
-      if (j >= n || failed.load()) break;
+      int q = next.fetch_add(1);
+      if (q >= n || failed.load()) break;
+      const int j = slot[(size_t)q];
+      const double t0 = now_s();
       const Tuple& t = r->tuples[(size_t)idx[j]];
-      bool ok = detoast(r, t.indep, indep_out[j], raw_size(t.indep), &scratch) &&
-                detoast(r, t.dep, dep_out[j], raw_size(t.dep), &scratch);
+      bool ok = detoast(r, t.indep, indep_out[j], raw_size(t.indep), &scratch, &copy[(size_t)w],
+                        &pglz[(size_t)w]) &&
+                detoast(r, t.dep, dep_out[j], raw_size(t.dep), &scratch, &copy[(size_t)w],
+                        &pglz[(size_t)w]);
+      busy[(size_t)w] += now_s() - t0;
       if (!ok) {
         failed.store(1);
         bool expected = false;
@@ -320,11 +464,19 @@ int cer_da_read(void* h, int n, const int* idx, uint8_t** indep_out, uint8_t** d
       }
     }
   };
-  nthreads = std::max(1, std::min(nthreads, n));
+  const double t0 = now_s();
   std::vector<std::thread> pool;
-  for (int i = 1; i < nthreads; ++i) pool.emplace_back(work);
-  work();
+  for (int i = 1; i < nthreads; ++i) pool.emplace_back(work, i);
+  work(0);
   for (auto& t : pool) t.join();
+  r->read_wall_s = now_s() - t0;
+  r->read_busy_s = r->read_copy_s = r->read_pglz_s = 0;
+  for (int i = 0; i < nthreads; ++i) {
+    r->read_busy_s += busy[(size_t)i];
+    r->read_copy_s += copy[(size_t)i];
+    r->read_pglz_s += pglz[(size_t)i];
+  }
+  r->read_threads = nthreads;
   if (failed.load()) {
     g_err = first_err;
     return -1;

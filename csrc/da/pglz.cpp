@@ -11,6 +11,7 @@
 // The decompressor is the hot path of Direct-Access ETL (83 525 s at 1 worker
 // in the reference, pure Python); it runs here as a tight native loop, one
 // value per thread (values are independent; a value is inherently serial).
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -108,12 +109,50 @@ extern "C" int64_t cer_pglz_compress(const uint8_t* src, int64_t n, uint8_t* dst
 // header) into exactly `rawsize` bytes.  Returns rawsize, or -1 if corrupt
 // (output overrun / underrun or input not fully consumed — the reference's
 // end-of-stream corruption check).
-extern "C" int64_t cer_pglz_decompress(const uint8_t* src, int64_t srclen, uint8_t* dst,
-                                       int64_t rawsize) {
-  const uint8_t* sp = src;
-  const uint8_t* const srcend = src + srclen;
-  uint8_t* dp = dst;
-  uint8_t* const destend = dst + rawsize;
+namespace {
+
+constexpr int64_t kGroupIn = 1 + 8 * 3;              // input bytes of one control group, at most
+constexpr int64_t kGroupOut = 8 * kMaxMatch + 16;    // output bytes (+ copy overshoot), at most
+
+// One control group with no bounds checks: the caller guarantees kGroupIn
+// input bytes at sp and kGroupOut output bytes at dp.  An all-literal group
+// is one 8-byte copy; a back-reference copies in 16- / 8-byte steps (the
+// overshoot stays inside the slack) unless it overlaps closer than 8 bytes
+// (byte loop: run-length).  False: a reference before the start of dst.
+inline bool group_fast(const uint8_t*& sp, uint8_t*& dp, const uint8_t* dst) {
+  uint8_t ctrl = *sp++;
+  if (ctrl == 0) {
+    std::memcpy(dp, sp, 8);
+    dp += 8;
+    sp += 8;
+    return true;
+  }
+  for (int k = 0; k < 8; ++k, ctrl >>= 1) {
+    if (ctrl & 1) {
+      int32_t len = (sp[0] & 0x0f) + 3;
+      const int32_t off = ((sp[0] & 0xf0) << 4) | sp[1];
+      sp += 2;
+      if (len == 18) len += *sp++;
+      if (off == 0 || off > dp - dst) return false;
+      const uint8_t* from = dp - off;
+      if (off >= 16) {
+        for (int32_t i = 0; i < len; i += 16) std::memcpy(dp + i, from + i, 16);
+      } else if (off >= 8) {
+        for (int32_t i = 0; i < len; i += 8) std::memcpy(dp + i, from + i, 8);
+      } else {
+        for (int32_t i = 0; i < len; ++i) dp[i] = from[i];
+      }
+      dp += len;
+    } else {
+      *dp++ = *sp++;
+    }
+  }
+  return true;
+}
+
+// every item checked; continues a stream whose output so far is [dst, dp)
+int64_t decode_checked(const uint8_t* sp, const uint8_t* srcend, const uint8_t* dst, uint8_t* dp,
+                       uint8_t* destend) {
   while (sp < srcend && dp < destend) {
     uint8_t ctrl = *sp++;
     for (int ctrlc = 0; ctrlc < 8 && sp < srcend; ++ctrlc) {
@@ -143,5 +182,88 @@ extern "C" int64_t cer_pglz_decompress(const uint8_t* src, int64_t srclen, uint8
     }
   }
   if (dp != destend || sp != srcend) return -1;
-  return rawsize;
+  return destend - dst;
+}
+
+}  // namespace
+
+extern "C" int64_t cer_pglz_decompress(const uint8_t* src, int64_t srclen, uint8_t* dst,
+                                       int64_t rawsize) {
+  const uint8_t* sp = src;
+  const uint8_t* const srcend = src + srclen;
+  uint8_t* dp = dst;
+  uint8_t* const destend = dst + rawsize;
+  // fast path while a whole control group cannot run past either buffer
+  while (srcend - sp >= kGroupIn && destend - dp >= kGroupOut)
+    if (!group_fast(sp, dp, dst)) return -1;
+  return decode_checked(sp, srcend, dst, dp, destend) < 0 ? -1 : rawsize;
+}
+
+// Decompress a pglz stream stored in pieces (the TOAST chunks of a value, in
+// order) without first copying them into one buffer: ptrs[i] / lens[i] are
+// the pieces, the stream starts `skip` bytes into piece 0.  A control group
+// that straddles a piece boundary is decoded from a small stitch buffer; the
+// last bytes (within a group of the end of the input or output) go through
+// the checked decoder.  Same result and corruption checks as
+// cer_pglz_decompress on the concatenated pieces.
+extern "C" int64_t cer_pglz_decompress_pieces(const uint8_t* const* ptrs, const int64_t* lens,
+                                              int n, int64_t skip, uint8_t* dst,
+                                              int64_t rawsize) {
+  if (n <= 0) return rawsize == 0 ? 0 : -1;
+  int si = 0;
+  while (si < n && skip >= lens[si]) skip -= lens[si++];
+  if (si >= n) return rawsize == 0 ? 0 : -1;
+  const uint8_t* sp = ptrs[si] + skip;
+  const uint8_t* se = ptrs[si] + lens[si];
+  uint8_t* dp = dst;
+  uint8_t* const destend = dst + rawsize;
+  uint8_t stitch[2 * kGroupIn];
+  while (destend - dp >= kGroupOut) {
+    if (se - sp >= kGroupIn) {
+      if (!group_fast(sp, dp, dst)) return -1;
+      continue;
+    }
+    // the group straddles the end of piece si: stitch its tail with the
+    // next pieces' head
+    const int64_t r = se - sp;
+    std::memcpy(stitch, sp, (size_t)r);
+    int64_t m = r;
+    int sj = si + 1;
+    int64_t oj = 0;
+    while (m < kGroupIn && sj < n) {
+      const int64_t take = std::min<int64_t>(kGroupIn - m, lens[sj] - oj);
+      std::memcpy(stitch + m, ptrs[sj] + oj, (size_t)take);
+      m += take;
+      oj += take;
+      if (oj == lens[sj]) {
+        ++sj;
+        oj = 0;
+      }
+    }
+    if (m < kGroupIn) break;                     // near the end of the input
+    const uint8_t* q = stitch;
+    if (!group_fast(q, dp, dst)) return -1;
+    int64_t c = q - stitch;
+    if (c < r) {
+      sp += c;
+      continue;
+    }
+    c -= r;                                      // bytes consumed past piece si
+    ++si;
+    while (si < n && c >= lens[si]) c -= lens[si++];
+    if (si >= n) {
+      sp = se = nullptr;
+      break;
+    }
+    sp = ptrs[si] + c;
+    se = ptrs[si] + lens[si];
+  }
+  // the rest (bounded: within one group of the end of the output or input)
+  std::vector<uint8_t> rest;
+  if (sp) {
+    rest.insert(rest.end(), sp, se);
+    for (int j = si + 1; j < n; ++j) rest.insert(rest.end(), ptrs[j], ptrs[j] + lens[j]);
+  }
+  return decode_checked(rest.data(), rest.data() + rest.size(), dst, dp, destend) < 0 ? -1
+                                                                                     : rawsize;
 }

@@ -2903,6 +2903,269 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
   }
 }
 
+// ===========================================================================
+// Wave-specialised fp32 weight gradient (wgrad_ws32)
+// ===========================================================================
+// The register-staged wgrad (wgrad_reg_body32) has every wave load, split,
+// store, wait at a block barrier and multiply in turn: one barrier per 32-deep
+// step, and one register set for the 128x128 tile (a second one spills), so
+// each step's L2 / HBM latency is covered by ONE step of MFMA work and about a
+// quarter of the wave time sits at barriers (profiles/r2_conv32_pmc_isa.md).
+// Here a 512-thread workgroup (one per CU) splits the roles:
+//  * waves 4-7 (loaders) keep WS_P steps of global loads in flight in
+//    registers, split fp32 -> (hi, lo) bf16 (HL operands are taken as they
+//    are) and write the TN images (tn_off_w, hi rows 0-31, lo rows 32-63)
+//    into an S-stage LDS ring;
+//  * waves 0-3 (consumers) read a stage's 32x32x16 fragments and issue its
+//    24 MFMAs (2 substeps x 3 passes x 2x2 tiles of a 64x64 wave tile),
+//    reading the NEXT stage's fragments under them.  They never wait at a
+//    block barrier.
+// Hand-off by two monotone LDS counters per stage: a loader wave adds 1 to
+// full[s] once its ds_writes of the stage have completed (lgkmcnt(0)); a
+// consumer wave adds 1 to free[s] once its fragment reads of the stage have
+// returned.  Step t (stage t % S) is readable when full[s] >= 4 (t / S + 1)
+// and writable when free[s] >= 4 (t / S).  Waves 0-3 and 4-7 land on the 4
+// SIMDs in the same order, so every SIMD holds one consumer and one loader:
+// the loader's split VALU and LDS writes issue in the 24 free cycles of each
+// 32-cycle 32x32x16 MFMA of its partner.  Counters and ring live in ONE
+// __shared__ array (a second LDS object can make hipcc drain vmcnt).
+constexpr int WS_THREADS = 512;
+constexpr int WS_S = 4;          // LDS ring stages
+constexpr int WS_P = 2;          // loader register sets (steps of loads in flight)
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+
+__device__ __forceinline__ void ws_wait(unsigned* c, unsigned target) {
+  lds_u32* lc = (lds_u32*)c;
+  while (__hip_atomic_load(lc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void ws_post(unsigned* c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add((lds_u32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int BM, int BN, int S>
+__device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_t* lds,
+                                              unsigned* cnt) {
+  constexpr int STAGE = (BM + BN) * BK;            // [64 x BM] A image + [64 x BN] B image
+  const int tiles_k = (p.K + BN - 1) / BN;
+  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
+  const int cfg = work / (tiles * p.splits);
+  const int rem = work - cfg * tiles * p.splits;
+  const int split = rem / tiles, tile = rem - split * tiles;
+  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
+  const int n0 = tn_ * BM, k0 = tk * BN;
+  const int ms = split * p.m_per_split;
+  const int me = min(p.Mred, ms + p.m_per_split);
+  const int T = ms < me ? (me - ms + KS - 1) / KS : 0;
+  unsigned* full = cnt;
+  unsigned* freed = cnt + S;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (wid >= 4) {
+    // ---------------- loaders ----------------
+    constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
+    constexpr int A_CH = KS * A_CPR / 256, B_CH = KS * B_CPR / 256;
+    constexpr int A_RSTEP = 256 / A_CPR, B_RSTEP = 256 / B_CPR;
+    const int tl = tid - 256;
+    const int a_col = 8 * (tl % A_CPR), b_col = 8 * (tl % B_CPR);
+    const int a_row0 = tl / A_CPR, b_row0 = tl / B_CPR;
+    const int kk0 = k0 + b_col;
+    const bool b_kok = kk0 < p.K;
+    KPos bk{0, 0, 0};
+    if (b_kok) bk = kpos_init(p.x, kk0);
+    const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
+    const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
+    const __amdgpu_buffer_rsrc_t rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
+    const __amdgpu_buffer_rsrc_t rX = make_rsrc(xb, p.x.bytes);
+    const bool a_nok = n0 + a_col < p.N;
+    uint4 ra[WS_P][2 * A_CH], rb[WS_P][2 * B_CH];
+    auto load = [&](int t, auto U) {
+      constexpr int u = decltype(U)::value;
+      const int mbase = ms + t * KS;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int m = mbase + a_row0 + A_RSTEP * i;
+        const uint32_t o = (m < me && a_nok) ? (uint32_t)(m * p.ldy + n0 + a_col) * 4u : OOB;
+        ra[u][2 * i] = bload(rDY, o);
+        ra[u][2 * i + 1] = bload(rDY, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
+        const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
+        const uint32_t o = b_kok ? off : OOB;
+        rb[u][2 * i] = bload(rX, o);
+        rb[u][2 * i + 1] = bload(rX, o + 16u);
+      }
+    };
+    auto store = [&](int st, auto U) {
+      constexpr int u = decltype(U)::value;
+      bf16_t* sa = lds + st * STAGE;
+      bf16_t* sb = sa + BK * BM;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int row = a_row0 + A_RSTEP * i;
+        uint4 h, l;
+        take_hi_lo(p.dy_hl != 0, ra[u][2 * i], ra[u][2 * i + 1], h, l);
+        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row, a_col)) = h;
+        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row + KS, a_col)) = l;
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const int row = b_row0 + B_RSTEP * i;
+        uint4 h, l;
+        take_hi_lo(p.x_hl != 0, rb[u][2 * i], rb[u][2 * i + 1], h, l);
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
+        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    // loads past the item's rows are issued anyway (out-of-range offsets:
+    // zeros, no memory traffic) so no branch guards a load and hipcc keeps
+    // counted vmcnt waits
+    load(0, I0{});
+    load(1, I1{});
+    auto step = [&](int t, auto U) {
+      const int st = t % S;
+      if (t >= S) ws_wait(&freed[st], 4u * (unsigned)(t / S));
+      store(st, U);
+      load(t + WS_P, U);
+      ws_post(&full[st]);
+    };
+    for (int t = 0; t < T; t += 2) {
+      step(t, I0{});
+      if (t + 1 >= T) break;
+      step(t + 1, I1{});
+    }
+    return;
+  }
+  // ---------------- consumers ----------------
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int wa = wid >> 1, wb = wid & 1;
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // tn_frag32 addresses, precomputed: for the 128-column images tn_off_w's
+  // swizzle XORs chunk bits 3-4 with row & 3 = q (every fragment row offset
+  // is a multiple of 4), so fragment i of wave column w starts at
+  // (8h + q) * 128 + 32 ((2w + i) ^ q) + 16g + 4pp; the substep / hi-lo row
+  // offsets are compile-time element offsets on top (one VGPR per i, not one
+  // per fragment read)
+  static_assert(BM == 128 && BN == 128, "wgrad_ws32: 128x128 tiles (tn_off_w<128>)");
+  const int fh = lane >> 5, fg = (lane >> 4) & 1, fq = (lane & 15) >> 2, fp = lane & 3;
+  int abase[FM], bbase[FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+    abase[i] = (8 * fh + fq) * BM + 32 * ((2 * wa + i) ^ fq) + 16 * fg + 4 * fp;
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    bbase[j] = (8 * fh + fq) * BN + 32 * ((2 * wb + j) ^ fq) + 16 * fg + 4 * fp;
+  auto frag = [&](const bf16_t* tile, int base, int row0, int cols) {
+    const bf16_t* p0 = tile + base + row0 * cols;
+    s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * cols));
+    s16x8 tt = __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, tt);
+  };
+  // one 16-deep substep's fragments of stage st (hi and lo of both operands)
+  struct Sub {
+    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
+  };
+  auto read_sub = [&](int st, int sub, Sub& F) {
+    const bf16_t* sa = lds + st * STAGE;
+    const bf16_t* sb = sa + BK * BM;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      F.ah[i] = frag(sa, abase[i], 16 * sub, BM);
+      F.al[i] = frag(sa, abase[i], KS + 16 * sub, BM);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      F.bh[j] = frag(sb, bbase[j], 16 * sub, BN);
+      F.bl[j] = frag(sb, bbase[j], KS + 16 * sub, BN);
+    }
+  };
+  auto mma_sub = [&](const Sub& F) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = mfma3w(F.ah[i], F.al[i], F.bh[j], F.bl[j], acc[i][j]);
+  };
+  // half-step pipeline: substep 1's fragments are read under substep 0's
+  // MFMAs, the next step's substep 0 under substep 1's.  The last step
+  // re-reads its own stage instead of a next one (min), so no read is
+  // conditional (a conditionally defined fragment set doubles the live
+  // registers and spills)
+  if (T > 0) {
+    Sub R0, R1;
+    ws_wait(&full[0], 4u);
+    read_sub(0, 0, R0);
+    for (int t = 0; t < T; ++t) {
+      const int st = t % S;
+      read_sub(st, 1, R1);
+      mma_sub(R0);
+      ws_post(&freed[st]);                     // every read of stage t has returned
+      const int tn = t + 1 < T ? t + 1 : t;
+      ws_wait(&full[tn % S], 4u * (unsigned)(tn / S + 1));
+      read_sub(tn % S, 0, R0);
+      mma_sub(R1);
+    }
+  }
+  // D[n][k]: k = lane & 31 (32 consecutive k per register: 128-B rows)
+  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
+  const bool split_k = p.splits > 1;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + wa * TM + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int k = k0 + wb * TN + 32 * j + r;
+        if (n < p.N && k < p.K && T > 0) {
+          float* d = dwb + (int64_t)n * p.K + k;
+          if (split_k)
+            atomicAdd(d, acc[i][j][e]);
+          else
+            *d = acc[i][j][e];
+        }
+      }
+}
+
+// batched: one work item per block (XCD-ordered), or -- a grid capped below
+// the item count (the side-stream batch) -- items walked block-strided
+template <int BM, int BN>
+__global__ __launch_bounds__(WS_THREADS, 2) void wgrad_ws32(WGBatch b) {
+  constexpr int STAGE = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) bf16_t lds[WS_S * STAGE + 4 * WS_S];
+  unsigned* cnt = reinterpret_cast<unsigned*>(lds + WS_S * STAGE);
+  const int total = b.start[b.n];
+  const int nwg = (int)gridDim.x;
+  if (threadIdx.x < 2 * WS_S) cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int w = blockIdx.x; w < total; w += nwg) {
+    const int work = nwg >= total ? xcd_remap(w, nwg) : w;
+    int i = 0;
+    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
+    wgrad_ws_item<BM, BN, WS_S>(b.p[i], work - b.start[i], lds, cnt);
+    if (w + nwg < total) {              // the next item restarts the ring
+      __syncthreads();
+      if (threadIdx.x < 2 * WS_S) cnt[threadIdx.x] = 0u;
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // per-config weight transpose for dgrad: W[N][T][C] -> Wt[C][T][N]
 // ---------------------------------------------------------------------------
@@ -3823,6 +4086,17 @@ CER_API int cer_wgrad_batch_add_grouped_f32(const float* x, int B, int H, int W,
                            dw_gstride);
 }
 
+// the wave-specialised kernel for 128x128 fp32 batches (CER_WGB_WS, A/B)
+static int g_wgb_ws = -1;
+static bool wgb_ws() {
+  if (g_wgb_ws < 0) {
+    const char* e = getenv("CER_WGB_WS");
+    g_wgb_ws = e ? atoi(e) : 0;
+  }
+  return g_wgb_ws > 0;
+}
+CER_API void cer_wgrad_batch_set_ws(int on) { g_wgb_ws = on ? 1 : 0; }
+
 // grid cap of the next fp32 batch flushes (0 = one block per work item)
 static int g_wgb_grid = 0;
 CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
@@ -3842,7 +4116,11 @@ static void wgb32_launch_sel(hipStream_t stream) {
     }
     bt.start[bt.n] = tot;
     const int grid = g_wgb_grid > 0 && g_wgb_grid < tot ? g_wgb_grid : tot;
-    if (tot > 0) wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
+    if (tot <= 0) continue;
+    if (BM == 128 && BN == 128 && wgb_ws())
+      wgrad_ws32<128, 128><<<grid, WS_THREADS, 0, stream>>>(bt);
+    else
+      wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
   }
 }
 

@@ -272,6 +272,51 @@ def test_wgrad_batch_wide_fp32_vs_fp64(vb):
     assert max(errs) < TOL, errs
 
 
+@pytest.mark.parametrize("grid", [0, 7])
+def test_wgrad_batch_ws_fp32_vs_fp64(grid):
+    """The wave-specialised batched wgrad (wgrad_ws32: loader waves -> LDS
+    ring -> MFMA waves, LDS-counter hand-off) over every aligned ResNet-50
+    shape at once, 8 configs and 1; grid = 7 walks the items persistently
+    (the side-stream batch's capped grid) and restarts the ring per item."""
+    from cerebro_ds_kpgi_amd.ops import _hip, streams
+    cases = [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0 and c[3] >= 8]
+    keep = streams._BATCH_VARIANT
+    L = _hip.lib()
+    streams.set_batch_variant(1)
+    L.cer_wgrad_batch_set_ws(1)
+    if grid:
+        L.cer_wgrad_batch_set_grid(grid)
+    try:
+        errs = []
+        made = []
+        for (B, H, W, cin, cout, k, s, p, G) in cases:
+            spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
+            a, refs = _make([spec], G)
+            torch.manual_seed(1)
+            x = torch.randn(B, H, W, G * cin, device="cuda").requires_grad_(True)
+            made.append((a, refs, x, (B, H, W, cin, cout, k, s, p, G)))
+        with streams.deferred_wgrad():
+            for a, refs, x, c in made:
+                y = P.conv2d(x, refs["w"], c[6], c[7])
+                torch.manual_seed(3)
+                y.backward(torch.randn_like(y))
+        torch.cuda.synchronize()
+        for a, refs, x, (B, H, W, cin, cout, k, s, p, G) in made:
+            torch.manual_seed(3)
+            w64 = _w64(refs["w"]).requires_grad_(True)
+            y64 = F.conv2d(_nchw(x.detach().double()), w64, None, s, p, 1, G)
+            y64.backward(_nchw(torch.randn(y64.shape[0], y64.shape[2], y64.shape[3], y64.shape[1],
+                                           device="cuda").double()))
+            dw64 = w64.grad.view(G, cout, cin, k, k).permute(0, 1, 3, 4, 2)
+            errs.append(_rel(a.grad.view(G, -1)[:, :dw64[0].numel()], dw64.reshape(G, -1)))
+    finally:
+        L.cer_wgrad_batch_set_ws(0)
+        L.cer_wgrad_batch_set_grid(0)
+        streams.set_batch_variant(keep)
+    print("wgrad batch ws grid", grid, ["%.1e" % e for e in errs])
+    assert max(errs) < TOL, errs
+
+
 @pytest.mark.parametrize("vd", [12, 13, 14])
 def test_bn_link_dgrad_epilogue_wide_fp32(vd):
     """BN-backward partials from the wide dgrad epilogue (epi32w BSTAT)."""
