@@ -69,7 +69,8 @@ def main():
                          "pglz reader; the ETL is reported separately (etl_da)")
     ap.add_argument("--configs", type=int, default=0,
                     help="diagnostic: train only the first K configs (per-GPU work of N = 8/K "
-                         "GPUs); the headline number always uses all 8")
+                         "GPUs), or K > 8 configs packed (more learning rates); the headline "
+                         "number always uses all 8")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -102,6 +103,13 @@ def main():
             grid["batch_size"] = [args.batch]
     msts = get_msts(grid)
     if args.configs:
+        if args.configs > len(msts):
+            # a wider pack than the grid (e.g. the hetero workload's 10
+            # NASNet configs as one G = 10 launch stream): more learning rates
+            base = list(msts)
+            msts = [dict(base[i % len(base)],
+                         learning_rate=base[i % len(base)]["learning_rate"] * (1 + i // len(base)))
+                    for i in range(args.configs)]
         msts = msts[:args.configs]
     S = len(msts)
     B = max(m["batch_size"] for m in msts)

@@ -1,16 +1,36 @@
 #!/bin/bash
 # the reference's secondary published workloads at N = 1 (fp32, HIP path):
 # model-size drill-down (8 configs each), e2e 16-config grid, the 48-config
-# hetero drill-down's per-config steps, and a dwconv (MobileNetV2) profile
+# hetero drill-down's per-config steps, and a dwconv (MobileNetV2) profile.
+#   bash scripts/gpu/secondary.sh hetero   -- only the 48-config hetero drill-down:
+#     pack rates (NASNet-Mobile bs4 G = 1 / 10, MobileNetV2 bs128 G = 1 / 8) and
+#     the CTQ (greedy) and UDAF (rotation) jobs at N = 1, 12 partitions of 512
+#     images
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r3sec
+O=gpurun_out/r4sec
 mkdir -p $O
 run() {  # name, bench args...
   local n=$1; shift
   timeout -k 10 400 python3 -u bench.py "$@" > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; exit 1; }
   echo "$n $(python3 -c "import json;d=json.load(open('$O/$n.json'));print(d['metric'],d['value'],d['ms_per_step'])")"
 }
+if [ "$1" = "hetero" ]; then
+  run nasnet_b4_g1 --model nasnetmobile --batch 4 --configs 1 --steps 60 --warmup 20
+  run nasnet_b4_g10 --model nasnetmobile --batch 4 --configs 10 --steps 60 --warmup 20
+  run mbv2_b128_g1 --model mobilenetv2 --batch 128 --configs 1 --steps 30 --warmup 10
+  run mbv2_b128_g8 --model mobilenetv2 --batch 128 --configs 8 --steps 30 --warmup 10
+  for A in ctq run_mop; do
+    timeout -k 10 1000 python3 -u -m cerebro_ds_kpgi_amd.runners.$A --run --num_epochs 1 \
+      --drill_down_hetro --size 1 --slots_per_gpu 12 --train_per_partition 512 \
+      --valid_per_partition 64 --backend hip --logs_root $O/het_$A/logs \
+      --models_root /tmp/het_models > $O/het_$A.log 2>&1 || { tail -20 $O/het_$A.log; exit 1; }
+    grep SUMMARY $O/het_$A.log | tail -1 | cut -c1-600
+    cp $O/het_$A/global.log $O/het_${A}_global.log 2>/dev/null
+  done
+  rm -rf /tmp/het_models
+  exit 0
+fi
 for M in mobilenetv2 resnet152 vgg16; do run size_$M --model $M --steps 30 --warmup 10; done
 run e2e16 --workload e2e16 --steps 20 --warmup 5 --steps_per_round 10
 run hetero_mbv2_b128 --model mobilenetv2 --batch 128 --configs 1 --steps 30 --warmup 10
