@@ -499,6 +499,13 @@ if os.environ.get("CER_FP32_WIDE", "1") != "0":
 _KSPLIT32 = (24, 26, 30, 32)
 if os.environ.get("CER_FP32_KSPLIT", "1") != "0":
     FP32_VARIANTS = {op: vs + (_KSPLIT32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
+# 36-47: wave-specialised twins of the wide register-staged fwd / dgrad
+# kernels (512 threads: 4 loader waves fill a 4-stage LDS ring, 4 MFMA waves
+# consume it; conv.hip kloop_ws), three tiles, with and without split-K
+# (CER_FP32_WS=0 leaves them out).
+_WS32 = (36, 37, 38, 42, 43, 44)
+if os.environ.get("CER_FP32_WS", "1") != "0":
+    FP32_VARIANTS = {op: vs + (_WS32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
 
 
 def _select(op, key, launch, dtype, after_tune=None):

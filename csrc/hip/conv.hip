@@ -2353,20 +2353,90 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
-template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
-__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTParams p) {
+constexpr int WS_THREADS = 512;
+constexpr int WS_S = 4;          // LDS ring stages
+constexpr int WS_P = 2;          // loader register sets (steps of loads in flight)
+typedef __attribute__((address_space(3))) unsigned lds_u32;
+
+__device__ __forceinline__ void ws_wait(unsigned* c, unsigned target) {
+  lds_u32* lc = (lds_u32*)c;
+  while (__hip_atomic_load(lc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+    __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void ws_post(unsigned* c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_add((lds_u32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// K loop of the wave-specialised fwd / dgrad twins (WS = 1): waves 4-7 run
+// the kernel's own load / store lambdas (register-staged global loads, two
+// sets in flight, hi/lo split, ds_write into stage t % S), waves 0-3 its mma
+// lambda on each stage; the same per-stage full / free LDS counters as
+// wgrad_ws32.  The load lambda is called in increasing step order (it keeps
+// an incremental im2col position) and past k1 (out-of-range or unused
+// loads, as kloop32 does), the lambdas see tid = threadIdx.x & 255.
+template <int S, typename Load, typename Store, typename Mma>
+__device__ __forceinline__ void kloop_ws(int k0, int k1, unsigned* cnt, Load&& load, Store&& store,
+                                         Mma&& mma) {
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  unsigned* full = cnt;
+  unsigned* freed = cnt + S;
+  const int T = k1 - k0;
+  if (threadIdx.x >= 256) {
+    load(k0, I0{});
+    load(k0 + 1, I1{});
+    auto step = [&](int t, auto U) {
+      const int st = t % S;
+      if (t >= S) ws_wait(&freed[st], 4u * (unsigned)(t / S));
+      store(st, U);
+      load(k0 + t + 2, U);
+      ws_post(&full[st]);
+    };
+    for (int t = 0; t < T; t += 2) {
+      step(t, I0{});
+      if (t + 1 >= T) break;
+      step(t + 1, I1{});
+    }
+  } else {
+    for (int t = 0; t < T; ++t) {
+      const int st = t % S;
+      ws_wait(&full[st], 4u * (unsigned)(t / S + 1));
+      mma(st);
+      ws_post(&freed[st]);
+    }
+  }
+}
+
+// WS = 1: the wave-specialised twin (512 threads: waves 4-7 load / split /
+// store into a WS_S-stage LDS ring, waves 0-3 run the MFMAs and, after the
+// loaders have exited, the split-K reduction and the epilogue; kloop_ws)
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1, int WS = 0>
+__global__ __launch_bounds__(NTHREADS * (WS ? 2 : WG),
+                             WS ? 2 : (WG == 1 ? 2 : 1))
+void igemm_nt32(NTParams p) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
+  static_assert(!WS || (WIDE && WG == 1 && GM != GM_SLOW), "WS: aligned wide kernels only");
+  constexpr int NST = WS ? WS_S : 2;                          // LDS stages
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
-  constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
+  constexpr int TILE_ELEMS = NST * (BM + BN) * BK;
+  constexpr int LDS_ELEMS = (TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN) + (WS ? 16 : 0);
   static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
                 "group hand-off must fit one group's LDS region");
   __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
   const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
   bf16_t* const lds = lds_all + grp * LDS_ELEMS;
+  unsigned* const wscnt = reinterpret_cast<unsigned*>(lds_all + LDS_ELEMS - 16);
+  if constexpr (WS != 0) {
+    if (threadIdx.x < 2 * WS_S) wscnt[threadIdx.x] = 0u;
+    __syncthreads();
+  }
 #define SA(buf) (lds + (buf) * (BM * BK))
-#define SB(buf) (lds + 2 * BM * BK + (buf) * (BN * BK))
+#define SB(buf) (lds + NST * BM * BK + (buf) * (BN * BK))
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
@@ -2396,7 +2466,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = fp32_sets<BM, BN, WIDE>();
+  constexpr int SETS = WS ? 2 : fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -2454,8 +2524,14 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nt32(NTP
   typename AccT<BM, BN, WIDE>::type acc;
   if constexpr (WIDE) {
     zero_accw<BM, BN>(acc);
-    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles,
-                  [&](int cur) { mma3w_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); });
+    auto mma = [&](int cur) { mma3w_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); };
+    if constexpr (WS != 0) {
+      kloop_ws<WS_S>(kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles, mma);
+      if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
+      __syncthreads();                           // every consumer is past its last ring read
+    } else {
+      kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
+    }
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   } else {
@@ -2599,20 +2675,28 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
-__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTParams p, int T,
-                                                                         FastDiv dCout) {
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1, int WS = 0>
+__global__ __launch_bounds__(NTHREADS * (WS ? 2 : WG),
+                             WS ? 2 : (WG == 1 ? 2 : 1))
+void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
+  static_assert(!WS || (WIDE && WG == 1), "WS: wide kernels only");
+  constexpr int NST = WS ? WS_S : 2;
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
   constexpr int B_CPR = BN / 8, B_CH = KS * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
-  constexpr int TILE_ELEMS = 2 * (BM + BN) * BK;
-  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
+  constexpr int TILE_ELEMS = NST * (BM + BN) * BK;
+  constexpr int LDS_ELEMS = (TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN) + (WS ? 16 : 0);
   static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
                 "group hand-off must fit one group's LDS region");
   __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
   const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
   bf16_t* const lds = lds_all + grp * LDS_ELEMS;
+  unsigned* const wscnt = reinterpret_cast<unsigned*>(lds_all + LDS_ELEMS - 16);
+  if constexpr (WS != 0) {
+    if (threadIdx.x < 2 * WS_S) wscnt[threadIdx.x] = 0u;
+    __syncthreads();
+  }
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
@@ -2638,7 +2722,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = fp32_sets<BM, BN>();
+  constexpr int SETS = WS ? 2 : fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -2667,7 +2751,7 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
   auto store_tiles = [&](int buf, auto S) {
     constexpr int s = decltype(S)::value;
     bf16_t* sa = lds + buf * (BM * BK);
-    bf16_t* sb = lds + 2 * BM * BK + buf * (BK * BN);
+    bf16_t* sb = lds + NST * BM * BK + buf * (BK * BN);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
@@ -2694,10 +2778,17 @@ __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1) void igemm_nn32(NTP
   typename AccT<BM, BN, WIDE>::type acc;
   if constexpr (WIDE) {
     zero_accw<BM, BN>(acc);
-    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, [&](int cur) {
-      mma3w_nn<BM, BN>(lds + cur * (BM * BK), lds + 2 * BM * BK + cur * (BK * BN), wm, wn, lane,
+    auto mma = [&](int cur) {
+      mma3w_nn<BM, BN>(lds + cur * (BM * BK), lds + NST * BM * BK + cur * (BK * BN), wm, wn, lane,
                        acc);
-    });
+    };
+    if constexpr (WS != 0) {
+      kloop_ws<WS_S>(kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles, mma);
+      if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
+      __syncthreads();                           // every consumer is past its last ring read
+    } else {
+      kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
+    }
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN, true>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   } else {
@@ -2929,24 +3020,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
 // the loader's split VALU and LDS writes issue in the 24 free cycles of each
 // 32-cycle 32x32x16 MFMA of its partner.  Counters and ring live in ONE
 // __shared__ array (a second LDS object can make hipcc drain vmcnt).
-constexpr int WS_THREADS = 512;
-constexpr int WS_S = 4;          // LDS ring stages
-constexpr int WS_P = 2;          // loader register sets (steps of loads in flight)
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-
-__device__ __forceinline__ void ws_wait(unsigned* c, unsigned target) {
-  lds_u32* lc = (lds_u32*)c;
-  while (__hip_atomic_load(lc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-    __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ void ws_post(unsigned* c) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_add((lds_u32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
 template <int BM, int BN, int S>
 __device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_t* lds,
                                               unsigned* cnt) {
@@ -3234,9 +3307,10 @@ static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) 
 static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
   if (g_variant[op] >= 0) {
     int v = g_variant[op];
-    int wide = v >= 24 ? 24 : v >= 12 ? 12 : 0;        // fp32 twins: 12-23, 24-35
+    // fp32 twins: 12-23 wide, 24-35 intra-block K split, 36-47 wave-specialised
+    int wide = v >= 36 ? 36 : v >= 24 ? 24 : v >= 12 ? 12 : 0;
     v -= wide;
-    if (op == 2 && wide >= 24) wide = 0;            // wgrad: no K-split twins
+    if (op == 2 && wide >= 24) wide = 0;            // wgrad: no K-split / ws twins here
     if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
     v += wide;
     if (((v / 3) & 1) && !pipe_ok) v -= 3;
@@ -3343,8 +3417,12 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
-                          bool wide = false, int wg = 1) {
+                          bool wide = false, int wg = 1, bool ws = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  if (ws && fast) {                // wave-specialised 32x32x16 twin, 512 threads
+    igemm_nt32<BM, BN, GM_FWD, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p);
+    return;
+  }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
       igemm_nt32<BM, BN, GM_FWD, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
@@ -3396,9 +3474,14 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   if (p.a_hl && !fast) return (int)hipErrorInvalidValue;
   const bool ring_ok = fast && p.a.Cg % KS == 0;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
-  bool wide = false;
+  bool wide = false, ws = false;
   int wg = 1;
-  if (v >= 24) {
+  if (v >= 36) {                                   // wave-specialised twins of 12-23
+    v -= 36;
+    if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
+    wide = p.bb.part == nullptr;
+    ws = wide && fast;
+  } else if (v >= 24) {
     wg = 2;
     v -= 24;
     if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
@@ -3418,9 +3501,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg, ws); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide, 1, ws); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg, ws); break;
   }
   return (int)hipGetLastError();
 }
@@ -3556,9 +3639,16 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
-                          bool wide = false, int wg = 1) {
+                          bool wide = false, int wg = 1, bool ws = false) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if (ws) {                        // wave-specialised 32x32x16 twin, 512 threads
+    if (strided)
+      igemm_nn32<BM, BN, GM_DGS, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+    else
+      igemm_nn32<BM, BN, GM_DG1, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+    return;
+  }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && !wide) {                         // intra-block K split, 512 threads
       if (strided)
@@ -3637,9 +3727,12 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       strided = st > 1;
     }
     int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
-    bool wide = false;
+    bool wide = false, ws = false;
     int wg = 1;
-    if (v >= 24) {                        // fp32 intra-block K-split twins
+    if (v >= 36) {                        // fp32 wave-specialised twins of 12-23
+      v -= 36;
+      wide = ws = f32;
+    } else if (v >= 24) {                 // fp32 intra-block K-split twins
       wg = f32 ? 2 : 1;
       v -= 24;
     } else if (v >= 12) {                 // fp32 32x32x16-MFMA twins of 0-11
@@ -3662,9 +3755,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     }
     if (f32) {
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg, ws); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1, ws); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg, ws); break;
       }
       return (int)hipGetLastError();
     }

@@ -220,6 +220,38 @@ def test_conv_intra_block_ksplit_fp32_vs_fp64(case, v):
         _hip.conv_set_variant(1, -1)
 
 
+@pytest.mark.parametrize("v", [36, 37, 38, 42, 43, 44])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_wave_specialised_fp32_vs_fp64(case, v):
+    """The wave-specialised twins (512-thread igemm_nt32 / igemm_nn32 with
+    WS = 1: loader waves -> 4-stage LDS ring -> MFMA waves, kloop_ws), fwd and
+    dgrad pinned, every tile, with and without split-K, on every conv case
+    (unaligned / generic-gather shapes fall back to the register kernels)."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(0, v)
+    _hip.conv_set_variant(1, v)
+    try:
+        test_conv_fp32_vs_fp64(case)
+    finally:
+        _hip.conv_set_variant(0, -1)
+        _hip.conv_set_variant(1, -1)
+
+
+@pytest.mark.parametrize("v", [36, 37, 42])
+def test_conv_bn_unit_wave_specialised_fp32_vs_fp64(v):
+    """BN statistics (fwd epilogue) and the BN-link dgrad epilogue run by the
+    MFMA waves of the wave-specialised twins after the loaders exited."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    _hip.conv_set_variant(0, v)
+    _hip.conv_set_variant(1, v)
+    try:
+        test_conv_bn_unit_fp32_vs_fp64(True, True, False)
+        test_bn_link_dgrad_epilogue_fp32()
+    finally:
+        _hip.conv_set_variant(0, -1)
+        _hip.conv_set_variant(1, -1)
+
+
 @pytest.mark.parametrize("v", [24, 26, 30])
 def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
     """BN statistics (fwd epilogue) and the BN-link dgrad epilogue from the
