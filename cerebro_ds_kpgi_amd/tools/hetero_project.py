@@ -43,6 +43,105 @@ def project(fast_img_s, slow_img_s, n_fast=38, n_slow=10, workers=(2, 4, 6, 8),
     return out
 
 
+def _pack_time(t1, tg, g_meas):
+    """Step time of a pack of g configs, linear between the measured
+    one-config (t1) and g_meas-config (tg) step times (a pack step costs a
+    fixed launch part plus a per-config part)."""
+    slope = (tg - t1) / max(g_meas - 1, 1)
+    return lambda g: 0.0 if g <= 0 else t1 + (g - 1) * slope
+
+
+def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_slow=4,
+                    valid_speedup=3.0, seed=2018):
+    """Makespan (s) of one epoch of the hetero workload on W GPUs with V
+    partitions each (P = W V), as THIS runtime executes it: a GPU trains the
+    models on its V partitions as packs (one launch stream per architecture:
+    pack step time t_fast(g) / t_slow(g) for g configs).  ``rotation``: the
+    UDAF round plan, every round ends at a barrier over all GPUs;
+    ``greedy``: CTQ, an idle GPU takes per idle partition the first runnable
+    (model, partition) pair of the shuffled list (scheduler classes of
+    ``scheduler.policies``)."""
+    import heapq
+    from ..scheduler.policies import GreedyScheduler, RotationScheduler
+    P = W * V
+    models = list(range(n_fast + n_slow))
+    slow = set(range(n_fast, n_fast + n_slow))
+    parts = list(range(P))
+    gpu_of = {p: p // V for p in parts}
+
+    def pack_seconds(ms):
+        ns = sum(1 for m in ms if m in slow)
+        nf = len(ms) - ns
+        tr = (TRAIN / P)
+        va = (VALID / P)
+        t = 0.0
+        if nf:
+            t += (tr / b_fast) * t_fast(nf) + (va / b_fast) * t_fast(nf) / valid_speedup
+        if ns:
+            t += (tr / b_slow) * t_slow(ns) + (va / b_slow) * t_slow(ns) / valid_speedup
+        return t
+
+    if policy == "rotation":
+        sch = RotationScheduler(models, parts, seed=seed)
+        sch.start_epoch(1)
+        total = 0.0
+        for rnd in sch.rounds:
+            per_gpu = {}
+            for p, m in rnd.items():
+                per_gpu.setdefault(gpu_of[p], []).append(m)
+            total += max((pack_seconds(ms) for ms in per_gpu.values()), default=0.0)
+        return total
+    sch = GreedyScheduler(models, parts, seed=seed, shuffle=True)
+    sch.start_epoch(1)
+    now, events, busy = 0.0, [], set()
+
+    def dispatch(g):
+        jobs = []
+        for p in range(g * V, (g + 1) * V):
+            if p in sch.idle_workers:
+                m = sch.assign(p)
+                if m is not None:
+                    jobs.append((m, p))
+        if jobs:
+            busy.add(g)
+            heapq.heappush(events, (now + pack_seconds([m for m, _ in jobs]), g, jobs))
+    for g in range(W):
+        dispatch(g)
+    while events:
+        now, g, jobs = heapq.heappop(events)
+        busy.discard(g)
+        for m, p in jobs:
+            sch.complete(m, p)
+        for h in range(W):
+            if h not in busy:
+                dispatch(h)
+    if not sch.epoch_done():
+        raise RuntimeError("packed greedy simulation stalled")
+    return now
+
+
+def project_packed(step_s, workers=(1, 2, 4, 6, 8), V=None, n_fast=38, n_slow=10, seeds=3,
+                   valid_speedup=3.0):
+    """Rotation vs greedy hours from MEASURED pack step times
+    ``step_s = {"fast": (t1, tg, g), "slow": (t1, tg, g)}`` (seconds per
+    packed step at 1 and g configs: bench.py --configs 1 / g)."""
+    tf = _pack_time(*step_s["fast"])
+    ts = _pack_time(*step_s["slow"])
+    out = []
+    for W in workers:
+        v = V or max(1, (n_fast + n_slow) // (W * 4))
+        rot = simulate_packed("rotation", n_fast, n_slow, W, v, tf, ts,
+                              valid_speedup=valid_speedup)
+        gr = min(simulate_packed("greedy", n_fast, n_slow, W, v, tf, ts, seed=s,
+                                 valid_speedup=valid_speedup) for s in range(seeds))
+        ref = REF_HOURS.get(W)
+        out.append({"workers": W, "slots_per_gpu": v, "rotation_h": rot / 3600.0,
+                    "greedy_h": gr / 3600.0, "speedup": rot / gr,
+                    "ref_udaf_h": ref[0] if ref else None, "ref_ctq_h": ref[1] if ref else None,
+                    "ref_speedup": ref[0] / ref[1] if ref else None})
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--fast_img_s", type=float, required=True,
@@ -50,7 +149,26 @@ def main(argv=None):
     ap.add_argument("--slow_img_s", type=float, required=True,
                     help="NASNetMobile bs4, one config alone, images/s")
     ap.add_argument("--valid_speedup", type=float, default=3.0)
+    ap.add_argument("--packed", default="",
+                    help="pack step times (s) as 'fast_t1,fast_tg,g_fast,slow_t1,slow_tg,g_slow' "
+                         "(bench.py ms_per_step / 1000 at --configs 1 and g): project the "
+                         "runtime's packed execution instead of one model per worker")
+    ap.add_argument("--slots_per_gpu", type=int, default=0)
     a = ap.parse_args(argv)
+    if a.packed:
+        f = [float(x) for x in a.packed.split(",")]
+        rows = project_packed({"fast": (f[0], f[1], int(f[2])), "slow": (f[3], f[4], int(f[5]))},
+                              V=a.slots_per_gpu or None, valid_speedup=a.valid_speedup)
+        print("| workers | slots / GPU | rotation (UDAF) h | greedy (CTQ) h | speedup | "
+              "reference UDAF / CTQ h | reference speedup |")
+        print("|---:|---:|---:|---:|---:|---|---:|")
+        for r in rows:
+            print("| {} | {} | {:.3f} | {:.3f} | {:.2f}x | {} / {} | {} |".format(
+                r["workers"], r["slots_per_gpu"], r["rotation_h"], r["greedy_h"], r["speedup"],
+                r["ref_udaf_h"], r["ref_ctq_h"],
+                "{:.2f}x".format(r["ref_speedup"]) if r["ref_speedup"] else "-"))
+        print(json.dumps(rows))
+        return rows
     rows = project(a.fast_img_s, a.slow_img_s, valid_speedup=a.valid_speedup)
     print("| workers | rotation (UDAF) h | greedy (CTQ) h | speedup | reference UDAF / CTQ h "
           "| reference speedup |")

@@ -114,3 +114,24 @@ def test_task_parallel_each_model_once():
                 done.append(m)
                 sch.complete(m, w)
     assert sorted(done) == list(range(5))
+
+
+def test_packed_hetero_projection():
+    """tools.hetero_project packed mode: the simulator trains every (model,
+    partition) pair once per epoch under both policies, a pack of g configs
+    costs the interpolated pack step, and one model per GPU with unit pack
+    cost reproduces the unpacked greedy / rotation ordering (rotation, with a
+    barrier per round, is never faster than greedy there)."""
+    from cerebro_ds_kpgi_amd.tools import hetero_project as hp
+    f = hp._pack_time(1.0, 4.0, 4)
+    assert f(0) == 0.0 and f(1) == 1.0 and f(4) == 4.0 and abs(f(2) - 2.0) < 1e-12
+    rows = hp.project_packed({"fast": (0.004, 0.02, 8), "slow": (0.017, 0.03, 10)},
+                             workers=(2, 8), V=1, seeds=2)
+    for r in rows:
+        assert r["rotation_h"] >= r["greedy_h"] * 0.999, r
+    # packing: at one GPU holding every partition the slow configs share packs
+    one = hp.project_packed({"fast": (0.004, 0.02, 8), "slow": (0.017, 0.03, 10)},
+                            workers=(1,), V=8, seeds=1)[0]
+    unpacked = hp.project_packed({"fast": (0.004, 0.032, 8), "slow": (0.017, 0.17, 10)},
+                                 workers=(1,), V=8, seeds=1)[0]
+    assert one["greedy_h"] < unpacked["greedy_h"] and one["rotation_h"] < unpacked["rotation_h"]
