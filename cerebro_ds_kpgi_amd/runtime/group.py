@@ -289,8 +289,7 @@ class _Working(object):
             return nsteps
         if self.graph is None:
             # eager warm-up on a side stream (real steps), then capture once
-            s = (torch.cuda.Stream() if os.environ.get("CER_WARM_SIDE", "1") == "1"
-                 else torch.cuda.current_stream())
+            s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             take_fallbacks()
             with torch.cuda.stream(s):
@@ -382,9 +381,7 @@ class _Working(object):
                     self.vgraph = torch.cuda.CUDAGraph()
                     # own memory pool (sharing the training graph's pool let the
                     # two graphs' temporaries alias: invalid eval results)
-                    pool = (self.graph.pool() if self.graph is not None and
-                            os.environ.get("CER_VG_SHARE", "0") == "1" else None)
-                    with torch.cuda.graph(self.vgraph, pool=pool,
+                    with torch.cuda.graph(self.vgraph,
                                           capture_error_mode="thread_local"):
                         self._vstep()
             while done < nsteps:
