@@ -228,9 +228,11 @@ def main():
         tune_log = os.environ.get("CER_TUNE_LOG")
         if tune_log and backend == "hip":
             from cerebro_ds_kpgi_amd.ops import _hip
+            tt = _hip.tune_times()
             with open(tune_log, "w") as f:
-                json.dump([[op, list(key), v] for (op, key), v in _hip.tuned_variants().items()],
-                          f)
+                # [op, problem key, chosen variant, {variant: ms per launch}]
+                json.dump([[op, list(key), v, tt.get((op, key), {})]
+                           for (op, key), v in _hip.tuned_variants().items()], f)
     eng.close()
     if da_root and ctx.rank == 0:
         import shutil

@@ -457,6 +457,7 @@ NVARIANTS = 12
 SPLITK_FLOATS = 1 << 24      # 64 MB of fp32 split-K partial slots per device
 _SPLITK = {}
 _TUNED = {}
+_TUNE_T = {}     # (op, problem key) -> {variant: best ms over reps} (tune logs)
 _PINNED = {}
 
 
@@ -520,12 +521,14 @@ def _select(op, key, launch, dtype, after_tune=None):
         v = -1
         if _tune_enabled() and not torch.cuda.is_current_stream_capturing():
             cands = FP32_VARIANTS[op] if dtype == torch.float32 else range(NVARIANTS)
-            v = _autotune(op, launch, after=after_tune, variants=cands)
+            times = {}
+            v = _autotune(op, launch, after=after_tune, variants=cands, times=times)
+            _TUNE_T[(op, key)] = times
         _TUNED[(op, key)] = v
     lib().cer_conv_set_variant(op, v)
 
 
-def _autotune(op, launch, reps=3, passes=None, after=None, variants=None):
+def _autotune(op, launch, reps=3, passes=None, after=None, variants=None, times=None):
     """Time every variant (``reps`` back-to-back launches after a warm one)
     over ``passes`` interleaved passes and keep each variant's best pass:
     one noisy measurement no longer pins a slow kernel for the whole run."""
@@ -548,6 +551,8 @@ def _autotune(op, launch, reps=3, passes=None, after=None, variants=None):
             if best_t[v] is None or t < best_t[v]:
                 best_t[v] = t
     best_v = min(variants, key=lambda v: best_t[v])
+    if times is not None:
+        times.update({v: t / reps for v, t in best_t.items()})
     if after is not None:
         after()
     return best_v
@@ -556,6 +561,11 @@ def _autotune(op, launch, reps=3, passes=None, after=None, variants=None):
 def tuned_variants():
     """{(op, problem key): variant} chosen so far (for logs / profiles)."""
     return dict(_TUNED)
+
+
+def tune_times():
+    """{(op, problem key): {variant: ms per launch}} measured by the autotune."""
+    return {k: dict(v) for k, v in _TUNE_T.items()}
 
 
 def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,

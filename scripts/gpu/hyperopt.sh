@@ -6,7 +6,7 @@
 # --hyperopt, reference run_cerebro_standalone_helper.py:315-376)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r3hyp
+O=gpurun_out/r4hyp
 mkdir -p $O
 R=/tmp/cer_hyp; rm -rf $R
 NT=${1:-8192}
