@@ -31,6 +31,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <utility>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -1957,6 +1958,7 @@ __device__ __forceinline__ void zero_accw(f32x16 (&acc)[BM / 64][BN / 64]) {
 
 __device__ __forceinline__ f32x16 mfma3w(const bf16x8& xh, const bf16x8& xl, const bf16x8& yh,
                                          const bf16x8& yl, f32x16 acc) {
+  if (CER_TIMING_1PASS) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, yh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl, yh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, yl, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh, yh, acc, 0, 0, 0);
@@ -2355,7 +2357,7 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
 constexpr int WS_THREADS = 512;
 constexpr int WS_S = 4;          // LDS ring stages
-constexpr int WS_P = 2;          // loader register sets (steps of loads in flight)
+constexpr int WS_P = 4;          // loader register sets (steps of global loads in flight)
 typedef __attribute__((address_space(3))) unsigned lds_u32;
 
 __device__ __forceinline__ void ws_wait(unsigned* c, unsigned target) {
@@ -2371,44 +2373,140 @@ __device__ __forceinline__ void ws_post(unsigned* c) {
     __hip_atomic_fetch_add((lds_u32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// K loop of the wave-specialised fwd / dgrad twins (WS = 1): waves 4-7 run
-// the kernel's own load / store lambdas (register-staged global loads, two
-// sets in flight, hi/lo split, ds_write into stage t % S), waves 0-3 its mma
-// lambda on each stage; the same per-stage full / free LDS counters as
-// wgrad_ws32.  The load lambda is called in increasing step order (it keeps
-// an incremental im2col position) and past k1 (out-of-range or unused
-// loads, as kloop32 does), the lambdas see tid = threadIdx.x & 255.
-template <int S, typename Load, typename Store, typename Mma>
-__device__ __forceinline__ void kloop_ws(int k0, int k1, unsigned* cnt, Load&& load, Store&& store,
-                                         Mma&& mma) {
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>), unrolled
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Consumer side of the wave-specialised K loops (waves 0-3): ONE MFMA wave
+// per SIMD, so nothing else hides its LDS latency.  Each step's two 16-deep
+// substeps are software-pipelined: substep 1's fragments are read under
+// substep 0's MFMAs, the next step's substep 0 under substep 1's.  The
+// sched_barriers keep the reads ahead of the MFMAs and the counter waits
+// behind them (without them hipcc sinks the reads to their use and floats
+// the waits up: either way the reads are waited for in full).
+// The last step re-reads its own stage instead of a next one, so no read is
+// conditional (a conditionally live fragment set spills).
+template <int S, typename Frag, typename Read, typename Mma>
+__device__ __forceinline__ void ws_consume(int T, unsigned* cnt, Read&& read, Mma&& mma) {
   unsigned* full = cnt;
   unsigned* freed = cnt + S;
-  const int T = k1 - k0;
-  if (threadIdx.x >= 256) {
-    load(k0, I0{});
-    load(k0 + 1, I1{});
-    auto step = [&](int t, auto U) {
-      const int st = t % S;
-      if (t >= S) ws_wait(&freed[st], 4u * (unsigned)(t / S));
-      store(st, U);
-      load(k0 + t + 2, U);
-      ws_post(&full[st]);
-    };
-    for (int t = 0; t < T; t += 2) {
-      step(t, I0{});
-      if (t + 1 >= T) break;
-      step(t + 1, I1{});
-    }
-  } else {
-    for (int t = 0; t < T; ++t) {
-      const int st = t % S;
-      ws_wait(&full[st], 4u * (unsigned)(t / S + 1));
-      mma(st);
-      ws_post(&freed[st]);
-    }
+  if (T <= 0) return;
+  Frag R0, R1;
+  ws_wait(&full[0], 4u);
+  read(0, 0, R0);
+  for (int t = 0; t < T; ++t) {
+    const int st = t % S;
+    read(st, 1, R1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(R0);
+    // the waits below are not memory operations to the scheduler: without
+    // this fence it hoists ws_post's lgkmcnt(0) above the MFMAs, right
+    // after the first one, and R1's reads are waited for in full there
+    __builtin_amdgcn_sched_barrier(0);
+    ws_post(&freed[st]);                        // every read of stage t has returned
+    const int tn = t + 1 < T ? t + 1 : t;
+    ws_wait(&full[tn % S], 4u * (unsigned)(tn / S + 1));
+    read(tn % S, 0, R0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(R1);
+    __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+// Loader side (waves 4-7): P register sets of global loads in flight; step t
+// waits for ring stage t % S to be released by all four consumers, splits and
+// stores register set t % P into it, refills that set with step t + P and
+// publishes the stage.  ``load`` is called in increasing step order (it may
+// keep an incremental im2col position) and past the last step (out-of-range
+// loads return zeros without memory traffic, as kloop32 does).
+template <int S, int P, typename Load, typename Store>
+__device__ __forceinline__ void ws_produce(int k0, int T, unsigned* cnt, Load&& load,
+                                           Store&& store) {
+  unsigned* full = cnt;
+  unsigned* freed = cnt + S;
+  static_for<P>([&](auto U) { load(k0 + decltype(U)::value, U); });
+  for (int t = 0; t < T; t += P) {
+    static_for<P>([&](auto U) {
+      const int tt = t + decltype(U)::value;
+      if (tt < T) {
+        const int st = tt % S;
+        if (tt >= S) ws_wait(&freed[st], 4u * (unsigned)(tt / S));
+        store(st, U);
+        load(k0 + tt + P, U);
+        ws_post(&full[st]);
+      }
+    });
+  }
+}
+
+// K loop of the wave-specialised fwd / dgrad twins (WS = 1): waves 4-7 run
+// the kernel's own load / store lambdas (register-staged global loads, WS_P
+// sets in flight, hi/lo split, ds_write into stage t % S), waves 0-3 read
+// fragments / issue MFMAs per stage (ws_consume); per-stage full / free LDS
+// counters as in wgrad_ws32.  The lambdas see tid = threadIdx.x & 255.
+template <int S, int P, typename Frag, typename Load, typename Store, typename Read, typename Mma>
+__device__ __forceinline__ void kloop_ws(int k0, int k1, unsigned* cnt, Load&& load, Store&& store,
+                                         Read&& read, Mma&& mma) {
+  if (threadIdx.x >= 256)
+    ws_produce<S, P>(k0, k1 - k0, cnt, load, store);
+  else
+    ws_consume<S, Frag>(k1 - k0, cnt, read, mma);
+}
+
+// fragments of one 16-deep substep of the wide (32x32x16) kernels' 64x64 wave tiles
+template <int BM, int BN>
+struct FragW {
+  bf16x8 ah[BM / 64], al[BM / 64], bh[BN / 64], bl[BN / 64];
+};
+
+// NT x NT images (fwd; mma3w_nt's reads)
+template <int BM, int BN>
+__device__ __forceinline__ void read_w_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                          int lane, int s, FragW<BM, BN>& F) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    F.ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
+    F.al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    F.bh[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 2 * s + h));
+    F.bl[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 4 + 2 * s + h));
+  }
+}
+
+// NT x TN images (dgrad; mma3w_nn's reads)
+template <int BM, int BN>
+__device__ __forceinline__ void read_w_nn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
+                                          int lane, int s, FragW<BM, BN>& F) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    F.ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
+    F.al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    F.bh[j] = tn_frag32<BN>(sb, 16 * s, wn * TN + 32 * j, lane);
+    F.bl[j] = tn_frag32<BN>(sb, KS + 16 * s, wn * TN + 32 * j, lane);
+  }
+}
+
+template <int BM, int BN>
+__device__ __forceinline__ void mma_w(const FragW<BM, BN>& F, f32x16 (&acc)[BM / 64][BN / 64]) {
+#pragma unroll
+  for (int i = 0; i < BM / 64; ++i)
+#pragma unroll
+    for (int j = 0; j < BN / 64; ++j) acc[i][j] = mfma3w(F.bh[j], F.bl[j], F.ah[i], F.al[i], acc[i][j]);
 }
 
 // WS = 1: the wave-specialised twin (512 threads: waves 4-7 load / split /
@@ -2466,7 +2564,7 @@ void igemm_nt32(NTParams p) {
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = WS ? 2 : fp32_sets<BM, BN, WIDE>();
+  constexpr int SETS = WS ? WS_P : fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -2526,7 +2624,10 @@ void igemm_nt32(NTParams p) {
     zero_accw<BM, BN>(acc);
     auto mma = [&](int cur) { mma3w_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); };
     if constexpr (WS != 0) {
-      kloop_ws<WS_S>(kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles, mma);
+      kloop_ws<WS_S, WS_P, FragW<BM, BN>>(
+          kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles,
+          [&](int st, int s, FragW<BM, BN>& F) { read_w_nt<BM, BN>(SA(st), SB(st), wm, wn, lane, s, F); },
+          [&](const FragW<BM, BN>& F) { mma_w<BM, BN>(F, acc); });
       if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
       __syncthreads();                           // every consumer is past its last ring read
     } else {
@@ -2722,7 +2823,7 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = WS ? 2 : fp32_sets<BM, BN>();
+  constexpr int SETS = WS ? WS_P : fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -2783,7 +2884,13 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
                        acc);
     };
     if constexpr (WS != 0) {
-      kloop_ws<WS_S>(kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles, mma);
+      bf16_t* const sb0 = lds + NST * BM * BK;
+      kloop_ws<WS_S, WS_P, FragW<BM, BN>>(
+          kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles,
+          [&](int st, int s, FragW<BM, BN>& F) {
+            read_w_nn<BM, BN>(lds + st * (BM * BK), sb0 + st * (BK * BN), wm, wn, lane, s, F);
+          },
+          [&](const FragW<BM, BN>& F) { mma_w<BM, BN>(F, acc); });
       if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
       __syncthreads();                           // every consumer is past its last ring read
     } else {
@@ -3034,8 +3141,6 @@ __device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_
   const int ms = split * p.m_per_split;
   const int me = min(p.Mred, ms + p.m_per_split);
   const int T = ms < me ? (me - ms + KS - 1) / KS : 0;
-  unsigned* full = cnt;
-  unsigned* freed = cnt + S;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (wid >= 4) {
     // ---------------- loaders ----------------
@@ -3095,25 +3200,10 @@ __device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
       }
     };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
     // loads past the item's rows are issued anyway (out-of-range offsets:
     // zeros, no memory traffic) so no branch guards a load and hipcc keeps
     // counted vmcnt waits
-    load(0, I0{});
-    load(1, I1{});
-    auto step = [&](int t, auto U) {
-      const int st = t % S;
-      if (t >= S) ws_wait(&freed[st], 4u * (unsigned)(t / S));
-      store(st, U);
-      load(t + WS_P, U);
-      ws_post(&full[st]);
-    };
-    for (int t = 0; t < T; t += 2) {
-      step(t, I0{});
-      if (t + 1 >= T) break;
-      step(t + 1, I1{});
-    }
+    ws_produce<S, WS_P>(0, T, cnt, load, store);
     return;
   }
   // ---------------- consumers ----------------
@@ -3173,26 +3263,7 @@ __device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_
       for (int j = 0; j < FN; ++j)
         acc[i][j] = mfma3w(F.ah[i], F.al[i], F.bh[j], F.bl[j], acc[i][j]);
   };
-  // half-step pipeline: substep 1's fragments are read under substep 0's
-  // MFMAs, the next step's substep 0 under substep 1's.  The last step
-  // re-reads its own stage instead of a next one (min), so no read is
-  // conditional (a conditionally defined fragment set doubles the live
-  // registers and spills)
-  if (T > 0) {
-    Sub R0, R1;
-    ws_wait(&full[0], 4u);
-    read_sub(0, 0, R0);
-    for (int t = 0; t < T; ++t) {
-      const int st = t % S;
-      read_sub(st, 1, R1);
-      mma_sub(R0);
-      ws_post(&freed[st]);                     // every read of stage t has returned
-      const int tn = t + 1 < T ? t + 1 : t;
-      ws_wait(&full[tn % S], 4u * (unsigned)(tn / S + 1));
-      read_sub(tn % S, 0, R0);
-      mma_sub(R1);
-    }
-  }
+  ws_consume<S, Sub>(T, cnt, read_sub, mma_sub);
   // D[n][k]: k = lane & 31 (32 consecutive k per register: 128-B rows)
   float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
   const bool split_k = p.splits > 1;
