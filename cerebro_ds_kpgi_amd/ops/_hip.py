@@ -502,10 +502,12 @@ if os.environ.get("CER_FP32_KSPLIT", "1") != "0":
     FP32_VARIANTS = {op: vs + (_KSPLIT32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
 # 36-47: wave-specialised twins of the wide register-staged fwd / dgrad
 # kernels (512 threads: 4 loader waves fill a 4-stage LDS ring, 4 MFMA waves
-# consume it; conv.hip kloop_ws), three tiles, with and without split-K
-# (CER_FP32_WS=0 leaves them out).
+# consume it; conv.hip kloop_ws), three tiles, with and without split-K.
+# Measured slower than the best of ids 0-35 on every ResNet-50 problem
+# (median 1.45x at 8 configs, profiles/r4_ws.md), so CER_FP32_WS=1 adds them
+# to the autotune for A/B runs only.
 _WS32 = (36, 37, 38, 42, 43, 44)
-if os.environ.get("CER_FP32_WS", "1") != "0":
+if os.environ.get("CER_FP32_WS", "0") != "0":
     FP32_VARIANTS = {op: vs + (_WS32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
 
 

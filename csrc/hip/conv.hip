@@ -2434,13 +2434,17 @@ __device__ __forceinline__ void ws_produce(int k0, int T, unsigned* cnt, Load&& 
   for (int t = 0; t < T; t += P) {
     static_for<P>([&](auto U) {
       const int tt = t + decltype(U)::value;
-      if (tt < T) {
-        const int st = tt % S;
+      const int st = tt % S;
+      const bool live = tt < T;
+      if (live) {
         if (tt >= S) ws_wait(&freed[st], 4u * (unsigned)(tt / S));
         store(st, U);
-        load(k0 + tt + P, U);
-        ws_post(&full[st]);
       }
+      // issued on every path: a load under a branch makes hipcc's vmcnt
+      // bookkeeping path-dependent, and it then drains every set (vmcnt(0))
+      // before each store instead of waiting for the one set it stores
+      load(k0 + tt + P, U);
+      if (live) ws_post(&full[st]);
     });
   }
 }
