@@ -450,6 +450,7 @@ class Coordinator(object):
             return
         if getattr(self, "_next_where", None) is None:
             nxt = RotationScheduler(list(self.sched.models), list(self.sched.workers))
+            nxt.pack_key_fn = self.sched.pack_key_fn      # the same order as the real one
             nxt.start_epoch(self.sched.epoch + 1)
             self._next_where = [{mm: p for p, mm in rnd.items()} for rnd in nxt.rounds]
         for s, where in enumerate(self._next_where):

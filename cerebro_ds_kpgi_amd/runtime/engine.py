@@ -91,6 +91,9 @@ class EngineOptions(object):
         # "lockstep" (a barrier per sub-epoch) or "auto" (async unless a
         # feature needs lock-step: sub-epoch checkpoints, task parallelism)
         self.runtime = kw.get("runtime", os.environ.get("CER_RUNTIME", "auto"))
+        # pack-aware scheduling order (policies.py): co-schedule configs that
+        # pack into one launch stream, most steps per visit first
+        self.pack_order = kw.get("pack_order", True)
         self.ctrl_timeout = kw.get("ctrl_timeout", 6 * 3600)
         # test hook: extra seconds per job of config m (heterogeneous jobs)
         self.sim_job_seconds = kw.get("sim_job_seconds", None)
@@ -166,6 +169,7 @@ class MOPEngine(object):
         self.holder = {m: None for m in range(S)}    # None = every rank has the init copy
         self.sched = make_scheduler(opts.scheduler, list(range(S)), list(range(self.P)),
                                     seed=opts.seed, shuffle=opts.shuffle)
+        self.sched.pack_key_fn = self.pack_order_key()
         self.models_info = collections.defaultdict(list)
         self.jobs_info = {}
         self.mst_state = {m: {"train_loss": [], "valid_loss": [], "train_top5_error": [],
@@ -604,6 +608,22 @@ class MOPEngine(object):
                              "sub-epoch resume".format(self.o.scheduler, self.o.ckpt_every))
         return rt == "async" or (rt == "auto" and not lock_only)
 
+    def pack_order_key(self):
+        """The schedulers' pack-aware order (``MOPScheduler.pack_key_fn``):
+        key(m) = (-steps per partition visit, pack key).  None with
+        ``pack_order`` off (the policies' own orders: rotation by config id,
+        greedy shuffled).  Reads the coordinator's config list at call time,
+        so configs added later (hyperopt) are keyed too."""
+        if not self.o.pack_order:
+            return None
+        n = max(int(self.n_train), 1)
+
+        def key(m):
+            mst = self._bk_msts()[m]
+            bs = max(int(mst["batch_size"]), 1)
+            return (-((n + bs - 1) // bs), tuple(str(v) for v in pack_key(mst)))
+        return key
+
     def async_scheduler(self, policy):
         """One scheduler per policy for the engine's lifetime (the greedy
         shuffle RNG continues across epochs and sessions)."""
@@ -616,6 +636,7 @@ class MOPEngine(object):
             else:
                 sch = GreedyScheduler(ids, list(range(self.P)), seed=self.o.seed,
                                       shuffle=self.o.shuffle)
+            sch.pack_key_fn = self.pack_order_key()
             self._asched[policy] = sch
         return sch
 

@@ -78,6 +78,22 @@ class MOPScheduler(object):
         self.idle_workers = set()
 
     # -- epoch lifecycle --------------------------------------------------
+    # Pack-aware order (set by the engine; None = the policy's own order):
+    # a key per model, sorted ascending.  The engine keys configs by
+    # (-steps per visit, pack key), so the configs with the most steps per
+    # partition visit come first and configs that pack into one launch
+    # stream (same architecture, batch size, optimizer) are adjacent.  The
+    # rotation then trains them in the same sub-epochs and the greedy policy
+    # hands them out first (longest-processing-time first): one G-config
+    # pack instead of G one-config ones spread over G rounds.  Ties keep the
+    # policy's order (the greedy shuffle stays random within a group).
+    pack_key_fn = None
+
+    def pack_sorted(self, items, model_of=lambda m: m):
+        if self.pack_key_fn is None:
+            return list(items)
+        return sorted(items, key=lambda it: self.pack_key_fn(model_of(it)))
+
     def start_epoch(self, epoch):
         self.epoch = epoch
         self.monitor = InvariantMonitor(self.models, self.workers)

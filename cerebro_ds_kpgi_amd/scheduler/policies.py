@@ -11,6 +11,10 @@
   pairs in a seeded shuffled order; an idle worker takes the first pair whose
   worker matches and whose model is idle.  Work-conserving, event driven (no
   busy-wait: the runtime calls ``assign`` on completion events).
+* Both take the engine's pack-aware order (``MOPScheduler.pack_key_fn``):
+  configs that pack into one launch stream are co-scheduled, the ones with
+  the most steps per visit first (the 48-config hetero drill-down:
+  ``profiles/r4_hetero.md``).
 * ``TaskParallelScheduler`` — Hyperopt-Spark semantics: one
   model per worker for the whole epoch over the *replicated* dataset.
 """
@@ -32,7 +36,7 @@ class RotationScheduler(MOPScheduler):
     def start_epoch(self, epoch):
         super(RotationScheduler, self).start_epoch(epoch)
         L = max(len(self.models), len(self.workers))
-        slots = list(self.models) + [None] * (L - len(self.models))
+        slots = self.pack_sorted(self.models) + [None] * (L - len(self.models))
         self.rounds = []
         for s in range(L):
             rnd = {}
@@ -91,6 +95,7 @@ class GreedyScheduler(MOPScheduler):
         super(GreedyScheduler, self).start_epoch(epoch)
         if self.shuffle:
             self.rng.shuffle(self.pending)
+        self.pending = self.pack_sorted(self.pending, model_of=lambda mw: mw[0])
 
     def assign(self, worker):
         if worker not in self.idle_workers:

@@ -86,18 +86,31 @@ def _decode_only(a):
     man = da.load_manifest(a.root)
     parts = [a.only] if a.only >= 0 else list(range(int(man["num_partitions"])))
     tot, ph = 0, {}
+    py = {"py_open_s": 0.0, "py_read_s": 0.0, "py_release_s": 0.0}
     t0 = time.perf_counter()
     for p in parts:
         for split in ("train", "valid"):
             d = da.seg_dir(a.root, p, man["dboid"])
+            ta = time.perf_counter()
             r = da.DirectAccessReader(os.path.join(d, str(man[split]["relfilenode"])),
                                       os.path.join(d, str(man[split]["toast_relfilenode"])),
                                       a.threads)
-            for _, _, x, y in r.read(a.threads):
+            tb = time.perf_counter()
+            recs = r.read(a.threads)
+            tc = time.perf_counter()
+            for _, _, x, y in recs:
                 tot += x.nbytes + y.nbytes
             for k, v in r.stats().items():
                 ph[k] = ph.get(k, 0.0) + v
+            # the decoded arrays' pages go back to the OS here, and the
+            # segment mappings are unmapped: both scale with the payload
+            del recs
             r.close()
+            td = time.perf_counter()
+            py["py_open_s"] += tb - ta
+            py["py_read_s"] += tc - tb
+            py["py_release_s"] += td - tc
+    ph.update(py)
     wall = time.perf_counter() - t0
     print(json.dumps({"partitions": parts, "threads": a.threads, "wall_s": round(wall, 3),
                       "payload_GB": round(tot / 1e9, 3),

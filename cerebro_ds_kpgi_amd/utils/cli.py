@@ -80,6 +80,9 @@ def get_main_parser():
                    help="data partitions (virtual workers) per GPU; 0 = auto")
     p.add_argument("--scheduler", choices=["rotation", "greedy", "task", "ma", "ddp"],
                    default="rotation")
+    p.add_argument("--pack_order", type=_bool, default=True,
+                   help="co-schedule configs that pack into one launch stream, most steps per "
+                        "partition visit first (false: the policies' own orders)")
     p.add_argument("--hop_optimizer_state", type=_bool, default=True,
                    help="ship Adam moments with the model (False = reset per sub-epoch, reference CTQ semantics)")
     p.add_argument("--l2_mode", choices=["adam_wd", "none"], default="adam_wd",

@@ -135,3 +135,57 @@ def test_packed_hetero_projection():
     unpacked = hp.project_packed({"fast": (0.004, 0.032, 8), "slow": (0.017, 0.17, 10)},
                                  workers=(1,), V=8, seeds=1)[0]
     assert one["greedy_h"] < unpacked["greedy_h"] and one["rotation_h"] < unpacked["rotation_h"]
+
+
+def _slow_first(slow):
+    # the engine's key shape: (-steps per visit, pack key)
+    return lambda m: (-128, ("nasnetmobile", "4")) if m in slow else (-4, ("mobilenetv2", "128"))
+
+
+def test_rotation_pack_order_coschedules_a_pack():
+    """Pack-aware rotation (MOPScheduler.pack_key_fn): the slow configs are
+    adjacent in the rotation order, so a sub-epoch holds all of them at once
+    (one G-config pack) and they finish in the fewest sub-epochs; every
+    (model, worker) pair is still trained exactly once."""
+    slow = {1, 4, 7}
+    models, workers = list(range(9)), list(range(3))
+    plain = RotationScheduler(models, workers)
+    packed = RotationScheduler(models, workers)
+    packed.pack_key_fn = _slow_first(slow)
+    rounds = {}
+    for name, sch in (("plain", plain), ("packed", packed)):
+        sch.start_epoch(0)
+        pairs = [(m, w) for rnd in sch.rounds for w, m in rnd.items()]
+        assert sorted(pairs) == sorted((m, w) for m in models for w in workers)
+        rounds[name] = [sum(m in slow for m in rnd.values()) for rnd in sch.rounds]
+    # the pack: some sub-epoch trains all three slow configs together, and
+    # the slow work spans fewer sub-epochs than in id order
+    assert max(rounds["packed"]) == 3 and max(rounds["plain"]) < 3
+    assert (sum(1 for c in rounds["packed"] if c) < sum(1 for c in rounds["plain"] if c))
+
+
+def test_greedy_pack_order_hands_out_slow_pack_first():
+    """Pack-aware greedy: longest-processing-time first -- in the first wave
+    every worker that can take a slow config does, so they run as one pack;
+    the invariants still hold over the epoch."""
+    slow = {2, 5}
+    models, workers = list(range(6)), list(range(4))
+    sch = GreedyScheduler(models, workers, seed=3)
+    sch.pack_key_fn = _slow_first(slow)
+    sch.start_epoch(0)
+    first = {w: sch.assign(w) for w in workers}
+    assert sum(m in slow for m in first.values()) == len(slow)
+    running = dict(first)
+    while running:
+        w = next(iter(running))
+        sch.complete(running.pop(w), w)
+        m = sch.assign(w)
+        if m is not None:
+            running[w] = m
+        for w2 in workers:
+            if w2 not in running:
+                m2 = sch.assign(w2)
+                if m2 is not None:
+                    running[w2] = m2
+    assert sch.epoch_done()
+    sch.monitor.check_epoch_complete()
