@@ -465,13 +465,24 @@ def _tune_enabled():
     return os.environ.get("CER_CONV_TUNE", "1") != "0"
 
 
+_LANE = [0]
+
+
+def set_lane(lane):
+    """Concurrency lane of the pack group whose steps run / are captured next
+    (runtime/group.py): groups on different lanes replay their graphs at the
+    same time on different streams (async_mop._run_batch), so each lane has
+    its own split-K workspace."""
+    _LANE[0] = int(lane)
+
+
 def _splitk_ready(device):
     """Register the persistent split-K workspace of this device with the
     library: one for a model's branch stream (ops.streams.branch_stream),
     one for everything else -- kernels of the two may run at once, so each
     has its own partial slots and arrival counters (the pointers are baked
-    into captured graphs)."""
-    key = (str(device), streams.on_branch(device))
+    into captured graphs) -- per concurrency lane (``set_lane``)."""
+    key = (str(device), streams.on_branch(device), _LANE[0])
     if _SPLITK.get("_current") == key:
         return
     ws = _SPLITK.get(key)

@@ -44,6 +44,7 @@ lock-step runtime).
 """
 
 import collections
+import contextlib
 import datetime
 import json
 import os
@@ -816,6 +817,42 @@ def run_worker(eng, chan, hops):
         _run_batch(eng, chan, hops, rec)
 
 
+class _Lanes(object):
+    """Concurrent pack groups within one batch.  When every group of the
+    batch is past its warm-up (``_Working.replay_ready``: its steps are graph
+    replays, no host-side op runs), group g's work goes to the stream of its
+    lane (``PackGroup.lane``; ``engine.lane_stream``) after that stream has
+    waited for the caller's (hop arrivals, parking); ``join`` makes the
+    caller's stream wait for every lane.  Groups sharing a lane share its
+    stream (and the lane's split-K workspace, baked into their graphs), so
+    they stay serialised.  Otherwise (a group still warming up: its eager
+    steps autotune kernels and must not be timed beside other work; CPU;
+    one group) everything runs on the caller's stream as before."""
+
+    def __init__(self, eng, working, valid):
+        self.active = (len(working) > 1 and eng.device.type == "cuda" and
+                       all(w.replay_ready(valid) for w in working.values()))
+        self.eng = eng
+        self.main = torch.cuda.current_stream() if self.active else None
+        self.used = {}
+        if self.active:
+            eng.lane_batches += 1
+
+    def on(self, grp):
+        if not self.active:
+            return contextlib.nullcontext()
+        st = self.used.get(grp.lane)
+        if st is None:
+            st = self.eng.lane_stream(grp.lane)
+            st.wait_stream(self.main)
+            self.used[grp.lane] = st
+        return torch.cuda.stream(st)
+
+    def join(self):
+        for st in self.used.values():
+            self.main.wait_stream(st)
+
+
 def _run_batch(eng, chan, hops, rec):
     from .engine import SoftFault
     rank = eng.ctx.rank
@@ -844,20 +881,26 @@ def _run_batch(eng, chan, hops, rec):
         for key, gj in per_group.items():
             working[key] = eng.groups[key].begin_batch(gj)
         steps_of = {}
+        # several pack groups whose steps are all graph replays run at once,
+        # one stream per lane (the groups' first steps -- eager warm-up with
+        # kernel autotuning, capture -- stay serial on the caller's stream)
+        lanes = _Lanes(eng, working, valid=False)
         for key, w in working.items():
             grp = eng.groups[key]
-            w.prepare(eng.o.hop_optimizer_state)
             B = grp.batch_size
             steps = eng.n_train // B
             if rec.get("max_steps"):
                 steps = min(steps, rec["max_steps"])
             steps_of[key] = steps
-            with tr.span("train", sync=eng._sync, arch=key[0], G=w.G, steps=steps):
+            with lanes.on(grp), tr.span("train", sync=eng._sync, arch=key[0], G=w.G,
+                                        steps=steps):
+                w.prepare(eng.o.hop_optimizer_state)
                 w.train_steps(steps)
                 delay = eng.o.sim_job_seconds
                 if delay:                            # test hook: heterogeneous job lengths
                     time.sleep(max(delay[m % len(delay)] for m, _ in w.jobs))
             trained += steps * B * w.G
+        lanes.join()
         # the states are final: park them (the home row is the committed
         # copy a hop or a retry starts from), then free the models
         for key in working:
@@ -866,6 +909,7 @@ def _run_batch(eng, chan, hops, rec):
             for m in models:
                 hops.mark_final(m)
         chan.post_event({"t": "train_done", "rank": rank, "models": models})
+        vlanes = _Lanes(eng, working, valid=True)
         for key, w in working.items():
             grp = eng.groups[key]
             B = grp.batch_size
@@ -873,11 +917,15 @@ def _run_batch(eng, chan, hops, rec):
             if rec.get("max_steps"):
                 full = max(eng.n_train // B, 1)
                 vsteps = max(1, -(-vsteps * steps_of[key] // full))
-            with tr.span("valid", sync=eng._sync, arch=key[0], G=w.G, steps=vsteps):
+            with vlanes.on(grp), tr.span("valid", sync=eng._sync, arch=key[0], G=w.G,
+                                         steps=vsteps):
                 w.validate(vsteps)
-                mets = w.read_metrics()
                 if eng.o.sim_valid_seconds:
                     time.sleep(eng.o.sim_valid_seconds)
+        vlanes.join()
+        for key, w in working.items():
+            B = eng.groups[key].batch_size
+            mets = w.read_metrics()                 # one host sync per group
             for row, (m, lp) in enumerate(w.jobs):
                 results.append({"model": m, "dist_key": eng.store.pids[lp], "metrics": mets[row],
                                 "steps": steps_of[key], "batch": B, "partition": lp})

@@ -94,6 +94,9 @@ class EngineOptions(object):
         # pack-aware scheduling order (policies.py): co-schedule configs that
         # pack into one launch stream, most steps per visit first
         self.pack_order = kw.get("pack_order", True)
+        # concurrency lanes (async_mop._Lanes); 1 = the groups of a batch run
+        # one after another
+        self.lanes = kw.get("lanes", LANES)
         self.ctrl_timeout = kw.get("ctrl_timeout", 6 * 3600)
         # test hook: extra seconds per job of config m (heterogeneous jobs)
         self.sim_job_seconds = kw.get("sim_job_seconds", None)
@@ -120,6 +123,12 @@ class SoftFault(RuntimeError):
 
 
 RESUME_FILE = "resume.json"
+
+# default concurrency lanes per rank (EngineOptions.lanes): pack groups of
+# one batch (different architectures / batch sizes, e.g. the hetero
+# drill-down or a TPE round) replay their step graphs on this many streams at
+# once (async_mop._run_batch); each lane has its own split-K workspace (64 MB)
+LANES = 4
 
 
 def default_sizes(dataset, P):
@@ -165,6 +174,8 @@ class MOPEngine(object):
             self.n_train, self.n_valid = self.store.n_train, self.store.n_valid
         self.groups = {}
         self.group_of = {}
+        self._lanes = {}
+        self.lane_batches = 0        # train / validation phases run on lane streams
         self._build_groups(range(S))
         self.holder = {m: None for m in range(S)}    # None = every rank has the init copy
         self.sched = make_scheduler(opts.scheduler, list(range(S)), list(range(self.P)),
@@ -221,6 +232,7 @@ class MOPEngine(object):
                 self.groups[key] = PackGroup(key, ms, self.msts, self.store, self.device,
                                              self.dtype, seed_base=self.o.seed * 100,
                                              use_graphs=self.o.use_graphs, l2=self.o.l2)
+                self.groups[key].lane = (len(self.groups) - 1) % max(1, self.o.lanes)
             for m in ms:
                 self.group_of[m] = self.groups[key]
 
@@ -607,6 +619,14 @@ class MOPEngine(object):
             raise ValueError("runtime='async' does not support scheduler={} / ckpt_every={} / "
                              "sub-epoch resume".format(self.o.scheduler, self.o.ckpt_every))
         return rt == "async" or (rt == "auto" and not lock_only)
+
+    def lane_stream(self, lane):
+        """The stream of concurrency lane ``lane`` (created on first use)."""
+        st = self._lanes.get(lane)
+        if st is None:
+            st = torch.cuda.Stream(device=self.device)
+            self._lanes[lane] = st
+        return st
 
     def pack_order_key(self):
         """The schedulers' pack-aware order (``MOPScheduler.pack_key_fn``):

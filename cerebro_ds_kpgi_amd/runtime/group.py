@@ -53,6 +53,9 @@ class PackGroup(object):
                            get_backend() == "hip")
         self.l2 = l2
         self.warmup_eager = warmup_eager
+        # concurrency lane (engine._build_groups): groups of one batch on
+        # different lanes replay on different streams at the same time
+        self.lane = 0
         proto = create_model_from_mst({"model": self.arch})
         self.layout = proto.layout
         self.home = Arena(self.layout, len(self.model_ids), device, compute_dtype, trainable=False)
@@ -247,7 +250,23 @@ class _Working(object):
         self.vacc.zero_()
 
     # ------------------------------------------------------------------
+    def _set_lane(self):
+        if self.stats_arena is not None:
+            from ..ops import _hip
+            _hip.set_lane(self.group.lane)
+
+    def replay_ready(self, valid=False):
+        """True when the next train (``valid``: validation) steps are pure
+        graph replays: no host-side op runs, so they may go to a lane stream
+        beside another group's (async_mop._run_batch)."""
+        if not self.group.use_graphs or self.eager_only:
+            return False
+        if valid:
+            return self.vgraph is not None and not self.veager and _VALID_GRAPH
+        return self.graph is not None and isinstance(self.graph, torch.cuda.CUDAGraph)
+
     def _step(self):
+        self._set_lane()
         if self.stats_arena is None:
             return self._step_body()
         from ..ops import _hip
@@ -352,6 +371,7 @@ class _Working(object):
         return sg
 
     def _vstep(self):
+        self._set_lane()
         g = self.group
         gather_batch(g.store, False, self.part_of_row, self.vcursor, g.batch_size,
                      self.vx, self.vy)

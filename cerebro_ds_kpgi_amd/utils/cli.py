@@ -83,6 +83,9 @@ def get_main_parser():
     p.add_argument("--pack_order", type=_bool, default=True,
                    help="co-schedule configs that pack into one launch stream, most steps per "
                         "partition visit first (false: the policies' own orders)")
+    p.add_argument("--lanes", type=int, default=4,
+                   help="pack groups of one batch replayed concurrently on this many streams "
+                        "(1 = one after another)")
     p.add_argument("--hop_optimizer_state", type=_bool, default=True,
                    help="ship Adam moments with the model (False = reset per sub-epoch, reference CTQ semantics)")
     p.add_argument("--l2_mode", choices=["adam_wd", "none"], default="adam_wd",
