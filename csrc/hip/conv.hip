@@ -1782,7 +1782,8 @@ __device__ __forceinline__ void mma3_tn(const bf16_t* sa, const bf16_t* sb, int 
     for (int j = 0; j < FN; ++j) acc[i][j] = mfma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
 }
 
-// fp32 epilogue of the NT / NN kernels, straight from the accumulators:
+// fp32 epilogue of the NT / NN kernels, straight from the accumulators
+// (reference form; epi32 below is the prefetching one):
 // lane (fr, fc) of wave (wm, wn) owns rows wm*TM + 16i + fr and channels
 // wn*TN + 16j + 4fc .. +3.  out = act(acc + bias) (+ addend), one 16-B
 // store per fragment; optional per-(M tile, channel) statistics partials:
@@ -1790,7 +1791,7 @@ __device__ __forceinline__ void mma3_tn(const bf16_t* sa, const bf16_t* sb, int 
 // (sum dz, sum dz*xhat) of a dgrad output (p.bb.part, BNBwdEpi).  xch: LDS
 // scratch of 4*BN floats.
 template <int BM, int BN>
-__device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
+__device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
                                       int lane, int tid) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
@@ -1899,6 +1900,190 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   if (!fstat && !bstat) return;
   // rows -> one deterministic partial per (M tile, channel): DPP over the 16
   // lanes of equal fc, then the two M-direction waves meet in LDS
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float sm = row16_sum(s[j][e]);
+      const float sq = row16_sum(q[j][e]);
+      if (fr == 0) {
+        const int nl = wn * TN + 16 * j + 4 * fc + e;
+        xch[(wm * 2) * BN + nl] = sm;
+        xch[(wm * 2 + 1) * BN + nl] = sq;
+      }
+    }
+  __syncthreads();
+  float* dst = fstat ? p.stats : bb.part;
+  const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
+  for (int t = tid; t < 2 * BN; t += NTHREADS) {
+    const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
+    if (n < p.N)
+      stat_store(dst, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                 p.stat_slabs);
+  }
+}
+
+// Epilogue operands as buffer descriptors: a null or unused source gets a
+// 0-byte descriptor, so its loads return zeros with no branch around them.
+// A load under a branch makes hipcc's vmcnt bookkeeping path-dependent and
+// it then drains (vmcnt(0)) at the next use: the reference epilogue, whose
+// per-channel parameters and per-fragment addend / BN-input loads sit in
+// such branches between stores, paid ~20 dependent memory round trips per
+// tile, which dominated the small-K (K = 64) dgrad / forward kernels.
+constexpr uint32_t EPI_BIG = 0x7ffffff0u;
+__device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ uint32_t bload_u8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)off, 0, 0);
+}
+
+// true when every epilogue tensor offset of this launch fits the 31-bit
+// buffer offsets (output rows of a strided dgrad: at most (st + 1)^2 per row)
+__device__ __forceinline__ bool epi_fits(const NTParams& p) {
+  const int64_t rows = p.o_st > 1 ? (int64_t)p.M * (p.o_st + 1) * (p.o_st + 1) : (int64_t)p.M;
+  return rows * p.ldc * 4 < (int64_t)EPI_BIG;
+}
+
+// fp32 epilogue of the NT / NN kernels, straight from the accumulators:
+// lane (fr, fc) of wave (wm, wn) owns rows wm*TM + 16i + fr and channels
+// wn*TN + 16j + 4fc .. +3.  Same outputs as epi32_ref, with every load of
+// the epilogue issued before its first use: the per-channel parameters
+// (bias, BN mean / invstd / gamma / beta) and the first row group's addend
+// and BN-input / mask operands together (one row group of <= 4 fragments:
+// every 64x64 tile; larger tiles walk 2-4 groups, one round trip each: a
+// second, double-buffered group spills the 128x128 kernels and costs the
+// 128x64 ones a wave per SIMD).
+// Unaligned channels, the y-form BN link (ym 1) and > 2 GB tensors take
+// epi32_ref.  xch: LDS scratch of 4*BN floats.
+template <int BM, int BN>
+__device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
+                                      float* xch, int cfg, int m0, int n0, int wm, int wn,
+                                      int lane, int tid) {
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  constexpr int CH = FM * FN <= 4 ? FM : (4 / FN > 0 ? 4 / FN : 1);   // rows per group
+  constexpr int NG = (FM + CH - 1) / CH;
+  const BNBwdEpi& bb = p.bb;
+  const bool fstat = p.stats != nullptr;
+  const bool bstat = bb.part != nullptr;
+  const bool vec = ((p.N | p.ldc) & 3) == 0;
+  if (!vec || (bstat && bb.ym == 1) || !epi_fits(p)) {
+    epi32_ref<BM, BN>(p, acc, xch, cfg, m0, n0, wm, wn, lane, tid);
+    return;
+  }
+  const int fr = lane & 15, fc = lane >> 4;
+  float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
+  const bool ymz = bstat && bb.ym == 2, ymm = bstat && bb.ym == 3;
+  const auto rBias = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
+  const auto rMean = make_rsrc(bb.mean, bstat ? EPI_BIG : 0u);
+  const auto rInv = make_rsrc(bb.invstd, bstat ? EPI_BIG : 0u);
+  const auto rGa = make_rsrc(bb.gamma, ymz ? EPI_BIG : 0u);
+  const auto rBe = make_rsrc(bb.beta, ymz ? EPI_BIG : 0u);
+  const auto rAd = make_rsrc(p.addend, p.addend ? EPI_BIG : 0u);
+  const auto rZ = make_rsrc(bb.z, bstat ? EPI_BIG : 0u);
+  const auto rMk = make_rsrc(bb.y, ymm ? EPI_BIG : 0u);
+  float bc[FN][4], mu[FN][4], is[FN][4], ga[FN][4], be[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+      const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
+      const uint32_t c = (uint32_t)cfg * (uint32_t)p.N + nn;
+      bc[j][e] = bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
+      mu[j][e] = bload_f32(rMean, c * 4u);
+      is[j][e] = bload_f32(rInv, c * 4u);
+      ga[j][e] = bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
+      be[j][e] = bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
+    }
+  // one row group's operands: [row in group][j]
+  uint4 ad[CH][FN], zz[CH][FN];
+  uint32_t mk[CH][FN];
+  int64_t orow[FM];
+  bool rok[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * TM + 16 * i + fr;
+    rok[i] = m < p.M;
+    orow[i] = m;
+    if (p.o_st > 1 && rok[i]) {
+      const RowPos r = decode_row(m, p.M, p.a);
+      orow[i] = ((int64_t)r.b * p.o_H + (int64_t)r.y * p.o_st) * p.o_W + (int64_t)r.x * p.o_st;
+    }
+  }
+  auto fetch = [&](int g) {
+#pragma unroll
+    for (int ii = 0; ii < CH; ++ii) {
+      const int i = g * CH + ii;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + 16 * j + 4 * fc;
+        const bool ok = i < FM && rok[i < FM ? i : 0] && n < p.N;
+        const int64_t el = orow[i < FM ? i : 0] * p.ldc + (int64_t)cfg * p.N + n;
+        const uint32_t off = ok ? (uint32_t)el * 4u : OOB;
+        ad[ii][j] = bload(rAd, off);
+        zz[ii][j] = bload(rZ, off);
+        mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+      }
+    }
+  };
+  fetch(0);
+  float sc[FN][4], sh[FN][4], s[FN][4], q[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      sc[j][e] = is[j][e] * ga[j][e];
+      sh[j][e] = be[j][e] - mu[j][e] * sc[j][e];
+      s[j][e] = q[j][e] = 0.f;
+    }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    if (g > 0) fetch(g);
+#pragma unroll
+    for (int ii = 0; ii < CH; ++ii) {
+      const int i = g * CH + ii;
+      if (i >= FM || !rok[i]) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + 16 * j + 4 * fc;
+        if (n >= p.N) continue;
+        const float av[4] = {__uint_as_float(ad[ii][j].x), __uint_as_float(ad[ii][j].y),
+                             __uint_as_float(ad[ii][j].z), __uint_as_float(ad[ii][j].w)};
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] + bc[j][e];
+          v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
+          v[e] += av[e];
+        }
+        *reinterpret_cast<float4*>(obase + orow[i] * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        if (fstat) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            s[j][e] += v[e];
+            q[j][e] += v[e] * v[e];
+          }
+        } else if (bstat) {
+          const float zv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
+                               __uint_as_float(zz[ii][j].z), __uint_as_float(zz[ii][j].w)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float dz = v[e];
+            if (ymz)
+              dz = (zv[e] * sc[j][e] + sh[j][e] + 0.f) > 0.f ? dz : 0.f;
+            else if (ymm) {
+              const float yv = (mk[ii][j] >> e) & 1u ? 1.f : 0.f;
+              dz = bb.act == 6 ? ((yv > 0.f && yv < 6.f) ? dz : 0.f) : (yv > 0.f ? dz : 0.f);
+            }
+            s[j][e] += dz;
+            q[j][e] += dz * (zv[e] - mu[j][e]) * is[j][e];
+          }
+        }
+      }
+    }
+  }
+  if (!fstat && !bstat) return;
 #pragma unroll
   for (int j = 0; j < FN; ++j)
 #pragma unroll
