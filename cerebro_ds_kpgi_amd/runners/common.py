@@ -199,6 +199,7 @@ def run_approach(approach, argv=None, shuffle=True):
         summary = {"approach": approach, "gpus": ctx.world, "configs": len(eng.msts),
                    "epochs": args.num_epochs, "makespan_s": makespan, "etl_s": etl,
                    "train_images": images, "agg_img_per_s": images / max(train_s, 1e-9),
+                   "lane_batches": getattr(eng, "lane_batches", 0),
                    "mst_state": {str(k): v for k, v in eng.mst_state.items()}}
         st = getattr(loader, "stats", None)
         if st and st.get("buffers"):

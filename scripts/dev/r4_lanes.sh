@@ -10,5 +10,7 @@ timeout -k 10 400 python -u -m pytest tests/test_lanes_gpu.py -x -q --timeout 30
 rc=$?
 tail -3 gpurun_out/r4sec/lanes_test.log
 if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Timeout" gpurun_out/r4sec/lanes_test.log | head -20; exit $rc; fi
+timeout -k 10 120 python3 -u scripts/dev/lanes_overlap.py > gpurun_out/r4sec/lanes_overlap.json 2>&1 || exit 1
+cat gpurun_out/r4sec/lanes_overlap.json
 bash scripts/gpu/secondary.sh hetero_jobs lanes || exit 1
 bash scripts/gpu/secondary.sh hetero_jobs packserial --lanes 1 || exit 1
