@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 4: the fp64-slab BN fold in one round trip + per-channel loads hoisted above it (bn.hip)
+# round 4: the fp64-slab BN fold in one round trip + per-channel loads hoisted above it (bn.hip),
+# and the wgrad batch item lookup without a dependent kernarg-load chain (conv.hip wgb_item)
 # as an A/B twin: numerics of every fp32 conv / BN-link
 # path on the twin, then the bench with the twin and without, same box
 cd "$GRAFT_REPO_ROOT" || exit 1
