@@ -52,7 +52,7 @@ def _pack_time(t1, tg, g_meas):
 
 
 def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_slow=4,
-                    valid_speedup=3.0, seed=2018):
+                    valid_speedup=3.0, seed=2018, pack_order=True):
     """Makespan (s) of one epoch of the hetero workload on W GPUs with V
     partitions each (P = W V), as THIS runtime executes it: a GPU trains the
     models on its V partitions as packs (one launch stream per architecture:
@@ -60,7 +60,9 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
     UDAF round plan, every round ends at a barrier over all GPUs;
     ``greedy``: CTQ, an idle GPU takes per idle partition the first runnable
     (model, partition) pair of the shuffled list (scheduler classes of
-    ``scheduler.policies``)."""
+    ``scheduler.policies``).  ``pack_order``: the engine's default
+    pack-aware order (``MOPEngine.pack_order_key``: most steps per visit
+    first, packs adjacent); False = the policies' own orders."""
     import heapq
     from ..scheduler.policies import GreedyScheduler, RotationScheduler
     P = W * V
@@ -81,8 +83,13 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
             t += (tr / b_slow) * t_slow(ns) + (va / b_slow) * t_slow(ns) / valid_speedup
         return t
 
+    def key(m):            # MOPEngine.pack_order_key: (-steps per visit, pack key)
+        b = b_slow if m in slow else b_fast
+        return (-(TRAIN / P / b), "slow" if m in slow else "fast")
+
     if policy == "rotation":
         sch = RotationScheduler(models, parts, seed=seed)
+        sch.pack_key_fn = key if pack_order else None
         sch.start_epoch(1)
         total = 0.0
         for rnd in sch.rounds:
@@ -92,6 +99,7 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
             total += max((pack_seconds(ms) for ms in per_gpu.values()), default=0.0)
         return total
     sch = GreedyScheduler(models, parts, seed=seed, shuffle=True)
+    sch.pack_key_fn = key if pack_order else None
     sch.start_epoch(1)
     now, events, busy = 0.0, [], set()
 
@@ -121,7 +129,7 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
 
 
 def project_packed(step_s, workers=(1, 2, 4, 6, 8), V=None, n_fast=38, n_slow=10, seeds=3,
-                   valid_speedup=3.0):
+                   valid_speedup=3.0, pack_order=True):
     """Rotation vs greedy hours from MEASURED pack step times
     ``step_s = {"fast": (t1, tg, g), "slow": (t1, tg, g)}`` (seconds per
     packed step at 1 and g configs: bench.py --configs 1 / g)."""
@@ -131,9 +139,10 @@ def project_packed(step_s, workers=(1, 2, 4, 6, 8), V=None, n_fast=38, n_slow=10
     for W in workers:
         v = V or max(1, (n_fast + n_slow) // (W * 4))
         rot = simulate_packed("rotation", n_fast, n_slow, W, v, tf, ts,
-                              valid_speedup=valid_speedup)
+                              valid_speedup=valid_speedup, pack_order=pack_order)
         gr = min(simulate_packed("greedy", n_fast, n_slow, W, v, tf, ts, seed=s,
-                                 valid_speedup=valid_speedup) for s in range(seeds))
+                                 valid_speedup=valid_speedup, pack_order=pack_order)
+                 for s in range(seeds))
         ref = REF_HOURS.get(W)
         out.append({"workers": W, "slots_per_gpu": v, "rotation_h": rot / 3600.0,
                     "greedy_h": gr / 3600.0, "speedup": rot / gr,
@@ -154,11 +163,14 @@ def main(argv=None):
                          "(bench.py ms_per_step / 1000 at --configs 1 and g): project the "
                          "runtime's packed execution instead of one model per worker")
     ap.add_argument("--slots_per_gpu", type=int, default=0)
+    ap.add_argument("--pack_order", default="true", choices=["true", "false"],
+                    help="the engine's pack-aware scheduling order (default) or the policies' own")
     a = ap.parse_args(argv)
     if a.packed:
         f = [float(x) for x in a.packed.split(",")]
         rows = project_packed({"fast": (f[0], f[1], int(f[2])), "slow": (f[3], f[4], int(f[5]))},
-                              V=a.slots_per_gpu or None, valid_speedup=a.valid_speedup)
+                              V=a.slots_per_gpu or None, valid_speedup=a.valid_speedup,
+                              pack_order=a.pack_order == "true")
         print("| workers | slots / GPU | rotation (UDAF) h | greedy (CTQ) h | speedup | "
               "reference UDAF / CTQ h | reference speedup |")
         print("|---:|---:|---:|---:|---:|---|---:|")
