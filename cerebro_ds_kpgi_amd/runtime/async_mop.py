@@ -386,12 +386,8 @@ class Coordinator(object):
         for r in range(self.world):
             if r in self.batch:
                 continue
-            jobs = []
-            for p in self.parts_of[r]:
-                if p in sched.idle_workers:
-                    m = sched.assign(p)
-                    if m is not None:
-                        jobs.append((m, p))
+            got = sched.assign_many([p for p in self.parts_of[r] if p in sched.idle_workers])
+            jobs = [(m, p) for p, m in got.items()]
             if jobs:
                 self._dispatch(r, jobs, epoch, self.round_base + self.epoch_nbatch)
 

@@ -106,6 +106,56 @@ class GreedyScheduler(MOPScheduler):
                 return m
         return None
 
+    def assign_many(self, workers):
+        """Assign idle models to the idle ``workers`` together ({worker:
+        model}): one wave of workers freed at once (a GPU's partition slots
+        at the end of its batch).  Without the pack-aware order this is
+        ``assign`` per worker (first runnable pair of the queue).  With it,
+        each key class (most steps per visit first) gets a MAXIMUM matching
+        of its idle models to the wave's still-free workers (augmenting
+        paths, visited in queue order): the first-fit loop left the slow
+        pack's tail at 2-3 configs per wave where each config still had a
+        free partition to go to (profiles/r4_hetero.md)."""
+        workers = [w for w in workers if w in self.idle_workers]
+        if self.pack_key_fn is None:
+            out = {}
+            for w in workers:
+                m = self.assign(w)
+                if m is not None:
+                    out[w] = m
+            return out
+        free = set(workers)
+        pend = [(m, w) for m, w in self.pending if w in free and m in self.idle_models]
+        keyed = {}
+        for m, _ in pend:
+            if m not in keyed:
+                keyed[m] = self.pack_key_fn(m)
+        match_w, match_m = {}, {}
+        for k in sorted(set(keyed.values())):
+            adj = {}
+            for m, w in pend:
+                if keyed[m] == k:
+                    adj.setdefault(m, []).append(w)
+
+            def augment(m, seen):
+                for w in adj[m]:
+                    if w in seen:
+                        continue
+                    seen.add(w)
+                    cur = match_w.get(w)
+                    if cur is None or (keyed[cur] == k and augment(cur, seen)):
+                        match_w[w] = m
+                        match_m[m] = w
+                        return True
+                return False
+            for m in adj:
+                if m not in match_m:
+                    augment(m, set())
+        for w in workers:                        # queue / worker order of the starts
+            if w in match_w:
+                self._start(match_w[w], w)
+        return {w: match_w[w] for w in workers if w in match_w}
+
 
 class TaskParallelScheduler(MOPScheduler):
     """Each job = one model trained on *all* partitions (replicated data).

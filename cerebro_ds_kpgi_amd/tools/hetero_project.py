@@ -104,12 +104,8 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
     now, events, busy = 0.0, [], set()
 
     def dispatch(g):
-        jobs = []
-        for p in range(g * V, (g + 1) * V):
-            if p in sch.idle_workers:
-                m = sch.assign(p)
-                if m is not None:
-                    jobs.append((m, p))
+        got = sch.assign_many([p for p in range(g * V, (g + 1) * V) if p in sch.idle_workers])
+        jobs = [(m, p) for p, m in got.items()]
         if jobs:
             busy.add(g)
             heapq.heappush(events, (now + pack_seconds([m for m, _ in jobs]), g, jobs))

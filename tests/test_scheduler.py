@@ -189,3 +189,22 @@ def test_greedy_pack_order_hands_out_slow_pack_first():
                     running[w2] = m2
     assert sch.epoch_done()
     sch.monitor.check_epoch_complete()
+
+
+def test_greedy_wave_matching_places_the_whole_slow_pack():
+    """assign_many with the pack-aware order: a maximum matching per key
+    class.  First-fit gives worker 0 model A and leaves B, whose only
+    remaining partition is 0, idle; the matching moves A to worker 1."""
+    sch = GreedyScheduler([0, 1, 2], [0, 1], seed=0, shuffle=False)
+    sch.pack_key_fn = lambda m: (-128,) if m in (0, 1) else (-4,)
+    sch.start_epoch(0)
+    # A = 0 may go to either worker, B = 1 has only worker 0 left
+    sch.pending = [(0, 0), (0, 1), (1, 0), (2, 0), (2, 1)]
+    sch.monitor.done.add((1, 1))
+    got = sch.assign_many([0, 1])
+    assert got == {0: 1, 1: 0}
+    # without the pack-aware order: the policy's own first-fit
+    plain = GreedyScheduler([0, 1, 2], [0, 1], seed=0, shuffle=False)
+    plain.start_epoch(0)
+    plain.pending = [(0, 0), (0, 1), (1, 0), (2, 0), (2, 1)]
+    assert plain.assign_many([0, 1]) == {0: 0, 1: 2}
