@@ -1,7 +1,7 @@
 #!/bin/bash
 # end of round: GPU tier, smoke, driver-shape bench, per-GPU work at
-# N = 1/2/4/8 (configs 8/4/2/1), steady-state kernel summaries at 1 and 8
-# configs, and a re-check of the side-batch knobs on the final build
+# N = 1/2/4/8 (configs 8/4/2/1), steady-state kernel summaries and step
+# timelines at 1 and 8 configs
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/final
@@ -27,5 +27,4 @@ for C in 1 8; do
   find $O/prof_c$C -name "*.db" -delete
   head -22 $O/prof_c$C.md
 done
-bash scripts/gpu/ab.sh sideknobs "CER_NONE=0 CER_WGB_SPLIT_GRID=64 CER_WGB_SPLIT_GRID=128 CER_WGB_SIDE_FRAC=0.4 CER_WGB_SIDE_FRAC=0.6" "8" 2
 exit $TIER_RC
