@@ -8,7 +8,7 @@
 #   bash scripts/gpu/workloads.sh size udaf|ctq -- the model-size drill-down
 #       (8 configs of MobileNetV2 / ResNet-50 / ResNet-152 / VGG-16, 3 epochs)
 #       at 1/32 of the ImageNet partition size, through run_mop (UDAF rotation)
-#       or run_ctq (greedy).
+#       or ctq (greedy).
 #   bash scripts/gpu/workloads.sh makespan      -- one full epoch of the headline
 #       8-config ResNet-50 grid at full ImageNet-112 partition sizes through
 #       DA-Cerebro standalone (synthetic data generated in HBM)
@@ -37,7 +37,7 @@ if [ "$1" = "criteo" ]; then
 fi
 if [ "$1" = "size" ]; then
   A=$2
-  [ "$A" = "udaf" ] && M=run_mop || M=run_ctq
+  [ "$A" = "udaf" ] && M=run_mop || M=ctq
   for ID in s m l x; do
     timeout -k 10 500 python3 -u -m cerebro_ds_kpgi_amd.runners.$M --run --num_epochs 3 \
       --drill_down_model_size --drill_down_model_size_identifier $ID --size 1 --backend hip \

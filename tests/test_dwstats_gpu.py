@@ -142,13 +142,16 @@ def test_standalone_bn_link_matches_own_pass(G, C, B, H, dtype, monkeypatch):
     assert _rel(g1, g0) < tol
 
 
-@pytest.mark.parametrize("G,C,B,H,s,dtype", [(8, 96, 4, 14, 1, torch.float32),
-                                             (2, 144, 3, 11, 2, torch.float32),
-                                             (4, 96, 4, 14, 2, torch.bfloat16)])
-def test_dwconv_dgrad_bn_link_matches_own_pass(G, C, B, H, s, dtype, monkeypatch):
+@pytest.mark.parametrize("G,C,B,H,s,pad,dtype", [
+    (8, 96, 4, 14, 1, 1, torch.float32), (2, 144, 3, 11, 2, 1, torch.float32),
+    (2, 144, 3, 14, 2, (0, 1, 0, 1), torch.float32), (1, 64, 2, 9, 2, (0, 1, 0, 1), torch.float32),
+    (4, 96, 4, 14, 2, 1, torch.bfloat16), (4, 96, 4, 14, 2, (0, 1, 0, 1), torch.bfloat16)])
+def test_dwconv_dgrad_bn_link_matches_own_pass(G, C, B, H, s, pad, dtype, monkeypatch):
     """1x1 conv_bn (ReLU6, link_out) -> dwconv -> BN (MobileNetV2's expansion
     unit and depthwise conv): the depthwise dgrad computes the expansion BN's
-    backward partials; against that BN's own backward pass."""
+    backward partials; against that BN's own backward pass.  Stride 2 with
+    both left-pad parities (symmetric 1 and Keras correct_pad (0, 1)): the
+    fused kernel's static dy column window depends on it."""
     from cerebro_ds_kpgi_amd.ops import _hip
     Ci = 32
     specs = [ParamSpec("w1", (C, 1, 1, Ci), "weight", fan_in=Ci)]
@@ -185,7 +188,7 @@ def test_dwconv_dgrad_bn_link_matches_own_pass(G, C, B, H, s, dtype, monkeypatch
             x = x0.clone().requires_grad_(True)
             h = P.conv_bn_act(x, r["w1"], r["g1"], r["b1"], r["rm1"], r["rv1"], 1, 0, 6,
                               link_out=link)
-            h = P.dwconv2d(h, r["dw"], s, 1, stats=True)
+            h = P.dwconv2d(h, r["dw"], s, pad, stats=True)
             o = P.bn_act(h, r["g2"], r["b2"], r["rm2"], r["rv2"], True, relu=6)
             torch.manual_seed(3)
             o.backward(torch.randn_like(o.float()).to(dtype))
