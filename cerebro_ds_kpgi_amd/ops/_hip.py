@@ -661,11 +661,13 @@ def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum
     Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4
     the repacked stem input (stem path) or None.  ``x`` may be HL (read as
     such); ``hl_out``: write y in HL format (its only consumer is a conv;
-    the caller guarantees the BN backward does not read y: no residual)."""
+    taken only without a residual and for act none / ReLU, the cases whose
+    BN backward never reads y)."""
     x_hl = is_hl(x)
     with _hl_operands(x_hl, 0):
         return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
-                                  eps, stride, pad, stem, x_hl, hl_out and residual is None)
+                                  eps, stride, pad, stem, x_hl,
+                                  hl_out and residual is None and _act_code(act) in (0, 1))
 
 
 def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,

@@ -136,9 +136,9 @@ struct NTParams {
 // into slab (tile % n) of an fp64 buffer [n][2][ldc] by fp64 atomics, so the
 // BN apply that consumes them reduces n slabs, not one per tile, and folds
 // the finalize (one BN launch per layer and direction instead of two).
-// fp64 makes the slab sums EXACT (a few dozen fp32 partials of similar
-// magnitude fit 53 bits), so the result does not depend on the atomics'
-// order: fp32 atomics here made two identical steps differ by 5 % in the
+// fp64 makes the slab sums near-deterministic (~1e-16 relative; a large layer
+// adds ~200 mixed-sign tile partials per slab, so the order can still round
+// in the last fp64 bit): fp32 atomics here made two identical steps differ by 5 % in the
 // gradients of a fresh ResNet-50 (50 BN layers amplify 1e-7 statistic noise;
 // scripts/debug/slab_determinism.py).  The caller hands zeroed buffers; the
 // slab count it gets back carries SLAB_F64 (bn.hip reads the fp64 format).
