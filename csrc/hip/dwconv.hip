@@ -41,6 +41,11 @@ struct DWGeom {
   int64_t w_gstride;
 };
 
+// Every tap accumulates with an explicit fma: the plain and the fused
+// (statistics / BN-link) kernels then round identically (hipcc may otherwise
+// split a contracted a * b + c into mul + add in one kernel and not the
+// other; the fused forward's y is tested bit for bit against the plain one).
+
 // V channels at p if ok, else zeros.  p must be a valid address either way
 // (callers clamp the pixel index): the load is unconditional and the zero a
 // select.  A load under a branch makes hipcc drain vmcnt where the branch
@@ -109,7 +114,8 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x,
 #pragma unroll
       for (int s = 0; s < K; ++s)
 #pragma unroll
-        for (int i = 0; i < V; ++i) acc[xi][i] += win[xi * ST + s][i] * wr[s][i];
+        for (int i = 0; i < V; ++i)
+          acc[xi][i] = __builtin_fmaf(win[xi * ST + s][i], wr[s][i], acc[xi][i]);
   }
 #pragma unroll
   for (int xi = 0; xi < DW_X; ++xi) {
@@ -166,7 +172,8 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
 #pragma unroll
         for (int s = 0; s < K; ++s)
 #pragma unroll
-          for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wr[s][i];
+          for (int i = 0; i < V; ++i) acc[xi][i] =
+                __builtin_fmaf(win[xi + K - 1 - s][i], wr[s][i], acc[xi][i]);
     } else {
 #pragma unroll
       for (int xi = 0; xi < DW_X; ++xi)
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
           float v[V];
           ldv<V>(dyrow + (int64_t)wo * GC, v);
 #pragma unroll
-          for (int i = 0; i < V; ++i) acc[xi][i] += v[i] * wr[s][i];
+          for (int i = 0; i < V; ++i) acc[xi][i] = __builtin_fmaf(v[i], wr[s][i], acc[xi][i]);
         }
     }
   }
@@ -259,7 +266,8 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_wgrad_kernel(const T* __r
 #pragma unroll
           for (int s = 0; s < K; ++s)
 #pragma unroll
-            for (int i = 0; i < V; ++i) acc[rr * K + s][i] += win[xi * ST + s][i] * g[xi][i];
+            for (int i = 0; i < V; ++i) acc[rr * K + s][i] =
+                  __builtin_fmaf(win[xi * ST + s][i], g[xi][i], acc[rr * K + s][i]);
       }
     }
   }
@@ -357,7 +365,8 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_fwd_stats_kernel(const T*
 #pragma unroll
           for (int s = 0; s < K; ++s)
 #pragma unroll
-            for (int i = 0; i < V; ++i) acc[xi][i] += win[xi * ST + s][i] * wk[r][s][i];
+            for (int i = 0; i < V; ++i)
+              acc[xi][i] = __builtin_fmaf(win[xi * ST + s][i], wk[r][s][i], acc[xi][i]);
       }
 #pragma unroll
       for (int xi = 0; xi < X; ++xi) {
@@ -481,7 +490,8 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_dgrad_bn_kernel(
 #pragma unroll
             for (int s = 0; s < K; ++s)
 #pragma unroll
-              for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wk[r][s][i];
+              for (int i = 0; i < V; ++i) acc[xi][i] =
+                    __builtin_fmaf(win[xi + K - 1 - s][i], wk[r][s][i], acc[xi][i]);
         }
       } else {
         // stride 2: dy row (hi + pt - r) / 2 exists only for even hi + pt - r.
@@ -520,7 +530,8 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_dgrad_bn_kernel(
               if ((a & 1) == 0) {
                 const int j = (a >> 1) + 1 - PAR;
 #pragma unroll
-                for (int i = 0; i < V; ++i) acc[xi][i] += win[sl][j][i] * wt[i];
+                for (int i = 0; i < V; ++i)
+                  acc[xi][i] = __builtin_fmaf(win[sl][j][i], wt[i], acc[xi][i]);
               }
             }
           }
