@@ -569,14 +569,8 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
 
 // fp64 slabs (conv.hip SLAB_F64: a few atomic-accumulated slabs [n][2][C]
 // of doubles, exact sums): every block sums its channels' n slabs in fp64,
-// one lane row per channel vector, and rounds once.  Thread row r loads slab
-// r, so all of a block's slab loads are one memory round trip (a loop of
-// dependent loads in one thread row cost one round trip PER SLAB: 8 of them
-// ahead of every folded BN apply, the latency-bound part of a one-config
-// step); thread row 0 then adds them from LDS in slab order 0..n-1, the
-// same order (and bits) as that loop, FOLD_PASS slabs per LDS pass.
+// one lane row per channel vector, and rounds once
 constexpr int SLAB_F64 = 1 << 24;
-constexpr int FOLD_PASS = 4;     // slabs per LDS pass: [FOLD_PASS][2][cb <= 256] doubles
 
 __device__ __forceinline__ void fold_partials_f64(const double* __restrict__ part, int nslab, int C,
                                                   const Map& mp, int cbk, float* red, float* a8,
@@ -584,45 +578,10 @@ __device__ __forceinline__ void fold_partials_f64(const double* __restrict__ par
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * VEC;
   float* fin = red;                              // [2][cb]
-  double a[VEC], b[VEC];
+  if (tr == 0 && c0 < C) {
+    double a[VEC], b[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) a[i] = b[i] = 0.0;
-  if (nslab <= mp.tr_n) {
-    double* dl = reinterpret_cast<double*>(red + 2 * mp.cb);   // [FOLD_PASS][2][cb]
-    const bool mine = tr < nslab && c0 < C;
-    double la[VEC], lb[VEC];
-    if (mine) {
-      const double* pa = part + (int64_t)tr * 2 * C + c0;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        la[i] = pa[i];
-        lb[i] = pa[C + i];
-      }
-    }
-    for (int p0 = 0; p0 < nslab; p0 += FOLD_PASS) {
-      if (mine && tr >= p0 && tr < p0 + FOLD_PASS) {
-        double* d = dl + (int64_t)((tr - p0) * 2) * mp.cb + tc * VEC;
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) {
-          d[i] = la[i];
-          d[mp.cb + i] = lb[i];
-        }
-      }
-      __syncthreads();
-      if (tr == 0 && c0 < C) {
-        const int p1 = min(nslab, p0 + FOLD_PASS);
-        for (int sl = p0; sl < p1; ++sl) {
-          const double* d = dl + (int64_t)((sl - p0) * 2) * mp.cb + tc * VEC;
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) {
-            a[i] += d[i];
-            b[i] += d[mp.cb + i];
-          }
-        }
-      }
-      __syncthreads();
-    }
-  } else if (tr == 0 && c0 < C) {               // more slabs than thread rows
+    for (int i = 0; i < VEC; ++i) a[i] = b[i] = 0.0;
     for (int sl = 0; sl < nslab; ++sl) {
       const double* pa = part + (int64_t)sl * 2 * C + c0;
 #pragma unroll
@@ -631,8 +590,6 @@ __device__ __forceinline__ void fold_partials_f64(const double* __restrict__ par
         b[i] += pa[C + i];
       }
     }
-  }
-  if (tr == 0 && c0 < C) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       fin[tc * VEC + i] = (float)a[i];
@@ -657,11 +614,7 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ part, int nsl
     fold_partials(part, nslab, C, mp, cbk, red, a8, b8);
 }
 
-// partial tree + [2][cb] (fp32 partials), or [2][cb] + [FOLD_PASS][2][cb]
-// doubles (fp64 slabs), cb <= 256
-constexpr int FOLD_LDS_F32 = 2 * BN_T * VEC + 2 * 32 * VEC;
-constexpr int FOLD_LDS_F64 = 2 * 32 * VEC + FOLD_PASS * 2 * 32 * VEC * 2;
-constexpr int FOLD_LDS = FOLD_LDS_F32 > FOLD_LDS_F64 ? FOLD_LDS_F32 : FOLD_LDS_F64;
+constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
 template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
@@ -673,17 +626,10 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  // gamma / beta do not depend on the statistics: their loads are in flight
-  // during the fold (surplus threads load channel 0 and exit after it)
-  const int cl = c0 < C ? c0 : 0;
-  const int g = cl / Cper, cc = cl - g * Cper;
-  float ga[VEC], be[VEC];
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
-  ld8((const T*)beta.p + g * beta.stride + cc, be);
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
   if (c0 >= C || tr >= mp.tr_n) return;
   const float inv_m = 1.f / (float)M;
   float mu[VEC], is[VEC], var[VEC];
@@ -693,6 +639,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     var[i] = fmaxf(b[i] * inv_m - mu[i] * mu[i], 0.f);
     is[i] = rsqrtf(var[i] + eps);
   }
+  const int g = c0 / Cper, cc = c0 - g * Cper;
   if (blockIdx.y == 0 && tr == 0) {          // one writer per channel
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -706,11 +653,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     }
   }
   float sc[VEC], sh[VEC];
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    sc[i] = is[i] * ga[i];
-    sh[i] = be[i] - mu[i] * sc[i];
-  }
+  bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;
@@ -751,23 +694,12 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  // the per-channel parameters do not depend on the fold: their loads are
-  // in flight during it (surplus threads load channel 0 and exit after it)
-  const int cl = c0 < C ? c0 : 0;
-  const int g = cl / Cper, cc = cl - g * Cper;
-  float ga[VEC], be[VEC], mu[VEC], is[VEC];
-  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
-  if (YM == YM_Z) ld8((const T*)beta.p + g * beta.stride + cc, be);
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    mu[i] = mean[cl + i];
-    is[i] = invstd[cl + i];
-  }
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
   if (c0 >= C || tr >= mp.tr_n) return;
+  const int g = c0 / Cper, cc = c0 - g * Cper;
   if (blockIdx.y == 0 && tr == 0) {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -775,21 +707,18 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
       dbeta[g * gstride + cc + i] = a[i];
     }
   }
-  float k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
+  float ga[VEC], mu[VEC], is[VEC], k1[VEC], k2[VEC], sdz[VEC], sc[VEC], sh[VEC];
+  ld8((const T*)gamma.p + g * gamma.stride + cc, ga);
   const float inv_m = 1.f / (float)M;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
+    mu[i] = mean[c0 + i];
+    is[i] = invstd[c0 + i];
     k1[i] = ga[i] * is[i];
     k2[i] = b[i] * inv_m;
     sdz[i] = a[i] * inv_m;
   }
-  if (YM == YM_Z) {
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      sc[i] = is[i] * ga[i];
-      sh[i] = be[i] - mu[i] * sc[i];
-    }
-  }
+  if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;

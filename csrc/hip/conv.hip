@@ -1502,25 +1502,13 @@ struct WGBatch {
 };
 static_assert(sizeof(WGBatch) <= 4096, "WGBatch must fit the 4 KB kernel-argument segment");
 
-// the batch item holding work index ``work``: start[] is sorted, so it is
-// the count of later item starts <= work.  Unrolled over constant indices,
-// the starts come in as a few wide scalar loads issued together (a scan
-// loop `while (work >= start[i + 1]) ++i` compiled to one dependent kernarg
-// load + wait per item passed: up to WGB_MAX round trips ahead of every
-// work item)
-__device__ __forceinline__ int wgb_item(const WGBatch& b, int work) {
-  int i = 0;
-#pragma unroll
-  for (int j = 1; j < WGB_MAX; ++j) i += (j < b.n && work >= b.start[j]) ? 1 : 0;
-  return i;
-}
-
 template <int BM, int BN, int KIND>  // KIND 0: register-staged, 1: LDS-DMA ring (2 stages)
 __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch(WGBatch b) {
   constexpr int LDSE = 2 * (BM + BN) * BK;   // both bodies use two stages
   __shared__ __attribute__((aligned(16))) bf16_t lds[LDSE];
   const int work = xcd_remap(blockIdx.x, gridDim.x);
-  const int i = wgb_item(b, work);
+  int i = 0;
+  while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
   const WGParams p = b.p[i];
   if (KIND == 0)
     wgrad_reg_body<BM, BN, GM_FWD>(p, work - b.start[i], lds);
@@ -3294,7 +3282,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
   const int nwg = (int)gridDim.x;
   for (int w = blockIdx.x; w < total; w += nwg) {
     const int work = nwg >= total ? xcd_remap(w, nwg) : w;
-    const int i = wgb_item(b, work);
+    int i = 0;
+    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     const WGParams p = b.p[i];
     wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
@@ -3499,7 +3488,8 @@ __global__ __launch_bounds__(WS_THREADS, 2) void wgrad_ws32(WGBatch b) {
   __syncthreads();
   for (int w = blockIdx.x; w < total; w += nwg) {
     const int work = nwg >= total ? xcd_remap(w, nwg) : w;
-    const int i = wgb_item(b, work);
+    int i = 0;
+    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     wgrad_ws_item<BM, BN, WS_S>(b.p[i], work - b.start[i], lds, cnt);
     if (w + nwg < total) {              // the next item restarts the ring
       __syncthreads();

@@ -29,36 +29,10 @@ namespace {
 constexpr int DW_V = 8;     // channels per thread
 constexpr int DW_X = 4;     // output columns per fwd thread
 
-// minimum waves per SIMD requested for the slab-loop kernels (wgrad, fwd +
-// stats, dgrad + BN).  2 caps them at 256 registers, which spills the
-// branch-free position bodies; at 1 a wave keeps a whole position in flight
-#ifndef CER_DW_MINW
-#define CER_DW_MINW 1
-#endif
-
 struct DWGeom {
   int B, H, W, C, G, Ho, Wo, pt, pl;
   int64_t w_gstride;
 };
-
-// Every tap accumulates with an explicit fma: the plain and the fused
-// (statistics / BN-link) kernels then round identically (hipcc may otherwise
-// split a contracted a * b + c into mul + add in one kernel and not the
-// other; the fused forward's y is tested bit for bit against the plain one).
-
-// V channels at p if ok, else zeros.  p must be a valid address either way
-// (callers clamp the pixel index): the load is unconditional and the zero a
-// select.  A load under a branch makes hipcc drain vmcnt where the branch
-// joins, so a window of guarded loads costs one memory round trip per filter
-// row; unconditional ones issue a whole position's loads back to back.
-template <int V, typename T>
-__device__ __forceinline__ void ldv_or0(const T* p, bool ok, float* v) {
-  ldv<V>(p, v);
-#pragma unroll
-  for (int i = 0; i < V; ++i) v[i] = ok ? v[i] : 0.f;
-}
-
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return min(max(v, lo), hi); }
 
 // filter row r of the V channels starting at packed channel gc0 (V = 8: one
 // config holds all 8, as C % 8 == 0)
@@ -99,23 +73,27 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x,
     for (int i = 0; i < V; ++i) acc[xi][i] = 0.f;
   for (int r = 0; r < K; ++r) {
     const int hi = ho * ST - d.pt + r;
-    const bool hok = hi >= 0 && hi < d.H;
+    if (hi < 0 || hi >= d.H) continue;
     float wr[K][V];
     load_wrow<K, V, T>(w, d, gc0, r, wr);
-    const T* xrow = x + ((int64_t)b * d.H + clampi(hi, 0, d.H - 1)) * d.W * GC + gc0;
+    const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
     float win[NWIN][V];
 #pragma unroll
     for (int j = 0; j < NWIN; ++j) {
       const int wi = wi0 + j;
-      ldv_or0<V>(xrow + (int64_t)clampi(wi, 0, d.W - 1) * GC, hok && wi >= 0 && wi < d.W, win[j]);
+      if (wi >= 0 && wi < d.W) {
+        ldv<V>(xrow + (int64_t)wi * GC, win[j]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+      }
     }
 #pragma unroll
     for (int xi = 0; xi < DW_X; ++xi)
 #pragma unroll
       for (int s = 0; s < K; ++s)
 #pragma unroll
-        for (int i = 0; i < V; ++i)
-          acc[xi][i] = __builtin_fmaf(win[xi * ST + s][i], wr[s][i], acc[xi][i]);
+        for (int i = 0; i < V; ++i) acc[xi][i] += win[xi * ST + s][i] * wr[s][i];
   }
 #pragma unroll
   for (int xi = 0; xi < DW_X; ++xi) {
@@ -165,15 +143,19 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
 #pragma unroll
       for (int j = 0; j < NWIN; ++j) {
         const int wo = wo_lo + j;
-        ldv_or0<V>(dyrow + (int64_t)clampi(wo, 0, d.Wo - 1) * GC, wo >= 0 && wo < d.Wo, win[j]);
+        if (wo >= 0 && wo < d.Wo) {
+          ldv<V>(dyrow + (int64_t)wo * GC, win[j]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+        }
       }
 #pragma unroll
       for (int xi = 0; xi < DW_X; ++xi)
 #pragma unroll
         for (int s = 0; s < K; ++s)
 #pragma unroll
-          for (int i = 0; i < V; ++i) acc[xi][i] =
-                __builtin_fmaf(win[xi + K - 1 - s][i], wr[s][i], acc[xi][i]);
+          for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wr[s][i];
     } else {
 #pragma unroll
       for (int xi = 0; xi < DW_X; ++xi)
@@ -186,7 +168,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
           float v[V];
           ldv<V>(dyrow + (int64_t)wo * GC, v);
 #pragma unroll
-          for (int i = 0; i < V; ++i) acc[xi][i] = __builtin_fmaf(v[i], wr[s][i], acc[xi][i]);
+          for (int i = 0; i < V; ++i) acc[xi][i] += v[i] * wr[s][i];
         }
     }
   }
@@ -208,7 +190,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(const T* __restrict__ dy,
 // Position lanes of a channel group reduce by shuffles, the 4 waves by LDS
 // atomics, then one fp32 atomic per (channel, tap) into the gradient arena.
 template <int K, int RB, int ST, int X, int V, typename T>
-__global__ __launch_bounds__(256, CER_DW_MINW) void dw_wgrad_kernel(const T* __restrict__ x,
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ dy,
                                                        float* __restrict__ dw,
                                                        int64_t dw_gstride, DWGeom d, int lcb,
@@ -242,32 +224,38 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_wgrad_kernel(const T* __r
       const int b = (int)bq;
       const int wo0 = xg * X;
       float g[X][V];
-      const int64_t yrow = ((int64_t)b * d.Ho + ho) * d.Wo;
 #pragma unroll
       for (int xi = 0; xi < X; ++xi) {
-        const int wo = wo0 + xi;
-        ldv_or0<V>(dy + (yrow + min(wo, d.Wo - 1)) * GC + gc0, wo < d.Wo, g[xi]);
+        if (wo0 + xi < d.Wo) {
+          ldv<V>(dy + (((int64_t)b * d.Ho + ho) * d.Wo + wo0 + xi) * GC + gc0, g[xi]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) g[xi][i] = 0.f;
+        }
       }
       const int wi0 = wo0 * ST - d.pl;
 #pragma unroll
       for (int rr = 0; rr < RB; ++rr) {
         const int hi = ho * ST - d.pt + r0 + rr;
-        const bool hok = hi >= 0 && hi < d.H;
-        const T* xrow = x + ((int64_t)b * d.H + clampi(hi, 0, d.H - 1)) * d.W * GC + gc0;
+        if (hi < 0 || hi >= d.H) continue;
+        const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
         float win[NWIN][V];
 #pragma unroll
         for (int j = 0; j < NWIN; ++j) {
           const int wi = wi0 + j;
-          ldv_or0<V>(xrow + (int64_t)clampi(wi, 0, d.W - 1) * GC, hok && wi >= 0 && wi < d.W,
-                     win[j]);
+          if (wi >= 0 && wi < d.W) {
+            ldv<V>(xrow + (int64_t)wi * GC, win[j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+          }
         }
 #pragma unroll
         for (int xi = 0; xi < X; ++xi)
 #pragma unroll
           for (int s = 0; s < K; ++s)
 #pragma unroll
-            for (int i = 0; i < V; ++i) acc[rr * K + s][i] =
-                  __builtin_fmaf(win[xi * ST + s][i], g[xi][i], acc[rr * K + s][i]);
+            for (int i = 0; i < V; ++i) acc[rr * K + s][i] += win[xi * ST + s][i] * g[xi][i];
       }
     }
   }
@@ -310,7 +298,7 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_wgrad_kernel(const T* __r
 // conv epilogue's SLAB_F64 format (conv.hip stat_store), which bn.hip's
 // fold-finalize apply reads.
 template <int ST, typename T>
-__global__ __launch_bounds__(256, CER_DW_MINW) void dw_fwd_stats_kernel(const T* __restrict__ x,
+__global__ __launch_bounds__(256) void dw_fwd_stats_kernel(const T* __restrict__ x,
                                                            const T* __restrict__ w,
                                                            T* __restrict__ y, DWGeom d, int lcb,
                                                            int pos_per_slab,
@@ -351,22 +339,25 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_fwd_stats_kernel(const T*
 #pragma unroll
       for (int r = 0; r < K; ++r) {
         const int hi = ho * ST - d.pt + r;
-        const bool hok = hi >= 0 && hi < d.H;
-        const T* xrow = x + ((int64_t)b * d.H + clampi(hi, 0, d.H - 1)) * d.W * GC + gc0;
+        if (hi < 0 || hi >= d.H) continue;
+        const T* xrow = x + ((int64_t)b * d.H + hi) * d.W * GC + gc0;
         float win[NWIN][V];
 #pragma unroll
         for (int j = 0; j < NWIN; ++j) {
           const int wi = wi0 + j;
-          ldv_or0<V>(xrow + (int64_t)clampi(wi, 0, d.W - 1) * GC, hok && wi >= 0 && wi < d.W,
-                     win[j]);
+          if (wi >= 0 && wi < d.W) {
+            ldv<V>(xrow + (int64_t)wi * GC, win[j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+          }
         }
 #pragma unroll
         for (int xi = 0; xi < X; ++xi)
 #pragma unroll
           for (int s = 0; s < K; ++s)
 #pragma unroll
-            for (int i = 0; i < V; ++i)
-              acc[xi][i] = __builtin_fmaf(win[xi * ST + s][i], wk[r][s][i], acc[xi][i]);
+            for (int i = 0; i < V; ++i) acc[xi][i] += win[xi * ST + s][i] * wk[r][s][i];
       }
 #pragma unroll
       for (int xi = 0; xi < X; ++xi) {
@@ -418,8 +409,8 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_fwd_stats_kernel(const T*
 // -- the conv dgrad epilogue's YM_Y arithmetic (conv.hip epi32 bnbwd), over
 // the STORED d.  Layout and reduction as dw_fwd_stats_kernel (positions are
 // 4 input columns); fp64 atomics into slab (blockIdx.y % nsl).
-template <int ST, int PAR, typename T>
-__global__ __launch_bounds__(256, CER_DW_MINW) void dw_dgrad_bn_kernel(
+template <int ST, typename T>
+__global__ __launch_bounds__(256) void dw_dgrad_bn_kernel(
     const T* __restrict__ dy, const T* __restrict__ w, T* __restrict__ dx, DWGeom d, int lcb,
     int pos_per_slab, const T* __restrict__ ybn, const T* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ invstd, int act,
@@ -455,100 +446,70 @@ __global__ __launch_bounds__(256, CER_DW_MINW) void dw_dgrad_bn_kernel(
       const int hi = (int)u - (int)bq * d.H;
       const int b = (int)bq;
       const int wi0 = xg * X;
-      // the BN operands of the 4 columns first: independent of the conv
-      const int64_t xrow = ((int64_t)b * d.H + hi) * d.W;
-      float yv[X][V], zv[X][V];
-#pragma unroll
-      for (int xi = 0; xi < X; ++xi) {
-        const int64_t off = (xrow + min(wi0 + xi, d.W - 1)) * GC + gc0;
-        ldv<V>(ybn + off, yv[xi]);
-        ldv<V>(z + off, zv[xi]);
-      }
       float acc[X][V];
 #pragma unroll
       for (int xi = 0; xi < X; ++xi)
 #pragma unroll
         for (int i = 0; i < V; ++i) acc[xi][i] = 0.f;
-      if constexpr (ST == 1) {
-        // window j <-> dy column wi0 + pl - (K - 1) + j of dy row hi + pt - r
-        constexpr int NWIN = X + K - 1;
-        const int wo_lo = wi0 + d.pl - (K - 1);
 #pragma unroll
-        for (int r = 0; r < K; ++r) {
-          const int ho = hi + d.pt - r;
-          const bool hok = ho >= 0 && ho < d.Ho;
-          const T* dyrow = dy + ((int64_t)b * d.Ho + clampi(ho, 0, d.Ho - 1)) * d.Wo * GC + gc0;
+      for (int r = 0; r < K; ++r) {
+        const int hn = hi + d.pt - r;
+        if (hn < 0 || hn % ST) continue;
+        const int ho = hn / ST;
+        if (ho >= d.Ho) continue;
+        const T* dyrow = dy + ((int64_t)b * d.Ho + ho) * d.Wo * GC + gc0;
+        if constexpr (ST == 1) {
+          constexpr int NWIN = X + K - 1;
+          const int wo_lo = wi0 + d.pl - (K - 1);
           float win[NWIN][V];
 #pragma unroll
           for (int j = 0; j < NWIN; ++j) {
             const int wo = wo_lo + j;
-            ldv_or0<V>(dyrow + (int64_t)clampi(wo, 0, d.Wo - 1) * GC, hok && wo >= 0 && wo < d.Wo,
-                       win[j]);
+            if (wo >= 0 && wo < d.Wo) {
+              ldv<V>(dyrow + (int64_t)wo * GC, win[j]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < V; ++i) win[j][i] = 0.f;
+            }
           }
 #pragma unroll
           for (int xi = 0; xi < X; ++xi)
 #pragma unroll
             for (int s = 0; s < K; ++s)
 #pragma unroll
-              for (int i = 0; i < V; ++i) acc[xi][i] =
-                    __builtin_fmaf(win[xi + K - 1 - s][i], wk[r][s][i], acc[xi][i]);
-        }
-      } else {
-        // stride 2: dy row (hi + pt - r) / 2 exists only for even hi + pt - r.
-        // Slot 0 = filter row p = (hi + pt) & 1, slot 1 = row 2 (live iff p == 0).
-        // Columns: tap (xi, s) reads dy column (wi0 + pl + xi - s) / 2 when
-        // even; with wi0 % 4 == 0 that parity and the window slot are fixed by
-        // PAR = pl & 1, so the three dy columns wb + j are a static window
-        const int hp = hi + d.pt, p = hp & 1;
-        const int ho0 = (hp - p) >> 1, ho1 = (hp - 2) >> 1;
-        const bool ok0 = ho0 < d.Ho, ok1 = p == 0 && hp >= 2 && ho1 < d.Ho;
-        const int wb = (wi0 >> 1) + ((d.pl - PAR) >> 1) - 1 + PAR;
-        const int64_t dyb = (int64_t)b * d.Ho;
-        float win[2][3][V];
+              for (int i = 0; i < V; ++i) acc[xi][i] += win[xi + K - 1 - s][i] * wk[r][s][i];
+        } else {
 #pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int ho = sl ? ho1 : ho0;
-          const bool hok = sl ? ok1 : ok0;
-          const T* dyrow = dy + (dyb + clampi(ho, 0, d.Ho - 1)) * d.Wo * GC + gc0;
+          for (int xi = 0; xi < X; ++xi)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const int wo = wb + j;
-            ldv_or0<V>(dyrow + (int64_t)clampi(wo, 0, d.Wo - 1) * GC, hok && wo >= 0 && wo < d.Wo,
-                       win[sl][j]);
-          }
-        }
+            for (int s = 0; s < K; ++s) {
+              const int wn = wi0 + xi + d.pl - s;
+              if (wn < 0 || wn % ST) continue;
+              const int wo = wn / ST;
+              if (wo >= d.Wo) continue;
+              float v[V];
+              ldv<V>(dyrow + (int64_t)wo * GC, v);
 #pragma unroll
-        for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-          for (int s = 0; s < K; ++s) {
-            float wt[V];
-#pragma unroll
-            for (int i = 0; i < V; ++i) wt[i] = sl ? wk[2][s][i] : (p ? wk[1][s][i] : wk[0][s][i]);
-#pragma unroll
-            for (int xi = 0; xi < X; ++xi) {
-              const int a = xi + PAR - s;  // compile-time after unrolling
-              if ((a & 1) == 0) {
-                const int j = (a >> 1) + 1 - PAR;
-#pragma unroll
-                for (int i = 0; i < V; ++i)
-                  acc[xi][i] = __builtin_fmaf(win[sl][j][i], wt[i], acc[xi][i]);
-              }
+              for (int i = 0; i < V; ++i) acc[xi][i] += v[i] * wk[r][s][i];
             }
-          }
+        }
       }
 #pragma unroll
       for (int xi = 0; xi < X; ++xi) {
-        const bool xok = wi0 + xi < d.W;
-        if (xok) stv<V>(dx + (xrow + wi0 + xi) * GC + gc0, acc[xi]);
+        if (wi0 + xi >= d.W) continue;
+        const int64_t off = (((int64_t)b * d.H + hi) * d.W + wi0 + xi) * GC + gc0;
+        stv<V>(dx + off, acc[xi]);
+        float yv[V], zv[V];
+        ldv<V>(ybn + off, yv);
+        ldv<V>(z + off, zv);
 #pragma unroll
         for (int i = 0; i < V; ++i) {
           float dd = acc[xi][i];
           if constexpr (!std::is_same<T, float>::value) dd = bf2f(f2bf(dd));
-          const float yy = yv[xi][i];
-          const bool pass = act == 6 ? (yy > 0.f && yy < 6.f) : act == 1 ? yy > 0.f : true;
-          const float dz = pass && xok ? dd : 0.f;
+          const bool pass = act == 6 ? (yv[i] > 0.f && yv[i] < 6.f) : act == 1 ? yv[i] > 0.f : true;
+          const float dz = pass ? dd : 0.f;
           sm[i] += dz;
-          sq[i] += dz * (zv[xi][i] - mu[i]) * is[i];
+          sq[i] += dz * (zv[i] - mu[i]) * is[i];
         }
       }
     }
@@ -801,14 +762,11 @@ static int dwconv_bwd_bn_t(const T* dy, const T* x, const T* z, const float* mea
   slabs = (Pn + per - 1) / per;
   dim3 grid(cblocks, (unsigned)slabs);
   if (st == 1)
-    dw_dgrad_bn_kernel<1, 0, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z,
-                                                          mean, invstd, act, part, nsl);
-  else if (pl % 2 == 0)
-    dw_dgrad_bn_kernel<2, 0, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z,
-                                                          mean, invstd, act, part, nsl);
+    dw_dgrad_bn_kernel<1, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z, mean,
+                                                       invstd, act, part, nsl);
   else
-    dw_dgrad_bn_kernel<2, 1, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z,
-                                                          mean, invstd, act, part, nsl);
+    dw_dgrad_bn_kernel<2, T><<<grid, 256, 0, stream>>>(dy, w, dx, d, lcb, (int)per, x, z, mean,
+                                                       invstd, act, part, nsl);
   launch_wgrad<DW_V, T>(x, dy, dw, dw_gstride, d, k, st, stream);
   return (int)hipGetLastError();
 }

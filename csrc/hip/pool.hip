@@ -121,22 +121,11 @@ __global__ __launch_bounds__(PT) void gavg_fwd_kernel(const T* __restrict__ x,
   const int c0 = (int)(t % cv) * V;
   const int b = (int)(t / cv);
   float acc[V] = {};
-  // 8 rows' loads in flight, then their adds in row order (the same sums as
-  // a one-row loop, which waited out one memory round trip per row)
-  constexpr int R = 8;
-  for (int i0 = 0; i0 < HW; i0 += R) {
-    float v[R][V];
+  for (int i = 0; i < HW; ++i) {
+    float v[V];
+    ldv<V>(x + ((int64_t)b * HW + i) * C + c0, v);
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      const int i = min(i0 + k, HW - 1);
-      ldv<V>(x + ((int64_t)b * HW + i) * C + c0, v[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-      if (i0 + k < HW) {
-#pragma unroll
-        for (int j = 0; j < V; ++j) acc[j] += v[k][j];
-      }
+    for (int j = 0; j < V; ++j) acc[j] += v[j];
   }
   const float inv = 1.f / (float)HW;
 #pragma unroll

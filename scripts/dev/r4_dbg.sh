@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r4dbg
 mkdir -p $O
-CER_HIP_LIB=libcerebro_hip_dwb.so timeout -k 10 120 python -u scripts/dev/dw_diff.py > $O/dw_diff.log 2>&1 || { tail -20 $O/dw_diff.log; exit 1; }
+PYTHONPATH=. CER_HIP_LIB=libcerebro_hip_dwb.so timeout -k 10 120 python -u scripts/dev/dw_diff.py > $O/dw_diff.log 2>&1 || { tail -20 $O/dw_diff.log; exit 1; }
 cat $O/dw_diff.log
 timeout -k 10 400 python -u -m pytest tests/test_lanes_gpu.py -x -q -s --timeout 380 --timeout-method thread > $O/lanes.log 2>&1
 rc=$?
