@@ -35,8 +35,11 @@ IMPLEMENTED = {"adam", "loss", "gather"}
 # atomics (conv.hip cer_conv_set_stat_slabs), so every BN apply folds its
 # finalize (0: one fp32 slab per M tile, plain stores, a separate finalize
 # launch for layers with many tiles).  Buffers come zeroed from the step's
-# stats arena.
-STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "8"))
+# stats arena.  Every BN apply block re-reads the slabs before its rows, one
+# memory round trip per slab, so fewer slabs are faster despite the denser
+# atomics: 2 vs 8 is +2.2 % at 8 ResNet-50 configs, +5.2 % at one, +3.3 %
+# on MobileNetV2 (profiles/r4_bn_slabs.md).
+STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "2"))
 SLAB_F64 = 1 << 24     # conv.hip: a returned slab count with this flag is fp64 slabs
 _RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
 

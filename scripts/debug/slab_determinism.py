@@ -44,4 +44,4 @@ g2, s2 = step()
 rel = ((g1.double() - g2.double()).norm() / g1.double().norm()).item()
 rs = ((s1.double() - s2.double()).norm() / s1.double().norm()).item()
 print("slabs={} eager-vs-eager grad rel {:.3e} state rel {:.3e}".format(
-    os.environ.get("CER_BN_ATOMIC_SLABS", "8"), rel, rs))
+    os.environ.get("CER_BN_ATOMIC_SLABS", "2"), rel, rs))
