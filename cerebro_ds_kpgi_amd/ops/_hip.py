@@ -249,6 +249,7 @@ _SIGS.update({
                        c_p, c_i64, c_i, c_p],
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
+    "cer_conv_set_addend_grid": [c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
     "cer_bn_bwd_part": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p,
@@ -831,16 +832,18 @@ def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend,
     # other consumer's freshly computed dx parked in a GradJoin and used
     # nowhere else -- the kernel then only touches the 1/4 of the pixels it
     # computes, instead of first copying the whole addend into a new dx
-    # (a BN link does not change this: conv.hip computes no BN-backward
-    # statistics in a strided dgrad with an addend, the BN runs its own pass)
-    if (consume_addend and addend is not None and kh == 1 and kw == 1 and pad == 0
-            and stride > 1 and addend.is_contiguous()):
+    strided1 = kh == 1 and kw == 1 and pad == 0 and stride > 1
+    if consume_addend and addend is not None and strided1 and addend.is_contiguous():
         dx = addend
     else:
         dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
     if bnlink is None:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
                            addend, wref=wref, dy_hl=dy_hl)
+        if strided1 and addend is None:
+            # zero off the stride grid: a later strided 1x1 dgrad that adds it
+            # can compute a BN link's statistics (conv.hip g_addend_grid)
+            dx._cer_grid_st = stride
         return dx
     link, ybn = bnlink
     L = lib()
@@ -856,11 +859,20 @@ def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend,
                                _ptr(lmask) if use_mask else _ptr(_same(ybn, dy)),
                                _ptr(link.mean), _ptr(link.invstd), c_p(gp), gs, c_p(bp), bs,
                                _act_code(link.act), 1 if link.has_res else 0, ctypes.byref(nslab))
+    # the addend (the other consumer's parked dx) is zero off this conv's
+    # stride grid: the epilogue sees every nonzero pixel, so it can compute
+    # the statistics (a ResNet stage transition: c1 and the shortcut)
+    grid = (BNLINK_GRID and addend is not None and strided1
+            and getattr(addend, "_cer_grid_st", 0) == stride)
+    if grid:
+        L.cer_conv_set_addend_grid(stride)
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
                            addend, bnstats=True, wref=wref, after_tune=part.zero_, dy_hl=dy_hl)
     finally:
         L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
+        if grid:
+            L.cer_conv_set_addend_grid(0)
     if nslab.value > 0:
         link.part, link.nslab = part, nslab.value
     return dx
@@ -1264,6 +1276,12 @@ def dwconv_fwd(x, wref, stride, pad):
 # statistics.  A sweep (0 / 4M / 16M, profiles/r3_secondary_published.md)
 # showed no size at which the plain forward + BN statistics pass wins, so 0.
 DW_STATS_MIN = int(os.environ.get("CER_DW_STATS_MIN", "0"))
+
+
+# a strided 1x1 dgrad whose GradJoin addend is zero off its stride grid (the
+# other strided 1x1 consumer's dx) computes the BN link's partials
+# (conv.hip g_addend_grid; 0 = the BN runs its own partials pass there)
+BNLINK_GRID = os.environ.get("CER_BN_LINK_GRID", "1") != "0"
 
 
 # stride-2 depthwise dgrads also compute the producing BN's backward partials

@@ -3886,6 +3886,15 @@ static BNBwdEpi g_bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nul
                                 0, 0, 0};
 static int* g_bb_nslab = nullptr;
 
+// the next strided-1x1 dgrads' addend is zero off their stride grid (st; 0:
+// unknown): a ResNet stage transition, where c1 and the projection shortcut
+// are both strided 1x1 convs of one BN output, so the first one's parked dx
+// holds zeros wherever the second one writes nothing.  Every nonzero dx pixel
+// then comes out of the second one's epilogue, which can compute the BN-link
+// statistics (the zero pixels add nothing to sum dz and sum dz * xhat).
+static int g_addend_grid = 0;
+CER_API void cer_conv_set_addend_grid(int st) { g_addend_grid = st; }
+
 // z, y, gamma, beta: bf16 for cer_conv_dgrad, fp32 for cer_conv_dgrad_f32
 CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
                                   const float* mean, const float* invstd, const void* gamma,
@@ -4002,9 +4011,10 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     if (f32) v = fp32_variant(v);
     set_splits(p, G, v, f32 ? KS : BK);
     const int kind = (v / 3) & 1;
-    // BN-backward statistics: every dx pixel must come out of the epilogue
-    // (a strided 1x1 dgrad leaves pixels at zero: fine without an addend)
-    if (g_bb.part && (p.o_st == 1 || !addend)) {
+    // BN-backward statistics: every nonzero dx pixel must come out of the
+    // epilogue (a strided 1x1 dgrad leaves pixels at zero: fine without an
+    // addend, or with one that is zero off the same grid)
+    if (g_bb.part && (p.o_st == 1 || !addend || g_addend_grid == p.o_st)) {
       p.bb = g_bb;
       p.stat_slabs = g_stat_slabs;
       int bm, bn;

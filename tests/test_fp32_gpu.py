@@ -469,12 +469,22 @@ def test_bn_link_dgrad_epilogue_fp32():
     assert max(errs.values()) < TOL, errs
 
 
-def test_bn_link_strided_gradjoin_inplace_fp32():
+def test_bn_link_strided_gradjoin_inplace_fp32(monkeypatch):
     """A ResNet stage transition: a BN output h feeds two strided 1x1 convs
     (c1 and the projection shortcut) joined by a GradJoin.  The second dgrad
     accumulates into the first one's dx IN PLACE (consume_addend) and is
-    BN-linked (it carries h's whole gradient).  dx, dgamma / dbeta of h's BN
-    and both weight gradients against fp64 autograd."""
+    BN-linked (it carries h's whole gradient).  The first dx is zero off the
+    stride grid, so the second dgrad's epilogue computes h's BN partials
+    (conv.hip g_addend_grid) and h's BN skips its own pass.  dx, dgamma /
+    dbeta of h's BN and both weight gradients against fp64 autograd."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    used = []
+    real = _hip.bn_act_bwd
+
+    def spy(*a, **k):
+        used.append(k.get("part") is not None)
+        return real(*a, **k)
+    monkeypatch.setattr(_hip, "bn_act_bwd", spy)
     B, H, C, G = 8, 14, 64, 2
     Co1, Co2 = 32, 128
     specs = [ParamSpec("w0", (C, 3, 3, C), "weight", fan_in=9 * C),
@@ -498,6 +508,8 @@ def test_bn_link_strided_gradjoin_inplace_fp32():
     g1, g2 = torch.randn_like(y1), torch.randn_like(y2)
     (y1 * g1).sum().add_((y2 * g2).sum()).backward()
     torch.cuda.synchronize()
+    # h's BN (the first unit) runs its backward last: with the epilogue's partials
+    assert used and used[-1], used
 
     def unit(inp, w, g, b, st, pad, mask):
         z = F.conv2d(inp, w, None, st, pad, 1, G)
