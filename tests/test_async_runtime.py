@@ -234,6 +234,19 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
     mean number of a boundary's transfers in flight (8 = one phase, 1 = a
     chain) and as groups per rank (one per boundary)."""
     world = 8
+    # a timing property on a shared CPU host: one retry when a scheduling
+    # hiccup splits the shifts (the chained service stays ~1-2.5 every time)
+    for attempt in range(2):
+        conc = _ring_run(tmp_path / str(attempt), world)
+        print("ring-shift concurrency per boundary:", [round(c, 2) for c in conc])
+        if statistics.median(conc) >= 3.0:
+            break
+    # (~7.8 on an idle host: every boundary is one phase)
+    assert statistics.median(conc) >= 3.0, conc
+
+
+def _ring_run(tmp_path, world):
+    tmp_path.mkdir(parents=True, exist_ok=True)
     mp.spawn(_ring_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     sends = []
     for r in range(world):
@@ -257,9 +270,7 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
         # skew between ranks -- the rotation is a data flow, not a barrier --
         # only lowers it)
         conc.append(sum(b - a for a, b in spans) / (t1 - t0))
-    print("ring-shift concurrency per boundary:", [round(c, 2) for c in conc])
-    # (~7.8 on an idle host: every boundary is one phase)
-    assert statistics.median(conc) >= 3.0, conc
+    return conc
 
 
 # ---------------------------------------------------------------------------
