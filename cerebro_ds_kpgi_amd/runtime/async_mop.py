@@ -54,7 +54,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from ..scheduler.policies import GreedyScheduler, RotationScheduler
+from ..scheduler.policies import RotationScheduler
 from ..utils.keys import model_key
 
 

@@ -14,7 +14,6 @@ import concurrent.futures as cf
 import glob
 import os
 import subprocess
-import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 LIBDIR = os.path.join(ROOT, "cerebro_ds_kpgi_amd", "_lib")
