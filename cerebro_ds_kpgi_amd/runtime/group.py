@@ -445,9 +445,10 @@ class _Working(object):
 # deferred_wgrad side_frac) for packs of at least _SIDE_MIN_G configs
 # (measured: +2 % at 8, +1 % at 4, -3 % at 1 config; r2_ab_wgrad_chunk.md;
 # 0.4 re-measured 0.5 % faster than 0.5 on the round-3 build,
-# profiles/r3_final.md)
+# profiles/r3_final.md; on the round-4 build +1.3 % at 2 configs and
+# -0.6 % at 1, so packs of >= 2 take it, profiles/r4_final.md)
 _SIDE_FRAC = float(os.environ.get("CER_WGB_SIDE_FRAC", "0.4"))
-_SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "4"))
+_SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "2"))
 # wgrad-batch rows per split for those packs (fewer, longer splits: +1 % at
 # 8 configs; one-config packs keep 1024, where 2048 is 1-2.5 % slower)
 _WIDE_ROWS = int(os.environ.get("CER_WGB_ROWS_WIDE", "2048"))
