@@ -285,10 +285,11 @@ class _Working(object):
         # stream during the rest of backward -- not under a gradient
         # all-reduce hook (DDP): its buckets start mid-backward and must see
         # final gradients, which a side batch still writing would break
-        frac = (_SIDE_FRAC if self.G >= _SIDE_MIN_G and self.grad_hook is None
+        wide = self.G >= _SIDE_MIN_G and self.G * g.batch_size >= _SIDE_MIN_IMAGES
+        frac = (_SIDE_FRAC if wide and self.grad_hook is None
                 and getattr(self.net, "grad_buckets", None) is None else 0.0)
         if self.x.device.type == "cuda" and get_backend() == "hip":
-            streams.set_batch_rows(_WIDE_ROWS if self.G >= _SIDE_MIN_G else 0)
+            streams.set_batch_rows(_WIDE_ROWS if wide else 0)
         with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self)):
             logits = self.net.forward(self.x, True)
             loss = softmax_ce(logits, self.y, self.acc, self.G)
@@ -449,6 +450,9 @@ class _Working(object):
 # -0.6 % at 1, so packs of >= 2 take it, profiles/r4_final.md)
 _SIDE_FRAC = float(os.environ.get("CER_WGB_SIDE_FRAC", "0.4"))
 _SIDE_MIN_G = int(os.environ.get("CER_WGB_SIDE_MIN_G", "2"))
+# ... and at least this many images per step (G x batch): small launch-bound
+# packs (NASNet-Mobile bs4 in the hetero drill-down) keep the serial batch
+_SIDE_MIN_IMAGES = int(os.environ.get("CER_WGB_SIDE_MIN_IMAGES", "64"))
 # wgrad-batch rows per split for those packs (fewer, longer splits: +1 % at
 # 8 configs; one-config packs keep 1024, where 2048 is 1-2.5 % slower)
 _WIDE_ROWS = int(os.environ.get("CER_WGB_ROWS_WIDE", "2048"))
