@@ -29,11 +29,18 @@ Parameters: 5 289 978 trainable + 36 738 moving statistics = 5 326 716, the
 Keras NASNetMobile count for 1000 classes.
 """
 
+import os
+
 import torch
 
 from .common import BN, Conv, Dense, PackedNet
 from ..ops import nn as P
 from ..runtime.arena import ParamSpec
+
+
+# the cells' branch additions folded into the last BN of a separable block
+# as its residual (CER_NASNET_FUSED_ADD=0: BN, then an add kernel)
+_FUSED_ADD = os.environ.get("CER_NASNET_FUSED_ADD", "1") != "0"
 
 
 def correct_pad(n, k):
@@ -146,7 +153,11 @@ class PackedNASNetMobile(PackedNet):
         self.build_layout()
 
     # ------------------------------------------------------------------
-    def _sep(self, x, blk, training):
+    def _sep(self, x, blk, training, plus=None):
+        """The separable block; ``plus``: the cell branch it is added to,
+        folded into the block's last BN as its residual (one BN apply
+        instead of BN + an add kernel; the residual gradient comes out of
+        the BN backward)"""
         k = blk.k
         x = torch.relu(x)
         if blk.stride == 2:
@@ -156,7 +167,9 @@ class PackedNASNetMobile(PackedNet):
         x = P.dwconv2d(x, self.ref(blk.dw1), blk.stride, pad)
         x = self.conv_bn(x, blk.pw1, blk.bn1, training, relu=True)
         x = P.dwconv2d(x, self.ref(blk.dw2), 1, k // 2)
-        return self.conv_bn(x, blk.pw2, blk.bn2, training, relu=False)
+        if plus is not None and not _FUSED_ADD:
+            return self.conv_bn(x, blk.pw2, blk.bn2, training, relu=False) + plus
+        return self.conv_bn(x, blk.pw2, blk.bn2, training, relu=False, residual=plus)
 
     def _adjust(self, p, adj, training):
         if adj.kind == "reduce":
@@ -174,19 +187,19 @@ class PackedNASNetMobile(PackedNet):
         p = self._adjust(ip if p is None else p, cell.adj, training)
         h = self.conv_bn(torch.relu(ip), cell.h, cell.hbn, training, relu=False)
         if cell.kind == "normal":
-            x1 = self._sep(h, cell.l1, training) + self._sep(p, cell.r1, training)
-            x2 = self._sep(p, cell.l2, training) + self._sep(p, cell.r2, training)
+            x1 = self._sep(h, cell.l1, training, plus=self._sep(p, cell.r1, training))
+            x2 = self._sep(p, cell.l2, training, plus=self._sep(p, cell.r2, training))
             x3 = P.avgpool2d(h, 3, 1, 1) + p
             x4 = 2.0 * P.avgpool2d(p, 3, 1, 1)     # Keras left4 + right4: the same pool twice
-            x5 = self._sep(h, cell.l5, training) + h
+            x5 = self._sep(h, cell.l5, training, plus=h)
             return P.cat_packed([p, x1, x2, x3, x4, x5], self.G), ip
         h3 = P._zero_pad(h, correct_pad(h.shape[1], 3) + correct_pad(h.shape[2], 3))
-        x1 = self._sep(h, cell.l1, training) + self._sep(p, cell.r1, training)
+        x1 = self._sep(h, cell.l1, training, plus=self._sep(p, cell.r1, training))
         mx = P.maxpool2d(h3, 3, 2, 0)              # reduction_left2 == reduction_right5
-        x2 = mx + self._sep(p, cell.r2, training)
-        x3 = P.avgpool2d(h3, 3, 2, 0) + self._sep(p, cell.r3, training)
+        x2 = self._sep(p, cell.r2, training, plus=mx)
+        x3 = self._sep(p, cell.r3, training, plus=P.avgpool2d(h3, 3, 2, 0))
         x4 = P.avgpool2d(x1, 3, 1, 1) + x2
-        x5 = self._sep(x1, cell.l4, training) + mx
+        x5 = self._sep(x1, cell.l4, training, plus=mx)
         return P.cat_packed([x2, x3, x4, x5], self.G), ip
 
     def forward(self, x, training):
