@@ -149,3 +149,167 @@ class Heartbeat(object):
         self._stop.set()
         for t in self._threads:
             t.join(timeout=5)
+
+
+# ---------------------------------------------------------------------------
+# hop watchdog
+# ---------------------------------------------------------------------------
+EXIT_HOP_STALL = 18
+
+
+class HopWatch(object):
+    """Bounded waits for the hop data plane.
+
+    A wedged RCCL group never raises before the process group's timeout
+    (30 min), so a hang in a multi-GPU run would burn the whole job with no
+    word on which hop stalled.  Every rank registers its in-flight hop
+    operations here (``begin`` / ``end``): the hop service's header and
+    payload groups, the lock-step runtime's boundary, and the main thread's
+    wait for an arrival whose record is already published.  A daemon thread
+    checks their ages every ``interval`` seconds; past ``bound()`` =
+    ``timeout_s`` + 2 x the longest job this rank has heard of (a published
+    hop's source can still be draining that job's kernels), or when another
+    rank has raised the job-wide abort flag in the rendezvous store, it
+
+    1. prints ``HOP WATCHDOG rank r: ...`` with every pending operation
+       (kind, age, hop ids, models, peers, bytes), the groups posted and the
+       last hops completed, to stderr,
+    2. writes the same record to ``{logs_root}/hop_stall_rank{r}.json``,
+    3. raises the abort flag (a local trigger) so every other rank reports
+       and exits too, and
+    4. ends the process with ``EXIT_HOP_STALL`` (``os._exit``: no re-exec,
+       no waiting on the wedged communicator).
+
+    ``abort(reason)`` is the same path for a hop error that would leave the
+    peers blocked in a group (e.g. ``HopOrderError`` on one endpoint)."""
+
+    def __init__(self, rank, world, timeout_s, store=None, key="cerebro_hopwatch",
+                 logs_root="", interval=0.5, on_fire=None):
+        self.rank, self.world = rank, world
+        self.timeout_s = float(timeout_s)
+        self.store = store
+        self.key = key + "/abort"
+        self.logs_root = logs_root
+        self.interval = interval
+        self.on_fire = on_fire or self._exit
+        self.pending = {}
+        self.lock = threading.Lock()
+        self.jmax = 0.0
+        self.groups = 0
+        self.done = []
+        self.fired = None
+        self._n = 0
+        self._stop = threading.Event()
+        self._thread = None
+
+    # -- registry ------------------------------------------------------------
+    def begin(self, kind, t0=None, **info):
+        with self.lock:
+            self._n += 1
+            self.pending[self._n] = dict(kind=kind, t0=time.time() if t0 is None else t0,
+                                         **info)
+            if kind == "group":
+                self.groups += 1
+            return self._n
+
+    def end(self, tok):
+        with self.lock:
+            rec = self.pending.pop(tok, None)
+            if rec is not None and rec.get("hops"):
+                self.done = (self.done + list(rec["hops"]))[-16:]
+
+    def note_job(self, seconds):
+        if seconds and seconds > self.jmax:
+            self.jmax = float(seconds)
+
+    def bound(self):
+        return self.timeout_s + 2.0 * self.jmax
+
+    # -- watch thread ----------------------------------------------------------
+    def start(self):
+        self._thread = threading.Thread(target=self._loop, name="cerebro-hopwatch",
+                                        daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+
+    def _remote_abort(self):
+        if self.store is None:
+            return None
+        try:
+            if self.store.check([self.key]):
+                return self.store.get(self.key).decode()
+        except Exception:
+            return None
+        return None
+
+    def check(self, now=None):
+        """The first stalled operation (or None)."""
+        now = time.time() if now is None else now
+        b = self.bound()
+        with self.lock:
+            for tok, rec in self.pending.items():
+                if now - rec["t0"] > b:
+                    return rec
+        return None
+
+    def _loop(self):
+        while not self._stop.wait(self.interval):
+            rec = self.check()
+            if rec is not None:
+                self._fire("{} stalled for {:.1f}s (bound {:.1f}s)".format(
+                    rec["kind"], time.time() - rec["t0"], self.bound()), local=True)
+                return
+            why = self._remote_abort()
+            if why is not None:
+                self._fire("abort raised by another rank: " + why, local=False)
+                return
+
+    def abort(self, reason):
+        """A hop error on this rank: stop every rank now (see class doc)."""
+        self._fire(reason, local=True)
+
+    def diagnostic(self, reason):
+        now = time.time()
+        with self.lock:
+            pend = [dict(rec, age_s=round(now - rec["t0"], 3)) for rec in self.pending.values()]
+            for p in pend:
+                p.pop("t0", None)
+            return {"rank": self.rank, "world": self.world, "time": now, "reason": reason,
+                    "bound_s": self.bound(), "pending": pend, "groups_posted": self.groups,
+                    "last_done": list(self.done)}
+
+    def _fire(self, reason, local):
+        import sys
+        if self.fired is not None:
+            return
+        d = self.diagnostic(reason)
+        self.fired = d
+        msg = "HOP WATCHDOG rank {}: {}; pending {}; groups posted {}; last hops done {}".format(
+            self.rank, reason, json.dumps(d["pending"]), d["groups_posted"], d["last_done"])
+        try:
+            sys.stderr.write(msg + "\n")
+            sys.stderr.flush()
+        except Exception:
+            pass
+        if self.logs_root:
+            try:
+                os.makedirs(self.logs_root, exist_ok=True)
+                with open(os.path.join(self.logs_root,
+                                       "hop_stall_rank{}.json".format(self.rank)), "w") as f:
+                    json.dump(d, f)
+            except Exception:
+                pass
+        if local and self.store is not None:
+            try:
+                self.store.set(self.key, "rank {}: {}".format(self.rank, reason))
+            except Exception:
+                pass
+        self.on_fire(d)
+
+    def _exit(self, diag):  # pragma: no cover - exercised in multi-process runs
+        os._exit(EXIT_HOP_STALL)

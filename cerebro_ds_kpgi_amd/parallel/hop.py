@@ -11,10 +11,29 @@ construction; ``validate_plan`` checks the pairing.
 All of a boundary's transfers are issued as one batched group
 (``batch_isend_irecv`` -> ``ncclGroupStart/Send/Recv/GroupEnd``) on the
 one hop communicator (``hop_group``), so independent links run concurrently.
+
+**Matching rules.**  RCCL ignores point-to-point tags: it pairs a send with
+a receive per peer, in posting order.  gloo pairs them by tag.  So that the
+CPU (gloo) tests exercise the rules the GPUs run under, every hop-plane
+operation is posted with tag 0 (``CER_HOP_TAGS=1`` restores per-transfer
+tags, for A/B only): gloo then matches per peer in posting order too, and
+an ordering bug fails on the CPU exactly as it would on RCCL.
+
+**Headers.**  Every transfer is preceded by a 4 x int64 header
+``[MAGIC, model, hop id, numel]`` in the same group; each receiver checks
+the headers it got against the transfers it posted.  Two ranks that
+disagree on the order (a swapped plan, a skipped hop) stop with
+``HopOrderError`` instead of silently swapping two models' states (a size
+mismatch cannot complete: the hop watchdog, ``health.HopWatch``, reports
+it).  The cost is one 32-byte message per hop.
 """
+
+import os
 
 import torch
 import torch.distributed as dist
+
+HDR_MAGIC = 0x43455242            # "CERB"
 
 
 class Move(object):
@@ -52,6 +71,19 @@ class HopChecksumError(RuntimeError):
     pass
 
 
+class HopOrderError(RuntimeError):
+    """Two endpoints posted their transfers in different orders."""
+
+
+def tags_on():
+    """Per-transfer tags (gloo-only matching aid); default off = RCCL rules."""
+    return os.environ.get("CER_HOP_TAGS", "0") == "1"
+
+
+def p2p(op, tensor, peer, group, tag):
+    return dist.P2POp(op, tensor, peer, group, tag=tag if tags_on() else 0)
+
+
 def checksum(t):
     """Position-sensitive fp64 digest of a state buffer (debug hop check):
     total sum, stride-7 subsample sum, first-half sum."""
@@ -61,56 +93,120 @@ def checksum(t):
                         v[:n // 2].sum(dtype=torch.float64)])
 
 
-def execute_moves(moves, rank, send_buf, recv_buf, group=None, check=False):
-    """Post this rank's part of the plan; returns after all transfers land.
+def _run_group(ops):
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
-    ``send_buf(model) -> tensor`` and ``recv_buf(model) -> tensor`` give the
-    contiguous buffers.  Model id doubles as the tag (gloo matching).
 
-    ``check`` (debug, ``CER_HOP_CHECK=1``; SURVEY.md §5.2 stream-ordering
-    checks): after the transfers every sender ships the digest of what it
-    sent, every receiver compares it with the digest of what landed, after a
-    device synchronisation — a hop racing a kernel that still writes the
-    buffer, or a mis-paired send/recv, raises ``HopChecksumError``.
-    """
-    n = _post(moves, rank, send_buf, recv_buf, group)
-    if not check or not n:
-        return n
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
-    ops, mine = [], {}
-    for mv in moves:
-        if mv.src == rank:
-            ops.append(dist.P2POp(dist.isend, checksum(send_buf(mv.model)), mv.dst, group,
-                                  tag=100000 + mv.model))
-        elif mv.dst == rank:
-            buf = recv_buf(mv.model)
-            mine[mv.model] = (checksum(buf), torch.empty(3, dtype=torch.float64,
-                                                         device=buf.device))
-            ops.append(dist.P2POp(dist.irecv, mine[mv.model][1], mv.src, group,
-                                  tag=100000 + mv.model))
-    for r in dist.batch_isend_irecv(ops):
-        r.wait()
-    for m, (got, sent) in mine.items():
+# test hook: reverse this rank's receive posting order (a mis-ordered plan)
+_TEST_SWAP_RECVS = False
+
+
+def post_transfers(items, rank, group, digest_of=None, watch=None):
+    """Post this rank's transfers as ONE group and wait for it.
+
+    ``items``: ``(hop_id, model, src, dst, buf)`` in the global hop order
+    (identical on both endpoints).  Every transfer is three consecutive
+    operations to / from its peer: the header, the payload and (with
+    ``digest_of``) an fp64 digest.  Headers ride in the same group as their
+    payloads on purpose: a group must stay one contiguous range of the
+    rank's transfers in global order for the deadlock-freedom argument
+    (``async_mop.HopService``); a separate header group before the payloads
+    breaks it (tests/test_async_runtime.py caught that design deadlocking
+    tag-blind).  After the group completes every receiver checks its
+    headers, so a mis-ordered pair raises ``HopOrderError`` before anyone
+    uses the states; a size mismatch cannot complete and is reported by the
+    hop watchdog.  Returns ``[(hop_id, model, buf, sent_digest_or_None)]``
+    for the receives.  ``watch`` (a ``health.HopWatch``) sees the group as
+    an in-flight operation."""
+    mine = [it for it in items if rank in (it[2], it[3])]
+    if _TEST_SWAP_RECVS:
+        rv = [i for i, it in enumerate(mine) if it[3] == rank]
+        for i, j in zip(rv, rv[::-1]):
+            if i < j:
+                mine[i], mine[j] = mine[j], mine[i]
+    if not mine:
+        return []
+    info = dict(hops=[it[0] for it in mine], models=[it[1] for it in mine],
+                peers=sorted({it[3] if it[2] == rank else it[2] for it in mine}),
+                bytes=sum(it[4].numel() * it[4].element_size() for it in mine))
+    tok = watch.begin("group", **info) if watch is not None else None
+    try:
+        ops, out = [], []
+        for hid, m, src, dst, buf in mine:
+            if src == rank:
+                h = torch.tensor([HDR_MAGIC, m, hid, buf.numel()], dtype=torch.int64,
+                                 device=buf.device)
+                ops.append(p2p(dist.isend, h, dst, group, tag=3 * hid))
+                ops.append(p2p(dist.isend, buf, dst, group, tag=3 * hid + 1))
+                if digest_of is not None:
+                    ops.append(p2p(dist.isend, digest_of(m, buf), dst, group, tag=3 * hid + 2))
+            else:
+                h = torch.zeros(4, dtype=torch.int64, device=buf.device)
+                ops.append(p2p(dist.irecv, h, src, group, tag=3 * hid))
+                ops.append(p2p(dist.irecv, buf, src, group, tag=3 * hid + 1))
+                sent = None
+                if digest_of is not None:
+                    sent = torch.empty(3, dtype=torch.float64, device=buf.device)
+                    ops.append(p2p(dist.irecv, sent, src, group, tag=3 * hid + 2))
+                out.append((hid, m, src, buf, sent, h))
+        _run_group(ops)
+    finally:
+        if tok is not None:
+            watch.end(tok)
+    for hid, m, src, buf, sent, h in out:
+        v = h.tolist()
+        if v != [HDR_MAGIC, m, hid, buf.numel()]:
+            raise HopOrderError(
+                "rank {} posted the receive of model {} (hop {}, {} elements) from rank {}, "
+                "but the sender's transfer in that slot is model {} (hop {}, {} elements, "
+                "magic {:#x}): the endpoints posted in different orders"
+                .format(rank, m, hid, buf.numel(), src, v[1], v[2], v[3], v[0]))
+    return [(hid, m, buf, sent) for hid, m, src, buf, sent, h in out]
+
+
+def verify_digests(recvs, rank):
+    for hid, m, buf, sent in recvs:
+        if sent is None:
+            continue
+        got = checksum(buf)
         if not torch.equal(got, sent):
             raise HopChecksumError("model {} arrived corrupted on rank {}: digest {} != sent {}"
                                    .format(m, rank, got.tolist(), sent.tolist()))
-    return n
 
 
-def _post(moves, rank, send_buf, recv_buf, group):
-    ops = []
-    for mv in moves:
+def execute_moves(moves, rank, send_buf, recv_buf, group=None, check=False, watch=None):
+    """Lock-step runtime: post this rank's part of the plan; returns after
+    all transfers land.  ``send_buf(model) -> tensor`` and
+    ``recv_buf(model) -> tensor`` give the contiguous buffers; a move's
+    index in the (replicated) plan is its hop id.
+
+    ``check`` (debug, ``CER_HOP_CHECK=1``; SURVEY.md §5.2 stream-ordering
+    checks): every sender ships the digest of its buffer (taken after a
+    device synchronisation, from a second ``send_buf`` call) right behind
+    the payload; every receiver compares it with the digest of what landed
+    -- a hop racing a kernel that still writes the buffer raises
+    ``HopChecksumError``."""
+    items = []
+    for i, mv in enumerate(moves):
         if mv.src == rank:
-            ops.append(dist.P2POp(dist.isend, send_buf(mv.model), mv.dst, group, tag=mv.model))
+            items.append((i, mv.model, mv.src, mv.dst, send_buf(mv.model)))
         elif mv.dst == rank:
-            ops.append(dist.P2POp(dist.irecv, recv_buf(mv.model), mv.src, group, tag=mv.model))
-    if not ops:
+            items.append((i, mv.model, mv.src, mv.dst, recv_buf(mv.model)))
+    if not items:
         return 0
-    reqs = dist.batch_isend_irecv(ops)
-    for r in reqs:
-        r.wait()
-    return len(ops)
+    digest_of = None
+    if check:
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+        def digest_of(m, buf):
+            return checksum(send_buf(m))
+    recvs = post_transfers(items, rank, group, digest_of=digest_of, watch=watch)
+    if check:
+        verify_digests(recvs, rank)
+    return len(items)
 
 
 def warm_p2p(world, rank, device, group=None):
@@ -128,10 +224,9 @@ def warm_p2p(world, rank, device, group=None):
         s = torch.full((16,), float(rank), device=device)
         r = torch.empty(16, device=device)
         bufs.append((s, r, peer))
-        ops.append(dist.P2POp(dist.isend, s, peer, group, tag=900000 + rank))
-        ops.append(dist.P2POp(dist.irecv, r, peer, group, tag=900000 + peer))
-    for q in dist.batch_isend_irecv(ops):
-        q.wait()
+        ops.append(p2p(dist.isend, s, peer, group, tag=900000 + rank))
+        ops.append(p2p(dist.irecv, r, peer, group, tag=900000 + peer))
+    _run_group(ops)
     for s, r, peer in bufs:
         if float(r[0]) != float(peer):
             raise RuntimeError("p2p warm-up: rank {} got {} from {}".format(rank, float(r[0]), peer))
@@ -155,4 +250,3 @@ def hop_group(world, rank, device, backend=None):
     g = dist.new_group(ranks=list(range(world)), backend=backend)
     warm_p2p(world, rank, device, group=g)
     return g
-

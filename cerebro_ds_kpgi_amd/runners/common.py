@@ -58,7 +58,7 @@ def _opts(args, scheduler, loader):
         slots_per_gpu=args.slots_per_gpu, scheduler=scheduler,
         n_train=args.train_per_partition, n_valid=args.valid_per_partition,
         compute_dtype=args.compute_dtype, hop_optimizer_state=args.hop_optimizer_state,
-        pack_order=getattr(args, "pack_order", True), lanes=getattr(args, "lanes", 4),
+        pack_order=getattr(args, "pack_order", True), lanes=getattr(args, "lanes", 1),
         l2=(args.l2_mode == "adam_wd"), logs_root=args.logs_root, models_root=args.models_root,
         seed=2018, shuffle=args.shuffle or scheduler == "greedy", fault_inject=args.fault_inject,
         dataset=("criteo" if args.criteo else None), store_loader=loader,
@@ -86,6 +86,10 @@ def hyperopt_grid(args):
     buckets = getattr(args, "hyperopt_batch_buckets", "none") or "none"
     if buckets != "none":
         grid["batch_size_buckets"] = [int(b) for b in buckets.split(",") if b]
+        from ..utils.logging import logs
+        logs("HYPEROPT: batch sizes restricted to {} -- NOT the reference search space "
+             "(every integer in [{}, {}]); results are not comparable with the reference's"
+             .format(grid["batch_size_buckets"], grid["batch_size"][0], grid["batch_size"][1]))
     return grid
 
 

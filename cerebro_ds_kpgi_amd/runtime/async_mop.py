@@ -225,6 +225,7 @@ class Coordinator(object):
         self._hop_buf = []                             # decided, not yet published hops
         self._hop_buf_t0 = 0.0
         self._train_s, self._train_n = 0.0, 0            # job training times (hold)
+        self._train_max = 0.0                            # longest (hop watchdog bound)
         self.thread = None
 
     # -- plumbing ----------------------------------------------------------
@@ -309,7 +310,12 @@ class Coordinator(object):
 
     def _wait_event(self):
         """Next event; buffered hops are published before blocking on it."""
-        while self._hop_buf and not self.chan.has_event(self.nev):
+        while self._hop_buf:
+            if time.time() - self._hop_buf_t0 >= self._hold_s():
+                self._flush_hops()                     # never held past the cap
+                break
+            if self.chan.has_event(self.nev):
+                break                                  # collect its hops too
             if not self._holding():
                 self._flush_hops()
                 break
@@ -433,7 +439,8 @@ class Coordinator(object):
         h = self.nhop
         if not self._hop_buf:
             self._hop_buf_t0 = time.time()
-        self._hop_buf.append((h, {"t": "hop", "m": m, "src": src, "dst": dst}))
+        self._hop_buf.append((h, {"t": "hop", "m": m, "src": src, "dst": dst,
+                                  "jt": self._train_max}))
         self.nhop += 1
         self.hop_sent[m] = (dst, h)
         return h
@@ -478,6 +485,7 @@ class Coordinator(object):
         if t == "train_done":
             self._train_s += time.time() - b["t0"]
             self._train_n += 1
+            self._train_max = max(self._train_max, time.time() - b["t0"])
             for m in ev["models"]:
                 p = next(p for mm, p, _, _ in b["jobs"] if mm == m)
                 self.sched.release_model(m, p)
@@ -621,6 +629,8 @@ class HopService(object):
         self.groups = 0                       # batch_isend_irecv groups posted
         self.spans = []                       # (t0, t1, "send"|"recv", model, peer)
         self.error = None
+        self.watch = eng.hop_watch                # parallel.health.HopWatch (or None)
+        self.seen = {}                            # hop id -> time its record was read
         self.thread = None
 
     def start(self):
@@ -647,13 +657,26 @@ class HopService(object):
         order the compute stream after it (device side)."""
         with self.lock:
             slot = self.arrived.setdefault(h, [threading.Event(), None])
-        while not slot[0].wait(1.0):
-            if self.error:
-                raise RuntimeError("hop service failed: " + self.error)
+        tok = None
+        try:
+            while not slot[0].wait(0.5):
+                if self.error:
+                    raise RuntimeError("hop service failed: " + self.error)
+                if tok is None and self.watch is not None:
+                    # bounded from the moment the record was published
+                    # (before that, the source is still training the model)
+                    with self.lock:
+                        ts = self.seen.get(h)
+                    if ts is not None:
+                        tok = self.watch.begin("arrival", t0=ts, hops=[h])
+        finally:
+            if tok is not None:
+                self.watch.end(tok)
         if slot[1] is not None:
             torch.cuda.current_stream().wait_event(slot[1])
         with self.lock:
             del self.arrived[h]
+            self.seen.pop(h, None)
 
     class _Quiet(object):
         def __init__(self, svc):
@@ -686,6 +709,11 @@ class HopService(object):
                 self._loop()
         except BaseException as e:
             self.error = "{}: {}".format(type(e).__name__, e)
+            if self.watch is not None:
+                # peers may sit in a group with this rank: stop every rank
+                # with a diagnostic rather than leave them blocked
+                self.watch.abort("hop service failed on rank {}: {}".format(
+                    self.rank, self.error))
 
     def _loop(self):
         h = 0
@@ -701,6 +729,13 @@ class HopService(object):
             stop = recs[-1][1]["t"] == "stop"
             mine = [(hid, r["m"], r["src"], r["dst"]) for hid, r in recs
                     if r["t"] == "hop" and self.rank in (r["src"], r["dst"])]
+            now = time.time()
+            with self.lock:
+                for hid, r in recs:
+                    if r["t"] == "hop" and r["dst"] == self.rank:
+                        self.seen[hid] = now
+            if self.watch is not None:
+                self.watch.note_job(max(r.get("jt", 0.0) for _, r in recs))
             if mine:
                 with self._cv:
                     while self._paused:
@@ -717,11 +752,11 @@ class HopService(object):
 
     def _post_group(self, items):
         """Post ``items`` (this rank's transfers, global order) as one group
-        and wait for it; then publish the arrivals."""
-        from ..parallel.hop import HopChecksumError, checksum
+        and wait for it (``parallel.hop.post_transfers``: headers checked
+        first, then the payloads); then publish the arrivals."""
+        from ..parallel.hop import checksum, post_transfers, verify_digests
         eng = self.eng
-        check = eng.o.hop_check
-        ops, recvs, nsend = [], [], 0
+        tx, nsend = [], 0
         t0 = time.time()
         for hid, m, src, dst in items:
             grp = eng.group_of[m]
@@ -732,38 +767,27 @@ class HopService(object):
                     ev = self.final.get(m)
                 if ev is not None:
                     self.stream.wait_event(ev)           # the parking copy only
-                ops.append(dist.P2POp(dist.isend, buf, dst, self.group, tag=m))
-                if check:
-                    ops.append(dist.P2POp(dist.isend, checksum(buf), dst, self.group,
-                                          tag=100000 + m))
                 nsend += 1
                 with self.lock:
                     self.bytes += buf.numel() * buf.element_size()
-            else:
-                ops.append(dist.P2POp(dist.irecv, buf, src, self.group, tag=m))
-                sent = None
-                if check:
-                    sent = torch.empty(3, dtype=torch.float64, device=buf.device)
-                    ops.append(dist.P2POp(dist.irecv, sent, src, self.group, tag=100000 + m))
-                recvs.append((hid, m, buf, sent))
-        with eng.tracer.span("hop", n=len(items), sends=nsend, recvs=len(recvs)):
+            tx.append((hid, m, src, dst, buf))
+        digest_of = (lambda m, b: checksum(b)) if eng.o.hop_check else None
+        with eng.tracer.span("hop", n=len(items), sends=nsend, recvs=len(tx) - nsend):
             if nsend and eng.o.sim_hop_seconds:           # test hook: slow links
                 time.sleep(eng.o.sim_hop_seconds)
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            if eng.o.sim_hop_stall == self.rank and self.watch is not None:
+                # test hook: this rank's first group wedges (a hung RCCL call)
+                self.watch.begin("group", hops=[it[0] for it in tx], stalled_by_test=True)
+                time.sleep(3600)
+            recvs = post_transfers(tx, self.rank, self.group, digest_of=digest_of,
+                                   watch=self.watch)
             done = None
             if self.cuda:
                 done = torch.cuda.Event()
                 done.record(self.stream)
                 self.stream.synchronize()
         self.groups += 1
-        for hid, m, buf, sent in recvs:
-            if sent is not None:
-                got = checksum(buf)
-                if not torch.equal(got, sent):
-                    raise HopChecksumError(
-                        "model {} arrived corrupted on rank {}: digest {} != sent {}"
-                        .format(m, self.rank, got.tolist(), sent.tolist()))
+        verify_digests(recvs, self.rank)
         t1 = time.time()
         with self.lock:
             self.busy += t1 - t0
@@ -938,6 +962,8 @@ def _run_batch(eng, chan, hops, rec):
         raise
     if eng._sync is not None:
         eng._sync()
+    if eng.hop_watch is not None:
+        eng.hop_watch.note_job(time.time() - t_start)
     if error is None:
         eng.train_images += trained
     eng.mark_progress(False)

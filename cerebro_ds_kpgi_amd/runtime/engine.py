@@ -102,6 +102,13 @@ class EngineOptions(object):
         self.sim_job_seconds = kw.get("sim_job_seconds", None)
         self.sim_valid_seconds = kw.get("sim_valid_seconds", 0.0)
         self.sim_hop_seconds = kw.get("sim_hop_seconds", 0.0)     # per hop (slow link)
+        # test hook: this rank's hop service wedges in its first group
+        self.sim_hop_stall = kw.get("sim_hop_stall", None)
+        # hop watchdog (parallel.health.HopWatch): an in-flight hop older
+        # than this + 2 x the longest job ends every rank with a diagnostic
+        # (0 = off)
+        self.hop_timeout = kw.get("hop_timeout",
+                                  float(os.environ.get("CER_HOP_TIMEOUT", "60")))
         # DDP baseline: gradient bucket size (MB per config row)
         self.ddp_bucket_mb = kw.get("ddp_bucket_mb", 32)
 
@@ -127,8 +134,13 @@ RESUME_FILE = "resume.json"
 # default concurrency lanes per rank (EngineOptions.lanes): pack groups of
 # one batch (different architectures / batch sizes, e.g. the hetero
 # drill-down or a TPE round) replay their step graphs on this many streams at
-# once (async_mop._run_batch); each lane has its own split-K workspace (64 MB)
-LANES = 4
+# once (async_mop._run_batch); each lane has its own split-K workspace (64 MB).
+# Default 1 (one after another): lanes measured makespan-neutral on the
+# hetero jobs (profiles/r4_hetero.md) and every extra stream competes for the
+# 4 hardware queues (stream_budget, profiles/r5_stream_budget.md)
+LANES = 1
+# hardware queues per process (HIP's default GPU_MAX_HW_QUEUES)
+HW_QUEUES = 4
 
 
 def default_sizes(dataset, P):
@@ -202,6 +214,7 @@ class MOPEngine(object):
         self._chan = None
         self._nsession = 0
         self._hop_group = None
+        self.hop_watch = None        # parallel.health.HopWatch while a run is armed
         if ctx.initialized and not self.task_parallel:
             # the hop data plane: one communicator, used only by the hop
             # service (async_mop.HopService / _hop_and_load), warmed here
@@ -232,7 +245,7 @@ class MOPEngine(object):
                 self.groups[key] = PackGroup(key, ms, self.msts, self.store, self.device,
                                              self.dtype, seed_base=self.o.seed * 100,
                                              use_graphs=self.o.use_graphs, l2=self.o.l2)
-                self.groups[key].lane = (len(self.groups) - 1) % max(1, self.o.lanes)
+                self.groups[key].lane = (len(self.groups) - 1) % self.effective_lanes()
             for m in ms:
                 self.group_of[m] = self.groups[key]
 
@@ -284,7 +297,7 @@ class MOPEngine(object):
                 w, row = row_of[m]
                 return w.recv_buffer(row, hopt)
             n = execute_moves(moves, rank, send_buf, recv_buf, group=self._hop_group,
-                              check=self.o.hop_check)
+                              check=self.o.hop_check, watch=self.hop_watch)
             if n:
                 for mv in moves:
                     if mv.src == rank:
@@ -359,6 +372,7 @@ class MOPEngine(object):
         """One sub-epoch; failed (config, partition) pairs are requeued."""
         pending = dict(rnd)
         trained = 0
+        t0 = time.time()
         self.mark_progress(True)
         for attempt in range(self.o.max_retries + 1):
             failed, images = self._attempt(pending, epoch, max_steps, attempt)
@@ -371,6 +385,9 @@ class MOPEngine(object):
                 self.round_idx, self.o.max_retries + 1))
         self.round_idx += 1
         self.mark_progress(False)
+        if self.hop_watch is not None:
+            # a boundary's hop waits for the slowest rank's previous round
+            self.hop_watch.note_job(time.time() - t0)
         return trained
 
     def _attempt(self, rnd, epoch, max_steps, attempt):
@@ -620,6 +637,42 @@ class MOPEngine(object):
                              "sub-epoch resume".format(self.o.scheduler, self.o.ckpt_every))
         return rt == "async" or (rt == "auto" and not lock_only)
 
+    def stream_budget(self, pack_sizes=None):
+        """The streams this engine can have active at once in training
+        (name -> what it carries), for the queue budget
+        (``profiles/r5_stream_budget.md``).  ``pack_sizes``: {pack key: G}
+        of one batch (default: every group at its size on this rank)."""
+        from ..models.resnet import _SC_BRANCH
+        from .group import _SIDE_MIN_G, _SIDE_MIN_IMAGES
+        out = {"compute": "step / validation graph replays, parking copies"}
+        if pack_sizes is None:
+            pack_sizes = {k: min(len(g.model_ids), self.V) for k, g in self.groups.items()}
+        for key, G in pack_sizes.items():
+            grp = self.groups[key]
+            if (_SC_BRANCH and grp.arch.startswith("resnet") and "nobn" not in grp.arch
+                    and self.dtype == torch.float32):
+                out["branch"] = "ResNet projection shortcuts (fork / join in the step graph)"
+            if G >= _SIDE_MIN_G and G * grp.batch_size >= _SIDE_MIN_IMAGES:
+                out["side_wgrad"] = "first ~40 % of the batched weight gradients"
+        nl = self.effective_lanes(len(pack_sizes))
+        for i in range(1, nl):
+            out["lane{}".format(i)] = "concurrent pack group"
+        if self.ctx.world > 1 and not self.task_parallel:
+            out["hop"] = "waits on parking events (RCCL's stream waits on it)"
+            out["rccl_hop"] = "send / recv kernels of the hop communicator"
+        return out
+
+    def effective_lanes(self, ngroups=None):
+        """Lanes actually used: at most ``o.lanes``, one per group, and -- at
+        world > 1 -- no more than leaves the hop's two streams within the
+        hardware queues."""
+        n = max(1, int(self.o.lanes))
+        if ngroups is not None:
+            n = min(n, max(1, ngroups))
+        if self.ctx.world > 1 and n > 1:
+            n = max(1, min(n, HW_QUEUES - 3))      # compute/branch + hop + RCCL
+        return n
+
     def lane_stream(self, lane):
         """The stream of concurrency lane ``lane`` (created on first use)."""
         st = self._lanes.get(lane)
@@ -732,6 +785,7 @@ class MOPEngine(object):
         t0 = time.time()
         first, skip, rng = (self._resume() if self.o.resume else (1, 0, None))
         hb = self._start_heartbeat()
+        self._arm_watch()
         if self.use_async(sub_epoch_resume=bool(skip or rng)):
             try:
                 if first <= num_epochs:
@@ -740,6 +794,7 @@ class MOPEngine(object):
             finally:
                 if hb is not None:
                     hb.stop()
+                self._disarm_watch()
             return time.time() - t0
         try:
             for epoch in range(first, num_epochs + 1):
@@ -775,7 +830,28 @@ class MOPEngine(object):
         finally:
             if hb is not None:
                 hb.stop()
+            self._disarm_watch()
         return time.time() - t0
+
+    def _arm_watch(self):
+        """Collective: arm the hop watchdog for one run (world > 1, hops on)."""
+        if (self.ctx.world <= 1 or self.task_parallel or not self.o.hop_timeout
+                or self.hop_watch is not None):
+            return None
+        from ..parallel.health import HopWatch
+        from .async_mop import rendezvous_addr, tcp_client
+        tok = self.ctx.broadcast_object(os.urandom(6).hex() if self.ctx.rank == 0 else None)
+        addr = rendezvous_addr()
+        store = tcp_client(addr, 60) if addr is not None else None
+        self.hop_watch = HopWatch(self.ctx.rank, self.ctx.world, self.o.hop_timeout,
+                                  store=store, key="cerebro_hopwatch/" + tok,
+                                  logs_root=self.o.logs_root).start()
+        return self.hop_watch
+
+    def _disarm_watch(self):
+        if self.hop_watch is not None:
+            self.hop_watch.stop()
+            self.hop_watch = None
 
     def _start_heartbeat(self):
         if not getattr(self.o, "heartbeat", 0) or not self.ctx.initialized:
@@ -856,12 +932,19 @@ class MOPEngine(object):
         packed steps are done (the schedule continues across epochs)."""
         if total_steps <= 0:
             return 0
+        self._arm_watch()
+        try:
+            return self._run_steps(total_steps, steps_per_round, epoch_start)
+        finally:
+            self._disarm_watch()
+
+    def _run_steps(self, total_steps, steps_per_round, epoch_start):
         if self.use_async() and self.o.scheduler == "rotation":
             n = -(-total_steps // steps_per_round)
             last = total_steps - (n - 1) * steps_per_round
             self._run_async(epoch_start, 1 << 30, None,
-                                  steps_of=_StepsPlan(steps_per_round, last, n),
-                                  round_budget=n)
+                            steps_of=_StepsPlan(steps_per_round, last, n),
+                            round_budget=n)
             return total_steps
         done = 0
         epoch = epoch_start

@@ -64,10 +64,12 @@ def get_main_parser():
     p.add_argument("--hyperopt_models", type=str, default="",
                    help="comma list replacing the hyperopt space's model choices (reference: "
                         "resnet18,resnet34; BASELINE config 5: resnet50)")
-    p.add_argument("--hyperopt_batch_buckets", type=str, default="16,32,64,128,256",
-                   help="batch sizes TPE chooses from (comma list inside the reference range "
-                        "[16, 256]); configs with equal (model, batch) train as one packed "
-                        "launch stream. 'none' = every integer in the range (reference space)")
+    p.add_argument("--hyperopt_batch_buckets", type=str, default="none",
+                   help="'none' (default) = the reference search space, every integer batch "
+                        "size in [16, 256] (run_ctq_hyperopt.py:85-90). Opt-in performance "
+                        "mode: a comma list of sizes inside that range (e.g. 16,32,64,128,256) "
+                        "that TPE chooses from, so configs with equal (model, batch) train as "
+                        "one packed launch stream -- a different search space, logged as such")
     # ---- MI355X engine flags ----
     p.add_argument("--synthetic", type=_bool, default=True,
                    help="generate ImageNet/Criteo-shaped data on the GPUs (no datasets offline)")
@@ -83,7 +85,7 @@ def get_main_parser():
     p.add_argument("--pack_order", type=_bool, default=True,
                    help="co-schedule configs that pack into one launch stream, most steps per "
                         "partition visit first (false: the policies' own orders)")
-    p.add_argument("--lanes", type=int, default=4,
+    p.add_argument("--lanes", type=int, default=1,
                    help="pack groups of one batch replayed concurrently on this many streams "
                         "(1 = one after another)")
     p.add_argument("--hop_optimizer_state", type=_bool, default=True,

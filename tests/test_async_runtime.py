@@ -223,7 +223,7 @@ def _ring_worker(rank, world, port, outdir):
     shutdown(ctx)
 
 
-def test_async_rotation_ring_shift_is_one_phase(tmp_path):
+def test_async_rotation_ring_shift_is_one_phase(tmp_path, monkeypatch):
     """8 ranks, rotation: at every sub-epoch boundary each rank sends its
     model to the next rank and receives one from the previous.  With a
     forced 0.1 s per transfer a boundary's eight sends overlap (one phase,
@@ -232,8 +232,12 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
     every rank: the coordinator publishes the ring shift as one burst and
     each rank posts it as one ``batch_isend_irecv`` group.  Measured as the
     mean number of a boundary's transfers in flight (8 = one phase, 1 = a
-    chain) and as groups per rank (one per boundary)."""
+    chain) and as groups per rank (one per boundary).
+
+    Runs under RCCL's matching rules (tag-blind, the default: gloo pairs the
+    operations per peer in posting order, as RCCL does)."""
     world = 8
+    monkeypatch.delenv("CER_HOP_TAGS", raising=False)
     # a timing property on a shared CPU host: one retry when a scheduling
     # hiccup splits the shifts (the chained service stays ~1-2.5 every time)
     for attempt in range(2):
@@ -241,7 +245,7 @@ def test_async_rotation_ring_shift_is_one_phase(tmp_path):
         print("ring-shift concurrency per boundary:", [round(c, 2) for c in conc])
         if statistics.median(conc) >= 3.0:
             break
-    # (~7.8 on an idle host: every boundary is one phase)
+    # (~7.6-7.9 on an idle host: every boundary is one phase)
     assert statistics.median(conc) >= 3.0, conc
 
 

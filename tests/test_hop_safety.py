@@ -1,0 +1,175 @@
+"""The hop data plane under RCCL's matching rules, and its watchdog (CPU, gloo).
+
+RCCL ignores point-to-point tags and pairs sends with receives per peer in
+posting order; the hop plane therefore posts every operation with tag 0
+(``parallel.hop.p2p``), which makes gloo match the same way, and every
+multi-rank test of the package runs under those rules.  This file adds the
+negative cases the verdict of round 4 asked for:
+
+* a rank that posts two receives in the wrong order is caught by the
+  transfer headers (``HopOrderError``), never silently swapping states;
+* when the swapped transfers differ in size the group cannot complete, and
+  the hop watchdog ends both ranks with ``EXIT_HOP_STALL`` and a diagnostic;
+* a rank whose hop service wedges (a hung RCCL call, simulated) ends every
+  rank of an engine run with ``EXIT_HOP_STALL`` and a per-rank record of the
+  pending hop ids, peers and bytes, within the bound;
+* ``CER_HOP_TAGS`` is off by default (tag-blind).
+"""
+
+import json
+import os
+import time
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from test_distributed import _free_port
+
+
+def _env(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "CEREBRO_BACKEND": "torch", "CEREBRO_QUIET": "1"})
+    os.environ.pop("CER_HOP_TAGS", None)
+    torch.set_num_threads(1)
+
+
+def _join_all(procs, timeout):
+    t0 = time.time()
+    for p in procs:
+        p.join(max(1.0, timeout - (time.time() - t0)))
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join(5)
+    return codes, time.time() - t0
+
+
+def _spawn(fn, world, *args):
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    return procs
+
+
+def test_default_is_tag_blind(monkeypatch):
+    from cerebro_ds_kpgi_amd.parallel import hop
+    monkeypatch.delenv("CER_HOP_TAGS", raising=False)
+    assert not hop.tags_on()
+    monkeypatch.setenv("CER_HOP_TAGS", "1")
+    assert hop.tags_on()
+
+
+# ---------------------------------------------------------------------------
+def _swap_worker(rank, world, port, outdir, sizes):
+    _env(rank, world, port)
+    from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
+    from cerebro_ds_kpgi_amd.parallel import hop
+    from cerebro_ds_kpgi_amd.parallel.health import HopWatch
+    ctx = init_distributed(device_type="cpu")
+    watch = HopWatch(rank, world, 3.0, store=torch.distributed.distributed_c10d._get_default_store(),
+                     key="t_swap", logs_root=outdir, interval=0.2).start()
+    rows = {m: torch.full((sizes[m],), float(m + 1)) for m in (0, 1)}
+    recv = {m: torch.zeros(sizes[m]) for m in (0, 1)}
+    moves = [hop.Move(0, 0, 1), hop.Move(1, 0, 1)]      # two models 0 -> 1, one boundary
+    hop._TEST_SWAP_RECVS = rank == 1                     # rank 1 posts its receives swapped
+    res = "ok"
+    try:
+        hop.execute_moves(moves, rank, lambda m: rows[m], lambda m: recv[m], watch=watch)
+    except hop.HopOrderError as e:
+        res = "order: " + str(e)
+    except Exception as e:                               # gloo size error
+        res = "error: {}: {}".format(type(e).__name__, e)
+    with open(os.path.join(outdir, "swap_{}.txt".format(rank)), "w") as f:
+        f.write(res)
+    watch.stop()
+    shutdown(ctx)
+
+
+def test_swapped_receives_raise_order_error(tmp_path):
+    """Same-size transfers posted in swapped order complete (RCCL would pair
+    them the same way) and the headers expose the swap."""
+    procs = _spawn(_swap_worker, 2, str(tmp_path), {0: 4096, 1: 4096})
+    codes, dt = _join_all(procs, 120)
+    assert codes == [0, 0], codes
+    r0 = open(tmp_path / "swap_0.txt").read()
+    r1 = open(tmp_path / "swap_1.txt").read()
+    assert r0 == "ok"
+    assert r1.startswith("order:") and "different orders" in r1, r1
+
+
+def test_swapped_receives_of_different_sizes_never_pass(tmp_path):
+    """Different sizes: the swapped pairing cannot complete.  gloo aborts
+    the receiving process on the size mismatch; a blocked group (RCCL) is
+    ended by the watchdog (exit code EXIT_HOP_STALL).  Either way the swap
+    never passes silently."""
+    procs = _spawn(_swap_worker, 2, str(tmp_path), {0: 4096, 1: 1024})
+    codes, dt = _join_all(procs, 120)
+    assert all(c is not None for c in codes), codes          # nobody hangs
+    res1 = (tmp_path / "swap_1.txt").read_text() if (tmp_path / "swap_1.txt").exists() else None
+    assert codes[1] != 0 or (res1 is not None and res1 != "ok"), (codes, res1)
+
+
+# ---------------------------------------------------------------------------
+def _stall_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from cerebro_ds_kpgi_amd.parallel import init_distributed, shutdown
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    from test_async_runtime import _cfgs
+    ctx = init_distributed(device_type="cpu")
+    eng = MOPEngine(_cfgs(world), ctx, EngineOptions(
+        n_train=16, n_valid=8, compute_dtype="fp32", slots_per_gpu=1, verbose=False,
+        ckpt_every="none", scheduler="rotation", runtime="async", hop_timeout=4.0,
+        sim_hop_stall=1, logs_root=outdir))
+    with open(os.path.join(outdir, "t0_{}.txt".format(rank)), "w") as f:
+        f.write(str(time.time()))
+    eng.run(2)
+    with open(os.path.join(outdir, "finished_{}.txt".format(rank)), "w") as f:
+        f.write("finished")
+    eng.close()
+    shutdown(ctx)
+
+
+def test_stalled_hop_service_ends_every_rank_with_diagnostic(tmp_path):
+    from cerebro_ds_kpgi_amd.parallel.health import EXIT_HOP_STALL
+    world = 2
+    procs = _spawn(_stall_worker, world, str(tmp_path))
+    codes, dt = _join_all(procs, 150)
+    assert codes == [EXIT_HOP_STALL] * world, codes
+    for r in range(world):
+        assert not (tmp_path / "finished_{}.txt".format(r)).exists()
+        d = json.load(open(tmp_path / "hop_stall_rank{}.json".format(r)))
+        assert d["rank"] == r
+        assert d["bound_s"] >= 4.0
+    d1 = json.load(open(tmp_path / "hop_stall_rank1.json"))
+    assert "stalled" in d1["reason"]
+    assert any(p["kind"] == "group" and p.get("stalled_by_test") for p in d1["pending"])
+    d0 = json.load(open(tmp_path / "hop_stall_rank0.json"))
+    # rank 0 either timed out on its own pending hop or took rank 1's abort;
+    # either way its record names what it was waiting for
+    assert "stalled" in d0["reason"] or "abort raised" in d0["reason"]
+    # within the bound (+ job time, detection interval and process start-up)
+    t_start = min(float(open(tmp_path / "t0_{}.txt".format(r)).read()) for r in range(world))
+    t_fire = max(json.load(open(tmp_path / "hop_stall_rank{}.json".format(r)))["time"]
+                 for r in range(world))
+    assert t_fire - t_start < 4.0 + 2 * max(d0["bound_s"], d1["bound_s"]) + 20, t_fire - t_start
+
+
+# ---------------------------------------------------------------------------
+def test_watch_bound_tracks_longest_job():
+    from cerebro_ds_kpgi_amd.parallel.health import HopWatch
+    fired = []
+    w = HopWatch(0, 2, 1.0, on_fire=fired.append)
+    tok = w.begin("group", hops=[3], peers=[1], bytes=10, t0=time.time() - 2.0)
+    assert w.check() is not None                 # 2 s > 1 s bound
+    w.note_job(5.0)
+    assert w.bound() == pytest.approx(11.0)
+    assert w.check() is None                     # a long job's tail is allowed
+    w.end(tok)
+    assert w.done == [3] and w.check() is None
+    w.abort("test")
+    assert fired and fired[0]["reason"] == "test"

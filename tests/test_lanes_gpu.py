@@ -23,7 +23,7 @@ def _run(one_lane):
             for bs in (8, 16) for lr in (1e-5, 1e-6)]
     eng = MOPEngine(msts, init_distributed(), EngineOptions(
         n_train=64, n_valid=16, slots_per_gpu=4, verbose=False, ckpt_every="none",
-        shuffle=False, scheduler="rotation", runtime="async"))
+        shuffle=False, scheduler="rotation", runtime="async", lanes=2))
     if one_lane:
         for g in eng.groups.values():
             g.lane = 0

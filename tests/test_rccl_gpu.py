@@ -14,6 +14,12 @@ tests/test_async_runtime.py.  Here, at world size 1 on the ``nccl`` backend
   the hop communicator (a self send/recv of a ResNet-50-sized state row),
   an arrival event the compute stream then waits on -- and the row arrives
   bit-exact;
+* RCCL's matching rule, which the tag-blind hop plane (``parallel.hop.p2p``)
+  and its gloo tests rely on: two self-transfers whose receives are posted
+  in swapped order, with distinct tags, pair in POSTING order (the tags are
+  ignored) -- and the transfer headers expose the swap;
+* the header + payload group of ``parallel.hop.post_transfers`` round-trips
+  its int64 headers on RCCL;
 * a MOP engine then runs one round with the RCCL process group live.
 """
 
@@ -74,6 +80,28 @@ torch.cuda.current_stream().wait_event(arrived["ev"])
 out["equal"] = bool(torch.equal(dst, row))
 out["GBps"] = n * 4 / 1e9 / arrived["s"]
 
+# RCCL pairs per peer in posting order, ignoring tags
+from cerebro_ds_kpgi_amd.parallel.hop import HDR_MAGIC
+def pair(swap):
+    pay = {{m: torch.full((4096,), float(m + 1), device=dev) for m in (0, 1)}}
+    hdr = {{m: torch.tensor([HDR_MAGIC, m, m, 4096], dtype=torch.int64, device=dev)
+           for m in (0, 1)}}
+    rp = {{m: torch.zeros(4096, device=dev) for m in (0, 1)}}
+    rh = {{m: torch.zeros(4, dtype=torch.int64, device=dev) for m in (0, 1)}}
+    ops = []
+    for m in (0, 1):
+        ops += [dist.P2POp(dist.isend, hdr[m], 0, hop, tag=10 + 2 * m),
+                dist.P2POp(dist.isend, pay[m], 0, hop, tag=11 + 2 * m)]
+    for m in ((1, 0) if swap else (0, 1)):
+        ops += [dist.P2POp(dist.irecv, rh[m], 0, hop, tag=10 + 2 * m),
+                dist.P2POp(dist.irecv, rp[m], 0, hop, tag=11 + 2 * m)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    torch.cuda.synchronize()
+    return {{m: (rh[m].tolist()[1], float(rp[m][0])) for m in (0, 1)}}
+out["in_order"] = pair(False)
+out["swapped"] = pair(True)
+
 # a MOP round with the RCCL process group live
 from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
 msts = [{{"learning_rate": lr, "lambda_value": 1e-4, "batch_size": 8, "model": "resnet18"}}
@@ -102,6 +130,11 @@ def test_hop_pattern_on_rccl_world1():
     out = json.loads(lines[-1][len("RESULT "):])
     print(out)
     assert out["equal"]
+    # posted in order: each receive gets its own transfer (header names it)
+    assert out["in_order"] == {"0": [0, 1.0], "1": [1, 2.0]}
+    # posted swapped: RCCL pairs by posting order, not by tag -- the receive
+    # posted first (model 1's) gets model 0's transfer, and its header says so
+    assert out["swapped"] == {"0": [1, 2.0], "1": [0, 1.0]}
     assert out["images"] > 0 and out["finite"]
 
 

@@ -162,7 +162,10 @@ def test_hyperopt_batch_buckets_pack_configs():
     from cerebro_ds_kpgi_amd.runners.common import hyperopt_grid
     from cerebro_ds_kpgi_amd.selection import hyperopt_helper as hh
     from cerebro_ds_kpgi_amd.utils.cli import get_main_parser
-    args = get_main_parser().parse_args(["--hyperopt_models", "resnet50"])
+    # default: the reference space
+    assert "batch_size_buckets" not in hyperopt_grid(get_main_parser().parse_args([]))
+    args = get_main_parser().parse_args(["--hyperopt_models", "resnet50",
+                                         "--hyperopt_batch_buckets", "16,32,64,128,256"])
     grid = hyperopt_grid(args)
     assert grid["batch_size_buckets"] == [16, 32, 64, 128, 256]
     hp, msts, trials, domain, rand, _ = hh.init_hyperopt(grid, argparse.Namespace(size=8))
