@@ -182,41 +182,18 @@ class _StatsArena(object):
     order during a step and zeroed ONCE at the step's start (one fill kernel,
     captured with the step's HIP graph) instead of a fill per layer.  Its
     size settles in the first (eager) step; a buffer it outgrows is kept
-    alive (earlier graphs may hold it).
-
-    Also the grid-barrier words of the fused conv + BN launches
-    (``conv.hip`` BNFwdFuse): two uint32 per launch, handed out in the same
-    call order every step (so a captured graph keeps its slots), never
-    zeroed -- the barrier leaves them reusable -- plus one error word."""
-
-    BAR_SLOTS = 1024
+    alive (earlier graphs may hold it)."""
 
     def __init__(self, device):
         self.device = device
         self.buf = None
         self.off = 0
         self.keep = []
-        self.bar = None
-        self.bar_off = 0
-        self.err = None
 
     def begin(self):
         self.off = 0
-        self.bar_off = 0
         if self.buf is not None:
             self.buf.zero_()
-
-    def take_bar(self):
-        """(barrier words, error word) for the next fused launch, or None."""
-        if self.bar is None:
-            self.bar = torch.zeros(2 * self.BAR_SLOTS, dtype=torch.int32, device=self.device)
-            self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-            _FUSE_ERR.append(self.err)
-        if self.bar_off >= self.BAR_SLOTS:
-            return None
-        t = self.bar[2 * self.bar_off:2 * self.bar_off + 2]
-        self.bar_off += 1
-        return t, self.err
 
     def take(self, n):
         n_al = (n + 63) // 64 * 64
@@ -234,22 +211,6 @@ class _StatsArena(object):
 
 
 _ARENA = [None]
-_FUSE_ERR = []          # error words of every stats arena (fused BN barrier timeouts)
-BN_FUSE_ENV = os.environ.get("CER_BN_FUSE", "1") != "0"
-BN_FUSE = BN_FUSE_ENV
-
-
-def set_bn_fuse(on):
-    """Fused conv + BN forward on / off, within ``CER_BN_FUSE``
-    (``runtime.engine``: off while concurrent lanes could run two barrier
-    kernels at once)."""
-    global BN_FUSE
-    BN_FUSE = bool(on) and BN_FUSE_ENV
-
-
-def bn_fuse_errors():
-    """Barrier timeouts of fused conv + BN launches so far (host sync)."""
-    return sum(int(e.item()) for e in _FUSE_ERR)
 
 
 def stats_step(arena):
@@ -261,10 +222,7 @@ def stats_step(arena):
 
 
 def new_stats_arena(device):
-    d = torch.device(device)
-    if d.type == "cuda" and d.index is None:
-        d = torch.device("cuda", torch.cuda.current_device())
-    return _StatsArena(d)
+    return _StatsArena(torch.device(device))
 
 
 def _stats_buffer(M, C, device):
@@ -336,12 +294,6 @@ _SIGS.update({
     "cer_bias_act_bwd": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_softmax_ce_f32": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_conv_dgrad_bnbwd_f32": None,
-    "cer_conv_bn_fwd_f32": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i,
-                            c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p,
-                            c_i64, c_p, c_p, c_p, c_f, c_f, c_i, c_i, c_p, c_p, c_p, c_p, c_p],
-    "cer_bn_fuse_enable": [c_i],
-    "cer_bn_fuse_why": [],
-    "cer_conv_dgrad_bnfuse": [c_p, c_p, c_p, c_p, c_i64, c_i, c_p, c_p, c_p, c_p],
 })
 _SIGS.pop("cer_conv_dgrad_bnbwd_f32")
 IMPLEMENTED |= {"conv", "bn", "pool", "bias", "linear"}
@@ -753,13 +705,6 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
         return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                              momentum, eps) + (x4,)
 
-    if _fuse_ok(x, cout, dev):
-        fz = _conv_bn_fused(x, z, part, B, H, W, cin, G, wp, wstr, cout, kh, kw, stride, pad,
-                            Ho, Wo, residual, gref, bref, rmref, rvref, act, momentum, eps,
-                            hl_out and hl_ok(z), x_hl)
-        if fz is not None:
-            return fz + (None,)
-
     def launch():
         rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
                                           kh, kw, stride, pad, _ptr(z), Ho, Wo,
@@ -770,78 +715,6 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     launch()
     return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                          momentum, eps, hl_out=hl_out and hl_ok(z)) + (None,)
-
-
-def _fuse_ok(x, cout, dev):
-    """The fused conv + BN forward applies (conv.hip BNFwdFuse): fp32, fp64
-    slabs from a step's stats arena, 8-aligned channels, not on the branch
-    stream (two barrier kernels must never run at once)."""
-    a = _ARENA[0]
-    return (BN_FUSE and x.dtype == torch.float32 and STAT_SLABS > 0 and cout % 8 == 0
-            and a is not None and a.device == torch.device(dev) and not streams.on_branch(dev))
-
-
-def _conv_bn_fused(x, z, part, B, H, W, cin, G, wp, wstr, cout, kh, kw, stride, pad, Ho, Wo,
-                   residual, gref, bref, rmref, rvref, act, momentum, eps, hl, x_hl):
-    """conv + BN forward in one call (cer_conv_bn_fwd_f32): fused behind a
-    grid barrier when the launch fits on the GPU at once, else the conv and
-    the folded BN apply.  Returns (y, z, mean, invstd) or None (no barrier
-    slot left)."""
-    slot = _ARENA[0].take_bar()
-    if slot is None:
-        return None
-    bar, err = slot
-    dev = x.device
-    C = G * cout
-    y = torch.empty_like(z)
-    mean = torch.empty(C, dtype=torch.float32, device=dev)
-    invstd = torch.empty(C, dtype=torch.float32, device=dev)
-    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
-    mask = new_mask(z) if mask_ok(z, _act_code(act), residual) else None
-    res = _same(residual, x) if residual is not None else None
-    gp, gs = gref.work_ptr()
-    bp, bs = bref.work_ptr()
-    rmp, rs = rmref.master_ptr()
-    rvp, _ = rvref.master_ptr()
-    fused = ctypes.c_int(0)
-    scratch = []
-
-    def run(rm, rv, mo, io, yo, mk):
-        rc = lib().cer_conv_bn_fwd_f32(
-            _ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride, pad, _ptr(z), Ho, Wo,
-            _ptr(part), _ptr(res), _ptr(yo), c_p(gp), gs, c_p(bp), bs, rm, rv, rs, _ptr(mo),
-            _ptr(io), _ptr(ws), eps, momentum, _act_code(act), 1 if hl else 0, _ptr(mk),
-            _ptr(bar), _ptr(err), ctypes.byref(fused), _stream())
-        _check(rc, "cer_conv_bn_fwd_f32")
-
-    def tune():
-        # timing launches: no running-statistics update, scratch outputs
-        if not scratch:
-            n = rmref.master().numel()
-            scratch.extend([torch.empty(rs * G + n, dtype=torch.float32, device=dev),
-                            torch.empty(rs * G + n, dtype=torch.float32, device=dev),
-                            torch.empty_like(mean), torch.empty_like(invstd),
-                            torch.empty_like(y), None if mask is None else torch.empty_like(mask)])
-        run(_ptr(scratch[0]), _ptr(scratch[1]), scratch[2], scratch[3], scratch[4], scratch[5])
-    _select(0, ("bnfuse", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo,
-                residual is not None, _act_code(act), bool(hl), mask is not None)
-            + (("hl",) * x_hl), tune, x.dtype, after_tune=part.zero_)
-    run(c_p(rmp), c_p(rvp), mean, invstd, y, mask)
-    FUSE_COUNTS["fused" if fused.value else "unfused"] += 1
-    if not fused.value:
-        FUSE_WHY[int(lib().cer_bn_fuse_why())] = FUSE_WHY.get(int(lib().cer_bn_fuse_why()), 0) + 1
-    if hl:
-        y._cer_hl = True
-    if mask is not None:
-        y._cer_mask = mask
-    return y, z, mean, invstd
-
-
-# conv + BN forward / dgrad + BN backward launches by path (tests, logs)
-FUSE_COUNTS = {"fused": 0, "unfused": 0, "bwd_fused": 0, "bwd_unfused": 0}
-# why a launch did not fuse (conv.hip cer_bn_fuse_why): 1 off, 2 no slabs / slot,
-# 3 alignment / size, 4 a wide or wave-specialised variant, 5 grid > one wave
-FUSE_WHY = {}
 
 
 def stem_ok(x, wref, stride, pad):
@@ -898,8 +771,7 @@ def stem_wgrad(x4, dy, wref, pad):
 
 
 def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                       addend=None, bnstats=False, wref=None, after_tune=None, dy_hl=False,
-                       fuse=False):
+                       addend=None, bnstats=False, wref=None, after_tune=None, dy_hl=False):
     _splitk_ready(dy.device)
     # transposed-weight scratch only for the unaligned fallback (NN kernel reads W in place)
     n_wt = G * cout * kh * kw * cin if (cout % 8 or cin % 8) else 1
@@ -926,8 +798,7 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
                                              cin, kh, kw, stride, pad, _ptr(scratch[0]), H, W,
                                              _ptr(scratch[0]), _stream()), "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats)
-            + (("hl",) * bool(dy_hl)) + (("bnfuse",) * bool(fuse)), tune, dy.dtype,
-            after_tune=after_tune)
+            + (("hl",) * bool(dy_hl)), tune, dy.dtype, after_tune=after_tune)
     launch()
 
 
@@ -995,40 +866,13 @@ def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend,
             and getattr(addend, "_cer_grid_st", 0) == stride)
     if grid:
         L.cer_conv_set_addend_grid(stride)
-    # the BN's whole backward with this dgrad (cer_conv_dgrad_bnfuse): fused
-    # into its epilogue when the grid fits the GPU at once
-    fz = None
-    if link.fusable and not strided1 and _fuse_ok(dy, 8, dy.device):
-        slot = _ARENA[0].take_bar()
-        if slot is not None:
-            hl = bool(link.hl_bwd and hl_ok(link.z))
-            dz = torch.empty_like(link.z)
-            dres = torch.empty_like(link.z) if link.has_res else None
-            wsb = torch.empty(2 * C, dtype=torch.float32, device=dy.device)
-            dgp, dgs = link.gref.grad_ptr()
-            dbp, _ = link.bref.grad_ptr()
-            fused = ctypes.c_int(0)
-            L.cer_conv_dgrad_bnfuse(_ptr(dz), _ptr(dres), c_p(dgp), c_p(dbp), dgs,
-                                    1 if hl else 0, _ptr(slot[0]), _ptr(slot[1]), _ptr(wsb),
-                                    ctypes.byref(fused))
-            fz = (dz, dres, hl, fused, wsb)
     try:
         _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
-                           addend, bnstats=True, wref=wref, after_tune=part.zero_, dy_hl=dy_hl,
-                           fuse=fz is not None)
+                           addend, bnstats=True, wref=wref, after_tune=part.zero_, dy_hl=dy_hl)
     finally:
         L.cer_conv_dgrad_bnbwd(None, None, None, None, None, None, 0, None, 0, 0, 0, None)
-        if fz is not None:
-            L.cer_conv_dgrad_bnfuse(None, None, None, None, 0, 0, None, None, None, None)
         if grid:
             L.cer_conv_set_addend_grid(0)
-    if fz is not None:
-        dz, dres, hl, fused, _ = fz
-        if hl:
-            dz._cer_hl = True
-        link.result = (dz, dres)
-        FUSE_COUNTS["bwd_fused" if fused.value else "bwd_unfused"] += 1
-        return dx
     if nslab.value > 0:
         link.part, link.nslab = part, nslab.value
     return dx

@@ -132,14 +132,11 @@ class BNLink(object):
     gradient comes out of one dgrad — a sole conv consumer, or two consumers
     joined by a GradJoin (the second arrival holds the full gradient)."""
     __slots__ = ("z", "mean", "invstd", "gref", "bref", "act", "has_res", "part", "nslab",
-                 "mask", "fusable", "hl_bwd", "result")
+                 "mask")
 
     def __init__(self):
         self.z = self.mean = self.invstd = self.gref = self.bref = self.mask = None
         self.act, self.has_res, self.part, self.nslab = 0, False, None, 0
-        # set by PackedConvBNAct: the consumer's dgrad may finish this BN's
-        # backward itself (ops._hip cer_conv_dgrad_bnfuse) -> result = (dz, dres)
-        self.fusable, self.hl_bwd, self.result = False, False, None
 
 
 def _bnlink_for(ctx, x, join, addend):
@@ -367,11 +364,6 @@ class PackedConvBNAct(torch.autograd.Function):
             link.z, link.mean, link.invstd = z, mean, invstd
             link.gref, link.bref, link.act, link.has_res = gref, bref, relu, ctx.has_res
             link.mask = ctx.mask
-            link.fusable = hip_ok
-            # the BN input gradient's format (backward: HL when this conv's
-            # dgrad and wgrad both read it)
-            link.hl_bwd = (hip_ok and ctx.x4 is None and wref.spec.shape[0] % 8 == 0
-                           and wref.spec.shape[3] % 8 == 0)
         ctx.save_for_backward(x, z, y, mean, invstd)
         return y
 
@@ -392,12 +384,7 @@ class PackedConvBNAct(torch.autograd.Function):
         hl_bwd = (ctx.x4 is None and use_hip("conv", x) and _bn_hip(z, gref)
                   and wref.spec.shape[0] % 8 == 0 and wref.spec.shape[3] % 8 == 0)
         link = ctx.link
-        if link is not None and link.result is not None:
-            # the consumer's dgrad finished this BN's backward (fused into its
-            # epilogue, or its folded apply right after it): dy was never stored
-            dz, dres = link.result
-            link.result = link.part = None
-        elif link is not None and link.part is not None:
+        if link is not None and link.part is not None:
             # partials from the consumer's dgrad epilogue
             dz, dres = _hip().bn_act_bwd(dy, z, y, mean, invstd, gref, bref, ctx.relu,
                                          ctx.has_res, part=link.part, nslab=link.nslab,

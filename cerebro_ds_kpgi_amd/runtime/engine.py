@@ -188,10 +188,6 @@ class MOPEngine(object):
         self.group_of = {}
         self._lanes = {}
         self.lane_batches = 0        # train / validation phases run on lane streams
-        if self.device.type == "cuda":
-            # concurrent lanes could run two grid-barrier kernels at once
-            from ..ops import _hip
-            _hip.set_bn_fuse(self.effective_lanes() <= 1)
         self._build_groups(range(S))
         self.holder = {m: None for m in range(S)}    # None = every rank has the init copy
         self.sched = make_scheduler(opts.scheduler, list(range(S)), list(range(self.P)),

@@ -31,7 +31,6 @@
 #include <stdlib.h>
 
 #include <type_traits>
-#include <unordered_map>
 #include <utility>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -105,53 +104,6 @@ struct BNBwdEpi {
   int ym, act;                  // mask mode (bn.hip YM_*) and activation code
 };
 
-// BatchNorm forward (finalize + scale / shift + residual + activation) fused
-// into the epilogue of the conv that produced its input, behind a grid
-// barrier (cer_conv_bn_fwd_f32).  Only for launches whose every block is
-// resident at once (launch_nt32_t checks the grid against the kernel's
-// occupancy): each epilogue block adds its tile's (sum, sum^2) into the fp64
-// slabs, all of them meet at the barrier, then every block finalizes its
-// own channels from the slabs and applies BN to the tile still in its
-// registers -- no BN kernel, no re-read of z.  Blocks of the first M tile
-// write mean / invstd and update the running statistics.
-struct BNFwdFuse {
-  int on = 0;                   // 0: a plain conv (+ statistics)
-  int act = 0, hl = 0, nblk = 0;  // activation, HL-format y, epilogue blocks of the launch
-  const float* gamma = nullptr;
-  int64_t gstride = 0;
-  const float* beta = nullptr;
-  int64_t bstride = 0;
-  float* rmean = nullptr;       // null: no running-statistics update (autotune launches)
-  float* rvar = nullptr;
-  int64_t rstride = 0;
-  float* mean_out = nullptr;    // [ldc]
-  float* invstd_out = nullptr;
-  const float* res = nullptr;   // residual [M][ldc] or null
-  float* y = nullptr;           // BN output [M][ldc] (fp32, or HL with hl)
-  uint8_t* mask = nullptr;      // activation bits [M][ldc / 8] or null (bn.hip YM_M)
-  unsigned* bar = nullptr;      // {arrivals, generation} (self-resetting)
-  int* err = nullptr;           // set on a barrier timeout (host checks cer_bn_fuse_error)
-  float eps = 0.f, momentum = 0.f;
-};
-
-// BatchNorm backward (finalize + apply) fused into the epilogue of the dgrad
-// that produces the BN's output gradient dy (the BN-link dgrad, BNBwdEpi),
-// behind the same grid barrier: the epilogue adds (sum dz, sum dz*xhat)
-// into the fp64 slabs, all blocks meet, then each block finalizes its
-// channels, writes dgamma / dbeta (first M tile) and turns its tile's dy --
-// still in registers, never stored -- into the BN input gradient dz (fp32
-// or HL) and the residual gradient.  cer_conv_dgrad_bnfuse.
-struct BNBwdFuse {
-  int on = 0, hl = 0, nblk = 0;
-  float* dz = nullptr;          // [M][ldc] BN input gradient (fp32, or HL with hl)
-  float* dres = nullptr;        // residual gradient [M][ldc] (fp32) or null
-  float* dgamma = nullptr;      // fp32 gradient arena, per-config stride dgstride
-  float* dbeta = nullptr;
-  int64_t dgstride = 0;
-  unsigned* bar = nullptr;
-  int* err = nullptr;
-};
-
 struct NTParams {
   GatherGeom a;
   int dgrad;              // generic path only: 0: hi = y*st - pad + r ; 1: (y + pad - r) / st
@@ -177,8 +129,6 @@ struct NTParams {
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
   int a_hl = 0;           // fp32 kernels: the A operand is in HL format (take_hi_lo)
-  BNFwdFuse fz;           // fused BN forward (fp32 NT kernels, epi32)
-  BNBwdFuse fb;           // fused BN backward (fp32 BN-link dgrads, epi32)
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
@@ -602,42 +552,6 @@ __device__ __forceinline__ bool last_arriver(unsigned* cnt, unsigned expected, i
   }
   __syncthreads();
   return *flag != 0;
-}
-
-// Grid barrier over the ``expected`` epilogue blocks of one launch (all of
-// them resident: the host only fuses launches that fit).  Ticket +
-// generation: the last arriver re-zeroes the ticket and bumps the
-// generation the others spin on, so the two words are reusable by the next
-// launch (graph replays) without a reset.  Every wave drains its memory
-// operations first (the fp64 statistics atomics are agent-scope, performed
-// at the coherence point), so no L2 writeback is needed.  A bounded spin:
-// on timeout (never expected) ``err`` is set and the block proceeds, so a
-// broken launch cannot hang the GPU; the host raises on the flag.
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned expected, int* err) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned g0 = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // g0 read before the ticket
-    const unsigned prev = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == expected - 1) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned spins = 0;
-      while (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 1023u) == 0u &&
-            (spins > (1u << 20) ||
-             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
 }
 
 __device__ __forceinline__ void st_sc1(float* p, float v) {
@@ -2007,7 +1921,6 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
       stat_store(dst, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
                  p.stat_slabs);
   }
-
 }
 
 // Epilogue operands as buffer descriptors: a null or unused source gets a
@@ -2144,9 +2057,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
           v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
           v[e] += av[e];
         }
-        if (!p.fb.on)             // fused BN backward: dy stays in registers
-          *reinterpret_cast<float4*>(obase + orow[i] * p.ldc + n) =
-              make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(obase + orow[i] * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
         if (fstat) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -2193,200 +2104,6 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
     if (n < p.N)
       stat_store(dst, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
                  p.stat_slabs);
-  }
-  if (bstat && p.fb.on) {
-    // ---- fused BN backward (BNBwdFuse): barrier, finalize, apply ----------
-    const BNBwdFuse& fb = p.fb;
-    grid_barrier(fb.bar, (unsigned)fb.nblk, fb.err);
-    {
-      const int tiles_m = (p.M + BM - 1) / BM;
-      const int ns = p.stat_slabs < tiles_m ? p.stat_slabs : tiles_m;
-      const float inv_m = 1.f / (float)p.M;
-      const double* pd = reinterpret_cast<const double*>(bb.part);
-      const float* gam = reinterpret_cast<const float*>(bb.gamma);
-      for (int t = tid; t < BN; t += NTHREADS) {
-        const int n = n0 + t;
-        float k1 = 0.f, sdz = 0.f, k2 = 0.f;
-        if (n < p.N) {
-          const int64_t c = (int64_t)cfg * p.N + n;
-          double a = 0.0, b = 0.0;
-          for (int sl = 0; sl < ns; ++sl) {
-            a += __hip_atomic_load(const_cast<double*>(pd + (int64_t)sl * 2 * p.ldc + c),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            b += __hip_atomic_load(const_cast<double*>(pd + ((int64_t)sl * 2 + 1) * p.ldc + c),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          const float af = (float)a, bf = (float)b;
-          k1 = gam[cfg * bb.gstride + n] * bb.invstd[c];
-          sdz = af * inv_m;
-          k2 = bf * inv_m;
-          if (m0 == 0) {
-            fb.dgamma[cfg * fb.dgstride + n] = bf;
-            fb.dbeta[cfg * fb.dgstride + n] = af;
-          }
-        }
-        xch[t] = k1;
-        xch[BN + t] = sdz;
-        xch[2 * BN + t] = k2;
-      }
-    }
-    __syncthreads();
-    float k1l[FN][4], sdl[FN][4], k2l[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int nl = wn * TN + 16 * j + 4 * fc + e;
-        k1l[j][e] = xch[nl];
-        sdl[j][e] = xch[BN + nl];
-        k2l[j][e] = xch[2 * BN + nl];
-      }
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (NG > 1) fetch(g);                    // NG == 1: the operands are still here
-#pragma unroll
-      for (int ii = 0; ii < CH; ++ii) {
-        const int i = g * CH + ii;
-        if (i >= FM || !rok[i]) continue;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int n = n0 + wn * TN + 16 * j + 4 * fc;
-          if (n >= p.N) continue;
-          const float av[4] = {__uint_as_float(ad[ii][j].x), __uint_as_float(ad[ii][j].y),
-                               __uint_as_float(ad[ii][j].z), __uint_as_float(ad[ii][j].w)};
-          const float zv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
-                               __uint_as_float(zz[ii][j].z), __uint_as_float(zz[ii][j].w)};
-          float o[4], dzv[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = acc[i][j][e] + bc[j][e];
-            v = p.act == 6 ? fminf(fmaxf(v, 0.f), 6.f) : (p.act ? fmaxf(v, 0.f) : v);
-            v += av[e];
-            float dz = v;
-            if (ymz)
-              dz = (zv[e] * sc[j][e] + sh[j][e] + 0.f) > 0.f ? dz : 0.f;
-            else if (ymm) {
-              const float yv = (mk[ii][j] >> e) & 1u ? 1.f : 0.f;
-              dz = bb.act == 6 ? ((yv > 0.f && yv < 6.f) ? dz : 0.f) : (yv > 0.f ? dz : 0.f);
-            }
-            dzv[e] = dz;
-            const float xh = (zv[e] - mu[j][e]) * is[j][e];
-            o[e] = k1l[j][e] * (dz - sdl[j][e] - xh * k2l[j][e]);
-          }
-          const int64_t el = orow[i] * p.ldc + (int64_t)cfg * p.N + n;
-          if (fb.hl) {
-            const uint32_t h0 = cvt_pk_bf16(o[0], o[1]), h1 = cvt_pk_bf16(o[2], o[3]);
-            const uint32_t l0 = cvt_pk_bf16(o[0] - __uint_as_float(h0 << 16),
-                                            o[1] - __uint_as_float(h0 & 0xffff0000u));
-            const uint32_t l1 = cvt_pk_bf16(o[2] - __uint_as_float(h1 << 16),
-                                            o[3] - __uint_as_float(h1 & 0xffff0000u));
-            float* yb = fb.dz + (el & ~(int64_t)7);
-            const int half = (int)((el >> 2) & 1);
-            *reinterpret_cast<uint2*>(yb + 2 * half) = make_uint2(h0, h1);
-            *reinterpret_cast<uint2*>(yb + 4 + 2 * half) = make_uint2(l0, l1);
-          } else {
-            *reinterpret_cast<float4*>(fb.dz + el) = make_float4(o[0], o[1], o[2], o[3]);
-          }
-          if (fb.dres)
-            *reinterpret_cast<float4*>(fb.dres + el) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
-        }
-      }
-    }
-    return;
-  }
-  if (!fstat || !p.fz.on) return;
-  // ---- fused BN forward (BNFwdFuse): barrier, finalize, apply -------------
-  const BNFwdFuse& f = p.fz;
-  grid_barrier(f.bar, (unsigned)f.nblk, f.err);
-  {
-    // this block's channels: the fp64 slab sums (as bn_apply_fwd_fold folds
-    // them, same float rounding), scale / shift into LDS
-    const int tiles_m = (p.M + BM - 1) / BM;
-    const int ns = p.stat_slabs < tiles_m ? p.stat_slabs : tiles_m;
-    const float inv_m = 1.f / (float)p.M;
-    const double* pd = reinterpret_cast<const double*>(p.stats);
-    for (int t = tid; t < BN; t += NTHREADS) {
-      const int n = n0 + t;
-      float scv = 0.f, shv = 0.f;
-      if (n < p.N) {
-        const int64_t c = (int64_t)cfg * p.N + n;
-        double a = 0.0, b = 0.0;
-        for (int sl = 0; sl < ns; ++sl) {
-          a += __hip_atomic_load(const_cast<double*>(pd + (int64_t)sl * 2 * p.ldc + c),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          b += __hip_atomic_load(const_cast<double*>(pd + ((int64_t)sl * 2 + 1) * p.ldc + c),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        const float mu = (float)a * inv_m;
-        const float var = fmaxf((float)b * inv_m - mu * mu, 0.f);
-        const float is = rsqrtf(var + f.eps);
-        scv = is * f.gamma[cfg * f.gstride + n];
-        shv = f.beta[cfg * f.bstride + n] - mu * scv;
-        if (m0 == 0) {                           // one writer per channel
-          f.mean_out[c] = mu;
-          f.invstd_out[c] = is;
-          if (f.rmean) {
-            float* rm = f.rmean + cfg * f.rstride + n;
-            float* rv = f.rvar + cfg * f.rstride + n;
-            const float unb = p.M > 1 ? var * (float)p.M / (float)(p.M - 1) : var;
-            *rm = (1.f - f.momentum) * *rm + f.momentum * mu;
-            *rv = (1.f - f.momentum) * *rv + f.momentum * unb;
-          }
-        }
-      }
-      xch[t] = scv;
-      xch[BN + t] = shv;
-    }
-  }
-  __syncthreads();
-  float scl[FN][4], shl[FN][4];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int nl = wn * TN + 16 * j + 4 * fc + e;
-      scl[j][e] = xch[nl];
-      shl[j][e] = xch[BN + nl];
-    }
-  const auto rRes = make_rsrc(f.res, f.res ? EPI_BIG : 0u);
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * TN + 16 * j + 4 * fc;
-      const bool ok = rok[i] && n < p.N;
-      const int64_t el = orow[i] * p.ldc + (int64_t)cfg * p.N + n;
-      const uint4 rr = bload(rRes, ok ? (uint32_t)el * 4u : OOB);
-      const float rv4[4] = {__uint_as_float(rr.x), __uint_as_float(rr.y), __uint_as_float(rr.z),
-                            __uint_as_float(rr.w)};
-      float o[4];
-      uint32_t bits = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float z = acc[i][j][e] + bc[j][e];            // the stored z
-        float t = z * scl[j][e] + shl[j][e] + rv4[e];
-        t = f.act == 6 ? fminf(fmaxf(t, 0.f), 6.f) : (f.act ? fmaxf(t, 0.f) : t);
-        o[e] = t;
-        bits |= (t > 0.f && (f.act != 6 || t < 6.f)) ? (1u << e) : 0u;
-      }
-      // the 8-channel group's other 4 bits sit on lane ^ 16 (fc ^ 1, same row)
-      const uint32_t other = f.mask ? (uint32_t)__shfl_xor((int)bits, 16) : 0u;
-      if (!ok) continue;
-      if (f.hl) {
-        const uint32_t h0 = cvt_pk_bf16(o[0], o[1]), h1 = cvt_pk_bf16(o[2], o[3]);
-        const uint32_t l0 = cvt_pk_bf16(o[0] - __uint_as_float(h0 << 16),
-                                        o[1] - __uint_as_float(h0 & 0xffff0000u));
-        const uint32_t l1 = cvt_pk_bf16(o[2] - __uint_as_float(h1 << 16),
-                                        o[3] - __uint_as_float(h1 & 0xffff0000u));
-        float* yb = f.y + (el & ~(int64_t)7);
-        const int half = (int)((el >> 2) & 1);
-        *reinterpret_cast<uint2*>(yb + 2 * half) = make_uint2(h0, h1);
-        *reinterpret_cast<uint2*>(yb + 4 + 2 * half) = make_uint2(l0, l1);
-      } else {
-        *reinterpret_cast<float4*>(f.y + el) = make_float4(o[0], o[1], o[2], o[3]);
-      }
-      if (f.mask && !(fc & 1)) f.mask[el >> 3] = (uint8_t)(bits | (other << 4));
-    }
   }
 }
 
@@ -3956,79 +3673,34 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
   return (int)hipGetLastError();
 }
 
-// ---- fused BN forward: is every block of the launch resident at once? ----
-// Blocks go to the 8 XCDs round-robin, so a grid fits when ceil(grid / 8)
-// blocks fit on one XCD's CUs at the kernel's occupancy.
-static int g_fused_last = 0;        // the last fp32 NT launch ran the fused BN
-static int g_fuse_why = 0;          // why it did not (cer_bn_fuse_why)
-CER_API int cer_bn_fuse_why() { return g_fuse_why; }
-
-static int device_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cus[dev]) hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev);
-  return cus[dev];
-}
-
-static bool fuse_fits(const void* kern, int threads, unsigned grid) {
-  static std::unordered_map<const void*, int> occ;
-  auto it = occ.find(kern);
-  if (it == occ.end()) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, threads, 0) != hipSuccess) n = 0;
-    it = occ.emplace(kern, n).first;
-  }
-  const int cus = device_cus();
-  constexpr int XCDS = 8;
-  if (it->second <= 0 || cus < XCDS) return false;
-  return (grid + XCDS - 1) / XCDS <= (unsigned)(it->second * (cus / XCDS));
-}
-
-template <typename Kern>
-static void go32(Kern kern, dim3 grid, int threads, NTParams p, hipStream_t stream) {
-  if (p.fz.on && !fuse_fits(reinterpret_cast<const void*>(kern), threads, grid.x)) {
-    p.fz.on = 0;
-    g_fuse_why = 5;
-  }
-  g_fused_last = p.fz.on;
-  hipLaunchKernelGGL(kern, grid, dim3(threads), 0, stream, p);
-}
-
 // ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
-static void launch_nt32_t(const NTParams& p0, int G, bool fast, int kind, hipStream_t stream,
+static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
                           bool wide = false, int wg = 1, bool ws = false) {
-  NTParams p = p0;
-  p.fz.nblk = (int)(ntiles(p.M, p.N, BM, BN) * G);   // epilogue blocks (one per tile)
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   if (ws && fast) {                // wave-specialised 32x32x16 twin, 512 threads
-    if (p.fz.on) g_fuse_why = 4;
-    p.fz.on = 0;
-    go32(igemm_nt32<BM, BN, GM_FWD, true, 1, 1>, grid, 2 * NTHREADS, p, stream);
+    igemm_nt32<BM, BN, GM_FWD, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p);
     return;
   }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
-      go32(igemm_nt32<BM, BN, GM_FWD, false, 2>, grid, 2 * NTHREADS, p, stream);
+      igemm_nt32<BM, BN, GM_FWD, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
       return;
     }
   }
-  if (wide) {                      // 32x32x16 MFMA twins (epi32w: never fused)
-    if (p.fz.on) g_fuse_why = 4;
-    p.fz.on = 0;
+  if (wide) {                      // 32x32x16 MFMA twins
     if (kind == 1) {
       if constexpr (BM * BN <= 128 * 64)
         if (p.K / KS >= 3) {
-          go32(pipe_nt32<BM, BN, 3, true>, grid, NTHREADS, p, stream);
+          pipe_nt32<BM, BN, 3, true><<<grid, NTHREADS, 0, stream>>>(p);
           return;
         }
-      go32(pipe_nt32<BM, BN, 2, true>, grid, NTHREADS, p, stream);
+      pipe_nt32<BM, BN, 2, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else if (!fast) {
-      go32(igemm_nt32<BM, BN, GM_SLOW, true>, grid, NTHREADS, p, stream);
+      igemm_nt32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else {
-      go32(igemm_nt32<BM, BN, GM_FWD, true>, grid, NTHREADS, p, stream);
+      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     }
     return;
   }
@@ -4036,14 +3708,14 @@ static void launch_nt32_t(const NTParams& p0, int G, bool fast, int kind, hipStr
     // 128x128: two stages keep 2 workgroups per CU (3 x 32 KiB would not)
     if constexpr (BM * BN <= 128 * 64)
       if (p.K / KS >= 3) {
-        go32(pipe_nt32<BM, BN, 3>, grid, NTHREADS, p, stream);
+        pipe_nt32<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(p);
         return;
       }
-    go32(pipe_nt32<BM, BN, 2>, grid, NTHREADS, p, stream);
+    pipe_nt32<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
   } else if (!fast)
-    go32(igemm_nt32<BM, BN, GM_SLOW>, grid, NTHREADS, p, stream);
+    igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
   else
-    go32(igemm_nt32<BM, BN, GM_FWD>, grid, NTHREADS, p, stream);
+    igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
 }
 
 static bool nt_fast32(const NTParams& p) {
@@ -4067,7 +3739,7 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   if (v >= 36) {                                   // wave-specialised twins of 12-23
     v -= 36;
     if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
-    wide = p.bb.part == nullptr && !p.fz.on;       // fused BN: epi32 kernels only
+    wide = p.bb.part == nullptr;
     ws = wide && fast;
   } else if (v >= 24) {
     wg = 2;
@@ -4076,8 +3748,8 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   } else if (v >= 12) {
     v -= 12;
     // BN-backward statistics (the unaligned-dgrad fallback) only in the NN
-    // kernels' wide epilogue; a fused BN forward only in epi32 (non-wide twin)
-    wide = p.bb.part == nullptr && !p.fz.on;
+    // kernels' wide epilogue
+    wide = p.bb.part == nullptr;
     if (((v / 3) & 1) && !ring_ok) v -= 3;
   }
   if (!fast) v = fp32_variant(v);
@@ -4136,107 +3808,6 @@ CER_API int cer_conv_fwd_stats_f32(const float* x, int B, int H, int W, int Cin,
                                    int* nslab, hipStream_t stream) {
   return conv_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, y, Ho, Wo,
                        nullptr, 0, 0, part, nslab, true, stream);
-}
-
-// conv + BN forward (training) in one call: the conv with the BN statistics
-// in its epilogue and, when the launch fits on the GPU at once, the BN
-// finalize / apply fused behind a grid barrier (BNFwdFuse); otherwise the
-// folded BN apply kernel (bn.hip) after it.  Same outputs either way: z (the
-// BN input), y (fp32 or HL), the activation bits (mask), mean / invstd and
-// the running-statistics update (skipped with null rmean: autotune timing).
-// *fused reports the path taken.  Needs fp64 slabs (cer_conv_set_stat_slabs
-// > 0), 8-aligned channels and no bias / activation in the conv.
-CER_API int cer_bn_fwd_train_part_f32(const float* x, const float* res, float* y,
-                                      const float* gamma, int64_t gamma_stride,
-                                      const float* beta, int64_t beta_stride, float* rmean,
-                                      float* rvar, int64_t rstat_stride, float* mean_out,
-                                      float* invstd_out, float* ws, float* part, int nslab,
-                                      int64_t M, int C, int Cper, float eps, float momentum,
-                                      int act, hipStream_t stream);
-CER_API void cer_bn_set_hl_out(int on);
-CER_API void cer_bn_set_mask_out(void* mask);
-
-static int g_bn_fuse = -1;          // CER_BN_FUSE (default 1)
-CER_API void cer_bn_fuse_enable(int on) { g_bn_fuse = on ? 1 : 0; }
-
-CER_API int cer_conv_bn_fwd_f32(const float* x, int B, int H, int W, int Cin, int G,
-                                const float* w, int64_t w_gstride, int Cout, int kh, int kw,
-                                int st, int pad, float* z, int Ho, int Wo, float* part,
-                                const float* res, float* y, const float* gamma, int64_t gstride,
-                                const float* beta, int64_t bstride, float* rmean, float* rvar,
-                                int64_t rstride, float* mean_out, float* invstd_out, float* ws,
-                                float eps, float momentum, int act, int hl, uint8_t* mask,
-                                unsigned* bar, int* err, int* fused, hipStream_t stream) {
-  if (g_bn_fuse < 0) {
-    const char* e = getenv("CER_BN_FUSE");
-    g_bn_fuse = e ? (atoi(e) != 0) : 1;
-  }
-  const int C = G * Cout;
-  const int64_t M = (int64_t)B * Ho * Wo;
-  NTParams p;
-  p.a = make_geom(x, B, G * Cin, Cin, H, W, Ho, Wo, kh, kw, st, pad, 4);
-  p.dgrad = 0;
-  p.w = reinterpret_cast<const bf16_t*>(w);
-  p.w_gstride = w_gstride;
-  p.out = reinterpret_cast<bf16_t*>(z);
-  p.ldc = C;
-  p.M = (int)M;
-  p.N = Cout;
-  p.K = kh * kw * Cin;
-  p.bias = nullptr;
-  p.act = 0;
-  p.o_st = 1;
-  p.o_H = Ho;
-  p.o_W = Wo;
-  p.stats = part;
-  p.a_hl = g_hl_x;
-  const bool can = g_bn_fuse && g_stat_slabs > 0 && bar && err && (Cout % 8 == 0) &&
-                   M * C * 4 < (int64_t)EPI_BIG && M < (1ll << 31);
-  g_fuse_why = !g_bn_fuse ? 1 : (!g_stat_slabs || !bar || !err) ? 2 : !can ? 3 : 0;
-  if (can) {
-    BNFwdFuse& f = p.fz;
-    f.on = 1;
-    f.act = act;
-    f.hl = hl;
-    f.gamma = gamma;
-    f.gstride = gstride;
-    f.beta = beta;
-    f.bstride = bstride;
-    f.rmean = rmean;
-    f.rvar = rvar;
-    f.rstride = rstride;
-    f.mean_out = mean_out;
-    f.invstd_out = invstd_out;
-    f.res = res;
-    f.y = y;
-    f.mask = mask;
-    f.bar = bar;
-    f.err = err;
-    f.eps = eps;
-    f.momentum = momentum;
-  }
-  int nslab = 0;
-  g_fused_last = 0;
-  int rc = run_nt32(p, G, stream, &nslab);
-  if (rc) return rc;
-  *fused = g_fused_last;
-  if (g_fused_last) return 0;
-  // not fused: the folded BN apply (bn.hip), same outputs
-  cer_bn_set_hl_out(hl);
-  cer_bn_set_mask_out(mask);
-  rc = cer_bn_fwd_train_part_f32(z, res, y, gamma, gstride, beta, bstride, rmean, rvar, rstride,
-                                 mean_out, invstd_out, ws, part, nslab, M, C, Cout, eps,
-                                 momentum, act, stream);
-  cer_bn_set_hl_out(0);
-  cer_bn_set_mask_out(nullptr);
-  return rc;
-}
-
-// barrier timeouts of fused launches so far (the host raises on != 0)
-CER_API int cer_bn_fuse_error(const int* err) {
-  int v = 0;
-  if (hipMemcpy(&v, err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return v;
 }
 
 // upper bound over tile choices: one slab per 64-row M tile
@@ -4335,105 +3906,38 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
   g_bb_nslab = part ? nslab_out : nullptr;
 }
 
-// fused BN backward of the next BN-link dgrads (cer_conv_dgrad_bnfuse)
-static BNBwdFuse g_fb;
-static float* g_fb_ws = nullptr;
-static int* g_fb_fused = nullptr;
-static int g_fused_last_b = 0;
-
-template <typename Kern>
-static void go_nn32(Kern kern, dim3 grid, int threads, NTParams p, int T, FastDiv dc,
-                    hipStream_t stream) {
-  if (p.fb.on && !fuse_fits(reinterpret_cast<const void*>(kern), threads, grid.x)) p.fb.on = 0;
-  g_fused_last_b = p.fb.on;
-  hipLaunchKernelGGL(kern, grid, dim3(threads), 0, stream, p, T, dc);
-}
-
 template <int BM, int BN>
-static void launch_nn32_t(const NTParams& p0, int G, int T, bool strided, hipStream_t stream,
+static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
                           bool wide = false, int wg = 1, bool ws = false) {
-  NTParams p = p0;
-  p.fb.nblk = (int)(ntiles(p.M, p.N, BM, BN) * G);   // epilogue blocks (one per tile)
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
   if (ws) {                        // wave-specialised 32x32x16 twin, 512 threads
-    p.fb.on = 0;
     if (strided)
-      go_nn32(igemm_nn32<BM, BN, GM_DGS, true, 1, 1>, grid, 2 * NTHREADS, p, T, dc, stream);
+      igemm_nn32<BM, BN, GM_DGS, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
     else
-      go_nn32(igemm_nn32<BM, BN, GM_DG1, true, 1, 1>, grid, 2 * NTHREADS, p, T, dc, stream);
+      igemm_nn32<BM, BN, GM_DG1, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
     return;
   }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && !wide) {                         // intra-block K split, 512 threads
       if (strided)
-        go_nn32(igemm_nn32<BM, BN, GM_DGS, false, 2>, grid, 2 * NTHREADS, p, T, dc, stream);
+        igemm_nn32<BM, BN, GM_DGS, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
       else
-        go_nn32(igemm_nn32<BM, BN, GM_DG1, false, 2>, grid, 2 * NTHREADS, p, T, dc, stream);
+        igemm_nn32<BM, BN, GM_DG1, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
       return;
     }
   }
-  if (wide) {                      // 32x32x16 MFMA twins (epi32w: never fused)
-    p.fb.on = 0;
+  if (wide) {                      // 32x32x16 MFMA twins
     if (strided)
-      go_nn32(igemm_nn32<BM, BN, GM_DGS, true>, grid, NTHREADS, p, T, dc, stream);
+      igemm_nn32<BM, BN, GM_DGS, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     else
-      go_nn32(igemm_nn32<BM, BN, GM_DG1, true>, grid, NTHREADS, p, T, dc, stream);
+      igemm_nn32<BM, BN, GM_DG1, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     return;
   }
   if (strided)
-    go_nn32(igemm_nn32<BM, BN, GM_DGS>, grid, NTHREADS, p, T, dc, stream);
+    igemm_nn32<BM, BN, GM_DGS><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
   else
-    go_nn32(igemm_nn32<BM, BN, GM_DG1>, grid, NTHREADS, p, T, dc, stream);
-}
-
-// the BN backward of a fusion-requested dgrad that did not fuse (its grid
-// exceeds one wave, or a wide variant ran): the folded BN apply (bn.hip)
-// over the dy the dgrad stored, into the same outputs -- so the autotune
-// times every variant with its BN backward, fused or not
-CER_API int cer_bn_bwd_part_f32(const float* dy, const float* x, const float* y,
-                                const float* mean, const float* invstd, const float* gamma,
-                                int64_t gs, const float* beta, int64_t bs, float* dgamma,
-                                float* dbeta, int64_t grad_stride, float* dx, float* dres,
-                                float* ws, float* part, int nslab, int64_t M, int C, int Cper,
-                                int act, hipStream_t stream);
-CER_API void cer_bn_set_mask_in(int on);
-
-static int fb_fallback(void* dy, int64_t M, int C, int Cper, hipStream_t stream) {
-  if (!g_bb_nslab || *g_bb_nslab <= 0) return (int)hipErrorInvalidValue;
-  cer_bn_set_hl_out(g_fb.hl);
-  cer_bn_set_mask_in(g_bb.ym == 3);
-  const int rc = cer_bn_bwd_part_f32(
-      reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(g_bb.z),
-      reinterpret_cast<const float*>(g_bb.y), g_bb.mean, g_bb.invstd,
-      reinterpret_cast<const float*>(g_bb.gamma), g_bb.gstride,
-      reinterpret_cast<const float*>(g_bb.beta), g_bb.bstride, g_fb.dgamma, g_fb.dbeta,
-      g_fb.dgstride, g_fb.dz, g_fb.dres, g_fb_ws, g_bb.part, *g_bb_nslab, M, C, Cper, g_bb.act,
-      stream);
-  cer_bn_set_hl_out(0);
-  cer_bn_set_mask_in(0);
-  return rc;
-}
-
-// fused BN backward for the NEXT BN-link dgrads (until cleared with dz ==
-// nullptr): the BN of cer_conv_dgrad_bnbwd is finished here -- dz (fp32, or
-// HL with hl), dres (null: none), dgamma / dbeta -- fused into the dgrad
-// epilogue when its grid fits the GPU at once, else by the folded BN apply
-// after it (ws: 2 * C floats of scratch); *fused reports the path.
-CER_API void cer_conv_dgrad_bnfuse(float* dz, float* dres, float* dgamma, float* dbeta,
-                                   int64_t dgstride, int hl, unsigned* bar, int* err, float* ws,
-                                   int* fused) {
-  g_fb = BNBwdFuse{};
-  g_fb.dz = dz;
-  g_fb.dres = dres;
-  g_fb.dgamma = dgamma;
-  g_fb.dbeta = dbeta;
-  g_fb.dgstride = dgstride;
-  g_fb.hl = hl;
-  g_fb.bar = bar;
-  g_fb.err = err;
-  g_fb_ws = ws;
-  g_fb_fused = fused;
+    igemm_nn32<BM, BN, GM_DG1><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
 }
 
 static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int G, const void* w,
@@ -4510,16 +4014,6 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     // BN-backward statistics: every nonzero dx pixel must come out of the
     // epilogue (a strided 1x1 dgrad leaves pixels at zero: fine without an
     // addend, or with one that is zero off the same grid)
-    const bool want_fb = f32 && g_fb.dz && g_bb.part && p.o_st == 1 && g_stat_slabs > 0 &&
-                         g_bb.ym != 1 && (int64_t)p.M * p.ldc * 4 < (int64_t)EPI_BIG;
-    if (want_fb) {
-      p.fb = g_fb;
-      p.fb.on = 1;
-      if (wide) {                         // fused: the non-wide twin (epi32)
-        wide = ws = false;
-      }
-    }
-    g_fused_last_b = 0;
     if (g_bb.part && (p.o_st == 1 || !addend || g_addend_grid == p.o_st)) {
       p.bb = g_bb;
       p.stat_slabs = g_stat_slabs;
@@ -4535,12 +4029,7 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
         case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1, ws); break;
         default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg, ws); break;
       }
-      int rc = (int)hipGetLastError();
-      if (g_fb.dz) {                      // fusion requested: the BN backward happens here
-        if (g_fb_fused) *g_fb_fused = g_fused_last_b;
-        if (!rc && !g_fused_last_b) rc = fb_fallback(dx, B * H * W, G * Cin, Cin, stream);
-      }
-      return rc;
+      return (int)hipGetLastError();
     }
     switch (v % 3) {
       case 0: launch_nn_t<64, 64>(p, G, T, kind, strided, stream); break;
@@ -4550,7 +4039,6 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     return (int)hipGetLastError();
   }
   if (g_bb_nslab) *g_bb_nslab = 0;       // fallback path: no BN statistics
-  if (g_fb.dz) return (int)hipErrorInvalidValue;   // fused BN backward: aligned kernels only
   dim3 tg(((Cout + 31) / 32) * ((Cin + 31) / 32), T, G);
   if (f32)
     transpose_w_kernel<float><<<tg, 256, 0, stream>>>(reinterpret_cast<const float*>(w),
