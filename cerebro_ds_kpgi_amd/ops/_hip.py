@@ -222,7 +222,10 @@ def stats_step(arena):
 
 
 def new_stats_arena(device):
-    return _StatsArena(torch.device(device))
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:   # "cuda" -> "cuda:<current>": the
+        d = torch.device("cuda", torch.cuda.current_device())   # per-launch device check
+    return _StatsArena(d)
 
 
 def _stats_buffer(M, C, device):
