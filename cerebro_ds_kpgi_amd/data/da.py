@@ -224,58 +224,96 @@ def write_partition(heap_path, toast_path, buffers, dist_key, toastrelid=99999,
 
 
 def write_dataset(root, dataset, num_partitions, n_train, n_valid, buffer_size=cat.TRAIN_BUFFER_SIZE,
-                  seed=cat.SEED, seg_bytes=SEG_BYTES, verbose=False):
+                  seed=cat.SEED, seg_bytes=SEG_BYTES, verbose=False, unique=None, jobs=1):
     """Synthetic packed tables for ``num_partitions`` segments + manifest.
     Buffers are converted to the float32 payload one at a time (a full
-    ImageNet partition is 24 GB as float32); ``verbose`` prints progress."""
-    import sys
-    import time
-    from . import synthetic
-    shapes = {"train": [], "valid": []}
-    for p in range(num_partitions):
-        for split, n, rel, toast in (("train", n_train, TRAIN_RELFILENODE, TRAIN_TOAST),
-                                     ("valid", n_valid, VALID_RELFILENODE, VALID_TOAST)):
-            s = seed * 1000 + 2 * p + (split == "valid")
-            if dataset == "imagenet":
-                x, y = synthetic.image_partition(n, seed=s)
-                x = x.numpy()                     # uint8; float32 per buffer below
-                classes = cat.NUM_CLASSES
-            elif dataset == "criteo":
-                idx, y = synthetic.criteo_partition(n, seed=s)
-                x = np.zeros((n, cat.INPUT_SHAPE_CRITEO[0]), dtype=np.float32)
-                np.put_along_axis(x, idx.numpy().astype(np.int64), 1.0, axis=1)
-                classes = cat.NUM_CLASSES_CRITEO
-            else:
-                raise ValueError(dataset)
-            yy = np.zeros((n, classes), dtype=np.int16)
-            yy[np.arange(n), y.numpy()] = 1
-            for bid, s0 in enumerate(range(0, n, buffer_size)):
-                e = min(n, s0 + buffer_size)
-                shapes[split].append({"dist_key": p, "buffer_id": bid,
-                                      "independent_var_shape": list(x[s0:e].shape),
-                                      "dependent_var_shape": [e - s0, classes]})
-            bufs = ((bid, x[s0:min(n, s0 + buffer_size)].astype(np.float32),
-                     yy[s0:min(n, s0 + buffer_size)])
-                    for bid, s0 in enumerate(range(0, n, buffer_size)))
-            nbuf = (n + buffer_size - 1) // buffer_size
-            t0 = time.time()
+    ImageNet partition is 24 GB as float32); ``verbose`` prints progress.
 
-            def log(i, nb, p=p, split=split, nbuf=nbuf, t0=t0):
-                if verbose:
-                    print("  partition {} {}: {}/{} buffers, {:.2f} GB in {:.1f}s".format(
-                        p, split, i, nbuf, nb / 1e9, time.time() - t0), flush=True)
-                    sys.stdout.flush()
-            d = seg_dir(root, p)
-            write_partition(os.path.join(d, str(rel)), os.path.join(d, str(toast)), bufs, p,
-                            toastrelid=toast, first_valueid=(p + 1) << 20, seg_bytes=seg_bytes,
-                            log=log)
+    ``unique``: only the first ``unique`` partitions are generated; segment
+    ``p >= unique`` is a directory of HARD LINKS to segment ``p % unique``'s
+    files (same bytes, so the same pages are walked, detoasted and decoded
+    again for it).  For disks that cannot hold every partition (8 full
+    ImageNet-112 partitions are ~105 GB stored); the manifest records the
+    links.  ``jobs``: partitions generated by that many processes at once."""
+    unique = num_partitions if not unique else min(int(unique), num_partitions)
+    args = [(root, dataset, p, n_train, n_valid, buffer_size, seed, seg_bytes, verbose)
+            for p in range(unique)]
+    if jobs > 1 and unique > 1:
+        import concurrent.futures as cf
+        import multiprocessing as mp     # spawn: a fork of a process with torch's
+        # intra-op thread pool running deadlocks in the child's first torch op
+        with cf.ProcessPoolExecutor(min(jobs, unique), mp_context=mp.get_context("spawn")) as ex:
+            parts = list(ex.map(_write_one, *zip(*args)))
+    else:
+        parts = [_write_one(*a) for a in args]
+    shapes = {"train": [], "valid": []}
+    for sh in parts:
+        for split in shapes:
+            shapes[split].extend(sh[split])
+    links = {}
+    for p in range(unique, num_partitions):
+        src, dst = seg_dir(root, p % unique), seg_dir(root, p)
+        os.makedirs(dst, exist_ok=True)
+        for f in sorted(os.listdir(src)):
+            if not os.path.exists(os.path.join(dst, f)):
+                os.link(os.path.join(src, f), os.path.join(dst, f))
+        links[str(p)] = p % unique
+        for split in shapes:
+            shapes[split].extend(dict(s, dist_key=p) for s in parts[p % unique][split])
     man = {"dataset": dataset, "num_partitions": num_partitions, "dboid": DBOID,
            "train": {"relfilenode": TRAIN_RELFILENODE, "toast_relfilenode": TRAIN_TOAST},
            "valid": {"relfilenode": VALID_RELFILENODE, "toast_relfilenode": VALID_TOAST},
            "shapes": shapes}
+    if links:
+        man["linked_segments"] = links
     with open(os.path.join(root, MANIFEST), "w") as f:
         json.dump(man, f)
     return man
+
+
+def _write_one(root, dataset, p, n_train, n_valid, buffer_size, seed, seg_bytes, verbose):
+    """One partition's train + valid tables; returns its manifest shapes."""
+    import sys
+    import time
+    from . import synthetic
+    shapes = {"train": [], "valid": []}
+    for split, n, rel, toast in (("train", n_train, TRAIN_RELFILENODE, TRAIN_TOAST),
+                                 ("valid", n_valid, VALID_RELFILENODE, VALID_TOAST)):
+        s = seed * 1000 + 2 * p + (split == "valid")
+        if dataset == "imagenet":
+            x, y = synthetic.image_partition(n, seed=s)
+            x = x.numpy()                     # uint8; float32 per buffer below
+            classes = cat.NUM_CLASSES
+        elif dataset == "criteo":
+            idx, y = synthetic.criteo_partition(n, seed=s)
+            x = np.zeros((n, cat.INPUT_SHAPE_CRITEO[0]), dtype=np.float32)
+            np.put_along_axis(x, idx.numpy().astype(np.int64), 1.0, axis=1)
+            classes = cat.NUM_CLASSES_CRITEO
+        else:
+            raise ValueError(dataset)
+        yy = np.zeros((n, classes), dtype=np.int16)
+        yy[np.arange(n), y.numpy()] = 1
+        for bid, s0 in enumerate(range(0, n, buffer_size)):
+            e = min(n, s0 + buffer_size)
+            shapes[split].append({"dist_key": p, "buffer_id": bid,
+                                  "independent_var_shape": list(x[s0:e].shape),
+                                  "dependent_var_shape": [e - s0, classes]})
+        bufs = ((bid, x[s0:min(n, s0 + buffer_size)].astype(np.float32),
+                 yy[s0:min(n, s0 + buffer_size)])
+                for bid, s0 in enumerate(range(0, n, buffer_size)))
+        nbuf = (n + buffer_size - 1) // buffer_size
+        t0 = time.time()
+
+        def log(i, nb, p=p, split=split, nbuf=nbuf, t0=t0):
+            if verbose:
+                print("  partition {} {}: {}/{} buffers, {:.2f} GB in {:.1f}s".format(
+                    p, split, i, nbuf, nb / 1e9, time.time() - t0), flush=True)
+                sys.stdout.flush()
+        d = seg_dir(root, p)
+        write_partition(os.path.join(d, str(rel)), os.path.join(d, str(toast)), bufs, p,
+                        toastrelid=toast, first_valueid=(p + 1) << 20, seg_bytes=seg_bytes,
+                        log=log)
+    return shapes
 
 
 # ---------------------------------------------------------------------------

@@ -147,6 +147,22 @@ def softmax_ce_fwd(logits, labels, acc, G, need_grad=True):
     return loss, d
 
 
+def softmax_ce_train(logits, labels, acc, G, head_bias=None):
+    """Training-step form (fp32): dlogits + metric accumulators, no loss
+    output (its gradient is a unit seed, ops/loss.py); with ``head_bias``
+    (the ParamRef of the act-free Dense that made the logits) its bias
+    gradient is accumulated here (cer_softmax_ce_f32_head)."""
+    logits = logits.contiguous()
+    B, GN = logits.shape
+    N = GN // G
+    d = torch.empty((B, GN), dtype=torch.float32, device=logits.device)
+    gp, gs = head_bias.grad_ptr() if head_bias is not None else (0, 0)
+    rc = lib().cer_softmax_ce_f32_head(_ptr(logits), _ptr(labels.contiguous()), _ptr(acc),
+                                       _ptr(d), c_p(gp), gs, B, G, N, _stream())
+    _check(rc, "cer_softmax_ce_f32_head")
+    return d
+
+
 _NORM = {}
 
 
@@ -192,7 +208,10 @@ class _StatsArena(object):
 
     def begin(self):
         self.off = 0
-        if self.buf is not None:
+        # eager steps zero here; a captured step relies on the previous
+        # step's optimizer launch, which zeroes the arena at its end
+        # (runtime/group.py, ops.optim._aux) -- one fill kernel less
+        if self.buf is not None and not torch.cuda.is_current_stream_capturing():
             self.buf.zero_()
 
     def take(self, n):
@@ -296,6 +315,8 @@ _SIGS.update({
     "cer_bias_act_fwd": [c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_bias_act_bwd": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_softmax_ce_f32": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
+    "cer_softmax_ce_f32_head": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p],
+    "cer_adam_set_aux": [c_p, c_p, c_i64],
     "cer_conv_dgrad_bnbwd_f32": None,
 })
 _SIGS.pop("cer_conv_dgrad_bnbwd_f32")
@@ -1229,11 +1250,16 @@ def linear_fwd(x, wref, bref, act):
     return y
 
 
-def linear_bwd(dy, x, y, wref, bref, act, need_dx):
+def linear_bwd(dy, x, y, wref, bref, act, need_dx, bias_done=False):
+    """``bias_done``: the bias gradient was accumulated by the loss that
+    consumed this act-free head (softmax_ce_train) -- no bias pass."""
     G = wref.G
     N, K = wref.spec.shape
     B = x.shape[0]
-    dz = bias_act_bwd(dy, y, bref, act) if bref is not None else _act(dy)
+    if bref is not None and not (bias_done and not act):
+        dz = bias_act_bwd(dy, y, bref, act)
+    else:
+        dz = _act(dy)
     xb = _act(x)
     _conv_wgrad_launch(xb, B, 1, 1, K, G, dz, 1, 1, N, 1, 1, 1, 0, wref)
     if not need_dx:

@@ -16,9 +16,22 @@ from .backend import use_hip
 
 class SoftmaxCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, acc, G):
+    def forward(ctx, logits, labels, acc, G, head=None, unit=False):
         B = logits.shape[0]
         N = logits.shape[1] // G
+        ctx.unit = unit
+        if unit and logits.dtype == torch.float32 and use_hip("loss", logits):
+            # training step: the caller seeds a unit gradient and reads the
+            # metrics from ``acc`` -- no loss values, and the head's bias
+            # gradient comes out of this kernel (``head`` = (bias ref, box))
+            from . import _hip
+            dlogits = _hip.softmax_ce_train(logits, labels, acc, G,
+                                            head[0] if head is not None else None)
+            if head is not None:
+                head[1][0] = True
+            ctx.save_for_backward(dlogits)
+            ctx.dtype = logits.dtype
+            return logits.new_empty(G)
         if use_hip("loss", logits):
             from . import _hip
             loss, dlogits = _hip.softmax_ce_fwd(logits, labels, acc, G)
@@ -46,14 +59,22 @@ class SoftmaxCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss):
         dlogits, = ctx.saved_tensors
+        if ctx.unit:                    # dloss is ones by the caller's contract
+            return dlogits.to(ctx.dtype), None, None, None, None, None
         B, GN = dlogits.shape
         G = dloss.shape[0]
         d = dlogits.view(B, G, GN // G) * dloss.view(1, G, 1)
-        return d.reshape(B, GN).to(ctx.dtype), None, None, None
+        return d.reshape(B, GN).to(ctx.dtype), None, None, None, None, None
 
 
-def softmax_ce(logits, labels, acc, G):
-    return SoftmaxCE.apply(logits, labels, acc, G)
+def softmax_ce(logits, labels, acc, G, head=None, unit=False):
+    """Per-config mean CE ``[G]``.  ``unit=True``: the caller back-propagates
+    a gradient of ones (``torch.autograd.backward(loss, ones)``), so the
+    backward returns dlogits as they are; on the fp32 HIP path the returned
+    loss values are then not computed (metrics live in ``acc``).  ``head``:
+    ``logits._cer_head`` of an act-free Dense (ops.nn.PackedLinear) whose
+    bias gradient the loss kernel then accumulates."""
+    return SoftmaxCE.apply(logits, labels, acc, G, head, unit)
 
 
 def eval_metrics(logits, labels, acc, G):

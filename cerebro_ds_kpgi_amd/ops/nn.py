@@ -573,11 +573,16 @@ class PackedLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, wref, bref, relu):
         ctx.wref, ctx.bref, ctx.relu = wref, bref, relu
+        # set by a loss that accumulated this layer's bias gradient itself
+        # (ops.loss.softmax_ce(head=y._cer_head))
+        ctx.head_box = [False]
         G = wref.G
         N, K = wref.spec.shape
         B = x.shape[0]
         if use_hip("linear", x):
             y = _hip().linear_fwd(x, wref, bref, relu)
+            if bref is not None and not relu:
+                y._cer_head = (bref, ctx.head_box)
         else:
             xg = x.view(B, G, K).transpose(0, 1)                       # [G, B, K]
             w = wref.work()                                             # [G, N, K]
@@ -596,7 +601,8 @@ class PackedLinear(torch.autograd.Function):
         wref, bref, relu = ctx.wref, ctx.bref, ctx.relu
         dy = dy.contiguous()
         if use_hip("linear", x):
-            dx = _hip().linear_bwd(dy, x, y, wref, bref, relu, ctx.needs_input_grad[0])
+            dx = _hip().linear_bwd(dy, x, y, wref, bref, relu, ctx.needs_input_grad[0],
+                                   bias_done=ctx.head_box[0])
             return dx, None, None, None, None
         G = wref.G
         N, K = wref.spec.shape

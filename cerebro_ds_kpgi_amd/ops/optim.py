@@ -18,12 +18,30 @@ from .backend import use_hip
 BETA1, BETA2, EPS = 0.9, 0.999, 1e-8
 
 
-def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
+def _aux(cursor, zero):
+    """Side jobs of the HIP optimizer launch (adam.hip cer_adam_set_aux):
+    advance the data ``cursor`` (int32 device scalar) and zero ``zero`` (an
+    fp32 buffer, the step's BN statistics arena) -- two small launches less
+    per step.  Returns True when the HIP launch will do them."""
+    from . import _hip
+    if cursor is None and zero is None:
+        return False
+    if zero is not None and zero.numel() % 4:
+        zero = None
+    _hip.lib().cer_adam_set_aux(_hip._ptr(cursor), _hip._ptr(zero),
+                                _hip.c_i64(zero.numel() if zero is not None else 0))
+    return True
+
+
+def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True, cursor=None, zero=None):
+    """``cursor`` / ``zero`` (HIP path only): see ``_aux``; returns True when
+    they were handled (else the caller advances the cursor itself)."""
     streams.join()
     if use_hip("adam", arena.state):
         from . import _hip
+        done = _aux(cursor, zero)
         _hip.adam_step(arena, beta1, beta2, eps, l2)
-        return
+        return done
     with torch.no_grad():
         arena.step.add_(1.0)
         t = arena.step                                                 # [G, 1]
@@ -39,19 +57,21 @@ def adam_step(arena, beta1=BETA1, beta2=BETA2, eps=EPS, l2=True):
         arena.sync_work()
         if arena.grad_clean:
             arena.grad.zero_()
+    return False
 
 
 SGD_MOMENTUM = 0.9
 
 
-def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
+def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True, cursor=None, zero=None):
     """``torch.optim.SGD(lr, momentum, weight_decay=lambda)``; the momentum
     buffer lives in the arena's first-moment slot."""
     streams.join()
     if use_hip("adam", arena.state):
         from . import _hip
+        done = _aux(cursor, zero)
         _hip.sgd_step(arena, momentum, l2)
-        return
+        return done
     with torch.no_grad():
         arena.step.add_(1.0)
         p, g, m = arena.params, arena.grad, arena.m
@@ -67,10 +87,13 @@ def sgd_step(arena, momentum=SGD_MOMENTUM, l2=True):
         arena.sync_work()
         if arena.grad_clean:
             arena.grad.zero_()
+    return False
 
 
-def optimizer_step(arena, name="adam", l2=True):
+def optimizer_step(arena, name="adam", l2=True, cursor=None, zero=None):
+    """Returns True when the HIP launch also advanced ``cursor`` / zeroed
+    ``zero`` (``_aux``)."""
     streams.join()          # side-stream weight gradients (ops.streams) land first
     if name == "sgd":
-        return sgd_step(arena, l2=l2)
-    return adam_step(arena, l2=l2)
+        return sgd_step(arena, l2=l2, cursor=cursor, zero=zero)
+    return adam_step(arena, l2=l2, cursor=cursor, zero=zero)

@@ -207,6 +207,7 @@ class _Working(object):
         self.part_of_row = torch.zeros(G, dtype=torch.int32, device=g.device)
         self.cursor = torch.zeros(1, dtype=torch.int32, device=g.device)
         self.acc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
+        self.unit_grad = torch.ones(G, dtype=torch.float32, device=g.device)
         self.vx, self.vy = input_buffers(g.store, G, B, g.dtype)
         self.vcursor = torch.zeros(1, dtype=torch.int32, device=g.device)
         self.vacc = torch.zeros(G, 4, dtype=torch.float32, device=g.device)
@@ -292,13 +293,22 @@ class _Working(object):
             streams.set_batch_rows(_WIDE_ROWS if wide else 0)
         with streams.deferred_wgrad(self.x.device.type == "cuda", side_frac=frac, key=id(self)):
             logits = self.net.forward(self.x, True)
-            loss = softmax_ce(logits, self.y, self.acc, self.G)
-            loss.sum().backward()
+            # a unit gradient seed (no loss reduction / fill kernels), and the
+            # head's bias gradient out of the loss kernel (ops.loss)
+            loss = softmax_ce(logits, self.y, self.acc, self.G,
+                              head=getattr(logits, "_cer_head", None), unit=True)
+            if loss.is_cuda:
+                torch.autograd.backward(loss, self.unit_grad)
+            else:               # (measured slower on the CPU autograd path)
+                loss.sum().backward()
         streams.join()
         if self.grad_hook is not None:
             self.grad_hook(self.arena)
-        optimizer_step(self.arena, g.optimizer, l2=g.l2)
-        self.cursor.add_(1)
+        # the optimizer launch also advances the cursor and zeroes the BN
+        # statistics arena for the next step (ops.optim._aux)
+        zero = self.stats_arena.buf if self.stats_arena is not None else None
+        if not optimizer_step(self.arena, g.optimizer, l2=g.l2, cursor=self.cursor, zero=zero):
+            self.cursor.add_(1)
 
     def train_steps(self, nsteps):
         done = 0

@@ -124,6 +124,89 @@ def simulate_packed(policy, n_fast, n_slow, W, V, t_fast, t_slow, b_fast=128, b_
     return now
 
 
+def simulate_classes(policy, classes, W, V, train=TRAIN, valid=VALID, valid_speedup=3.0,
+                     seed=2018, pack_order=True):
+    """General form of ``simulate_packed``: ``classes`` = [{"name", "n",
+    "batch", "t": g -> seconds per packed step of g configs}]; every class
+    is its own pack key (architecture, batch size).  Returns the makespan (s)
+    of one epoch on W GPUs with V partitions each."""
+    import heapq
+    from ..scheduler.policies import GreedyScheduler, RotationScheduler
+    P = W * V
+    cls_of = []
+    for ci, c in enumerate(classes):
+        cls_of += [ci] * int(c["n"])
+    models = list(range(len(cls_of)))
+    parts = list(range(P))
+    gpu_of = {p: p // V for p in parts}
+
+    def pack_seconds(ms):
+        per = {}
+        for m in ms:
+            per[cls_of[m]] = per.get(cls_of[m], 0) + 1
+        t = 0.0
+        for ci, g in per.items():
+            c = classes[ci]
+            t += (train / P / c["batch"]) * c["t"](g) + \
+                (valid / P / c["batch"]) * c["t"](g) / valid_speedup
+        return t
+
+    def key(m):
+        c = classes[cls_of[m]]
+        return (-(train / P / c["batch"]), c["name"])
+
+    if policy == "rotation":
+        sch = RotationScheduler(models, parts, seed=seed)
+        sch.pack_key_fn = key if pack_order else None
+        sch.start_epoch(1)
+        total = 0.0
+        for rnd in sch.rounds:
+            per_gpu = {}
+            for p, m in rnd.items():
+                per_gpu.setdefault(gpu_of[p], []).append(m)
+            total += max((pack_seconds(ms) for ms in per_gpu.values()), default=0.0)
+        return total
+    sch = GreedyScheduler(models, parts, seed=seed, shuffle=True)
+    sch.pack_key_fn = key if pack_order else None
+    sch.start_epoch(1)
+    now, events, busy = 0.0, [], set()
+
+    def dispatch(g):
+        got = sch.assign_many([p for p in range(g * V, (g + 1) * V) if p in sch.idle_workers])
+        jobs = [(m, p) for p, m in got.items()]
+        if jobs:
+            busy.add(g)
+            heapq.heappush(events, (now + pack_seconds([m for m, _ in jobs]), g, jobs))
+    for g in range(W):
+        dispatch(g)
+    while events:
+        now, g, jobs = heapq.heappop(events)
+        busy.discard(g)
+        for m, p in jobs:
+            sch.complete(m, p)
+        for h in range(W):
+            if h not in busy:
+                dispatch(h)
+    if not sch.epoch_done():
+        raise RuntimeError("packed greedy simulation stalled")
+    return now
+
+
+def project_classes(classes, workers=(1, 2, 4, 8), n_partitions=8, seeds=3, valid_speedup=3.0,
+                    train=TRAIN, valid=VALID):
+    """Rotation vs greedy makespans of a class workload (BASELINE config 4,
+    ``--classes``) with the reference's 8 partitions spread over W GPUs."""
+    out = []
+    for W in workers:
+        V = max(1, n_partitions // W)
+        rot = simulate_classes("rotation", classes, W, V, train, valid, valid_speedup)
+        gr = min(simulate_classes("greedy", classes, W, V, train, valid, valid_speedup, seed=s)
+                 for s in range(seeds))
+        out.append({"workers": W, "slots_per_gpu": V, "rotation_s": rot, "greedy_s": gr,
+                    "speedup": rot / gr})
+    return out
+
+
 def project_packed(step_s, workers=(1, 2, 4, 6, 8), V=None, n_fast=38, n_slow=10, seeds=3,
                    valid_speedup=3.0, pack_order=True):
     """Rotation vs greedy hours from MEASURED pack step times
@@ -149,9 +232,9 @@ def project_packed(step_s, workers=(1, 2, 4, 6, 8), V=None, n_fast=38, n_slow=10
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--fast_img_s", type=float, required=True,
+    ap.add_argument("--fast_img_s", type=float, default=0.0,
                     help="MobileNetV2 bs128, one config alone, images/s")
-    ap.add_argument("--slow_img_s", type=float, required=True,
+    ap.add_argument("--slow_img_s", type=float, default=0.0,
                     help="NASNetMobile bs4, one config alone, images/s")
     ap.add_argument("--valid_speedup", type=float, default=3.0)
     ap.add_argument("--packed", default="",
@@ -161,7 +244,29 @@ def main(argv=None):
     ap.add_argument("--slots_per_gpu", type=int, default=0)
     ap.add_argument("--pack_order", default="true", choices=["true", "false"],
                     help="the engine's pack-aware scheduling order (default) or the policies' own")
+    ap.add_argument("--classes", default="",
+                    help="generic class workload, ';'-separated 'name,n,batch,t1,tg,g' (pack "
+                         "step seconds at 1 and g configs), e.g. BASELINE config 4: "
+                         "resnet50_b32,2,32,...;vgg16_b64,2,64,... (fast / slow ignored)")
+    ap.add_argument("--partitions", type=int, default=8)
+    ap.add_argument("--train_images", type=int, default=TRAIN)
     a = ap.parse_args(argv)
+    if a.classes:
+        classes = []
+        for item in a.classes.split(";"):
+            f = item.split(",")
+            classes.append({"name": f[0], "n": int(f[1]), "batch": int(f[2]),
+                            "t": _pack_time(float(f[3]), float(f[4]), int(f[5]))})
+        rows = project_classes(classes, n_partitions=a.partitions, valid_speedup=a.valid_speedup,
+                               train=a.train_images,
+                               valid=int(a.train_images * VALID / TRAIN))
+        print("| workers | slots / GPU | rotation (UDAF) s | greedy (CTQ) s | rotation / greedy |")
+        print("|---:|---:|---:|---:|---:|")
+        for r in rows:
+            print("| {} | {} | {:.1f} | {:.1f} | {:.2f}x |".format(
+                r["workers"], r["slots_per_gpu"], r["rotation_s"], r["greedy_s"], r["speedup"]))
+        print(json.dumps(rows))
+        return rows
     if a.packed:
         f = [float(x) for x in a.packed.split(",")]
         rows = project_packed({"fast": (f[0], f[1], int(f[2])), "slow": (f[3], f[4], int(f[5]))},

@@ -22,9 +22,14 @@ def main(argv=None):
     ap.add_argument("--train", type=int, default=cat.IMAGENET_COUNT_PER_PAR)
     ap.add_argument("--valid", type=int, default=cat.IMAGENET_VALID_TOTAL // 8)
     ap.add_argument("--buffer_size", type=int, default=cat.TRAIN_BUFFER_SIZE)
+    ap.add_argument("--unique", type=int, default=0,
+                    help="generate only this many partitions; the rest are hard links to "
+                         "them (for a disk smaller than the whole dataset)")
+    ap.add_argument("--jobs", type=int, default=1, help="partitions generated concurrently")
     a = ap.parse_args(argv)
     t = time.time()
-    da.write_dataset(a.root, a.dataset, a.partitions, a.train, a.valid, a.buffer_size, verbose=True)
+    da.write_dataset(a.root, a.dataset, a.partitions, a.train, a.valid, a.buffer_size,
+                     verbose=True, unique=a.unique or None, jobs=a.jobs)
     print("wrote {} partitions to {} in {:.1f}s".format(a.partitions, a.root, time.time() - t))
 
 

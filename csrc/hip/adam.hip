@@ -13,9 +13,34 @@
 // without a memset per layer.
 #include "common.h"
 
-__global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G) {
+// + the group's data cursor (the next step's batch, runtime/group.py), so the
+// step's tail is one small launch instead of two
+__global__ void adam_inc_step(float* state, int64_t row_stride, int64_t off_step, int G,
+                              int* cursor) {
   int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < G) state[g * row_stride + off_step] += 1.0f;
+  if (cursor && g == 0) cursor[0] += 1;
+}
+
+// Side jobs of the NEXT optimizer launch (cer_adam_set_aux; cleared by it):
+// the data cursor to advance, and a buffer to zero -- the BN statistics
+// arena of the step (ops/_hip.py _StatsArena), zeroed here at the end of a
+// step for the next one instead of by a fill kernel at its start.
+static int* g_aux_cursor = nullptr;
+static float* g_aux_zero = nullptr;
+static int64_t g_aux_zero_n = 0;
+CER_API void cer_adam_set_aux(int* cursor, float* zero, int64_t zero_n) {
+  g_aux_cursor = cursor;
+  g_aux_zero = zero;
+  g_aux_zero_n = zero ? zero_n : 0;
+}
+
+// grid-stride share of blocks (x, 0) in zeroing n floats (n % 4 == 0)
+__device__ __forceinline__ void aux_zero(float* z, int64_t n) {
+  if (!z || blockIdx.y != 0) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; k < n; k += stride)
+    *reinterpret_cast<float4*>(z + k) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // WRITE_BF16: also write the bf16 compute shadow of the params (bf16 mode);
@@ -25,7 +50,9 @@ __global__ __launch_bounds__(256) void adam_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
-    const float* __restrict__ wd, float b1, float b2, float eps, int l2) {
+    const float* __restrict__ wd, float b1, float b2, float eps, int l2, float* zero,
+    int64_t zero_n) {
+  aux_zero(zero, zero_n);
   const int g = blockIdx.y;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (i >= n_train) return;
@@ -77,17 +104,21 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
                           int zero_grad, bf16_t* work, int64_t work_stride, const float* lr,
                           const float* wd, int G, float b1, float b2, float eps, int l2,
                           hipStream_t stream) {
-  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
-  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
+                                                      g_aux_cursor);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
   if (work)
     adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
                                                  off_step, grad, grad_stride, zero_grad, work,
-                                                 work_stride, lr, wd, b1, b2, eps, l2);
+                                                 work_stride, lr, wd, b1, b2, eps, l2, g_aux_zero,
+                                                 g_aux_zero_n);
   else
     adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
                                                   off_step, grad, grad_stride, zero_grad, nullptr,
-                                                  0, lr, wd, b1, b2, eps, l2);
+                                                  0, lr, wd, b1, b2, eps, l2, g_aux_zero,
+                                                  g_aux_zero_n);
+  cer_adam_set_aux(nullptr, nullptr, 0);
   return (int)hipGetLastError();
 }
 
@@ -101,7 +132,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
-    const float* __restrict__ wd, float mu, int l2) {
+    const float* __restrict__ wd, float mu, int l2, float* zero, int64_t zero_n) {
+  aux_zero(zero, zero_n);
   const int g = blockIdx.y;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
   if (i >= n_train) return;
@@ -144,15 +176,18 @@ CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int6
                          bf16_t* work, int64_t work_stride, const float* lr, const float* wd,
                          int G, float momentum, int l2, hipStream_t stream) {
   if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
-  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G);
+  if (g_aux_zero_n % 4 != 0) return (int)hipErrorInvalidValue;
+  adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
+                                                      g_aux_cursor);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
   if (work)
     sgd_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step, grad,
                                                grad_stride, zero_grad, work, work_stride, lr, wd,
-                                               momentum, l2);
+                                               momentum, l2, g_aux_zero, g_aux_zero_n);
   else
     sgd_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step,
                                                 grad, grad_stride, zero_grad, nullptr, 0, lr, wd,
-                                                momentum, l2);
+                                                momentum, l2, g_aux_zero, g_aux_zero_n);
+  cer_adam_set_aux(nullptr, nullptr, 0);
   return (int)hipGetLastError();
 }

@@ -3264,6 +3264,102 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   }
 }
 
+// LDS-DMA ring wgrad body for HL operands (profiles/r4_ws.md
+// "what the measurements point to"): dy and x are both already split into
+// (hi, lo) bf16 pairs in HBM (HL format: per 8 channels 16 B of hi, then
+// 16 B of lo), so a stage needs no VGPR staging, no split VALU and no
+// ds_write -- every 16-B chunk goes global -> LDS by buffer_load ... lds
+// straight into the register body's LDS image ([64 rows][COLS]: rows 0-31
+// the hi halves of the stage's 32 reduction rows, rows 32-63 the lo halves,
+// tn_off swizzle), which mma3_tn reads unchanged.  Lane i of a DMA
+// instruction fills 16-B slot (i % 16) of image row (base + i / 16); the
+// slot's chunk is column group tn_col16(row, slot), half (row >> 5).  An
+// S-stage ring (ring_loop) keeps S - 1 stages in flight.  Padding taps and
+// rows past the split's range load from out-of-range offsets: zeros.
+template <int BM, int BN, int S>
+__device__ __forceinline__ void wgrad_ring_body32(const WGParams& p, int work, bf16_t* lds) {
+  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int AROWS = 512 / BM, AC16 = BM / 8, BROWS = 512 / BN, BC16 = BN / 8;
+  const int tiles_k = (p.K + BN - 1) / BN;
+  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
+  const int cfg = work / (tiles * p.splits);
+  const int rem = work - cfg * tiles * p.splits;
+  const int split = rem / tiles, tile = rem - split * tiles;
+  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
+  const int n0 = tn_ * BM, k0 = tk * BN;
+  const int ms = split * p.m_per_split;
+  const int me = min(p.Mred, ms + p.m_per_split);
+  if (ms >= me) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wid >> 1, wb = wid & 1;
+  const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
+  const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
+  const auto rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
+  const auto rX = make_rsrc(xb, p.x.bytes);
+  int arow[AJ];
+  uint32_t aoff[AJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    arow[j] = (wid * AJ + j) * AROWS + lane / AC16;          // image row 0..63
+    const int n = n0 + 8 * tn_col16<BM>(arow[j], lane % AC16);
+    aoff[j] = n < p.N ? ((uint32_t)((arow[j] & 31) * p.ldy + n) * 4u + 16u * (arow[j] >> 5))
+                      : OOB;
+  }
+  int brow[BJ];
+  KPos bk[BJ];
+  bool bok[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    brow[j] = (wid * BJ + j) * BROWS + lane / BC16;
+    const int k = k0 + 8 * tn_col16<BN>(brow[j], lane % BC16);
+    bok[j] = k < p.K;
+    bk[j] = kpos_init(p.x, bok[j] ? k : 0);
+  }
+  auto issue = [&](int mt, int st) {
+    bf16_t* sa = lds + st * STAGE;
+    bf16_t* sb = sa + BM * BK;
+    const int mbase = ms + mt * KS, lim = me - mbase;
+    const uint32_t so = (uint32_t)mbase * (uint32_t)p.ldy * 4u;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j)
+      glds16(rDY, sa + (wid * AJ + j) * 512, (arow[j] & 31) < lim ? aoff[j] : OOB, so);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const RowA ra = row_init<GM_FWD>(p.x, mbase + (brow[j] & 31), me);
+      const uint32_t off = a_off<GM_FWD, 4>(p.x, ra, bk[j].r, bk[j].s, bk[j].c);
+      glds16(rX, sb + (wid * BJ + j) * 512, bok[j] ? off + 16u * (uint32_t)(brow[j] >> 5) : OOB,
+             0);
+    }
+  };
+  f32x4 acc[BM / 32][BN / 32];
+  zero_acc<BM, BN>(acc);
+  ring_loop<S, LPW>((me - ms + KS - 1) / KS, issue, [&](int st) {
+    mma3_tn<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wa, wb, lane, acc);
+  });
+  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
+  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
+  const int fr = lane & 15, fc = lane >> 4;
+  const bool split_k = p.splits > 1;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wa * TM + 16 * i + 4 * fc + e;
+        const int k = k0 + wb * TN + 16 * j + fr;
+        if (n < p.N && k < p.K) {
+          float* d = dwb + (int64_t)n * p.K + k;
+          if (split_k)
+            atomicAdd(d, acc[i][j][e]);
+          else
+            *d = acc[i][j][e];
+        }
+      }
+}
+
 template <int BM, int BN, int GM, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
@@ -3286,6 +3382,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
     while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     const WGParams p = b.p[i];
     wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
+    if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
+  }
+}
+
+// batched fp32 weight gradients, LDS-DMA ring twin (CER_WGB_RING = S stages):
+// items whose dy and x are both HL take wgrad_ring_body32, the others the
+// register body (same LDS image, so one kernel serves a mixed batch)
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32r(WGBatch b) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[S * (BM + BN) * BK];
+  const int total = b.start[b.n];
+  const int nwg = (int)gridDim.x;
+  for (int w = blockIdx.x; w < total; w += nwg) {
+    const int work = nwg >= total ? xcd_remap(w, nwg) : w;
+    int i = 0;
+    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
+    const WGParams p = b.p[i];
+    if (p.x_hl && p.dy_hl)
+      wgrad_ring_body32<BM, BN, S>(p, work - b.start[i], lds);
+    else
+      wgrad_reg_body32<BM, BN, GM_FWD>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
   }
 }
@@ -4460,6 +4577,18 @@ static bool wgb_ws() {
 }
 CER_API void cer_wgrad_batch_set_ws(int on) { g_wgb_ws = on ? 1 : 0; }
 
+// LDS-DMA ring for the HL items of fp32 batches: stages (0 = off;
+// CER_WGB_RING; 3 stages only for tiles up to 128x64: 2 workgroups per CU)
+static int g_wgb_ring = -1;
+static int wgb_ring() {
+  if (g_wgb_ring < 0) {
+    const char* e = getenv("CER_WGB_RING");
+    g_wgb_ring = e ? atoi(e) : 0;
+  }
+  return g_wgb_ring;
+}
+CER_API void cer_wgrad_batch_set_ring(int stages) { g_wgb_ring = stages > 0 ? stages : 0; }
+
 // grid cap of the next fp32 batch flushes (0 = one block per work item)
 static int g_wgb_grid = 0;
 CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
@@ -4482,6 +4611,10 @@ static void wgb32_launch_sel(hipStream_t stream) {
     if (tot <= 0) continue;
     if (BM == 128 && BN == 128 && wgb_ws())
       wgrad_ws32<128, 128><<<grid, WS_THREADS, 0, stream>>>(bt);
+    else if (!WIDE && wgb_ring() == 2)
+      wgrad_batch32r<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(bt);
+    else if (!WIDE && wgb_ring() == 3 && BM * BN <= 128 * 64)
+      wgrad_batch32r<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(bt);
     else
       wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
   }

@@ -22,7 +22,8 @@ constexpr int CE_MAXPER = 8;  // N <= 2048
 template <typename T, typename TD>
 __global__ __launch_bounds__(CE_THREADS) void softmax_ce_kernel(
     const T* __restrict__ logits, const int* __restrict__ labels, float* __restrict__ acc,
-    float* __restrict__ loss_out, TD* __restrict__ dlogits, int B, int G, int N) {
+    float* __restrict__ loss_out, TD* __restrict__ dlogits, int B, int G, int N,
+    float* __restrict__ dbias = nullptr, int64_t dbias_stride = 0) {
   __shared__ float smem[16];
   const int b = blockIdx.x, g = blockIdx.y;
   const int64_t base = (int64_t)b * G * N + (int64_t)g * N;
@@ -56,7 +57,11 @@ __global__ __launch_bounds__(CE_THREADS) void softmax_ce_kernel(
       int j = threadIdx.x + k * CE_THREADS;
       if (j < N) {
         float p = __expf(z[k] - mx) * inv_se;
-        st1(dlogits + base + j, (p - (j == lab ? 1.f : 0.f)) * inv_b);
+        const float d = (p - (j == lab ? 1.f : 0.f)) * inv_b;
+        st1(dlogits + base + j, d);
+        // the head linear's bias gradient (sum over the batch of dlogits),
+        // accumulated into the zeroed gradient arena (cer_softmax_ce_f32_head)
+        if (dbias) atomicAdd(dbias + (int64_t)g * dbias_stride + j, d);
       }
     }
   }
@@ -94,5 +99,20 @@ CER_API int cer_softmax_ce_f32(const float* logits, const int* labels, float* ac
   softmax_ce_kernel<float, float><<<dim3(B, G), CE_THREADS, 0, stream>>>(logits, labels, acc,
                                                                           loss_out, dlogits, B, G,
                                                                           N);
+  return (int)hipGetLastError();
+}
+
+// training step form: no per-config loss output (the engine reads the
+// metric accumulators; the backward seeds a unit gradient), and the bias
+// gradient of the head linear that produced the logits (an act-free Dense:
+// d bias = sum_b dlogits) added into ``dbias`` (config stride dbias_stride,
+// zeroed: the optimizer clears the gradient it consumes), so the linear's
+// backward needs no bias pass
+CER_API int cer_softmax_ce_f32_head(const float* logits, const int* labels, float* acc,
+                                    float* dlogits, float* dbias, int64_t dbias_stride, int B,
+                                    int G, int N, hipStream_t stream) {
+  if (N > CE_THREADS * CE_MAXPER) return (int)hipErrorInvalidValue;
+  softmax_ce_kernel<float, float><<<dim3(B, G), CE_THREADS, 0, stream>>>(
+      logits, labels, acc, nullptr, dlogits, B, G, N, dbias, dbias_stride);
   return (int)hipGetLastError();
 }

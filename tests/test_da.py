@@ -212,3 +212,23 @@ def test_loader_reused_for_two_windows(tmp_path):
     loader.prefetch([1])
     tx, ty, vx, vy = loader(1)
     assert tx.shape[0] == 6 and first[0].shape[0] == 6
+
+
+def test_linked_segments_and_parallel_writer(tmp_path):
+    """``unique``: segments past it are hard links to the generated ones
+    (read back as separate partitions); ``jobs`` > 1 writes the same bytes
+    as the serial writer."""
+    import torch
+    serial, par = str(tmp_path / "s"), str(tmp_path / "p")
+    da.write_dataset(serial, "imagenet", 3, n_train=7, n_valid=3, buffer_size=4)
+    man = da.write_dataset(par, "imagenet", 3, n_train=7, n_valid=3, buffer_size=4,
+                           unique=2, jobs=2)
+    assert man["linked_segments"] == {"2": 0}
+    for f in os.listdir(da.seg_dir(par, 2)):
+        a, b = (os.stat(os.path.join(da.seg_dir(par, q), f)) for q in (0, 2))
+        assert a.st_ino == b.st_ino
+    assert len(man["shapes"]["train"]) == 6 and {s["dist_key"] for s in man["shapes"]["train"]} == {0, 1, 2}
+    ls, lp = da.da_partition_loader(serial, "cpu"), da.da_partition_loader(par, "cpu")
+    for q in (0, 1):
+        assert all(torch.equal(a, b) for a, b in zip(ls(q), lp(q)))
+    assert all(torch.equal(a, b) for a, b in zip(lp(0), lp(2)))
