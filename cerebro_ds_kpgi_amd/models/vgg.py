@@ -51,15 +51,23 @@ class PackedVGG16(PackedNet):
     def _init_specs(self):
         pass
 
+    # the block's max pool finishes its last conv's ReLU / bias backward
+    # (MaxPoolHip + BiasActLink); VGG16Flat's SAME pools pad, so not there
+    _pool_links = True
+
     def _pool(self, x):
         return P.maxpool2d(x, 2, 2, 0)
 
     def forward(self, x, training):
         first = True
         for blk in self.convs:
-            for conv, bias in blk:
+            for li, (conv, bias) in enumerate(blk):
+                # a conv's output feeds only the next conv (whose dgrad epilogue
+                # then applies its ReLU' and bias gradient) or, last in the
+                # block, only the max pool (whose backward does)
                 x = P.conv2d_bias_act(x, self.ref(conv.w), self.ref(bias), conv.stride, conv.pad,
-                                      act=1, anchor=self.anchor if first else None)
+                                      act=1, anchor=self.anchor if first else None,
+                                      link_out=li + 1 < len(blk) or self._pool_links)
                 first = False
             x = self._pool(x)
             nxt = self.convs.index(blk) + 1

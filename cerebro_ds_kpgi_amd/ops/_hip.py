@@ -274,6 +274,7 @@ _SIGS.update({
     "cer_conv_set_addend_grid": [c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
+    "cer_conv_dgrad_babwd": [c_p, c_i64, c_p, c_i, c_p],
     "cer_bn_bwd_part": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p,
                         c_p, c_p, c_p, c_i, c_i64, c_i, c_i, c_i, c_p],
     "cer_wgrad_batch_add": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
@@ -294,11 +295,12 @@ _SIGS.update({
     "cer_conv_stats_floats": [c_i64, c_i],
     "cer_stem_ok": [c_i, c_i, c_i, c_i, c_i],
     "cer_bn_apply_fwd": [c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i64, c_i, c_i, c_i, c_p],
-    "cer_stem_wpk_elems": [c_i, c_i, c_i, c_i],
+    "cer_stem_wpk_elems": [c_i, c_i, c_i, c_i, c_i],
+    "cer_stem_cp": [c_i],
     "cer_stem_fwd": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
-                     c_p, c_i, c_i, c_p, c_p, c_p],
-    "cer_stem_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p,
-                       c_i64, c_p],
+                     c_p, c_i, c_i, c_p, c_p, c_p, c_i64, c_i, c_p],
+    "cer_stem_wgrad": [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p,
+                       c_p, c_i64, c_p],
     "cer_bn_fwd_train_part": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
                               c_p, c_p, c_i, c_i64, c_i, c_i, c_f, c_f, c_i, c_p],
     "cer_bn_fwd_train": [c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p, c_p,
@@ -308,7 +310,9 @@ _SIGS.update({
     "cer_bn_bwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p,
                    c_p, c_p,
                    c_i64, c_i, c_i, c_i, c_p],
-    "cer_maxpool_fwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "cer_maxpool_fwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
+    "cer_maxpool_bwd_relu_bias": [c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                                  c_i, c_i, c_i, c_p],
     "cer_maxpool_bwd": [c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p],
     "cer_gavgpool_fwd": [c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_gavgpool_bwd": [c_p, c_p, c_i, c_i, c_i, c_p],
@@ -630,10 +634,10 @@ def conv2d_fwd(x, wref, stride, pad, bref=None, act=0):
     assert GC == G * cin, (x.shape, wref.spec.shape, G)
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
-    if bref is None and act == 0 and stem_ok(x, wref, stride, pad):
-        # narrow-input stem (e.g. ResNet's 7x7/2 on RGB in validation): the
-        # pixel-pair MFMA path instead of the element-gather fallback
-        return stem_fwd_stats(x, wref, stride, pad)[0]
+    if stem_ok(x, wref, stride, pad):
+        # narrow-input stem (ResNet's 7x7/2 on RGB in validation, VGG's
+        # 3x3/1): the repacked MFMA path instead of the element-gather fallback
+        return stem_fwd_stats(x, wref, stride, pad, bref, act, stats=False)[0]
     y = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
@@ -715,14 +719,16 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     wp, wstr = wref.work_ptr()
     nslab = ctypes.c_int(0)
     if stem:
-        x4 = torch.empty((G, B, H, W, 4), dtype=x.dtype, device=dev)
-        wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
+        mode = stem_mode(x, wref, stride, pad)
+        x4 = torch.empty((G, B, H, W, int(L.cer_stem_cp(mode))), dtype=x.dtype, device=dev)
+        wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=x.dtype,
                           device=dev)
 
         def launch():        # conv + BN statistics partials (no running-stat side effects)
             _check(_fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                       stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
-                                      _ptr(part), ctypes.byref(nslab), _stream()), "cer_stem_fwd")
+                                      _ptr(part), ctypes.byref(nslab), None, 0, 0, _stream()),
+                   "cer_stem_fwd")
         _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype,
                 after_tune=part.zero_)
         launch()
@@ -741,14 +747,21 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
                          momentum, eps, hl_out=hl_out and hl_ok(z)) + (None,)
 
 
-def stem_ok(x, wref, stride, pad):
-    """Narrow-input stem eligible for the pixel-pair path (cer_stem_fwd)."""
+def stem_mode(x, wref, stride, pad):
+    """conv.hip STEM_*: 2 = pixel pairs (Cin <= 4, stride 2), 1 = channels
+    padded to 8 (Cin < 8, stride 1), 0 = not a narrow-input stem."""
     cout, kh, kw, cin = wref.spec.shape
-    return bool(lib().cer_stem_ok(cin, x.shape[2], kw, stride, pad))
+    return int(lib().cer_stem_ok(cin, x.shape[2], kw, stride, pad))
 
 
-def stem_fwd_stats(x, wref, stride, pad):
-    """Stem conv via the repacked pixel-pair geometry, with BN partials.
+def stem_ok(x, wref, stride, pad):
+    """Narrow-input first layer eligible for the repacked stem path (cer_stem_fwd)."""
+    return stem_mode(x, wref, stride, pad) != 0
+
+
+def stem_fwd_stats(x, wref, stride, pad, bref=None, act=0, stats=True):
+    """Stem conv via the repacked geometry (pixel pairs or 8-channel pixels),
+    with BN partials (``stats``) or bias + activation in the epilogue.
     Returns (z, part, nslab, x4) — x4 (the repacked input) feeds the wgrad."""
     x = _act(x)
     B, H, W, GC = x.shape
@@ -756,41 +769,45 @@ def stem_fwd_stats(x, wref, stride, pad):
     cout, kh, kw, cin = wref.spec.shape
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
+    mode = stem_mode(x, wref, stride, pad)
     z = torch.empty((B, Ho, Wo, G * cout), dtype=x.dtype, device=x.device)
-    x4 = torch.empty((G, B, H, W, 4), dtype=x.dtype, device=x.device)
     L = lib()
-    wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=x.dtype,
+    x4 = torch.empty((G, B, H, W, int(L.cer_stem_cp(mode))), dtype=x.dtype, device=x.device)
+    wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=x.dtype,
                       device=x.device)
-    part = _stats_buffer(B * Ho * Wo, G * cout, x.device)
+    part = _stats_buffer(B * Ho * Wo, G * cout, x.device) if stats else None
     nslab = ctypes.c_int(0)
     wp, ws = wref.work_ptr()
+    bp, bs = bref.work_ptr() if bref is not None else (0, 0)
 
     def launch():
         rc = _fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
                                 _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
-                                ctypes.byref(nslab), _stream())
+                                ctypes.byref(nslab), c_p(bp), bs, _act_code(act), _stream())
         _check(rc, "cer_stem_fwd")
-    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, x.dtype,
-            after_tune=part.zero_)
+    _select(0, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G, stats, bref is not None,
+                _act_code(act)), launch, x.dtype,
+            after_tune=part.zero_ if part is not None else None)
     launch()
     return z, part, nslab.value, x4
 
 
-def stem_wgrad(x4, dy, wref, pad):
+def stem_wgrad(x4, dy, wref, pad, stride=2):
     dy = _same(dy, x4)
     G, B, H, W, _ = x4.shape
     _, Ho, Wo, _ = dy.shape
     cout, kh, kw, cin = wref.spec.shape
     L = lib()
-    dwp = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw)), dtype=torch.float32,
+    mode = int(L.cer_stem_ok(cin, W, kw, stride, pad))
+    dwp = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=torch.float32,
                       device=dy.device)
     gp, gs = wref.grad_ptr()
 
     def launch():
-        rc = _fn("cer_stem_wgrad", x4)(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw, pad,
-                                  _ptr(dwp), c_p(gp), gs, _stream())
+        rc = _fn("cer_stem_wgrad", x4)(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw,
+                                  stride, pad, _ptr(dwp), c_p(gp), gs, _stream())
         _check(rc, "cer_stem_wgrad")
-    _select(2, ("stem", B, H, W, cin, cout, kh, kw, pad, G), launch, dy.dtype)
+    _select(2, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, dy.dtype)
     launch()
 
 
@@ -826,7 +843,8 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
     launch()
 
 
-def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consume_addend=False):
+def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consume_addend=False,
+                 balink=None):
     """dx of the conv; ``addend`` (same shape and dtype as dx) is added in the
     GEMM epilogue (the other consumer's gradient of a shared input).
     ``consume_addend=True`` (only ops.nn's GradJoin passes it: it owns the
@@ -835,11 +853,48 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
     ``bnlink`` = (link, y): dx is the input gradient of the BatchNorm whose
     output y this conv consumed — the epilogue also computes that BN's
     backward partials into ``link.part`` / ``link.nslab`` (ops.nn.BNLink).
-    ``dy`` may be HL (read as such)."""
+    ``balink`` (ops.nn.BiasActLink): dx is the output gradient of a conv +
+    bias + activation layer (its output y is this conv's input); if the
+    epilogue can apply it (fp32, aligned, stride 1, no addend) dx comes back
+    as dz = act'(y) * dx with the bias gradient accumulated, and
+    ``balink.done`` is set.  ``dy`` may be HL (read as such)."""
     dy_hl = is_hl(dy)
     with _hl_operands(0, dy_hl):
+        if balink is not None and addend is None and bnlink is None:
+            return _conv2d_dgrad_balink(_act(dy, hl_ok=dy_hl), wref, xshape, stride, pad, balink,
+                                        dy_hl)
         return _conv2d_dgrad(_act(dy, hl_ok=dy_hl), wref, xshape, stride, pad, addend, bnlink,
                              consume_addend, dy_hl)
+
+
+def _conv2d_dgrad_balink(dy, wref, xshape, stride, pad, balink, dy_hl):
+    B, Ho, Wo, _ = dy.shape
+    _, H, W, _ = xshape
+    G = wref.G
+    cout, kh, kw, cin = wref.spec.shape
+    wp, ws = wref.work_ptr()
+    link, y = balink
+    bref = link.bref
+    link.done = False
+    if y.dtype != torch.float32 or is_hl(y):
+        return _conv2d_dgrad(dy, wref, xshape, stride, pad, None, None, False, dy_hl)
+    dx = torch.empty((B, H, W, G * cin), dtype=dy.dtype, device=dy.device)
+    if not bref.arena.grad_clean:
+        bref.grad().zero_()           # the epilogue accumulates into it
+    gp, gs = bref.grad_ptr()
+    done = ctypes.c_int(0)
+    L = lib()
+    L.cer_conv_dgrad_babwd(c_p(gp), gs, _ptr(_same(y, dy)), _act_code(link.act),
+                           ctypes.byref(done))
+    try:
+        # the timing launches of the autotune add into the bias gradient too
+        _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad, dx, H, W,
+                           None, bnstats="bias", wref=wref, after_tune=bref.grad().zero_,
+                           dy_hl=dy_hl)
+    finally:
+        L.cer_conv_dgrad_babwd(None, 0, None, 0, None)
+    link.done = done.value > 0
+    return dx
 
 
 def _conv2d_dgrad(dy, wref, xshape, stride, pad, addend, bnlink, consume_addend, dy_hl):
@@ -1169,7 +1224,9 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
 # ---------------------------------------------------------------------------
 # pooling / bias+act (csrc/hip/pool.hip)
 # ---------------------------------------------------------------------------
-def maxpool_fwd(x, k, s, p):
+def maxpool_fwd(x, k, s, p, relu_bit=False):
+    """``relu_bit``: also mark in each argmax byte whether the window max is
+    > 0 (for maxpool_bwd_relu_bias; C % 8 == 0, k*k <= 128)."""
     x = _act(x)
     B, H, W, C = x.shape
     Ho = (H + 2 * p - k) // s + 1
@@ -1177,7 +1234,7 @@ def maxpool_fwd(x, k, s, p):
     y = torch.empty((B, Ho, Wo, C), dtype=x.dtype, device=x.device)
     arg = torch.empty((B, Ho, Wo, C), dtype=torch.uint8, device=x.device)
     rc = _fn("cer_maxpool_fwd", x)(_ptr(x), _ptr(y), _ptr(arg), B, H, W, C, Ho, Wo, k, s, p,
-                               _stream())
+                               1 if relu_bit else 0, _stream())
     _check(rc, "cer_maxpool_fwd")
     return y, (arg, k, s, p)
 
@@ -1190,6 +1247,30 @@ def maxpool_bwd(dy, saved, xshape):
     rc = _fn("cer_maxpool_bwd", dy)(_ptr(_act(dy)), _ptr(arg), _ptr(dx), B, H, W, C, Ho, Wo, k, s, p,
                                _stream())
     _check(rc, "cer_maxpool_bwd")
+    return dx
+
+
+def maxpool_relu_bias_ok(x, k, bref, act):
+    """The pool's input is a ReLU conv + bias output this pass can finish."""
+    return (x.dtype == torch.float32 and x.shape[-1] % 8 == 0 and bref.spec.shape[0] % 8 == 0
+            and k * k <= 128 and _act_code(act) == 1 and not is_hl(x))
+
+
+def maxpool_bwd_relu_bias(dy, saved, xshape, bref):
+    """dz of the ReLU conv + bias layer under the pool (its ReLU' applied) and
+    that layer's bias gradient, in one pass (pool.hip
+    maxpool_bwd_relu_bias_kernel; the forward ran with relu_bit)."""
+    arg, k, s, p = saved
+    B, H, W, C = xshape
+    _, Ho, Wo, _ = dy.shape
+    dx = torch.empty((B, H, W, C), dtype=dy.dtype, device=dy.device)
+    if not bref.arena.grad_clean:
+        bref.grad().zero_()
+    gp, gs = bref.grad_ptr()
+    rc = _fn("cer_maxpool_bwd_relu_bias", dy)(_ptr(_act(dy)), _ptr(arg), _ptr(dx), c_p(gp), gs,
+                                              bref.spec.shape[0], B, H, W, C, Ho, Wo, k, s, p,
+                                              _stream())
+    _check(rc, "cer_maxpool_bwd_relu_bias")
     return dx
 
 

@@ -139,6 +139,23 @@ class BNLink(object):
         self.act, self.has_res, self.part, self.nslab = 0, False, None, 0
 
 
+# CER_BIAS_LINKS=0: every conv + bias + activation layer runs its own bias_act_bwd
+BIAS_LINKS = os.environ.get("CER_BIAS_LINKS", "1") != "0"
+
+
+class BiasActLink(object):
+    """Forward-time handle from a conv + bias + activation output y to the
+    conv that is its SOLE consumer (``y._cer_balink``; VGG's conv -> conv).
+    In backward the consumer's dgrad output is y's whole gradient, so its
+    epilogue applies act'(y) and accumulates the bias gradient
+    (``conv2d_dgrad(balink=...)``, conv.hip YM_BIAS); ``done`` then tells the
+    producer's backward to skip its bias_act_bwd pass."""
+    __slots__ = ("bref", "act", "done")
+
+    def __init__(self, bref, act):
+        self.bref, self.act, self.done = bref, act, False
+
+
 def _bnlink_for(ctx, x, join, addend):
     """(link, y) when this conv's dx will be the full input gradient of a linked BN."""
     link = getattr(ctx, "bnlink", None)
@@ -155,6 +172,7 @@ class PackedConv2d(torch.autograd.Function):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join = None
         ctx.bnlink = getattr(x, "_cer_bnlink", None)
+        ctx.balink = getattr(x, "_cer_balink", None)
         y = _conv_forward(x, wref, stride, pad)
         ctx.save_for_backward(x)
         return y
@@ -177,8 +195,10 @@ class PackedConv2d(torch.autograd.Function):
                 bnl = _bnlink_for(ctx, x, join, addend)
                 if addend is not None:
                     join = None
+                bal = getattr(ctx, "balink", None) if join is None and addend is None else None
                 dx = h.conv2d_dgrad(dy, wref, x.shape, stride, pad, addend=addend, bnlink=bnl,
-                                    consume_addend=addend is not None)
+                                    consume_addend=addend is not None,
+                                    balink=None if bal is None else (bal, x))
             # off the critical path: overlaps the dgrad chain below (ops.streams);
             # issued before a park, so the event the other consumer waits on
             # also orders this stream's wgrad (a branch-stream backward launched
@@ -208,10 +228,20 @@ class PackedConvBiasAct(torch.autograd.Function):
     fused into the HIP GEMM epilogue (one bf16 rounding, no extra pass)."""
 
     @staticmethod
-    def forward(ctx, x, anchor, wref, bref, stride, pad, act):
+    def forward(ctx, x, anchor, wref, bref, stride, pad, act, link=None):
         ctx.wref, ctx.bref, ctx.stride, ctx.pad, ctx.act = wref, bref, stride, pad, act
+        ctx.join = None
+        ctx.bnlink = None
+        ctx.balink = getattr(x, "_cer_balink", None)    # x: a linked layer's output
+        ctx.link = link                                 # this layer's own output
+        ctx.x4 = None
         if use_hip("conv", x) and use_hip("bias", x):
-            y = _hip().conv2d_fwd(x, wref, stride, pad, bref, act)
+            h = _hip()
+            if not x.requires_grad and h.stem_ok(x, wref, stride, pad):
+                # narrow first layer (VGG's 3x3/1 on RGB): repacked input, kept for the wgrad
+                y, _, _, ctx.x4 = h.stem_fwd_stats(x, wref, stride, pad, bref, act, stats=False)
+            else:
+                y = h.conv2d_fwd(x, wref, stride, pad, bref, act)
         else:
             w = _torch_weight(wref)
             z = F.conv2d(_nchw(x), w, None, stride, pad, 1, wref.G)
@@ -223,13 +253,29 @@ class PackedConvBiasAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, y = ctx.saved_tensors
-        dz = PackedBiasAct.backward_core(dy.contiguous(), y, ctx.bref, ctx.act)
+        link = ctx.link
+        if link is not None and link.done:
+            dz = dy.contiguous()           # act'(y) applied, bias gradient added by the consumer
+            link.done = False
+        else:
+            dz = PackedBiasAct.backward_core(dy.contiguous(), y, ctx.bref, ctx.act)
+        if ctx.x4 is not None:
+            _hip().stem_wgrad(ctx.x4, dz, ctx.wref, ctx.pad, ctx.stride)
+            ctx.x4 = None
+            return None, None, None, None, None, None, None, None
         dx, _, _, _, _ = PackedConv2d.backward_core(ctx, x, dz, ctx.needs_input_grad[0])
-        return dx, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None
 
 
-def conv2d_bias_act(x, wref, bref, stride=1, pad=0, act=1, anchor=None):
-    return PackedConvBiasAct.apply(x, anchor, wref, bref, stride, pad, act)
+def conv2d_bias_act(x, wref, bref, stride=1, pad=0, act=1, anchor=None, link_out=False):
+    """``link_out``: the output's only consumer is another conv (its whole
+    gradient comes out of that conv's dgrad), which then applies this layer's
+    activation derivative and bias gradient in its epilogue (BiasActLink)."""
+    link = BiasActLink(bref, act) if link_out and BIAS_LINKS and act in (1, 6) else None
+    y = PackedConvBiasAct.apply(x, anchor, wref, bref, stride, pad, act, link)
+    if link is not None:
+        y._cer_balink = link
+    return y
 
 
 # ---------------------------------------------------------------------------
@@ -400,7 +446,7 @@ class PackedConvBNAct(torch.autograd.Function):
             dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
             x4, wref, pad = ctx.x4, ctx.wref, ctx.pad
-            _hip().stem_wgrad(x4, dz, wref, pad)
+            _hip().stem_wgrad(x4, dz, wref, pad, ctx.stride)
             ctx.x4 = None
             dx = None
         else:
@@ -524,9 +570,19 @@ def bias_act(x, bref, relu=True):
 # ---------------------------------------------------------------------------
 
 class MaxPoolHip(torch.autograd.Function):
+    """``x`` may be a linked conv + bias + ReLU output (BiasActLink, set by
+    the model when the pool is its sole consumer): the backward then returns
+    that layer's dz (ReLU' applied) and writes its bias gradient in the same
+    pass (pool.hip maxpool_bwd_relu_bias_kernel)."""
+
     @staticmethod
     def forward(ctx, x, k, s, p):
-        y, saved = _hip().maxpool_fwd(x, k, s, p)
+        link = getattr(x, "_cer_balink", None)
+        h = _hip()
+        if link is not None and not h.maxpool_relu_bias_ok(x, k, link.bref, link.act):
+            link = None
+        ctx.link = link
+        y, saved = h.maxpool_fwd(x, k, s, p, relu_bit=link is not None)
         ctx.save_for_backward(saved[0])
         ctx.geom = saved[1:]
         ctx.xshape = x.shape
@@ -535,7 +591,13 @@ class MaxPoolHip(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         arg, = ctx.saved_tensors
-        dx = _hip().maxpool_bwd(dy.contiguous(), (arg,) + ctx.geom, ctx.xshape)
+        link = ctx.link
+        if link is not None:
+            dx = _hip().maxpool_bwd_relu_bias(dy.contiguous(), (arg,) + ctx.geom, ctx.xshape,
+                                              link.bref)
+            link.done = True
+        else:
+            dx = _hip().maxpool_bwd(dy.contiguous(), (arg,) + ctx.geom, ctx.xshape)
         return dx, None, None, None
 
 

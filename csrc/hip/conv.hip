@@ -129,6 +129,8 @@ struct NTParams {
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
   int a_hl = 0;           // fp32 kernels: the A operand is in HL format (take_hi_lo)
+  int zfill = 0;          // fp32 strided 1x1 dgrad without addend: the epilogue zeroes
+                          // the o_st^2 - 1 pixels next to each written one (zfill_siblings)
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
@@ -174,6 +176,53 @@ __device__ __forceinline__ int64_t stat_base(int tile, int slabs, int ldc, int c
 
 static int stat_nslab(int tiles_m, int slabs) {
   return slabs ? (tiles_m > slabs ? slabs : tiles_m) | SLAB_F64 : tiles_m;
+}
+
+// Strided 1x1 dgrad without an addend (p.zfill): GEMM row m writes dx pixel
+// (b, y*st, x*st); the other st*st - 1 pixels of its st x st block get no
+// gradient.  The epilogue stores their zeros next to the written pixel (every
+// dx pixel lies in exactly one block), instead of a fill kernel over the
+// whole dx before the launch -- one dependent launch less per stage
+// transition.  cnt = 4 (vector) or 1 channels at obase[. + n].
+__device__ __forceinline__ void zfill_siblings(float* obase, int64_t orow, int64_t n, int st,
+                                               int oH, int oW, int64_t ldc, int cnt) {
+  const int x = (int)(orow % oW);
+  const int y = (int)((orow / oW) % oH);
+  for (int dy = 0; dy < st; ++dy)
+    for (int dx = 0; dx < st; ++dx) {
+      if ((dy | dx) == 0 || y + dy >= oH || x + dx >= oW) continue;
+      float* d = obase + (orow + (int64_t)dy * oW + dx) * ldc + n;
+      if (cnt == 4)
+        *reinterpret_cast<float4*>(d) = make_float4(0.f, 0.f, 0.f, 0.f);
+      else
+        *d = 0.f;
+    }
+}
+
+// BNBwdEpi mode YM_BIAS ("bias-act link", cer_conv_dgrad_babwd): the dgrad
+// output is the output gradient of a conv + bias + activation layer whose
+// activation y = act(conv + b) this conv consumed (VGG's conv -> conv).  The
+// epilogue applies the activation derivative itself -- dz = act'(y) * dx is
+// what it writes -- and adds the tile's per-channel sum of dz into the bias
+// gradient (fp32 atomics; the optimizer clears the gradient it consumes), so
+// the layer's separate bias_act_bwd pass over (dy, y, dz) disappears.
+// Fields: part = the bias gradient, z = y (fp32 [M][ldc]), gstride = the
+// bias-gradient stride per config, act = 1 (ReLU) / 6 (ReLU6).
+constexpr int YM_BIAS = 4;
+
+__device__ __forceinline__ bool act_pass(int act, float y) {
+  return act == 6 ? (y > 0.f && y < 6.f) : (act ? y > 0.f : true);
+}
+
+// the block's per-channel sums (xch rows 0 and 2: the two M-direction waves)
+// into the bias gradient
+template <int BN>
+__device__ __forceinline__ void bias_link_store(const BNBwdEpi& bb, const float* xch, int cfg,
+                                                int n0, int N, int tid) {
+  for (int nl = tid; nl < BN; nl += NTHREADS) {
+    const int n = n0 + nl;
+    if (n < N) atomicAdd(bb.part + (int64_t)cfg * bb.gstride + n, xch[nl] + xch[2 * BN + nl]);
+  }
 }
 
 
@@ -1819,7 +1868,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
                         : 0.f;
       s[j][e] = q[j][e] = 0.f;
       mu[j][e] = is[j][e] = sc[j][e] = sh[j][e] = 0.f;
-      if (bstat) {
+      if (bstat && bb.ym != YM_BIAS) {
         const int64_t c = (int64_t)cfg * p.N + nn;
         mu[j][e] = bb.mean[c];
         is[j][e] = bb.invstd[c];
@@ -1856,13 +1905,28 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
           const float4 a = *reinterpret_cast<const float4*>(adb + go);
           v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
         }
+        if (bstat && bb.ym == YM_BIAS) {
+          const float4 y4 = *reinterpret_cast<const float4*>(zb + go);
+          const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = act_pass(bb.act, yv[e]) ? v[e] : 0.f;
+            s[j][e] += v[e];
+          }
+        }
         *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.zfill) zfill_siblings(obase, orow, n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (n + e < p.N) {
             if (adb) v[e] += adb[go + e];
+            if (bstat && bb.ym == YM_BIAS) {
+              v[e] = act_pass(bb.act, zb[go + e]) ? v[e] : 0.f;
+              s[j][e] += v[e];
+            }
             obase[go + e] = v[e];
+            if (p.zfill) zfill_siblings(obase, orow, n + e, p.o_st, p.o_H, p.o_W, p.ldc, 1);
           }
       }
       if (fstat) {
@@ -1871,7 +1935,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
           s[j][e] += v[e];
           q[j][e] += v[e] * v[e];
         }
-      } else if (bstat) {      // host-gated: vec
+      } else if (bstat && bb.ym != YM_BIAS) {      // host-gated: vec
         const float4 z4 = *reinterpret_cast<const float4*>(zb + go);
         const float zv[4] = {z4.x, z4.y, z4.z, z4.w};
         float yv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1913,6 +1977,10 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
       }
     }
   __syncthreads();
+  if (bstat && bb.ym == YM_BIAS) {
+    bias_link_store<BN>(bb, xch, cfg, n0, p.N, tid);
+    return;
+  }
   float* dst = fstat ? p.stats : bb.part;
   const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
@@ -1974,9 +2042,10 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   const int fr = lane & 15, fc = lane >> 4;
   float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
   const bool ymz = bstat && bb.ym == 2, ymm = bstat && bb.ym == 3;
+  const bool ymb = bstat && bb.ym == YM_BIAS;
   const auto rBias = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
-  const auto rMean = make_rsrc(bb.mean, bstat ? EPI_BIG : 0u);
-  const auto rInv = make_rsrc(bb.invstd, bstat ? EPI_BIG : 0u);
+  const auto rMean = make_rsrc(bb.mean, bstat && !ymb ? EPI_BIG : 0u);
+  const auto rInv = make_rsrc(bb.invstd, bstat && !ymb ? EPI_BIG : 0u);
   const auto rGa = make_rsrc(bb.gamma, ymz ? EPI_BIG : 0u);
   const auto rBe = make_rsrc(bb.beta, ymz ? EPI_BIG : 0u);
   const auto rAd = make_rsrc(p.addend, p.addend ? EPI_BIG : 0u);
@@ -2057,14 +2126,24 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
           v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
           v[e] += av[e];
         }
+        if (ymb) {                   // bias-act link: dz = act'(y) * dx, written
+          const float yv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
+                               __uint_as_float(zz[ii][j].z), __uint_as_float(zz[ii][j].w)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = act_pass(bb.act, yv[e]) ? v[e] : 0.f;
+            s[j][e] += v[e];
+          }
+        }
         *reinterpret_cast<float4*>(obase + orow[i] * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        if (p.zfill) zfill_siblings(obase, orow[i], n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
         if (fstat) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             s[j][e] += v[e];
             q[j][e] += v[e] * v[e];
           }
-        } else if (bstat) {
+        } else if (bstat && !ymb) {
           const float zv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
                                __uint_as_float(zz[ii][j].z), __uint_as_float(zz[ii][j].w)};
 #pragma unroll
@@ -2097,6 +2176,10 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       }
     }
   __syncthreads();
+  if (bstat && bb.ym == YM_BIAS) {
+    bias_link_store<BN>(bb, xch, cfg, n0, p.N, tid);
+    return;
+  }
   float* dst = fstat ? p.stats : bb.part;
   const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
@@ -2376,7 +2459,7 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
                        : 0.f;
         s[g][e] = q[g][e] = 0.f;
         mu[g][e] = is[g][e] = sc[g][e] = sh[g][e] = 0.f;
-        if (bstat) {
+        if (bstat && bb.ym != YM_BIAS) {
           const int64_t c = (int64_t)cfg * p.N + nn;
           mu[g][e] = bb.mean[c];
           is[g][e] = bb.invstd[c];
@@ -2407,13 +2490,28 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
             const float4 a = *reinterpret_cast<const float4*>(adb + go);
             v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
           }
+          if (bstat && bb.ym == YM_BIAS) {
+            const float4 y4 = *reinterpret_cast<const float4*>(zb + go);
+            const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = act_pass(bb.act, yv[e]) ? v[e] : 0.f;
+              s[g][e] += v[e];
+            }
+          }
           *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
+          if (p.zfill) zfill_siblings(obase, orow[i], n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (n + e < p.N) {
               if (adb) v[e] += adb[go + e];
+              if (bstat && bb.ym == YM_BIAS) {
+                v[e] = act_pass(bb.act, zb[go + e]) ? v[e] : 0.f;
+                s[g][e] += v[e];
+              }
               obase[go + e] = v[e];
+              if (p.zfill) zfill_siblings(obase, orow[i], n + e, p.o_st, p.o_H, p.o_W, p.ldc, 1);
             }
         }
         if (fstat) {
@@ -2422,7 +2520,7 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
             s[g][e] += v[e];
             q[g][e] += v[e] * v[e];
           }
-        } else if (bstat) {      // host-gated: vec
+        } else if (bstat && bb.ym != YM_BIAS) {      // host-gated: vec
           const float4 z4 = *reinterpret_cast<const float4*>(zb + go);
           const float zv[4] = {z4.x, z4.y, z4.z, z4.w};
           float yv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -2468,6 +2566,10 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
   }
   if (!fstat && !bstat) return;
   __syncthreads();
+  if (bstat && bb.ym == YM_BIAS) {
+    bias_link_store<BN>(bb, xch, cfg, n0, p.N, tid);
+    return;
+  }
   float* dst = fstat ? p.stats : bb.part;
   const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
   for (int t = tid; t < 2 * BN; t += NTHREADS) {
@@ -4012,6 +4114,13 @@ static int* g_bb_nslab = nullptr;
 static int g_addend_grid = 0;
 CER_API void cer_conv_set_addend_grid(int st) { g_addend_grid = st; }
 
+// strided 1x1 fp32 dgrads without an addend zero their off-grid pixels in the
+// epilogue (NTParams::zfill; CER_DGRAD_ZFILL=0: a fill kernel first)
+static const int g_zfill = [] {
+  const char* e = getenv("CER_DGRAD_ZFILL");
+  return e ? atoi(e) : 1;
+}();
+
 // z, y, gamma, beta: bf16 for cer_conv_dgrad, fp32 for cer_conv_dgrad_f32
 CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
                                   const float* mean, const float* invstd, const void* gamma,
@@ -4021,6 +4130,20 @@ CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
                   mean, invstd, reinterpret_cast<const bf16_t*>(gamma), gstride,
                   reinterpret_cast<const bf16_t*>(beta), bstride, bn_mask_mode(act, has_res), act};
   g_bb_nslab = part ? nslab_out : nullptr;
+}
+
+// bias-act link (YM_BIAS) for the NEXT fp32 cer_conv_dgrad calls, until
+// cleared with dbias == nullptr: dbias = the linked layer's bias gradient
+// (fp32, config stride dbstride), y = its fp32 output act(conv + b), act =
+// its activation code.  *done_out is set non-zero by a launch that applied it
+// (aligned NN path, stride 1, no addend); zero means the caller runs the
+// layer's own bias_act_bwd.
+CER_API void cer_conv_dgrad_babwd(float* dbias, int64_t dbstride, const void* y, int act,
+                                  int* done_out) {
+  g_bb = BNBwdEpi{dbias, reinterpret_cast<const bf16_t*>(y), nullptr, nullptr, nullptr, nullptr,
+                  dbstride, nullptr, 0, YM_BIAS, act};
+  g_bb_nslab = dbias ? done_out : nullptr;
+  if (!dbias) g_bb.ym = 0;
 }
 
 template <int BM, int BN>
@@ -4098,6 +4221,8 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       const size_t bytes = (size_t)es * B * H * W * G * Cin;
       if (addend) {
         if (addend != dx) cer_copy_async(dx, addend, bytes, stream);   // in place: nothing to copy
+      } else if (f32 && g_zfill) {
+        p.zfill = 1;                     // the epilogue writes the off-grid zeros
       } else {
         cer_zero_async(dx, bytes, stream);
       }
@@ -4131,7 +4256,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     // BN-backward statistics: every nonzero dx pixel must come out of the
     // epilogue (a strided 1x1 dgrad leaves pixels at zero: fine without an
     // addend, or with one that is zero off the same grid)
-    if (g_bb.part && (p.o_st == 1 || !addend || g_addend_grid == p.o_st)) {
+    const bool bb_ok = g_bb.ym == YM_BIAS ? f32 && p.o_st == 1 && !addend
+                                          : p.o_st == 1 || !addend || g_addend_grid == p.o_st;
+    if (g_bb.part && bb_ok) {
       p.bb = g_bb;
       p.stat_slabs = g_stat_slabs;
       int bm, bn;
@@ -4694,25 +4821,31 @@ CER_API int cer_wgrad_splits(int Mred, int N, int K, int G) {
 // 16-B chunk is one (row tap, pair tap) and the aligned MFMA path applies.
 // Weights are re-laid [N][kh][kw'][8] per step (zeros on padded taps /
 // channels); the wgrad runs on the same geometry and is folded back.
+// STEM_PAD8 (Cin < 8, stride 1: VGG's 3x3/1 block1_conv1): no pixel pairs;
+// the image is repacked per config as [B][H][W][8] (channels Cin..7 = 0) and
+// the weights as [N][kh][kw][8], so every tap is one aligned 8-channel chunk
+// (K = kh*kw*8) at the price of 8/Cin x the MFMA work on a tiny layer.
 // ---------------------------------------------------------------------------
+enum { STEM_NONE = 0, STEM_PAD8 = 1, STEM_PAIR = 2 };
 template <typename E>
 __global__ __launch_bounds__(256) void stem_repack_kernel(const E* __restrict__ x,
                                                           E* __restrict__ x4, int64_t P,
-                                                          int G, int C) {
+                                                          int G, int C, int CP) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, config)
   if (i >= P * G) return;
   const int64_t p = i / G;
   const int g = (int)(i - p * G);
   const E* src = x + p * G * C + (int64_t)g * C;
-  E* dst = x4 + ((int64_t)g * P + p) * 4;
-  for (int c = 0; c < 4; ++c) dst[c] = c < C ? src[c] : (E)0;
+  E* dst = x4 + ((int64_t)g * P + p) * CP;
+  for (int c = 0; c < CP; ++c) dst[c] = c < C ? src[c] : (E)0;
 }
 
 template <typename E>
 __global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ w,
                                                           int64_t w_gstride,
                                                           E* __restrict__ wp, int N, int kh,
-                                                          int kw, int C, int kwp, int G) {
+                                                          int kw, int C, int kwp, int G,
+                                                          int pad8) {
   const int64_t per = (int64_t)N * kh * kwp * 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= per * G) return;
@@ -4724,7 +4857,8 @@ __global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ 
   t /= kwp;
   const int r = (int)(t % kh);
   const int n = (int)(t / kh);
-  const int px = q >> 2, c = q & 3, s = 2 * sp + px - 1;
+  // pad8 (STEM_PAD8): tap sp, channel q; else pixel pairs
+  const int px = pad8 ? 0 : q >> 2, c = pad8 ? q : q & 3, s = pad8 ? sp : 2 * sp + px - 1;
   E v = 0;
   if (s >= 0 && s < kw && c < C) v = w[g * w_gstride + (((int64_t)n * kh + r) * kw + s) * C + c];
   wp[i] = v;
@@ -4733,7 +4867,8 @@ __global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ 
 __global__ __launch_bounds__(256) void stem_fold_grad_kernel(const float* __restrict__ dwp,
                                                              float* __restrict__ dw,
                                                              int64_t dw_gstride, int N, int kh,
-                                                             int kw, int C, int kwp, int G) {
+                                                             int kw, int C, int kwp, int G,
+                                                             int pad8) {
   const int64_t per = (int64_t)N * kh * kw * C;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= per * G) return;
@@ -4745,25 +4880,43 @@ __global__ __launch_bounds__(256) void stem_fold_grad_kernel(const float* __rest
   t /= kw;
   const int r = (int)(t % kh);
   const int n = (int)(t / kh);
+  if (pad8) {                                          // STEM_PAD8
+    dw[g * dw_gstride + (((int64_t)n * kh + r) * kw + s) * C + c] =
+        dwp[((((int64_t)g * N + n) * kh + r) * kw + s) * 8 + c];
+    return;
+  }
   const int sp = (s + 1) >> 1, px = (s + 1) & 1;
   dw[g * dw_gstride + (((int64_t)n * kh + r) * kw + s) * C + c] =
       dwp[((((int64_t)g * N + n) * kh + r) * kwp + sp) * 8 + px * 4 + c];
 }
 
-static int stem_kwp(int kw) { return kw / 2 + 1; }
-
+// the stem geometry of a first layer (STEM_*): pixel pairs for Cin <= 4,
+// stride 2, odd padding, even width; channel padding to 8 for Cin < 8 at
+// stride 1; none otherwise
 CER_API int cer_stem_ok(int Cin, int W, int kw, int st, int pad) {
-  return (Cin <= 4 && st == 2 && (pad & 1) && (W % 2) == 0 && kw >= 2) ? 1 : 0;
+  if (Cin <= 4 && st == 2 && (pad & 1) && (W % 2) == 0 && kw >= 2) return STEM_PAIR;
+  if (Cin < 8 && st == 1) return STEM_PAD8;
+  return STEM_NONE;
 }
 
-// scratch sizes (elements): x4 = B*H*W*4*G bf16, wpk = G*Cout*kh*kwp*8 bf16
-CER_API int64_t cer_stem_wpk_elems(int G, int Cout, int kh, int kw) {
-  return (int64_t)G * Cout * kh * stem_kwp(kw) * 8;
+static int stem_kwp(int kw, int mode) { return mode == STEM_PAD8 ? kw : kw / 2 + 1; }
+// channels per pixel of the repacked input
+static int stem_cp(int mode) { return mode == STEM_PAD8 ? 8 : 4; }
+
+// scratch sizes (elements): x4 = G*B*H*W*cer_stem_cp, wpk = G*Cout*kh*kwp*8
+CER_API int64_t cer_stem_wpk_elems(int G, int Cout, int kh, int kw, int mode) {
+  return (int64_t)G * Cout * kh * stem_kwp(kw, mode) * 8;
 }
+CER_API int cer_stem_cp(int mode) { return stem_cp(mode); }
 
 static GatherGeom stem_geom(const void* x4, int B, int H, int W, int Ho, int Wo, int kh,
-                            int kw, int pad) {
-  const int kwp = stem_kwp(kw);
+                            int kw, int pad, int mode) {
+  if (mode == STEM_PAD8) {
+    GatherGeom g = make_geom(x4, B, 8, 8, H, W, Ho, Wo, kh, kw, 1, pad);
+    g.cfg_off = (int64_t)B * H * W * 8;
+    return g;
+  }
+  const int kwp = stem_kwp(kw, mode);
   GatherGeom g = make_geom(x4, B, 8, 8, H, W / 2, Ho, Wo, kh, kwp, 2, pad);
   g.st_w = 1;
   g.pad_w = (pad + 1) / 2;
@@ -4774,28 +4927,30 @@ static GatherGeom stem_geom(const void* x4, int B, int H, int W, int Ho, int Wo,
 static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* x4, void* wpk, void* y, int Ho, int Wo, float* part,
-                         int* nslab, bool f32, hipStream_t stream) {
-  if (!cer_stem_ok(Cin, W, kw, st, pad)) return (int)hipErrorInvalidValue;
+                         int* nslab, const void* bias, int64_t bias_gstride, int act, bool f32,
+                         hipStream_t stream) {
+  const int mode = cer_stem_ok(Cin, W, kw, st, pad);
+  if (mode == STEM_NONE) return (int)hipErrorInvalidValue;
   const int64_t P = (int64_t)B * H * W;
-  const int kwp = stem_kwp(kw);
+  const int kwp = stem_kwp(kw, mode), cp = stem_cp(mode);
   const int64_t nw = (int64_t)G * Cout * kh * kwp * 8;
   if (f32) {
     stem_repack_kernel<float><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
-        reinterpret_cast<const float*>(x), reinterpret_cast<float*>(x4), P, G, Cin);
+        reinterpret_cast<const float*>(x), reinterpret_cast<float*>(x4), P, G, Cin, cp);
     stem_pack_w_kernel<float><<<cer_blocks(nw, 256), 256, 0, stream>>>(
         reinterpret_cast<const float*>(w), w_gstride, reinterpret_cast<float*>(wpk), Cout, kh, kw,
-        Cin, kwp, G);
+        Cin, kwp, G, mode == STEM_PAD8);
   } else {
     stem_repack_kernel<bf16_t><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
-        reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(x4), P, G, Cin);
+        reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(x4), P, G, Cin, cp);
     stem_pack_w_kernel<bf16_t><<<cer_blocks(nw, 256), 256, 0, stream>>>(
         reinterpret_cast<const bf16_t*>(w), w_gstride, reinterpret_cast<bf16_t*>(wpk), Cout, kh,
-        kw, Cin, kwp, G);
+        kw, Cin, kwp, G, mode == STEM_PAD8);
   }
   NTParams p;
-  p.a = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
-  // the whole [G][B][H][W/2][8] buffer is the buffer-load range
-  const uint64_t bytes = (uint64_t)G * P * 4 * (f32 ? 4 : 2);
+  p.a = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad, mode);
+  // the whole [G][B][H][W][cp] buffer is the buffer-load range
+  const uint64_t bytes = (uint64_t)G * P * cp * (f32 ? 4 : 2);
   p.a.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   p.dgrad = 0;
   p.w = reinterpret_cast<const bf16_t*>(wpk);
@@ -4805,9 +4960,9 @@ static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
   p.M = B * Ho * Wo;
   p.N = Cout;
   p.K = kh * kwp * 8;
-  p.bias = nullptr;
-  p.bias_gstride = 0;
-  p.act = 0;
+  p.bias = reinterpret_cast<const bf16_t*>(bias);
+  p.bias_gstride = bias ? bias_gstride : 0;
+  p.act = act;
   p.o_st = 1;
   p.o_H = Ho;
   p.o_W = Wo;
@@ -4815,33 +4970,38 @@ static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
   return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
 
-// repack + weight re-layout + forward conv (+ BN partials when part != null)
+// repack + weight re-layout + forward conv (+ BN partials when part != null;
+// + bias and activation in the epilogue when bias != null / act != 0)
 CER_API int cer_stem_fwd(const bf16_t* x, int B, int H, int W, int Cin, int G, const bf16_t* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          bf16_t* x4, bf16_t* wpk, bf16_t* y, int Ho, int Wo, float* part,
-                         int* nslab, hipStream_t stream) {
+                         int* nslab, const bf16_t* bias, int64_t bias_gstride, int act,
+                         hipStream_t stream) {
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nslab, false, stream);
+                       Wo, part, nslab, bias, bias_gstride, act, false, stream);
 }
 
 // fp32 twin: x4 / wpk / y fp32 (same element counts)
 CER_API int cer_stem_fwd_f32(const float* x, int B, int H, int W, int Cin, int G, const float* w,
                              int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                              float* x4, float* wpk, float* y, int Ho, int Wo, float* part,
-                             int* nslab, hipStream_t stream) {
+                             int* nslab, const float* bias, int64_t bias_gstride, int act,
+                             hipStream_t stream) {
   return stem_fwd_impl(x, B, H, W, Cin, G, w, w_gstride, Cout, kh, kw, st, pad, x4, wpk, y, Ho,
-                       Wo, part, nslab, true, stream);
+                       Wo, part, nslab, bias, bias_gstride, act, true, stream);
 }
 
 // dW of the stem from the repacked input; dwp: fp32 scratch of
 // cer_stem_wpk_elems floats (zeroed here when the reduction is split)
 static int stem_wgrad_impl(const void* x4, int B, int H, int W, int Cin, int G, const void* dy,
-                           int Ho, int Wo, int Cout, int kh, int kw, int pad, float* dwp,
+                           int Ho, int Wo, int Cout, int kh, int kw, int st, int pad, float* dwp,
                            float* dw, int64_t dw_gstride, bool f32, hipStream_t stream) {
-  const int kwp = stem_kwp(kw);
+  const int mode = cer_stem_ok(Cin, W, kw, st, pad);
+  if (mode == STEM_NONE) return (int)hipErrorInvalidValue;
+  const int kwp = stem_kwp(kw, mode);
   WGParams p;
-  p.x = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad);
-  const uint64_t bytes = (uint64_t)G * B * H * W * 4 * (f32 ? 4 : 2);
+  p.x = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad, mode);
+  const uint64_t bytes = (uint64_t)G * B * H * W * stem_cp(mode) * (f32 ? 4 : 2);
   p.x.bytes = bytes < (1ull << 31) ? (uint32_t)bytes : 0u;
   p.dy = reinterpret_cast<const bf16_t*>(dy);
   p.ldy = G * Cout;
@@ -4866,20 +5026,22 @@ static int stem_wgrad_impl(const void* x4, int B, int H, int W, int Cin, int G, 
   }
   const int64_t n = (int64_t)G * Cout * kh * kw * Cin;
   stem_fold_grad_kernel<<<cer_blocks(n, 256), 256, 0, stream>>>(dwp, dw, dw_gstride, Cout, kh, kw,
-                                                                Cin, kwp, G);
+                                                                Cin, kwp, G, mode == STEM_PAD8);
   return (int)hipGetLastError();
 }
 
 CER_API int cer_stem_wgrad(const bf16_t* x4, int B, int H, int W, int Cin, int G,
-                           const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
-                           float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
-  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, pad, dwp, dw, dw_gstride,
-                         false, stream);
+                           const bf16_t* dy, int Ho, int Wo, int Cout, int kh, int kw, int st,
+                           int pad, float* dwp, float* dw, int64_t dw_gstride,
+                           hipStream_t stream) {
+  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, st, pad, dwp, dw,
+                         dw_gstride, false, stream);
 }
 
 CER_API int cer_stem_wgrad_f32(const float* x4, int B, int H, int W, int Cin, int G,
-                               const float* dy, int Ho, int Wo, int Cout, int kh, int kw, int pad,
-                               float* dwp, float* dw, int64_t dw_gstride, hipStream_t stream) {
-  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, pad, dwp, dw, dw_gstride,
-                         true, stream);
+                               const float* dy, int Ho, int Wo, int Cout, int kh, int kw, int st,
+                               int pad, float* dwp, float* dw, int64_t dw_gstride,
+                               hipStream_t stream) {
+  return stem_wgrad_impl(x4, B, H, W, Cin, G, dy, Ho, Wo, Cout, kh, kw, st, pad, dwp, dw,
+                         dw_gstride, true, stream);
 }

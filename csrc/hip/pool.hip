@@ -15,7 +15,7 @@ __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x
                                                          T* __restrict__ y,
                                                          uint8_t* __restrict__ arg, int B, int H,
                                                          int W, int C, int Ho, int Wo, int k,
-                                                         int s, int pad) {
+                                                         int s, int pad, int relu_bit) {
   const int64_t t = (int64_t)blockIdx.x * PT + threadIdx.x;
   const int cv = C / V;
   const int64_t total = (int64_t)B * Ho * Wo * cv;
@@ -51,6 +51,10 @@ __global__ __launch_bounds__(PT) void maxpool_fwd_kernel(const T* __restrict__ x
   }
   const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
   stv<V>(y + o, best);
+  if (relu_bit) {                 // the window max is > 0: its ReLU was active (k*k <= 128)
+#pragma unroll
+    for (int i = 0; i < V; ++i) bi[i] |= best[i] > 0.f ? 0x80 : 0;
+  }
   if constexpr (V == 8) {
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
@@ -108,6 +112,80 @@ __global__ __launch_bounds__(PT) void maxpool_bwd_kernel(const T* __restrict__ d
     }
   }
   stv<V>(dx + (((int64_t)b * H + h) * W + w) * C + c0, acc);
+}
+
+// Max-pool backward fused with the backward of the conv + bias + ReLU layer
+// that produced the pool's input (VGG's last conv of a block; ops.nn
+// BiasActLink): the forward stored bit 7 of each argmax byte = "the window
+// max is > 0" (relu_bit), so the input gradient of the pool IS the ReLU'ed
+// dz -- dz(p) = dy(window) where p is the window's argmax and its value was
+// > 0 -- and the same pass sums dz per channel into the layer's bias
+// gradient (fp32 atomics, one per channel and block; the optimizer clears
+// the gradient it consumes).  Replaces maxpool_bwd + bias_act_bwd, which
+// read and wrote the full-resolution tensor three more times.
+// Block = cw channel groups (8 channels each) x lanes pixel rows; blockIdx.y
+// walks pixel chunks of ppb pixels.
+template <typename T>
+__global__ __launch_bounds__(PT) void maxpool_bwd_relu_bias_kernel(
+    const T* __restrict__ dy, const uint8_t* __restrict__ arg, T* __restrict__ dx,
+    float* __restrict__ dbias, int64_t gstride, int Cper, int B, int H, int W, int C, int Ho,
+    int Wo, int k, int s, int pad, int64_t ppb) {
+  constexpr int V = 8;
+  __shared__ float red[PT * V];
+  const int cv = C / V;
+  const int cw = cv < PT ? cv : PT;
+  const int lanes = PT / cw;
+  const int j = threadIdx.x % cw, l = threadIdx.x / cw;
+  const int cg = blockIdx.x * cw + j;
+  const bool on = l < lanes && cg < cv;
+  const int c0 = cg * V;
+  const int64_t P = (int64_t)B * H * W;
+  const int64_t p0 = (int64_t)blockIdx.y * ppb;
+  const int64_t p1 = p0 + ppb < P ? p0 + ppb : P;
+  float sum[V] = {};
+  if (on) {
+    for (int64_t pix = p0 + l; pix < p1; pix += lanes) {
+      const int w = (int)(pix % W);
+      const int64_t bh = pix / W;
+      const int h = (int)(bh % H);
+      const int b = (int)(bh / H);
+      float acc[V] = {};
+      int ho0 = (h + pad - k + 1 + s - 1) / s;
+      if (h + pad - k + 1 < 0) ho0 = 0;
+      const int ho1 = min(Ho - 1, (h + pad) / s);
+      int wo0 = (w + pad - k + 1 + s - 1) / s;
+      if (w + pad - k + 1 < 0) wo0 = 0;
+      const int wo1 = min(Wo - 1, (w + pad) / s);
+      for (int ho = ho0; ho <= ho1; ++ho) {
+        for (int wo = wo0; wo <= wo1; ++wo) {
+          const uint32_t want = 0x80u | (uint32_t)((h + pad - ho * s) * k + (w + pad - wo * s));
+          const int64_t o = (((int64_t)b * Ho + ho) * Wo + wo) * C + c0;
+          float g[V];
+          ldv<V>(dy + o, g);
+          const uint2 packed = *reinterpret_cast<const uint2*>(arg + o);
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            const uint32_t word = i < 4 ? packed.x : packed.y;
+            if (((word >> (8 * (i & 3))) & 0xffu) == want) acc[i] += g[i];
+          }
+        }
+      }
+      stv<V>(dx + pix * C + c0, acc);
+#pragma unroll
+      for (int i = 0; i < V; ++i) sum[i] += acc[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[threadIdx.x * V + i] = sum[i];
+  __syncthreads();
+  if (on && l == 0) {
+    for (int ll = 1; ll < lanes; ++ll)
+#pragma unroll
+      for (int i = 0; i < V; ++i) sum[i] += red[(ll * cw + j) * V + i];
+    const int g = c0 / Cper, cc = c0 - g * Cper;
+#pragma unroll
+    for (int i = 0; i < V; ++i) atomicAdd(dbias + (int64_t)g * gstride + cc + i, sum[i]);
+  }
 }
 
 // global average pool: x [B, HW, C] -> y [B, C]
@@ -246,15 +324,38 @@ __global__ __launch_bounds__(PT) void bias_act_bwd_scalar(const T* __restrict__ 
 
 template <typename T>
 static int cer_maxpool_fwd_t(const T* x, T* y, uint8_t* arg, int B, int H, int W, int C,
-                            int Ho, int Wo, int k, int s, int pad, hipStream_t stream) {
-  if (k * k > 255) return (int)hipErrorInvalidValue;
+                            int Ho, int Wo, int k, int s, int pad, int relu_bit,
+                            hipStream_t stream) {
+  if (k * k > 255 || (relu_bit && (k * k > 128 || C % 8))) return (int)hipErrorInvalidValue;
   // 8 channels per thread when C % 8 == 0, else 1 (ragged widths)
   if (C % 8 == 0)
     maxpool_fwd_kernel<T, 8><<<cer_blocks((int64_t)B * Ho * Wo * (C / 8), PT), PT, 0, stream>>>(
-        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad);
+        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad, relu_bit);
   else
     maxpool_fwd_kernel<T, 1><<<cer_blocks((int64_t)B * Ho * Wo * C, PT), PT, 0, stream>>>(
-        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad);
+        x, y, arg, B, H, W, C, Ho, Wo, k, s, pad, 0);
+  return (int)hipGetLastError();
+}
+
+// dz of the pooled conv + bias + ReLU layer and its bias gradient (see
+// maxpool_bwd_relu_bias_kernel); the forward ran with relu_bit = 1
+template <typename T>
+static int cer_maxpool_bwd_relu_bias_t(const T* dy, const uint8_t* arg, T* dx, float* dbias,
+                                      int64_t gstride, int Cper, int B, int H, int W, int C,
+                                      int Ho, int Wo, int k, int s, int pad, hipStream_t stream) {
+  if (C % 8 || Cper % 8 || k * k > 128) return (int)hipErrorInvalidValue;
+  const int cv = C / 8;
+  const int cw = cv < PT ? cv : PT;
+  const int gx = (cv + cw - 1) / cw;
+  const int64_t P = (int64_t)B * H * W;
+  const int lanes = PT / cw;
+  // ~2048 blocks, at least 4 pixels per lane
+  int64_t gy = (2048 + gx - 1) / gx;
+  int64_t ppb = (P + gy - 1) / gy;
+  if (ppb < 4 * lanes) ppb = 4 * lanes;
+  gy = (P + ppb - 1) / ppb;
+  maxpool_bwd_relu_bias_kernel<T><<<dim3((unsigned)gx, (unsigned)gy), PT, 0, stream>>>(
+      dy, arg, dx, dbias, gstride, Cper, B, H, W, C, Ho, Wo, k, s, pad, ppb);
   return (int)hipGetLastError();
 }
 
@@ -447,8 +548,16 @@ static int cer_avgpool_bwd_t(const T* dy, T* dx, int B, int H, int W, int C, int
 
 #define CER_POOL_ENTRY_POINTS(T, SFX)                                                            \
   CER_API int cer_maxpool_fwd##SFX(const T* x, T* y, uint8_t* arg, int B, int H, int W, int C,  \
-                                   int Ho, int Wo, int k, int s, int pad, hipStream_t st) {      \
-    return cer_maxpool_fwd_t<T>(x, y, arg, B, H, W, C, Ho, Wo, k, s, pad, st);                   \
+                                   int Ho, int Wo, int k, int s, int pad, int relu_bit,          \
+                                   hipStream_t st) {                                             \
+    return cer_maxpool_fwd_t<T>(x, y, arg, B, H, W, C, Ho, Wo, k, s, pad, relu_bit, st);         \
+  }                                                                                              \
+  CER_API int cer_maxpool_bwd_relu_bias##SFX(const T* dy, const uint8_t* arg, T* dx,            \
+                                             float* dbias, int64_t gstride, int Cper, int B,     \
+                                             int H, int W, int C, int Ho, int Wo, int k, int s,  \
+                                             int pad, hipStream_t st) {                          \
+    return cer_maxpool_bwd_relu_bias_t<T>(dy, arg, dx, dbias, gstride, Cper, B, H, W, C, Ho, Wo, \
+                                          k, s, pad, st);                                        \
   }                                                                                              \
   CER_API int cer_maxpool_bwd##SFX(const T* dy, const uint8_t* arg, T* dx, int B, int H, int W, \
                                    int C, int Ho, int Wo, int k, int s, int pad,                 \
