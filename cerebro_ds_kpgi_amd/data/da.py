@@ -412,7 +412,9 @@ def da_partition_loader(root, device, nthreads=16, stats=None):
     # (partition, split) decodes run concurrently ahead of the consumer
     # (bounded: each holds its decompressed payload in pinned memory)
     import concurrent.futures as cf
-    WINDOW = 4
+    # each decode holds its decompressed payload in pinned memory (25 GB for
+    # a full ImageNet-112 train split): CER_DA_WINDOW bounds the host memory
+    WINDOW = max(1, int(os.environ.get("CER_DA_WINDOW", "4")))
     jobs, futs = [], {}
     # the decode pool lives while a prefetch window is open: created lazily
     # on the first submit, shut down once the window drains (every prefetched

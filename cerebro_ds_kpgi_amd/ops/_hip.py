@@ -282,6 +282,8 @@ _SIGS.update({
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_set_grid": [c_i],
     "cer_wgrad_batch_set_rows": [c_i],
+    "cer_wgrad_batch_set_ring": [c_i],
+    "cer_wgrad_batch_set_narrow": [c_i],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
     "cer_bn_set_hl_out": [c_i],

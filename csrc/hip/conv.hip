@@ -129,8 +129,6 @@ struct NTParams {
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
   int a_hl = 0;           // fp32 kernels: the A operand is in HL format (take_hi_lo)
-  int zfill = 0;          // fp32 strided 1x1 dgrad without addend: the epilogue zeroes
-                          // the o_st^2 - 1 pixels next to each written one (zfill_siblings)
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
@@ -176,27 +174,6 @@ __device__ __forceinline__ int64_t stat_base(int tile, int slabs, int ldc, int c
 
 static int stat_nslab(int tiles_m, int slabs) {
   return slabs ? (tiles_m > slabs ? slabs : tiles_m) | SLAB_F64 : tiles_m;
-}
-
-// Strided 1x1 dgrad without an addend (p.zfill): GEMM row m writes dx pixel
-// (b, y*st, x*st); the other st*st - 1 pixels of its st x st block get no
-// gradient.  The epilogue stores their zeros next to the written pixel (every
-// dx pixel lies in exactly one block), instead of a fill kernel over the
-// whole dx before the launch -- one dependent launch less per stage
-// transition.  cnt = 4 (vector) or 1 channels at obase[. + n].
-__device__ __forceinline__ void zfill_siblings(float* obase, int64_t orow, int64_t n, int st,
-                                               int oH, int oW, int64_t ldc, int cnt) {
-  const int x = (int)(orow % oW);
-  const int y = (int)((orow / oW) % oH);
-  for (int dy = 0; dy < st; ++dy)
-    for (int dx = 0; dx < st; ++dx) {
-      if ((dy | dx) == 0 || y + dy >= oH || x + dx >= oW) continue;
-      float* d = obase + (orow + (int64_t)dy * oW + dx) * ldc + n;
-      if (cnt == 4)
-        *reinterpret_cast<float4*>(d) = make_float4(0.f, 0.f, 0.f, 0.f);
-      else
-        *d = 0.f;
-    }
 }
 
 // BNBwdEpi mode YM_BIAS ("bias-act link", cer_conv_dgrad_babwd): the dgrad
@@ -1915,7 +1892,6 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
           }
         }
         *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
-        if (p.zfill) zfill_siblings(obase, orow, n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -1926,7 +1902,6 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
               s[j][e] += v[e];
             }
             obase[go + e] = v[e];
-            if (p.zfill) zfill_siblings(obase, orow, n + e, p.o_st, p.o_H, p.o_W, p.ldc, 1);
           }
       }
       if (fstat) {
@@ -2136,7 +2111,6 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
           }
         }
         *reinterpret_cast<float4*>(obase + orow[i] * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-        if (p.zfill) zfill_siblings(obase, orow[i], n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
         if (fstat) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -2471,6 +2445,20 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
           }
         }
       }
+    // bias-act link: this block's y operands, all loads in flight before the
+    // first use (one memory round trip per 32-channel block, as in epi32)
+    float4 ypre[FM][4];
+    if (bstat && bb.ym == YM_BIAS && vec) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int n = nb + 8 * g;
+          ypre[i][g] = rok[i] && n < p.N
+                           ? *reinterpret_cast<const float4*>(zb + orow[i] * p.ldc + n)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (!rok[i]) continue;
@@ -2491,8 +2479,7 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
             v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
           }
           if (bstat && bb.ym == YM_BIAS) {
-            const float4 y4 = *reinterpret_cast<const float4*>(zb + go);
-            const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+            const float yv[4] = {ypre[i][g].x, ypre[i][g].y, ypre[i][g].z, ypre[i][g].w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               v[e] = act_pass(bb.act, yv[e]) ? v[e] : 0.f;
@@ -2500,7 +2487,6 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
             }
           }
           *reinterpret_cast<float4*>(obase + go) = make_float4(v[0], v[1], v[2], v[3]);
-          if (p.zfill) zfill_siblings(obase, orow[i], n, p.o_st, p.o_H, p.o_W, p.ldc, 4);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -2511,7 +2497,6 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
                 s[g][e] += v[e];
               }
               obase[go + e] = v[e];
-              if (p.zfill) zfill_siblings(obase, orow[i], n + e, p.o_st, p.o_H, p.o_W, p.ldc, 1);
             }
         }
         if (fstat) {
@@ -4114,13 +4099,6 @@ static int* g_bb_nslab = nullptr;
 static int g_addend_grid = 0;
 CER_API void cer_conv_set_addend_grid(int st) { g_addend_grid = st; }
 
-// strided 1x1 fp32 dgrads without an addend zero their off-grid pixels in the
-// epilogue (NTParams::zfill; CER_DGRAD_ZFILL=0: a fill kernel first)
-static const int g_zfill = [] {
-  const char* e = getenv("CER_DGRAD_ZFILL");
-  return e ? atoi(e) : 1;
-}();
-
 // z, y, gamma, beta: bf16 for cer_conv_dgrad, fp32 for cer_conv_dgrad_f32
 CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
                                   const float* mean, const float* invstd, const void* gamma,
@@ -4221,8 +4199,6 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       const size_t bytes = (size_t)es * B * H * W * G * Cin;
       if (addend) {
         if (addend != dx) cer_copy_async(dx, addend, bytes, stream);   // in place: nothing to copy
-      } else if (f32 && g_zfill) {
-        p.zfill = 1;                     // the epilogue writes the off-grid zeros
       } else {
         cer_zero_async(dx, bytes, stream);
       }
@@ -4721,14 +4697,13 @@ static int g_wgb_grid = 0;
 CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
 
 template <int BM, int BN, bool WIDE = false>
-static void wgb32_launch_sel(hipStream_t stream) {
-  const int n = g_wgq32_n;
+static void wgb32_launch_sel(hipStream_t stream, const int* idx, int n) {
   for (int b0 = 0; b0 < n; b0 += WGB_MAX) {
     WGBatch bt;
     bt.n = n - b0 < WGB_MAX ? n - b0 : WGB_MAX;
     int tot = 0;
     for (int i = 0; i < bt.n; ++i) {
-      const int k = b0 + i;
+      const int k = idx[b0 + i];
       bt.p[i] = g_wgq32[k];
       bt.start[i] = tot;
       tot += (int)(ntiles(bt.p[i].N, bt.p[i].K, BM, BN) * bt.p[i].splits * g_wgq32_G[k]);
@@ -4747,12 +4722,42 @@ static void wgb32_launch_sel(hipStream_t stream) {
   }
 }
 
+// Items whose output-channel count N is at most 64 in a 128-row-tile batch
+// would leave half of every tile's rows empty (VGG block 1, ResNet stage 2):
+// they go to a second launch with 64x64 tiles (CER_WGB_NARROW=0: one launch).
+static int g_wgb_narrow = -1;
+static bool wgb_narrow() {
+  if (g_wgb_narrow < 0) {
+    const char* e = getenv("CER_WGB_NARROW");
+    g_wgb_narrow = e ? atoi(e) : 1;
+  }
+  return g_wgb_narrow > 0;
+}
+CER_API void cer_wgrad_batch_set_narrow(int on) { g_wgb_narrow = on ? 1 : 0; }
+
 template <int BM, int BN>
 static int wgb32_launch(hipStream_t stream, bool wide = false) {
-  if (wide)
-    wgb32_launch_sel<BM, BN, true>(stream);
-  else
-    wgb32_launch_sel<BM, BN>(stream);
+  static int idx[4096], nar[4096];
+  int n = 0, nn = 0;
+  const bool split = BM == 128 && wgb_narrow();
+  for (int k = 0; k < g_wgq32_n; ++k) {
+    if (split && g_wgq32[k].N <= 64)
+      nar[nn++] = k;
+    else
+      idx[n++] = k;
+  }
+  if (nn > 0) {
+    if (wide)
+      wgb32_launch_sel<64, 64, true>(stream, nar, nn);
+    else
+      wgb32_launch_sel<64, 64>(stream, nar, nn);
+  }
+  if (n > 0) {
+    if (wide)
+      wgb32_launch_sel<BM, BN, true>(stream, idx, n);
+    else
+      wgb32_launch_sel<BM, BN>(stream, idx, n);
+  }
   return (int)hipGetLastError();
 }
 
@@ -4893,9 +4898,14 @@ __global__ __launch_bounds__(256) void stem_fold_grad_kernel(const float* __rest
 // the stem geometry of a first layer (STEM_*): pixel pairs for Cin <= 4,
 // stride 2, odd padding, even width; channel padding to 8 for Cin < 8 at
 // stride 1; none otherwise
+// (CER_STEM_PAD8=0: stride-1 narrow first layers take the generic gather, A/B)
+static const int g_stem_pad8 = [] {
+  const char* e = getenv("CER_STEM_PAD8");
+  return e ? atoi(e) : 1;
+}();
 CER_API int cer_stem_ok(int Cin, int W, int kw, int st, int pad) {
   if (Cin <= 4 && st == 2 && (pad & 1) && (W % 2) == 0 && kw >= 2) return STEM_PAIR;
-  if (Cin < 8 && st == 1) return STEM_PAD8;
+  if (Cin < 8 && st == 1 && g_stem_pad8) return STEM_PAD8;
   return STEM_NONE;
 }
 

@@ -188,6 +188,86 @@ __global__ __launch_bounds__(PT) void maxpool_bwd_relu_bias_kernel(
   }
 }
 
+// The same for a tiling pool (k == s, no padding, H % k == W % k == 0:
+// VGG's 2x2/2): one thread per (pooled pixel, 8 channels) reads dy and the
+// argmax bytes ONCE and writes its whole k x k window (dz at the argmax if
+// its ReLU was active, zeros elsewhere), four pooled pixels' loads in flight
+// per thread.  Few blocks (~512 per launch): every block adds one partial
+// per channel into the bias gradient, and thousands of same-address fp32
+// atomics per channel serialise in L2 (the first version, 8192 blocks, ran at
+// 0.9 TB/s; profiles/r5_vgg.md).
+template <typename T>
+__global__ __launch_bounds__(PT) void maxpool_bwd_relu_bias_tiled_kernel(
+    const T* __restrict__ dy, const uint8_t* __restrict__ arg, T* __restrict__ dx,
+    float* __restrict__ dbias, int64_t gstride, int Cper, int B, int H, int W, int C, int Ho,
+    int Wo, int k, int64_t qpb) {
+  constexpr int V = 8, U = 4;
+  __shared__ float red[PT * V];
+  const int cv = C / V;
+  const int cw = cv < PT ? cv : PT;
+  const int lanes = PT / cw;
+  const int j = threadIdx.x % cw, l = threadIdx.x / cw;
+  const int cg = blockIdx.x * cw + j;
+  const bool on = l < lanes && cg < cv;
+  const int c0 = cg * V;
+  const int64_t Q = (int64_t)B * Ho * Wo;
+  const int64_t q0 = (int64_t)blockIdx.y * qpb;
+  const int64_t q1 = q0 + qpb < Q ? q0 + qpb : Q;
+  float sum[V] = {};
+  if (on) {
+    for (int64_t qb = q0 + l; qb < q1; qb += U * lanes) {
+      float g[U][V];
+      uint2 pk[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {            // all loads first
+        const int64_t q = qb + (int64_t)u * lanes;
+        if (q < q1) {
+          ldv<V>(dy + q * C + c0, g[u]);
+          pk[u] = *reinterpret_cast<const uint2*>(arg + q * C + c0);
+        } else {
+          pk[u] = make_uint2(0u, 0u);
+#pragma unroll
+          for (int i = 0; i < V; ++i) g[u][i] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t q = qb + (int64_t)u * lanes;
+        if (q >= q1) break;
+        uint32_t a[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          a[i] = ((i < 4 ? pk[u].x : pk[u].y) >> (8 * (i & 3))) & 0xffu;
+          if (a[i] & 0x80u) sum[i] += g[u][i];
+        }
+        const int wo = (int)(q % Wo);
+        const int64_t bho = q / Wo;
+        const int ho = (int)(bho % Ho);
+        const int b = (int)(bho / Ho);
+        for (int r = 0; r < k; ++r)
+          for (int t = 0; t < k; ++t) {
+            const uint32_t want = 0x80u | (uint32_t)(r * k + t);
+            float o[V];
+#pragma unroll
+            for (int i = 0; i < V; ++i) o[i] = a[i] == want ? g[u][i] : 0.f;
+            stv<V>(dx + (((int64_t)b * H + ho * k + r) * W + wo * k + t) * C + c0, o);
+          }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[threadIdx.x * V + i] = sum[i];
+  __syncthreads();
+  if (on && l == 0) {
+    for (int ll = 1; ll < lanes; ++ll)
+#pragma unroll
+      for (int i = 0; i < V; ++i) sum[i] += red[(ll * cw + j) * V + i];
+    const int g = c0 / Cper, cc = c0 - g * Cper;
+#pragma unroll
+    for (int i = 0; i < V; ++i) atomicAdd(dbias + (int64_t)g * gstride + cc + i, sum[i]);
+  }
+}
+
 // global average pool: x [B, HW, C] -> y [B, C]
 template <typename T, int V>
 __global__ __launch_bounds__(PT) void gavg_fwd_kernel(const T* __restrict__ x,
@@ -349,8 +429,20 @@ static int cer_maxpool_bwd_relu_bias_t(const T* dy, const uint8_t* arg, T* dx, f
   const int gx = (cv + cw - 1) / cw;
   const int64_t P = (int64_t)B * H * W;
   const int lanes = PT / cw;
-  // ~2048 blocks, at least 4 pixels per lane
-  int64_t gy = (2048 + gx - 1) / gx;
+  if (k == s && pad == 0 && H == Ho * k && W == Wo * k) {
+    // tiling pool: thread per pooled pixel; ~512 blocks (bias atomics per
+    // channel), >= 4 pooled pixels per lane
+    const int64_t Q = (int64_t)B * Ho * Wo;
+    int64_t gy = (512 + gx - 1) / gx;
+    int64_t qpb = (Q + gy - 1) / gy;
+    if (qpb < 4 * lanes) qpb = 4 * lanes;
+    gy = (Q + qpb - 1) / qpb;
+    maxpool_bwd_relu_bias_tiled_kernel<T><<<dim3((unsigned)gx, (unsigned)gy), PT, 0, stream>>>(
+        dy, arg, dx, dbias, gstride, Cper, B, H, W, C, Ho, Wo, k, qpb);
+    return (int)hipGetLastError();
+  }
+  // ~512 blocks (bias atomics per channel), at least 4 pixels per lane
+  int64_t gy = (512 + gx - 1) / gx;
   int64_t ppb = (P + gy - 1) / gy;
   if (ppb < 4 * lanes) ppb = 4 * lanes;
   gy = (P + ppb - 1) / ppb;

@@ -22,7 +22,7 @@ cat $O/host.txt
 { du -sh $R/da8; df -h /tmp | tail -1; } >> $O/make.log
 tail -5 $O/make.log
 echo "cerebro-da, Start time: $(date "+%Y-%m-%d %H:%M:%S")" > $O/global.log
-timeout -k 10 900 python -u -m cerebro_ds_kpgi_amd.runners.run_da_cerebro_standalone --run \
+CER_DA_WINDOW=${WINDOW:-2} timeout -k 10 900 python -u -m cerebro_ds_kpgi_amd.runners.run_da_cerebro_standalone --run \
   --num_epochs 1 --drill_down_scalability --size 1 --backend hip --da --da_root $R/da8 \
   --train_per_partition 160160 --valid_per_partition 6250 \
   --logs_root $O/cerebro-da --models_root $R/models > $O/client.log 2>&1

@@ -267,14 +267,18 @@ def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
         _hip.conv_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("vb", [12, 13, 14])
-def test_wgrad_batch_wide_fp32_vs_fp64(vb):
-    """Batched (deferred) fp32 weight gradients on the wide kernels
-    (cer_wgrad_batch_flush with ids 12-14) over three layers at once."""
-    from cerebro_ds_kpgi_amd.ops import streams
+@pytest.mark.parametrize("narrow", [True, False])
+@pytest.mark.parametrize("vb", [1, 12, 13, 14])
+def test_wgrad_batch_wide_fp32_vs_fp64(vb, narrow):
+    """Batched (deferred) fp32 weight gradients on the register 128x128 and
+    the wide kernels (cer_wgrad_batch_flush with ids 1, 12-14) over three
+    layers at once; ``narrow``: the 64-output-channel layer goes to its own
+    64x64-tile launch (CER_WGB_NARROW, the default) or stays in the batch."""
+    from cerebro_ds_kpgi_amd.ops import _hip, streams
     cases = [CONV_CASES[0], CONV_CASES[1], CONV_CASES[5]]
     keep = streams._BATCH_VARIANT
     streams.set_batch_variant(vb)
+    _hip.lib().cer_wgrad_batch_set_narrow(1 if narrow else 0)
     try:
         errs = []
         made = []
@@ -300,7 +304,8 @@ def test_wgrad_batch_wide_fp32_vs_fp64(vb):
             errs.append(_rel(a.grad.view(G, -1)[:, :dw64[0].numel()], dw64.reshape(G, -1)))
     finally:
         streams.set_batch_variant(keep)
-    print("wgrad batch wide", vb, ["%.1e" % e for e in errs])
+        _hip.lib().cer_wgrad_batch_set_narrow(1)
+    print("wgrad batch wide", vb, narrow, ["%.1e" % e for e in errs])
     assert max(errs) < TOL, errs
 
 
