@@ -4722,9 +4722,10 @@ static void wgb32_launch_sel(hipStream_t stream, const int* idx, int n) {
   }
 }
 
-// Items whose output-channel count N is at most 64 in a 128-row-tile batch
-// would leave half of every tile's rows empty (VGG block 1, ResNet stage 2):
-// they go to a second launch with 64x64 tiles (CER_WGB_NARROW=0: one launch).
+// Items whose output-channel count N (tile rows) or reduction width K (tile
+// columns) is at most 64 would leave half of every 128x128 tile empty (VGG
+// block 1, ResNet stage 2): they go to their own launches with 64x64 /
+// 128x64 tiles (CER_WGB_NARROW=0: one launch).
 static int g_wgb_narrow = -1;
 static bool wgb_narrow() {
   if (g_wgb_narrow < 0) {
@@ -4736,28 +4737,33 @@ static bool wgb_narrow() {
 CER_API void cer_wgrad_batch_set_narrow(int on) { g_wgb_narrow = on ? 1 : 0; }
 
 template <int BM, int BN>
+static void wgb32_launch_one(hipStream_t stream, bool wide, const int* idx, int n) {
+  if (n <= 0) return;
+  if (wide)
+    wgb32_launch_sel<BM, BN, true>(stream, idx, n);
+  else
+    wgb32_launch_sel<BM, BN>(stream, idx, n);
+}
+
+template <int BM, int BN>
 static int wgb32_launch(hipStream_t stream, bool wide = false) {
-  static int idx[4096], nar[4096];
-  int n = 0, nn = 0;
-  const bool split = BM == 128 && wgb_narrow();
+  // 128x128 batches: items with N <= 64 output channels take 64x64 tiles,
+  // items with a K <= 64 reduction width (1x1 convs of 64 input channels)
+  // 128x64 tiles; the rest stay on the batch's tile
+  static int idx[4096], narn[4096], nark[4096];
+  int n = 0, nn = 0, nk = 0;
+  const bool split = BM == 128 && BN == 128 && wgb_narrow();
   for (int k = 0; k < g_wgq32_n; ++k) {
     if (split && g_wgq32[k].N <= 64)
-      nar[nn++] = k;
+      narn[nn++] = k;
+    else if (split && g_wgq32[k].K <= 64)
+      nark[nk++] = k;
     else
       idx[n++] = k;
   }
-  if (nn > 0) {
-    if (wide)
-      wgb32_launch_sel<64, 64, true>(stream, nar, nn);
-    else
-      wgb32_launch_sel<64, 64>(stream, nar, nn);
-  }
-  if (n > 0) {
-    if (wide)
-      wgb32_launch_sel<BM, BN, true>(stream, idx, n);
-    else
-      wgb32_launch_sel<BM, BN>(stream, idx, n);
-  }
+  wgb32_launch_one<64, 64>(stream, wide, narn, nn);
+  wgb32_launch_one<128, 64>(stream, wide, nark, nk);
+  wgb32_launch_one<BM, BN>(stream, wide, idx, n);
   return (int)hipGetLastError();
 }
 
