@@ -247,30 +247,10 @@ def new_stats_arena(device):
     return _StatsArena(d)
 
 
-# CER_BN_SLAB_TILES = T > 0: a layer with many M tiles (the stem, ResNet
-# stage 2: hundreds of 64-row tiles adding into the same channel addresses)
-# gets ceil(tiles / T) slabs, between CER_BN_ATOMIC_SLABS and 16, so fewer
-# fp64 atomics serialise per address (0: every layer STAT_SLABS)
-SLAB_TILES = int(os.environ.get("CER_BN_SLAB_TILES", "0"))
-_SLABS_SET = [STAT_SLABS]
-
-
-def _slabs_for(M):
-    tiles = (M + 63) // 64
-    if SLAB_TILES <= 0:
-        return STAT_SLABS
-    return max(STAT_SLABS, min(16, -(-tiles // SLAB_TILES)))
-
-
 def _stats_buffer(M, C, device):
-    """Zeroed buffer for a conv epilogue's BN partials of an [M, C] output
-    (and the slab count of the conv launch that follows, _slabs_for)."""
+    """Zeroed buffer for a conv epilogue's BN partials of an [M, C] output."""
     if STAT_SLABS > 0:          # [slabs][2][C] doubles (conv.hip SLAB_F64)
-        slabs = _slabs_for(M)
-        if slabs != _SLABS_SET[0]:
-            lib().cer_conv_set_stat_slabs(slabs)
-            _SLABS_SET[0] = slabs
-        n = min(slabs, (M + 63) // 64) * 2 * C * 2
+        n = min(STAT_SLABS, (M + 63) // 64) * 2 * C * 2
     else:
         n = int(lib().cer_conv_stats_floats(M, C))
     a = _ARENA[0]

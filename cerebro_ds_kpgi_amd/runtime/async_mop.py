@@ -838,28 +838,36 @@ def run_worker(eng, chan, hops):
 
 
 class _Lanes(object):
-    """Concurrent pack groups within one batch.  When every group of the
-    batch is past its warm-up (``_Working.replay_ready``: its steps are graph
-    replays, no host-side op runs), group g's work goes to the stream of its
-    lane (``PackGroup.lane``; ``engine.lane_stream``) after that stream has
-    waited for the caller's (hop arrivals, parking); ``join`` makes the
-    caller's stream wait for every lane.  Groups sharing a lane share its
-    stream (and the lane's split-K workspace, baked into their graphs), so
-    they stay serialised.  Otherwise (a group still warming up: its eager
-    steps autotune kernels and must not be timed beside other work; CPU;
-    one group) everything runs on the caller's stream as before."""
+    """Concurrent pack groups within one batch.  A group past its warm-up
+    (``_Working.replay_ready``: its steps are graph replays, no host-side op
+    runs) sends its work to the stream of its lane (``PackGroup.lane``;
+    ``engine.lane_stream``) after that stream has waited for the caller's
+    (hop arrivals, parking); ``join`` makes the caller's stream wait for every
+    lane.  Groups sharing a lane share its stream (and the lane's split-K
+    workspace, baked into their graphs), so they stay serialised.  A group
+    still warming up (its eager steps autotune kernels and must not be timed
+    beside other work) runs on the caller's stream BEFORE any lane work is
+    issued (``order``): in a Hyperopt run new trials keep bringing new pack
+    groups, and a batch with one warming group used to run all of its groups
+    serially.  On the CPU, or with fewer than two ready groups, everything
+    runs on the caller's stream."""
 
     def __init__(self, eng, working, valid):
-        self.active = (len(working) > 1 and eng.device.type == "cuda" and
-                       all(w.replay_ready(valid) for w in working.values()))
+        cuda = eng.device.type == "cuda"
+        self.ready = {k for k, w in working.items() if cuda and w.replay_ready(valid)}
+        self.active = len(self.ready) > 1
         self.eng = eng
         self.main = torch.cuda.current_stream() if self.active else None
         self.used = {}
         if self.active:
             eng.lane_batches += 1
 
-    def on(self, grp):
-        if not self.active:
+    def order(self, working):
+        """Group keys, warming-up groups first (they run on the caller's stream)."""
+        return sorted(working, key=lambda k: k in self.ready)
+
+    def on(self, grp, key=None):
+        if not self.active or (key is not None and key not in self.ready):
             return contextlib.nullcontext()
         st = self.used.get(grp.lane)
         if st is None:
@@ -905,14 +913,15 @@ def _run_batch(eng, chan, hops, rec):
         # one stream per lane (the groups' first steps -- eager warm-up with
         # kernel autotuning, capture -- stay serial on the caller's stream)
         lanes = _Lanes(eng, working, valid=False)
-        for key, w in working.items():
+        for key in lanes.order(working):
+            w = working[key]
             grp = eng.groups[key]
             B = grp.batch_size
             steps = eng.n_train // B
             if rec.get("max_steps"):
                 steps = min(steps, rec["max_steps"])
             steps_of[key] = steps
-            with lanes.on(grp), tr.span("train", sync=eng._sync, arch=key[0], G=w.G,
+            with lanes.on(grp, key), tr.span("train", sync=eng._sync, arch=key[0], G=w.G,
                                         steps=steps):
                 w.prepare(eng.o.hop_optimizer_state)
                 w.train_steps(steps)
@@ -930,14 +939,15 @@ def _run_batch(eng, chan, hops, rec):
                 hops.mark_final(m)
         chan.post_event({"t": "train_done", "rank": rank, "models": models})
         vlanes = _Lanes(eng, working, valid=True)
-        for key, w in working.items():
+        for key in vlanes.order(working):
+            w = working[key]
             grp = eng.groups[key]
             B = grp.batch_size
             vsteps = eng.n_valid // B
             if rec.get("max_steps"):
                 full = max(eng.n_train // B, 1)
                 vsteps = max(1, -(-vsteps * steps_of[key] // full))
-            with vlanes.on(grp), tr.span("valid", sync=eng._sync, arch=key[0], G=w.G,
+            with vlanes.on(grp, key), tr.span("valid", sync=eng._sync, arch=key[0], G=w.G,
                                          steps=vsteps):
                 w.validate(vsteps)
                 if eng.o.sim_valid_seconds:

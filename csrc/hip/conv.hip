@@ -4722,10 +4722,9 @@ static void wgb32_launch_sel(hipStream_t stream, const int* idx, int n) {
   }
 }
 
-// Items whose output-channel count N (tile rows) or reduction width K (tile
-// columns) is at most 64 would leave half of every 128x128 tile empty (VGG
-// block 1, ResNet stage 2): they go to their own launches with 64x64 /
-// 128x64 tiles (CER_WGB_NARROW=0: one launch).
+// Items whose output-channel count N (tile rows) is at most 64 would leave
+// half of every 128x128 tile empty (VGG block 1, ResNet stage 2): they go to
+// their own launch with 64x64 tiles (CER_WGB_NARROW=0: one launch).
 static int g_wgb_narrow = -1;
 static bool wgb_narrow() {
   if (g_wgb_narrow < 0) {
@@ -4747,22 +4746,19 @@ static void wgb32_launch_one(hipStream_t stream, bool wide, const int* idx, int 
 
 template <int BM, int BN>
 static int wgb32_launch(hipStream_t stream, bool wide = false) {
-  // 128x128 batches: items with N <= 64 output channels take 64x64 tiles,
-  // items with a K <= 64 reduction width (1x1 convs of 64 input channels)
-  // 128x64 tiles; the rest stay on the batch's tile
-  static int idx[4096], narn[4096], nark[4096];
-  int n = 0, nn = 0, nk = 0;
+  // 128x128 batches: items with N <= 64 output channels take 64x64 tiles;
+  // the rest stay on the batch's tile.  (Routing K <= 64 items to 128x64
+  // tiles as well measured neutral-to-slower on ResNet-50: profiles/r5_final.md)
+  static int idx[4096], narn[4096];
+  int n = 0, nn = 0;
   const bool split = BM == 128 && BN == 128 && wgb_narrow();
   for (int k = 0; k < g_wgq32_n; ++k) {
     if (split && g_wgq32[k].N <= 64)
       narn[nn++] = k;
-    else if (split && g_wgq32[k].K <= 64)
-      nark[nk++] = k;
     else
       idx[n++] = k;
   }
   wgb32_launch_one<64, 64>(stream, wide, narn, nn);
-  wgb32_launch_one<128, 64>(stream, wide, nark, nk);
   wgb32_launch_one<BM, BN>(stream, wide, idx, n);
   return (int)hipGetLastError();
 }

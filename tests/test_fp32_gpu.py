@@ -272,11 +272,10 @@ def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
 def test_wgrad_batch_wide_fp32_vs_fp64(vb, narrow):
     """Batched (deferred) fp32 weight gradients on the register 128x128 and
     the wide kernels (cer_wgrad_batch_flush with ids 1, 12-14) over three
-    layers at once; ``narrow``: the 64-output-channel layer and the
-    64-input-channel 1x1 layer go to their own 64x64 / 128x64-tile launches
-    (CER_WGB_NARROW, the default) or stay in the batch."""
+    layers at once; ``narrow``: the 64-output-channel layer goes to its own
+    64x64-tile launch (CER_WGB_NARROW, the default) or stays in the batch."""
     from cerebro_ds_kpgi_amd.ops import _hip, streams
-    # N = 64 (64x64 launch), K = 64 (128x64 launch), two wide layers
+    # N = 64 (its own 64x64 launch), a K = 64 1x1 layer and two wide layers
     cases = [CONV_CASES[0], CONV_CASES[1], CONV_CASES[5], (8, 14, 14, 64, 256, 1, 1, 0, 4)]
     keep = streams._BATCH_VARIANT
     streams.set_batch_variant(vb)
