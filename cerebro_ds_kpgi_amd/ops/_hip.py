@@ -272,6 +272,8 @@ _SIGS.update({
     "cer_wgrad_splits": [c_i, c_i, c_i, c_i],
     "cer_conv_set_variant": [c_i, c_i],
     "cer_conv_set_addend_grid": [c_i],
+    "cer_conv_set_addend_mask": [c_p],
+    "cer_bn_set_dres_skip": [c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
     "cer_conv_dgrad_babwd": [c_p, c_i64, c_p, c_i, c_p],
@@ -861,6 +863,24 @@ def conv2d_dgrad(dy, wref, xshape, stride, pad, addend=None, bnlink=None, consum
     as dz = act'(y) * dx with the bias gradient accumulated, and
     ``balink.done`` is set.  ``dy`` may be HL (read as such)."""
     dy_hl = is_hl(dy)
+    if addend is not None and getattr(addend, "masked_grad", False):
+        # a residual gradient never stored: dres = mask * dy (ops.nn.MaskedGrad)
+        # joins in the epilogue through the bit mask where the launch can
+        # apply it, else it is materialised here
+        strided1 = wref.spec.shape[1] == 1 and wref.spec.shape[2] == 1 and pad == 0 and stride > 1
+        cout, cin = wref.spec.shape[0], wref.spec.shape[3]
+        if (strided1 or cout % 8 or cin % 8 or addend.dy.dtype != torch.float32
+                or is_hl(addend.dy) or addend.dy.numel() * 4 >= (1 << 31)):
+            addend = addend.materialize()
+        else:
+            L = lib()
+            L.cer_conv_set_addend_mask(_ptr(addend.mask))
+            try:
+                with _hl_operands(0, dy_hl):
+                    return _conv2d_dgrad(_act(dy, hl_ok=dy_hl), wref, xshape, stride, pad,
+                                         addend.dy, bnlink, False, dy_hl)
+            finally:
+                L.cer_conv_set_addend_mask(None)
     with _hl_operands(0, dy_hl):
         if balink is not None and addend is None and bnlink is None:
             return _conv2d_dgrad_balink(_act(dy, hl_ok=dy_hl), wref, xshape, stride, pad, balink,
@@ -1183,13 +1203,36 @@ def bn_act_fwd_eval(x, residual, gref, bref, rmref, rvref, act, eps):
     return y
 
 
+@contextlib.contextmanager
+def _dres_skip(on):
+    if not on:
+        yield
+        return
+    L = lib()
+    L.cer_bn_set_dres_skip(1)
+    try:
+        yield
+    finally:
+        L.cer_bn_set_dres_skip(0)
+
+
+def dres_skip_ok(x, gref, act, has_res, mask):
+    """The residual gradient of this BN backward can stay unwritten (the
+    consumer recomputes it as mask * dy, ops.nn.MaskedGrad): fp32, aligned,
+    a ReLU residual join whose forward stored its mask as bits."""
+    return (has_res and mask is not None and _act_code(act) == 1 and x.dtype == torch.float32
+            and x.shape[-1] % 8 == 0 and gref.spec.shape[0] % 8 == 0)
+
+
 def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nslab=0,
-               hl_out=False, mask=None):
+               hl_out=False, mask=None, skip_dres=False):
     """BN backward; ``part`` / ``nslab``: the (sum dz, sum dz*xhat) partials
     already computed by the dgrad epilogue that produced dy.  ``hl_out``: dx
     (the conv-output gradient) in HL format for the conv's dgrad / wgrad
     (tagged ``_cer_hl``); the residual gradient stays fp32.  ``mask``: the
-    forward's activation bits of a residual join, read instead of y."""
+    forward's activation bits of a residual join, read instead of y.
+    ``skip_dres`` (``dres_skip_ok``): the residual gradient is not written
+    (returned as None; bn.hip cer_bn_set_dres_skip)."""
     use_mask = mask is not None and has_res and _act_code(act) in (1, 6)
     if use_mask:
         y = mask
@@ -1199,7 +1242,8 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
     M = x.numel() // C
     Cper = gref.spec.shape[0]
     dx = torch.empty_like(x)
-    dres = torch.empty_like(x) if has_res else None
+    skip_dres = skip_dres and use_mask
+    dres = torch.empty_like(x) if has_res and not skip_dres else None
     ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
     gp, gs = gref.work_ptr()
     bp, bs = bref.work_ptr()
@@ -1207,7 +1251,7 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
     dbp, _ = bref.grad_ptr()
     if hl_out:
         dx._cer_hl = True
-    with _hl_out(hl_out), mask_in(use_mask):
+    with _hl_out(hl_out), mask_in(use_mask), _dres_skip(skip_dres):
         if part is not None and nslab > 0:
             rc = _fn("cer_bn_bwd_part", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd),
                                        c_p(gp), gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs,

@@ -115,11 +115,50 @@ class GradJoin(object):
         return self.take()
 
 
+class MaskedGrad(object):
+    """A residual join's gradient dres = mask * dy that was never stored: the
+    BN backward of a ReLU(BN(z) + residual) unit skips writing it
+    (``bn_act_bwd(skip_dres=True)``) and parks this in the residual's
+    GradJoin; the other consumer's dgrad epilogue adds dy where the forward's
+    activation bits are set (``conv2d_dgrad``, conv.hip addend_mask).  Saves a
+    full-size write and keeps the read the same (dy instead of dres).
+    ``materialize()`` is the fallback for any other consumer."""
+    __slots__ = ("dy", "mask")
+    masked_grad = True
+
+    def __init__(self, dy, mask):
+        self.dy, self.mask = dy, mask
+
+    @property
+    def is_cuda(self):
+        return self.dy.is_cuda
+
+    @property
+    def device(self):
+        return self.dy.device
+
+    def record_stream(self, s):
+        self.dy.record_stream(s)
+        self.mask.record_stream(s)
+
+    def materialize(self):
+        C = self.dy.shape[-1]
+        bits = (self.mask.view(-1, C // 8).unsqueeze(-1) >>
+                torch.arange(8, device=self.mask.device, dtype=torch.uint8)) & 1
+        return self.dy * bits.view(self.dy.shape).to(self.dy.dtype)
+
+
+# CER_DRES_LAZY=0: residual gradients are stored by the BN backward as before
+DRES_LAZY = os.environ.get("CER_DRES_LAZY", "1") != "0"
+
+
 def _join_after(join, g):
     """Join a gradient computed without the fused add (torch paths)."""
     if join is None or g is None:
         return g
     other = join.join(g)
+    if other is not None and getattr(other, "masked_grad", False):
+        other = other.materialize()
     return None if other is None else g + other
 
 
@@ -430,19 +469,26 @@ class PackedConvBNAct(torch.autograd.Function):
         hl_bwd = (ctx.x4 is None and use_hip("conv", x) and _bn_hip(z, gref)
                   and wref.spec.shape[0] % 8 == 0 and wref.spec.shape[3] % 8 == 0)
         link = ctx.link
+        # first arrival at the residual's join: park dres = mask * dy unstored
+        lazy = (DRES_LAZY and ctx.res_join is not None and ctx.needs_input_grad[1]
+                and ctx.res_join.pending is None and _bn_hip(z, gref)
+                and _hip().dres_skip_ok(z, gref, ctx.relu, ctx.has_res, ctx.mask))
+        mask = ctx.mask
         if link is not None and link.part is not None:
             # partials from the consumer's dgrad epilogue
             dz, dres = _hip().bn_act_bwd(dy, z, y, mean, invstd, gref, bref, ctx.relu,
                                          ctx.has_res, part=link.part, nslab=link.nslab,
-                                         hl_out=hl_bwd, mask=ctx.mask)
+                                         hl_out=hl_bwd, mask=ctx.mask, skip_dres=lazy)
             link.part = None
         else:
             dz, dres = _bn_backward(ctx, dy, z, y, mean, invstd, gref, bref, hl_out=hl_bwd,
-                                    mask=ctx.mask)
+                                    mask=ctx.mask, skip_dres=lazy)
         if link is not None:
             link.z = link.mean = link.invstd = link.mask = None
         ctx.mask = None
-        if ctx.res_join is not None and ctx.needs_input_grad[1]:
+        if lazy and dres is None:
+            ctx.res_join.join(MaskedGrad(dy, mask))
+        elif ctx.res_join is not None and ctx.needs_input_grad[1]:
             dres = _join_after(ctx.res_join, dres)
         if ctx.x4 is not None:
             x4, wref, pad = ctx.x4, ctx.wref, ctx.pad
@@ -457,10 +503,11 @@ class PackedConvBNAct(torch.autograd.Function):
                 None, None, None)
 
 
-def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False, mask=None):
+def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False, mask=None,
+                 skip_dres=False):
     if _bn_hip(x, gref):
         return _hip().bn_act_bwd(dy, x, y, mean, invstd, gref, bref, ctx.relu, ctx.has_res,
-                                 hl_out=hl_out, mask=mask)
+                                 hl_out=hl_out, mask=mask, skip_dres=skip_dres)
     C = x.shape[-1]
     dz = _act_grad(dy.reshape(-1, C).float(), y.reshape(-1, C), ctx.relu)
     n = dz.shape[0]

@@ -817,6 +817,13 @@ static int g_mask_in = 0;
 CER_API void cer_bn_set_mask_out(void* mask) { g_mask_out = reinterpret_cast<uint8_t*>(mask); }
 CER_API void cer_bn_set_mask_in(int on) { g_mask_in = on ? 1 : 0; }
 
+// the NEXT backward launches of a residual-join BN leave dres unwritten
+// (cer_bn_set_dres_skip; ops.nn.MaskedGrad: the consumer of the residual's
+// gradient recomputes dres = mask * dy in its dgrad epilogue instead of
+// reading a stored copy); aligned widths only
+static int g_dres_skip = 0;
+CER_API void cer_bn_set_dres_skip(int on) { g_dres_skip = on ? 1 : 0; }
+
 int bn_mask_mode(int act, int has_res) {
   if (act == 0) return YM_NONE;
   if (act == 1 && !has_res && g_zmask) return YM_Z;
@@ -870,7 +877,7 @@ static int bn_bwd_ragged(const T* dy, const T* x, const T* y, const float* mean,
                          const T* beta, int64_t beta_stride, float* dgamma, float* dbeta,
                          int64_t grad_stride, T* dx, T* dres, float* ws, float* part, int64_t M,
                          int C, int Cper, int act, hipStream_t stream) {
-  if (act >> 8) return (int)hipErrorInvalidValue;
+  if (act >> 8 || g_dres_skip) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C, 1);
   dim3 rg, ag;
   int rrows, arows;
@@ -1050,7 +1057,8 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
   // mask source: none / y / recomputed from x (see the header); a residual
   // join's mask depends on the residual, so it needs y
-  const int ym = bn_mask_mode(act, dres != nullptr);
+  const int ym = bn_mask_mode(act, dres != nullptr || g_dres_skip);
+  if (g_dres_skip) dres = nullptr;
   const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
   const int nslab = pre_nslab > 0 ? pre_nslab : (int)rg.y;
   if (pre_nslab <= 0) {

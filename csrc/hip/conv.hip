@@ -124,6 +124,9 @@ struct NTParams {
   const bf16_t* addend = nullptr;  // optional: out += addend (same layout as out), rounded once
                                    // (dgrad of a tensor with two consumers: the other one's
                                    // input gradient joins here instead of in an add kernel)
+  const uint8_t* addend_mask = nullptr;  // fp32: the addend counts only where this bit mask
+                                         // ([M][ldc / 8] bytes) is set (a residual join's
+                                         // dres = mask * dy, never stored: ops.nn.MaskedGrad)
   BNBwdEpi bb = BNBwdEpi{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0,
                          0, 0};
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
@@ -189,6 +192,13 @@ constexpr int YM_BIAS = 4;
 
 __device__ __forceinline__ bool act_pass(int act, float y) {
   return act == 6 ? (y > 0.f && y < 6.f) : (act ? y > 0.f : true);
+}
+
+// the addend-mask bits of element el (of [M][ldc]) and the next 3 (el % 4 ==
+// 0 on the vector paths: one byte); all set without a mask
+__device__ __forceinline__ uint32_t addend_bits(const NTParams& p, int64_t el) {
+  if (!p.addend_mask) return 0xfu;
+  return (uint32_t)p.addend_mask[el >> 3] >> (uint32_t)(el & 7);
 }
 
 // the block's per-channel sums (xch rows 0 and 2: the two M-direction waves)
@@ -1880,7 +1890,11 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
       if (vec) {
         if (adb) {
           const float4 a = *reinterpret_cast<const float4*>(adb + go);
-          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+          const uint32_t am = addend_bits(p, go + (int64_t)cfg * p.N);
+          v[0] += am & 1u ? a.x : 0.f;
+          v[1] += am & 2u ? a.y : 0.f;
+          v[2] += am & 4u ? a.z : 0.f;
+          v[3] += am & 8u ? a.w : 0.f;
         }
         if (bstat && bb.ym == YM_BIAS) {
           const float4 y4 = *reinterpret_cast<const float4*>(zb + go);
@@ -1896,7 +1910,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (n + e < p.N) {
-            if (adb) v[e] += adb[go + e];
+            if (adb && (addend_bits(p, go + e + (int64_t)cfg * p.N) & 1u)) v[e] += adb[go + e];
             if (bstat && bb.ym == YM_BIAS) {
               v[e] = act_pass(bb.act, zb[go + e]) ? v[e] : 0.f;
               s[j][e] += v[e];
@@ -2024,6 +2038,8 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   const auto rGa = make_rsrc(bb.gamma, ymz ? EPI_BIG : 0u);
   const auto rBe = make_rsrc(bb.beta, ymz ? EPI_BIG : 0u);
   const auto rAd = make_rsrc(p.addend, p.addend ? EPI_BIG : 0u);
+  const bool amask = p.addend_mask != nullptr;
+  const auto rAm = make_rsrc(p.addend_mask, amask ? EPI_BIG : 0u);
   const auto rZ = make_rsrc(bb.z, bstat ? EPI_BIG : 0u);
   const auto rMk = make_rsrc(bb.y, ymm ? EPI_BIG : 0u);
   float bc[FN][4], mu[FN][4], is[FN][4], ga[FN][4], be[FN][4];
@@ -2042,7 +2058,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
     }
   // one row group's operands: [row in group][j]
   uint4 ad[CH][FN], zz[CH][FN];
-  uint32_t mk[CH][FN];
+  uint32_t mk[CH][FN], amk[CH][FN];
   int64_t orow[FM];
   bool rok[FM];
 #pragma unroll
@@ -2068,6 +2084,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         ad[ii][j] = bload(rAd, off);
         zz[ii][j] = bload(rZ, off);
         mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+        amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
       }
     }
   };
@@ -2099,7 +2116,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         for (int e = 0; e < 4; ++e) {
           v[e] = acc[i][j][e] + bc[j][e];
           v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
-          v[e] += av[e];
+          v[e] += !amask || ((amk[ii][j] >> e) & 1u) ? av[e] : 0.f;
         }
         if (ymb) {                   // bias-act link: dz = act'(y) * dx, written
           const float yv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
@@ -2476,7 +2493,11 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
         if (vec) {
           if (adb) {
             const float4 a = *reinterpret_cast<const float4*>(adb + go);
-            v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+            const uint32_t am = addend_bits(p, go + (int64_t)cfg * p.N);
+            v[0] += am & 1u ? a.x : 0.f;
+            v[1] += am & 2u ? a.y : 0.f;
+            v[2] += am & 4u ? a.z : 0.f;
+            v[3] += am & 8u ? a.w : 0.f;
           }
           if (bstat && bb.ym == YM_BIAS) {
             const float yv[4] = {ypre[i][g].x, ypre[i][g].y, ypre[i][g].z, ypre[i][g].w};
@@ -2491,7 +2512,7 @@ __device__ __forceinline__ void epi32w(const NTParams& p, const f32x16 (&acc)[BM
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (n + e < p.N) {
-              if (adb) v[e] += adb[go + e];
+              if (adb && (addend_bits(p, go + e + (int64_t)cfg * p.N) & 1u)) v[e] += adb[go + e];
               if (bstat && bb.ym == YM_BIAS) {
                 v[e] = act_pass(bb.act, zb[go + e]) ? v[e] : 0.f;
                 s[g][e] += v[e];
@@ -4099,6 +4120,15 @@ static int* g_bb_nslab = nullptr;
 static int g_addend_grid = 0;
 CER_API void cer_conv_set_addend_grid(int st) { g_addend_grid = st; }
 
+// the next fp32 cer_conv_dgrad calls' addend is masked by these bits
+// ([M][ldc / 8] bytes, NTParams::addend_mask; nullptr: off).  Only the
+// aligned, non-strided NN path applies it: the others return an error
+// instead of adding the unmasked addend.
+static const uint8_t* g_addend_mask = nullptr;
+CER_API void cer_conv_set_addend_mask(const void* m) {
+  g_addend_mask = reinterpret_cast<const uint8_t*>(m);
+}
+
 // z, y, gamma, beta: bf16 for cer_conv_dgrad, fp32 for cer_conv_dgrad_f32
 CER_API void cer_conv_dgrad_bnbwd(float* part, const void* z, const void* y,
                                   const float* mean, const float* invstd, const void* gamma,
@@ -4170,6 +4200,12 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
   const int ctot_dy = cout_tot ? cout_tot : G * Cout;
   NTParams p;
   p.addend = reinterpret_cast<const bf16_t*>(addend);  // dx = dgrad + addend (null: dx = dgrad)
+  if (g_addend_mask) {
+    const bool strided1 = kh == 1 && kw == 1 && pad == 0 && st > 1;
+    if (!f32 || !addend || strided1 || Cout % 8 || Cin % 8 || cout_tot || cin_tot)
+      return (int)hipErrorInvalidValue;
+    p.addend_mask = g_addend_mask;
+  }
   p.stats = nullptr;
   p.bias = nullptr;
   p.bias_gstride = 0;
@@ -4188,6 +4224,7 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     p.a_hl = g_hl_dy;
     if (p.a_hl && (cout_tot || cin_tot)) return (int)hipErrorInvalidValue;   // grouped: no HL
   }
+  if (p.addend_mask && !aligned) return (int)hipErrorInvalidValue;
   if (aligned) {
     p.w = reinterpret_cast<const bf16_t*>(w);
     p.w_gstride = w_gstride;
