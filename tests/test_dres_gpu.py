@@ -57,7 +57,8 @@ def test_lazy_residual_gradient_matches_stored(model):
     d = ((g1.double() - g0.double()).norm() / g0.double().norm()).item()
     print(model, "masked residual gradients", n1, "grad rel diff", d)
     assert n0 == 0 and n1 >= (12 if model == "resnet50" else 5)
-    assert torch.equal(l1, l0)
+    # (losses to rounding: the fp64 BN-statistics atomics' order varies run to run)
+    assert ((l1 - l0).abs() / l0.abs()).max().item() < 1e-6
     assert torch.isfinite(g1).all()
     assert d < 1e-5, d
 
