@@ -616,7 +616,7 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ part, int nsl
 
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
-template <typename T, int AU = 2>
+template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
     float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
@@ -656,6 +656,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
   bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
     float v[AU][VEC], rv[AU][VEC];
 #pragma unroll
@@ -683,7 +684,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
   }
 }
 
-template <typename T, int YM, int AU = 2>
+template <typename T, int YM>
 __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     const float* __restrict__ part, int nslab, float* dgamma, float* dbeta, int64_t gstride,
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
@@ -720,6 +721,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
   if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
   for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
     float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
 #pragma unroll
@@ -782,25 +784,6 @@ static int fold_rows() {
     if (g_fold_rows < 1) g_fold_rows = 16;
   }
   return g_fold_rows;
-}
-
-// folded applies (the default path): rows in flight per thread
-// (CER_BN_FOLD_AU: 2 or 4) and target block count (CER_BN_FOLD_TARGET)
-static int g_fold_au = 0, g_fold_target = 0;
-static int fold_au() {
-  if (!g_fold_au) {
-    const char* e = getenv("CER_BN_FOLD_AU");
-    g_fold_au = (e && atoi(e) == 4) ? 4 : 2;
-  }
-  return g_fold_au;
-}
-static int fold_target() {
-  if (!g_fold_target) {
-    const char* e = getenv("CER_BN_FOLD_TARGET");
-    g_fold_target = e ? atoi(e) : APPLY_TARGET;
-    if (g_fold_target < 64) g_fold_target = APPLY_TARGET;
-  }
-  return g_fold_target;
 }
 
 // rows in flight per thread of the streaming apply kernels (CER_BN_AU: 2 or 4)
@@ -953,17 +936,12 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
   if ((nslab & SLAB_F64) || nslab <= fold_max()) {     // fp64 slabs: always few
     dim3 fg;
     int frows;
-    make_grid(M, C, mp, fold_target(), fold_rows(), &fg, &frows);
-    if (fold_au() == 4)
-      bn_apply_fwd_fold<T, 4><<<fg, BN_T, 0, stream>>>(
-          part, nslab, mean_out, invstd_out, rmean, rvar, rstat_stride, eps, momentum, x, res, y,
-          Strided{gamma, gamma_stride}, Strided{beta, beta_stride}, M, C, Cper, frows, act_k, mp,
-          g_mask_out);
-    else
-      bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(
-          part, nslab, mean_out, invstd_out, rmean, rvar, rstat_stride, eps, momentum, x, res, y,
-          Strided{gamma, gamma_stride}, Strided{beta, beta_stride}, M, C, Cper, frows, act_k, mp,
-          g_mask_out);
+    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
+    bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
+                                               rstat_stride, eps, momentum, x, res, y,
+                                               Strided{gamma, gamma_stride},
+                                               Strided{beta, beta_stride}, M, C, Cper, frows, act_k,
+                                               mp, g_mask_out);
     return (int)hipGetLastError();
   }
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
@@ -1100,23 +1078,24 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   if ((nslab & SLAB_F64) || nslab <= fold_max()) {
     dim3 fg;
     int frows;
-    make_grid(M, C, mp, fold_target(), fold_rows(), &fg, &frows);
-#define CER_BWD_FOLD(YMV, AUV)                                                                  \
-  bn_apply_bwd_fold<T, YMV, AUV><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,           \
-                                                         grad_stride, dy, x, y, mean, invstd, gs, \
-                                                         bs, dx, dres, M, C, Cper, frows, act_k,  \
-                                                         mp)
-    const bool au4 = fold_au() == 4;
-    if (ym == YM_NONE) {
-      if (au4) CER_BWD_FOLD(YM_NONE, 4); else CER_BWD_FOLD(YM_NONE, 2);
-    } else if (ym == YM_Z) {
-      if (au4) CER_BWD_FOLD(YM_Z, 4); else CER_BWD_FOLD(YM_Z, 2);
-    } else if (ym == YM_M) {
-      if (au4) CER_BWD_FOLD(YM_M, 4); else CER_BWD_FOLD(YM_M, 2);
-    } else {
-      if (au4) CER_BWD_FOLD(YM_Y, 4); else CER_BWD_FOLD(YM_Y, 2);
-    }
-#undef CER_BWD_FOLD
+    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
+    if (ym == YM_NONE)
+      bn_apply_bwd_fold<T, YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+                                                          grad_stride, dy, x, y, mean, invstd, gs,
+                                                          bs, dx, dres, M, C, Cper, frows, act_k,
+                                                          mp);
+    else if (ym == YM_Z)
+      bn_apply_bwd_fold<T, YM_Z><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
+    else if (ym == YM_M)
+      bn_apply_bwd_fold<T, YM_M><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
+    else
+      bn_apply_bwd_fold<T, YM_Y><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
+                                                       grad_stride, dy, x, y, mean, invstd, gs, bs,
+                                                       dx, dres, M, C, Cper, frows, act_k, mp);
     return (int)hipGetLastError();
   }
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
