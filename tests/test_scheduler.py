@@ -208,3 +208,25 @@ def test_greedy_wave_matching_places_the_whole_slow_pack():
     plain.start_epoch(0)
     plain.pending = [(0, 0), (0, 1), (1, 0), (2, 0), (2, 1)]
     assert plain.assign_many([0, 1]) == {0: 0, 1: 2}
+
+
+def test_class_projection_bounds():
+    """tools.hetero_project --classes (BASELINE config 4): both policies train
+    every (model, partition) pair; with one slot per GPU they tie at N = 8
+    (each sub-epoch waits for the slowest model), more GPUs never take longer,
+    and a class-homogeneous workload gives rotation = greedy at N = 1."""
+    from cerebro_ds_kpgi_amd.tools import hetero_project as hp
+
+    def cls(name, n, b, t1, tg, g):
+        return {"name": name, "n": n, "batch": b, "t": hp._pack_time(t1, tg, g)}
+    classes = [cls("r50_b32", 2, 32, 0.0038, 0.0052, 2), cls("r50_b64", 2, 64, 0.0051, 0.0080, 2),
+               cls("vgg_b32", 2, 32, 0.0080, 0.0113, 2), cls("vgg_b64", 2, 64, 0.0120, 0.0182, 2)]
+    rows = hp.project_classes(classes, workers=(1, 2, 4, 8), seeds=2, train=2048, valid=81)
+    by = {r["workers"]: r for r in rows}
+    assert abs(by[8]["speedup"] - 1.0) < 1e-9
+    for a, b in ((1, 2), (2, 4), (4, 8)):
+        assert by[b]["greedy_s"] <= by[a]["greedy_s"] * 1.001
+        assert by[b]["rotation_s"] <= by[a]["rotation_s"] * 1.001
+    same = hp.project_classes([cls("r50_b32", 8, 32, 0.0038, 0.0052, 2)], workers=(1,), seeds=1,
+                              train=2048, valid=81)[0]
+    assert abs(same["speedup"] - 1.0) < 0.05, same
