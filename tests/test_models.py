@@ -131,3 +131,45 @@ def test_resnet_gradjoin_equals_autograd_sum(name, monkeypatch):
         grads.append((a.grad.clone(), x.grad.clone()))
     torch.testing.assert_close(grads[0][0], grads[1][0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-5, atol=1e-6)
+
+
+def test_masked_grad_materialize_cpu():
+    """ops.nn.MaskedGrad (the residual gradient the BN backward no longer
+    stores): materialize() = dy where the activation bit is set, 0 elsewhere,
+    with the bn.hip bit layout (one byte per 8 channels, bit i = channel i)."""
+    import torch
+    from cerebro_ds_kpgi_amd.ops import nn as P
+    torch.manual_seed(0)
+    dy = torch.randn(2, 3, 5, 24)
+    keep = torch.rand(dy.shape) > 0.4
+    w = (1 << torch.arange(8)).to(torch.int32)
+    mask = (keep.view(-1, 3, 8).to(torch.int32) * w).sum(-1).to(torch.uint8).view(2, 3, 5, 3)
+    g = P.MaskedGrad(dy, mask)
+    assert not g.is_cuda and g.device == dy.device
+    assert torch.equal(g.materialize(), dy * keep)
+    # a torch-path join adds the materialised value
+    j = P.GradJoin()
+    j.join(g)
+    other = torch.ones_like(dy)
+    assert torch.equal(P._join_after(j, other), other + dy * keep)
+
+
+def test_lanes_order_runs_warm_groups_first():
+    """runtime.async_mop._Lanes: groups still warming up come first (they run
+    on the caller's stream before any lane work is issued); on the CPU the
+    lanes are inactive and every group stays on the caller's stream."""
+    import types
+    from cerebro_ds_kpgi_amd.runtime.async_mop import _Lanes
+
+    class W(object):
+        def __init__(self, ready):
+            self.r = ready
+
+        def replay_ready(self, valid):
+            return self.r
+    eng = types.SimpleNamespace(device=types.SimpleNamespace(type="cpu"), lane_batches=0)
+    working = {"a": W(True), "b": W(False), "c": W(True)}
+    lanes = _Lanes(eng, working, valid=False)
+    assert not lanes.active and lanes.ready == set()
+    lanes.ready = {"a", "c"}                     # as on a GPU with two ready groups
+    assert lanes.order(working) == ["b", "a", "c"]
