@@ -97,21 +97,19 @@ class PackedNet(object):
                         link_out and self.bn_links)
 
     def conv_bn(self, x, c, b, training, relu=True, residual=None, anchor=False, join=None,
-                res_join=None, link_out=False, hl_out=False, defer=False):
+                res_join=None, link_out=False, hl_out=False):
         """act(BN(conv(x)) + residual); in training the conv epilogue feeds BN
         its batch statistics (ops.nn.PackedConvBNAct).  ``join`` / ``res_join``:
         a ``P.GradJoin`` shared with the other consumer of ``x`` / ``residual``
         (the two input gradients are summed in a dgrad epilogue).  ``hl_out``:
         the output's only consumer is the next ``conv_bn`` (HL operand format,
-        ops.nn.conv_bn_act).  ``defer`` (no activation): the output is only the
-        residual of the next ``conv_bn``, whose BN apply applies this BN too
-        (ops.nn.PendingBN)."""
+        ops.nn.conv_bn_act)."""
         if not training:
             return self.bn(self.conv(x, c, anchor), b, training, relu, residual)
         return P.conv_bn_act(x, self.ref(c.w), self.ref(b.g), self.ref(b.b), self.ref(b.rm),
                              self.ref(b.rv), c.stride, c.pad, relu, residual, self.bn_momentum,
                              self.bn_eps, self.anchor if anchor else None, join, res_join,
-                             link_out and self.bn_links, hl_out, defer)
+                             link_out and self.bn_links, hl_out)
 
     def bucket_mark(self, x, first_spec_above):
         """Gradient-bucket boundary: in backward, once the gradient reaches

@@ -40,9 +40,6 @@ from ..ops.backend import get_backend
 # c1 / c2 in forward and, being created after c1, its backward runs ahead of
 # c1's (autograd's order) on the branch stream, beside c2 / c1's backward
 _SC_BRANCH = os.environ.get("CER_SC_BRANCH", "1") == "1"
-# the shortcut's BN apply deferred into the block's last apply, which
-# computes act(BN(z) + BN_s(zs)) (ops.nn.PendingBN; CER_SC_DEFER=1: on)
-_SC_DEFER = os.environ.get("CER_SC_DEFER", "0") == "1"
 
 _BOTTLENECK = {50: [3, 4, 6, 3], 101: [3, 4, 23, 3], 152: [3, 8, 36, 3]}
 _BASIC = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}
@@ -143,8 +140,7 @@ class PackedResNet(PackedNet):
                 fork = torch.cuda.Event()
                 fork.record(cur)
             elif "cs" in blk:
-                sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j,
-                                  defer=_SC_DEFER)
+                sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False, join=j)
             rj = None if "cs" in blk else j
             if "cs" not in blk:
                 sc = x
@@ -163,7 +159,7 @@ class PackedResNet(PackedNet):
                 try:
                     with torch.cuda.stream(bs):
                         sc = self.conv_bn(x, blk["cs"], blk["bs"], training, relu=False,
-                                          join=j, defer=_SC_DEFER)
+                                          join=j)
                 finally:
                     streams.set_branch_parent(x.device.index, None)
             if self.bottleneck:

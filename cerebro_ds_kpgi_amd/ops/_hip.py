@@ -274,7 +274,6 @@ _SIGS.update({
     "cer_conv_set_addend_grid": [c_i],
     "cer_conv_set_addend_mask": [c_p],
     "cer_bn_set_dres_skip": [c_i],
-    "cer_bn_set_res_bn": [c_p, c_i, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p, c_i64],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
     "cer_conv_dgrad_babwd": [c_p, c_i64, c_p, c_i, c_p],
@@ -682,36 +681,33 @@ def conv2d_fwd_stats(x, wref, stride, pad):
 
 
 def _bn_from_part(z, part, nslab, residual, gref, bref, rmref, rvref, act, momentum, eps,
-                  hl_out=False, res_bn=None):
+                  hl_out=False):
     mask = new_mask(z) if mask_ok(z, _act_code(act), residual) else None
     y, mean, invstd = bn_act_fwd_train_part(z, residual, gref, bref, rmref, rvref, act, momentum,
-                                            eps, part, nslab, hl_out=hl_out, mask=mask,
-                                            res_bn=res_bn)
+                                            eps, part, nslab, hl_out=hl_out, mask=mask)
     if mask is not None:
         y._cer_mask = mask
     return y, z, mean, invstd
 
 
 def conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                      stride, pad, stem=False, hl_out=False, res_bn=None):
+                      stride, pad, stem=False, hl_out=False):
     """Fused training unit: conv (+ BN statistics into the fp64 slabs in the
     GEMM epilogue) then one BN-apply pass that folds the finalize.
     Returns (y, z, mean, invstd, x4) — z the conv output (BN input), x4
     the repacked stem input (stem path) or None.  ``x`` may be HL (read as
     such); ``hl_out``: write y in HL format (its only consumer is a conv;
     taken only without a residual and for act none / ReLU, the cases whose
-    BN backward never reads y); ``res_bn``: the residual is a deferred BN's
-    input (ops.nn.PendingBN; not on the stem path)."""
+    BN backward never reads y)."""
     x_hl = is_hl(x)
     with _hl_operands(x_hl, 0):
         return _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum,
                                   eps, stride, pad, stem, x_hl,
-                                  hl_out and residual is None and _act_code(act) in (0, 1),
-                                  res_bn)
+                                  hl_out and residual is None and _act_code(act) in (0, 1))
 
 
 def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentum, eps,
-                       stride, pad, stem, x_hl=False, hl_out=False, res_bn=None):
+                       stride, pad, stem, x_hl=False, hl_out=False):
     x = _act(x, hl_ok=x_hl)
     B, H, W, GC = x.shape
     G = wref.G
@@ -752,7 +748,7 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
             launch, x.dtype, after_tune=part.zero_)
     launch()
     return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
-                         momentum, eps, hl_out=hl_out and hl_ok(z), res_bn=res_bn) + (None,)
+                         momentum, eps, hl_out=hl_out and hl_ok(z)) + (None,)
 
 
 def stem_mode(x, wref, stride, pad):
@@ -1161,40 +1157,11 @@ def bn_act_fwd_train(x, residual, gref, bref, rmref, rvref, act, momentum, eps):
     return y, mean, invstd
 
 
-@contextlib.contextmanager
-def _res_bn(pend):
-    """The next BN apply's residual is ``pend``'s BN input (bn.hip
-    cer_bn_set_res_bn): that BN is applied inside the apply, and its
-    statistics / running statistics are written there."""
-    if pend is None:
-        yield
-        return
-    gp, gs = pend.gref.work_ptr()
-    bp, bs = pend.bref.work_ptr()
-    rmp, rs = pend.rmref.master_ptr()
-    rvp, _ = pend.rvref.master_ptr()
-    L = lib()
-    L.cer_bn_set_res_bn(_ptr(pend.part), int(pend.nslab), c_p(gp), gs, c_p(bp), bs,
-                        _ptr(pend.mean), _ptr(pend.invstd), c_p(rmp), c_p(rvp), rs)
-    try:
-        yield
-    finally:
-        L.cer_bn_set_res_bn(None, 0, None, 0, None, 0, None, None, None, None, 0)
-
-
-def res_bn_ok(z, nslab, gref):
-    """A conv_bn unit's BN apply may be deferred into its consumer's apply
-    (ops.nn.PendingBN): fp32, aligned widths, fp64 conv-epilogue slabs."""
-    return (z.dtype == torch.float32 and z.shape[-1] % 8 == 0 and gref.spec.shape[0] % 8 == 0
-            and bool(int(nslab) & SLAB_F64))
-
-
 def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, eps, part,
-                          nslab, hl_out=False, mask=None, res_bn=None):
+                          nslab, hl_out=False, mask=None):
     """BN forward from conv-epilogue partials (cer_conv_fwd_stats);
     ``hl_out``: y in HL format (tagged ``_cer_hl``); ``mask``: also write
-    the activation mask as bits (``mask_ok`` / ``new_mask``); ``res_bn``: the
-    residual is a deferred BN's input (``_res_bn``, ops.nn.PendingBN)."""
+    the activation mask as bits (``mask_ok`` / ``new_mask``)."""
     x = _act(x)
     C = x.shape[-1]
     M = x.numel() // C
@@ -1208,7 +1175,7 @@ def bn_act_fwd_train_part(x, residual, gref, bref, rmref, rvref, act, momentum, 
     rmp, rs = rmref.master_ptr()
     rvp, _ = rvref.master_ptr()
     res = _same(residual, x) if residual is not None else None
-    with _hl_out(hl_out), _mask_out(mask), _res_bn(res_bn):
+    with _hl_out(hl_out), _mask_out(mask):
         rc = _fn("cer_bn_fwd_train_part", x)(_ptr(x), _ptr(res), _ptr(y), c_p(gp), gs, c_p(bp),
                                          bs, c_p(rmp), c_p(rvp), rs, _ptr(mean), _ptr(invstd),
                                          _ptr(ws), _ptr(part), int(nslab), M, C, Cper, eps,

@@ -400,51 +400,6 @@ class PackedBNAct(torch.autograd.Function):
         return dx, dres, None, None, None, None, None, None, None, None
 
 
-class PendingBN:
-    """A conv_bn unit whose BN apply is deferred into its consumer's apply:
-    ResNet's projection shortcut (no activation), whose output is read only
-    as the residual of its block's last unit.  That unit's apply computes
-    act(BN(z) + BN_s(zs)) (bn.hip ResBN), so the shortcut's own apply launch
-    and its output tensor disappear.  The shortcut unit returns its conv
-    output zs itself, tagged ``_cer_pending_bn``; the consumer's apply writes
-    this BN's mean / invstd (which the shortcut's backward reads) and its
-    running statistics.  Any other consumer calls ``materialize`` (the
-    deferred apply, on its own)."""
-
-    def __init__(self, z, part, nslab, gref, bref, rmref, rvref, momentum, eps):
-        self.z, self.part, self.nslab = z, part, nslab
-        self.gref, self.bref, self.rmref, self.rvref = gref, bref, rmref, rvref
-        self.momentum, self.eps = momentum, eps
-        C = z.shape[-1]
-        self.mean = torch.empty(C, dtype=torch.float32, device=z.device)
-        self.invstd = torch.empty(C, dtype=torch.float32, device=z.device)
-        self.done = False
-
-    def claim(self):
-        """The consumer's apply takes the deferred BN (once)."""
-        assert not self.done, "a deferred BN was applied twice"
-        self.done = True
-        if self.z.is_cuda:       # (made on the branch stream, used on this one)
-            cur = torch.cuda.current_stream(self.z.device)
-            for t in (self.part, self.mean, self.invstd):
-                t.record_stream(cur)
-        return self
-
-    def materialize(self):
-        """BN_s(zs) as a tensor (a consumer that cannot fuse the apply)."""
-        self.claim()
-        y, mean, invstd = _hip().bn_act_fwd_train_part(
-            self.z, None, self.gref, self.bref, self.rmref, self.rvref, False, self.momentum,
-            self.eps, self.part, self.nslab)
-        self.mean.copy_(mean)
-        self.invstd.copy_(invstd)
-        return y
-
-
-def _pending(t):
-    return getattr(t, "_cer_pending_bn", None) if t is not None else None
-
-
 class PackedConvBNAct(torch.autograd.Function):
     """y = act(BN(conv(x)) + residual) in training mode — the ResNet unit.
 
@@ -456,7 +411,7 @@ class PackedConvBNAct(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad, relu,
-                momentum, eps, join=None, res_join=None, link=None, hl_box=None, pend_box=None):
+                momentum, eps, join=None, res_join=None, link=None, hl_box=None):
         ctx.wref, ctx.stride, ctx.pad = wref, stride, pad
         ctx.join, ctx.res_join = join, res_join
         ctx.bnlink = getattr(x, "_cer_bnlink", None)     # x is a linked BN's output
@@ -472,35 +427,14 @@ class PackedConvBNAct(torch.autograd.Function):
         # a branch-stream unit (models/resnet.py shortcut): the stream its
         # block forked from, which consumes its input gradient in backward
         ctx.parent = streams.branch_parent(x.device) if x.is_cuda else None
-        pend = _pending(residual)        # the residual is a deferred BN's input (PendingBN)
-        if pend is not None and not (hip_ok and residual.dtype == torch.float32
-                                     and not pend.done):
-            residual = pend.materialize()
-            pend = None
         if hip_ok:
             h = _hip()
             ctx.x_hl = h.is_hl(x)        # an HL-format input (see conv_bn_act hl_out)
             # narrow first layer: pixel-pair path; its repacked input feeds the wgrad
             stem = not x.requires_grad and h.stem_ok(x, wref, stride, pad)
-            if pend is not None and stem:
-                residual, pend = pend.materialize(), None
-            y = None
-            if (pend_box is not None and not stem and residual is None and not relu
-                    and not ctx.x_hl and x.dtype == torch.float32):
-                # this unit's apply is deferred into its consumer's (PendingBN)
-                z, part, nslab = h.conv2d_fwd_stats(x, wref, stride, pad)
-                if h.res_bn_ok(z, nslab, gref):
-                    pb = PendingBN(z, part, nslab, gref, bref, rmref, rvref, momentum, eps)
-                    y, mean, invstd = z, pb.mean, pb.invstd
-                    pend_box[0] = pb
-                else:
-                    y, z, mean, invstd = h._bn_from_part(z, part, nslab, None, gref, bref, rmref,
-                                                         rvref, relu, momentum, eps)
-            if y is None:
-                y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
-                    x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride,
-                    pad, stem=stem, hl_out=hl_box is not None and not stem and residual is None,
-                    res_bn=pend.claim() if pend is not None else None)
+            y, z, mean, invstd, ctx.x4 = h.conv_bn_fwd_train(
+                x, wref, gref, bref, rmref, rvref, residual, relu, momentum, eps, stride, pad,
+                stem=stem, hl_out=hl_box is not None and not stem and residual is None)
             # a residual join's activation mask as bits (ops._hip mask_ok)
             ctx.mask = getattr(y, "_cer_mask", None)
             if hl_box is not None:
@@ -566,7 +500,7 @@ class PackedConvBNAct(torch.autograd.Function):
         if ctx.parent is not None and dx is not None:
             dx.record_stream(ctx.parent)      # consumed on the parent stream
         return (dx, dres, None, None, None, None, None, None, None, None, None, None, None, None,
-                None, None, None, None)
+                None, None, None)
 
 
 def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False, mask=None,
@@ -591,7 +525,7 @@ def _bn_backward(ctx, dy, x, y, mean, invstd, gref, bref, hl_out=False, mask=Non
 
 def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, residual=None,
                 momentum=0.1, eps=1e-5, anchor=None, join=None, res_join=None, link_out=False,
-                hl_out=False, defer=False):
+                hl_out=False):
     """``join``: GradJoin shared with the other consumer of ``x``;
     ``res_join``: GradJoin shared with the other consumer of ``residual``;
     ``link_out``: the output's whole gradient comes out of one consumer dgrad
@@ -600,16 +534,11 @@ def conv_bn_act(x, wref, gref, bref, rmref, rvref, stride=1, pad=0, relu=True, r
     it is written in HL format (``_hip.is_hl``: the pre-split operand of the
     consumer's 3-pass kernels, bit-identical operands, no split VALU there).
     (Folding the BN apply into the consumer conv's operand loads was measured
-    slower at 1, 2 and 8 configs and removed: profiles/r3_resnet50_1cfg_fp32.md.)
-    ``defer`` (no activation): the output's only consumer is the ``residual``
-    of another conv_bn_act, whose apply applies this BN too (PendingBN)."""
+    slower at 1, 2 and 8 configs and removed: profiles/r3_resnet50_1cfg_fp32.md.)"""
     link = BNLink() if link_out else None
     box = [False] if hl_out else None
-    pbox = [None] if defer and not relu and residual is None else None
     y = PackedConvBNAct.apply(x, residual, anchor, wref, gref, bref, rmref, rvref, stride, pad,
-                              relu, momentum, eps, join, res_join, link, box, pbox)
-    if pbox is not None and pbox[0] is not None:
-        y._cer_pending_bn = pbox[0]
+                              relu, momentum, eps, join, res_join, link, box)
     if link is not None:
         y._cer_bnlink = link
     if box is not None and box[0]:

@@ -614,134 +614,46 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ part, int nsl
     fold_partials(part, nslab, C, mp, cbk, red, a8, b8);
 }
 
-// two fp64 slab sets of the same channels at once (bn_apply_fwd_fold RBN)
-__device__ __forceinline__ void fold2_f64(const double* __restrict__ p1, int n1,
-                                          const double* __restrict__ p2, int n2, int C,
-                                          const Map& mp, int cbk, float* red, float* a8,
-                                          float* b8, float* a28, float* b28) {
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = cbk * mp.cb + tc * VEC;
-  float* fin = red;                              // [4][cb]
-  if (tr == 0 && c0 < C) {
-    double a[VEC], b[VEC], a2[VEC], b2[VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) a[i] = b[i] = a2[i] = b2[i] = 0.0;
-    const int n = n1 > n2 ? n1 : n2;
-    for (int sl = 0; sl < n; ++sl) {
-      const double* pa = p1 + (int64_t)sl * 2 * C + c0;
-      const double* pb = p2 + (int64_t)sl * 2 * C + c0;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        if (sl < n1) {
-          a[i] += pa[i];
-          b[i] += pa[C + i];
-        }
-        if (sl < n2) {
-          a2[i] += pb[i];
-          b2[i] += pb[C + i];
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      fin[tc * VEC + i] = (float)a[i];
-      fin[mp.cb + tc * VEC + i] = (float)b[i];
-      fin[2 * mp.cb + tc * VEC + i] = (float)a2[i];
-      fin[3 * mp.cb + tc * VEC + i] = (float)b2[i];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    a8[i] = fin[tc * VEC + i];
-    b8[i] = fin[mp.cb + tc * VEC + i];
-    a28[i] = fin[2 * mp.cb + tc * VEC + i];
-    b28[i] = fin[3 * mp.cb + tc * VEC + i];
-  }
-}
-
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
-// A residual that is itself the output of a BatchNorm whose apply was
-// deferred (cer_bn_set_res_bn): ResNet's projection shortcut BN(conv_s(x)).
-// The main path's apply reads the shortcut's conv output zs and folds ITS
-// fp64 slabs too -- out = act(BN(z) + BN_s(zs)) -- so the shortcut's own
-// apply launch and its output tensor (a write and a read of the block's
-// output size) disappear.  The shortcut's mean / invstd (its backward) and
-// running statistics are written here.  part == nullptr: off.
-struct ResBN {
-  const float* part;            // the shortcut conv's fp64 slabs (nslab carries SLAB_F64)
-  int nslab;
-  Strided gamma, beta;
-  float* mean_out;
-  float* invstd_out;
-  float* rmean;
-  float* rvar;
-  int64_t rstat_stride;
-};
-
-// batch mean / invstd of 8 channels from their (sum, sum^2); the block row 0
-// lanes write them and update the running statistics
-__device__ __forceinline__ void bn_stats8(const float* a, const float* b, int64_t M, float eps,
-                                          float momentum, int c0, int g, int cc, bool writer,
-                                          float* mean_out, float* invstd_out, float* rmean,
-                                          float* rvar, int64_t rstat_stride, float* mu, float* is) {
+template <typename T>
+__global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
+    const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
+    float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
+    const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
+    int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp,
+    uint8_t* __restrict__ mask_out) {
+  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
+  act &= 0xff;
+  __shared__ float red[FOLD_LDS];
+  float a[VEC], b[VEC];
+  fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const float inv_m = 1.f / (float)M;
-  float var[VEC];
+  float mu[VEC], is[VEC], var[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     mu[i] = a[i] * inv_m;
     var[i] = fmaxf(b[i] * inv_m - mu[i] * mu[i], 0.f);
     is[i] = rsqrtf(var[i] + eps);
   }
-  if (!writer) return;
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    mean_out[c0 + i] = mu[i];
-    invstd_out[c0 + i] = is[i];
-    float* rm = rmean + g * rstat_stride + cc + i;
-    float* rv = rvar + g * rstat_stride + cc + i;
-    const float unb = M > 1 ? var[i] * (float)M / (float)(M - 1) : var[i];
-    *rm = (1.f - momentum) * *rm + momentum * mu[i];
-    *rv = (1.f - momentum) * *rv + momentum * unb;
-  }
-}
-
-// RBN: the residual is a deferred BN's input (ResBN above)
-template <typename T, bool RBN = false>
-__global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
-    const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
-    float* rvar, int64_t rstat_stride, float eps, float momentum, const T* __restrict__ x,
-    const T* __restrict__ res, T* __restrict__ y, Strided gamma, Strided beta,
-    int64_t M, int C, int Cper, int rows_per_slab, int act, Map mp,
-    uint8_t* __restrict__ mask_out, ResBN rb = ResBN{}) {
-  const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
-  act &= 0xff;
-  __shared__ float red[FOLD_LDS];
-  float a[VEC], b[VEC], a2[VEC], b2[VEC];
-  if (RBN)   // fp64 slabs of both (the host checks), loads of the two in flight together
-    fold2_f64(reinterpret_cast<const double*>(part), nslab & (SLAB_F64 - 1),
-              reinterpret_cast<const double*>(rb.part), rb.nslab & (SLAB_F64 - 1), C, mp,
-              blockIdx.x, red, a, b, a2, b2);
-  else
-    fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  if (c0 >= C || tr >= mp.tr_n) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
-  const bool writer = blockIdx.y == 0 && tr == 0;      // one writer per channel
-  float mu[VEC], is[VEC];
-  bn_stats8(a, b, M, eps, momentum, c0, g, cc, writer, mean_out, invstd_out, rmean, rvar,
-            rstat_stride, mu, is);
+  if (blockIdx.y == 0 && tr == 0) {          // one writer per channel
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      mean_out[c0 + i] = mu[i];
+      invstd_out[c0 + i] = is[i];
+      float* rm = rmean + g * rstat_stride + cc + i;
+      float* rv = rvar + g * rstat_stride + cc + i;
+      const float unb = M > 1 ? var[i] * (float)M / (float)(M - 1) : var[i];
+      *rm = (1.f - momentum) * *rm + momentum * mu[i];
+      *rv = (1.f - momentum) * *rv + momentum * unb;
+    }
+  }
   float sc[VEC], sh[VEC];
   bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
-  float sc2[VEC], sh2[VEC];
-  if (RBN) {
-    float mu2[VEC], is2[VEC];
-    bn_stats8(a2, b2, M, eps, momentum, c0, g, cc, writer, rb.mean_out, rb.invstd_out, rb.rmean,
-              rb.rvar, rb.rstat_stride, mu2, is2);
-    bn_scale_shift<T>(rb.gamma, rb.beta, g, cc, mu2, is2, sc2, sh2);
-  }
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
   const int64_t r1 = min(M, r0 + rows_per_slab);
   constexpr int AU = 2;
@@ -762,8 +674,7 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
       float o[VEC];
 #pragma unroll
       for (int i = 0; i < VEC; ++i)
-        o[i] = act_fwd(v[u][i] * sc[i] + sh[i] +
-                           (RBN ? rv[u][i] * sc2[i] + sh2[i] : (res ? rv[u][i] : 0.f)), act);
+        o[i] = act_fwd(v[u][i] * sc[i] + sh[i] + (res ? rv[u][i] : 0.f), act);
       if (hl)
         st8_hl(y + rr * C + c0, o);
       else
@@ -913,21 +824,6 @@ CER_API void cer_bn_set_mask_in(int on) { g_mask_in = on ? 1 : 0; }
 static int g_dres_skip = 0;
 CER_API void cer_bn_set_dres_skip(int on) { g_dres_skip = on ? 1 : 0; }
 
-// the residual of the NEXT training-mode forward apply is a deferred BN's
-// input (ResBN; ops.nn.PendingBN): its fp64 slabs, parameters and the
-// buffers its statistics go to.  part == nullptr clears it.  Only the folded
-// apply (fp64 slabs of both BNs, aligned widths) takes it: other launches
-// return hipErrorInvalidValue while it is set.
-static ResBN g_res_bn{};
-CER_API void cer_bn_set_res_bn(const float* part, int nslab, const void* gamma,
-                               int64_t gamma_stride, const void* beta, int64_t beta_stride,
-                               float* mean_out, float* invstd_out, float* rmean, float* rvar,
-                               int64_t rstat_stride) {
-  g_res_bn = part ? ResBN{part, nslab, Strided{gamma, gamma_stride}, Strided{beta, beta_stride},
-                          mean_out, invstd_out, rmean, rvar, rstat_stride}
-                  : ResBN{};
-}
-
 int bn_mask_mode(int act, int has_res) {
   if (act == 0) return YM_NONE;
   if (act == 1 && !has_res && g_zmask) return YM_Z;
@@ -1021,10 +917,6 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
                              int C, int Cper, float eps, float momentum, int act,
                              hipStream_t stream) {
   const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
-  const bool rbn = g_res_bn.part != nullptr;
-  if (rbn && (!res || !(nslab & SLAB_F64) || !(g_res_bn.nslab & SLAB_F64) || C % VEC ||
-              Cper % VEC))
-    return (int)hipErrorInvalidValue;                   // deferred residual BN: fp64 folds only
   if (C % VEC || Cper % VEC) {
     if (nslab > 0) return (int)hipErrorInvalidValue;    // conv-epilogue partials: aligned only
     return bn_fwd_train_ragged(x, res, y, gamma, gamma_stride, beta, beta_stride, rmean, rvar,
@@ -1045,17 +937,11 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
     dim3 fg;
     int frows;
     make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
-    if (rbn)
-      bn_apply_fwd_fold<T, true><<<fg, BN_T, 0, stream>>>(
-          part, nslab, mean_out, invstd_out, rmean, rvar, rstat_stride, eps, momentum, x, res, y,
-          Strided{gamma, gamma_stride}, Strided{beta, beta_stride}, M, C, Cper, frows, act_k, mp,
-          g_mask_out, g_res_bn);
-    else
-      bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean,
-                                                 rvar, rstat_stride, eps, momentum, x, res, y,
-                                                 Strided{gamma, gamma_stride},
-                                                 Strided{beta, beta_stride}, M, C, Cper, frows,
-                                                 act_k, mp, g_mask_out);
+    bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
+                                               rstat_stride, eps, momentum, x, res, y,
+                                               Strided{gamma, gamma_stride},
+                                               Strided{beta, beta_stride}, M, C, Cper, frows, act_k,
+                                               mp, g_mask_out);
     return (int)hipGetLastError();
   }
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
@@ -1108,7 +994,7 @@ static int cer_bn_apply_fwd_t(const T* x, const T* res, T* y, const float* ws,
                              int64_t beta_stride, int64_t M, int C, int Cper, int act,
                              hipStream_t stream) {
   const int act_k = act | (sizeof(T) == 4 ? g_bn_hl << 8 : 0);   // + HL output bit
-  if (C % VEC || Cper % VEC || g_res_bn.part) return (int)hipErrorInvalidValue;
+  if (C % VEC || Cper % VEC) return (int)hipErrorInvalidValue;
   const Map mp = make_map(C);
   dim3 ag;
   int arows;
@@ -1131,7 +1017,6 @@ static int cer_bn_fwd_eval_t(const T* x, const T* res, T* y, const T* gamma,
                             int64_t gamma_stride, const T* beta, int64_t beta_stride,
                             const float* rmean, const float* rvar, int64_t rstat_stride,
                             int64_t M, int C, int Cper, float eps, int act, hipStream_t stream) {
-  if (g_res_bn.part) return (int)hipErrorInvalidValue;
   const bool rag = (C % VEC) || (Cper % VEC);
   const Map mp = make_map(C, rag ? 1 : VEC);
   dim3 ag;

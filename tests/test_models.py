@@ -133,34 +133,6 @@ def test_resnet_gradjoin_equals_autograd_sum(name, monkeypatch):
     torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-5, atol=1e-6)
 
 
-def test_sc_defer_torch_path_is_plain(monkeypatch):
-    """The deferred shortcut BN (ops.nn.PendingBN) is a HIP-path fusion: on the
-    torch path ``defer`` leaves the shortcut unit a plain conv -> BN, so a
-    ResNet-50 step is the same with and without it."""
-    from cerebro_ds_kpgi_amd.models import create_model_from_mst, resnet
-    from cerebro_ds_kpgi_amd.ops import nn as P
-    from cerebro_ds_kpgi_amd.ops import set_backend
-    from cerebro_ds_kpgi_amd.runtime.arena import Arena
-    set_backend("torch")
-    made = []
-    monkeypatch.setattr(P.PendingBN, "__init__", lambda self, *a, **k: made.append(1))
-    outs = []
-    for defer in (True, False):
-        monkeypatch.setattr(resnet, "_SC_DEFER", defer)
-        net = create_model_from_mst({"model": "resnet50"})
-        a = Arena(net.layout, 1, "cpu", torch.float32)
-        a.init_model(0, 3)
-        net.bind(a)
-        torch.manual_seed(0)
-        x = torch.randn(2, 64, 64, 3)
-        y = net.forward(x, True)
-        y.square().sum().backward()
-        outs.append((y.detach(), a.grad.clone(), a.master.clone()))
-    assert not made
-    for u, v in zip(*outs):
-        assert torch.equal(u, v)
-
-
 def test_masked_grad_materialize_cpu():
     """ops.nn.MaskedGrad (the residual gradient the BN backward no longer
     stores): materialize() = dy where the activation bit is set, 0 elsewhere,
