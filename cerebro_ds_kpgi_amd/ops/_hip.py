@@ -577,13 +577,18 @@ def _select(op, key, launch, dtype, after_tune=None):
     lib().cer_conv_set_variant(op, v)
 
 
+# interleaved timing passes per variant (4 picked the same kernels as 2:
+# r2_ab_kernel_knobs.md)
+TUNE_PASSES = 2
+
+
 def _autotune(op, launch, reps=3, passes=None, after=None, variants=None, times=None):
     """Time every variant (``reps`` back-to-back launches after a warm one)
     over ``passes`` interleaved passes and keep each variant's best pass:
     one noisy measurement no longer pins a slow kernel for the whole run."""
     L = lib()
     if passes is None:
-        passes = int(os.environ.get("CER_TUNE_PASSES", "2"))
+        passes = TUNE_PASSES
     variants = list(range(NVARIANTS) if variants is None else variants)
     best_t = dict.fromkeys(variants)
     for _ in range(max(1, passes)):

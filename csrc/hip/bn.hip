@@ -773,28 +773,10 @@ static int fold_max() {
 }
 CER_API void cer_bn_set_fold(int max_slabs) { g_fold_max = max_slabs; }
 
-// minimum rows per block of a folded apply: every block re-reads the layer's
-// partials, so fewer, fatter blocks cut the redundant L2 traffic
-// (CER_BN_FOLD_ROWS, default 16 = the plain apply grid)
-static int g_fold_rows = 0;
-static int fold_rows() {
-  if (!g_fold_rows) {
-    const char* e = getenv("CER_BN_FOLD_ROWS");
-    g_fold_rows = e ? atoi(e) : 16;
-    if (g_fold_rows < 1) g_fold_rows = 16;
-  }
-  return g_fold_rows;
-}
-
-// rows in flight per thread of the streaming apply kernels (CER_BN_AU: 2 or 4)
-static int g_apply_au = 0;
-static int apply_au() {
-  if (!g_apply_au) {
-    const char* e = getenv("CER_BN_AU");
-    g_apply_au = (e && atoi(e) == 4) ? 4 : 2;
-  }
-  return g_apply_au;
-}
+// minimum rows per block of a folded apply: the plain apply grid's 16 (fatter
+// blocks re-read the partials less but measured flat: r2_ab_kernel_knobs.md;
+// so did 4 instead of 2 rows in flight per thread, the apply kernels' AU)
+constexpr int FOLD_ROWS = 16;
 
 // ReLU mask recomputed from the BN input in backward (YM_Z); 0 = always read y
 static int g_zmask = 1;
@@ -936,7 +918,7 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
   if ((nslab & SLAB_F64) || nslab <= fold_max()) {     // fp64 slabs: always few
     dim3 fg;
     int frows;
-    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
+    make_grid(M, C, mp, APPLY_TARGET, FOLD_ROWS, &fg, &frows);
     bn_apply_fwd_fold<T><<<fg, BN_T, 0, stream>>>(part, nslab, mean_out, invstd_out, rmean, rvar,
                                                rstat_stride, eps, momentum, x, res, y,
                                                Strided{gamma, gamma_stride},
@@ -947,16 +929,10 @@ static int bn_fwd_train_impl(const T* x, const T* res, T* y, const T* gamma,
   bn_finalize_fwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, mean_out,
                                                           invstd_out, rmean, rvar, rstat_stride,
                                                           M, C, Cper, eps, momentum);
-  if (apply_au() == 4)
-    bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                                Strided{gamma, gamma_stride},
-                                                Strided{beta, beta_stride}, M, C, Cper, arows,
-                                                act_k, mp, g_mask_out);
-  else
-    bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                             Strided{gamma, gamma_stride},
-                                             Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
-                                             mp, g_mask_out);
+  bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                           Strided{gamma, gamma_stride},
+                                           Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
+                                           mp, g_mask_out);
   return (int)hipGetLastError();
 }
 
@@ -999,16 +975,10 @@ static int cer_bn_apply_fwd_t(const T* x, const T* res, T* y, const float* ws,
   dim3 ag;
   int arows;
   make_grid(M, C, mp, APPLY_TARGET, APPLY_MIN_ROWS, &ag, &arows);
-  if (apply_au() == 4)
-    bn_apply_fwd<T, 0, 4><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                                Strided{gamma, gamma_stride},
-                                                Strided{beta, beta_stride}, M, C, Cper, arows,
-                                                act_k, mp);
-  else
-    bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
-                                             Strided{gamma, gamma_stride},
-                                             Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
-                                             mp);
+  bn_apply_fwd<T, 0><<<ag, BN_T, 0, stream>>>(x, res, y, ws, nullptr, nullptr, 0, 0.f,
+                                           Strided{gamma, gamma_stride},
+                                           Strided{beta, beta_stride}, M, C, Cper, arows, act_k,
+                                           mp);
   return (int)hipGetLastError();
 }
 
@@ -1078,7 +1048,7 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   if ((nslab & SLAB_F64) || nslab <= fold_max()) {
     dim3 fg;
     int frows;
-    make_grid(M, C, mp, APPLY_TARGET, fold_rows(), &fg, &frows);
+    make_grid(M, C, mp, APPLY_TARGET, FOLD_ROWS, &fg, &frows);
     if (ym == YM_NONE)
       bn_apply_bwd_fold<T, YM_NONE><<<fg, BN_T, 0, stream>>>(part, nslab, dgamma, dbeta,
                                                           grad_stride, dy, x, y, mean, invstd, gs,
@@ -1101,29 +1071,17 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   bn_finalize_bwd<<<cer_blocks(C, FIN_C), FIN_C * FIN_L, 0, stream>>>(part, nslab, ws, dgamma, dbeta,
                                                           grad_stride, C, Cper);
   if (ym == YM_NONE) {
-    if (apply_au() == 4)
-      bn_apply_bwd<T, YM_NONE, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
-                                                     C, Cper, arows, act_k, mp, bs);
-    else
-      bn_apply_bwd<T, YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
-                                                     C, Cper, arows, act_k, mp, bs);
+    bn_apply_bwd<T, YM_NONE><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M,
+                                                   C, Cper, arows, act_k, mp, bs);
   } else if (ym == YM_Z) {
-    if (apply_au() == 4)
-      bn_apply_bwd<T, YM_Z, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act_k, mp, bs);
-    else
-      bn_apply_bwd<T, YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act_k, mp, bs);
+    bn_apply_bwd<T, YM_Z><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                Cper, arows, act_k, mp, bs);
   } else if (ym == YM_M) {
     bn_apply_bwd<T, YM_M><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
                                                 Cper, arows, act_k, mp, bs);
   } else {
-    if (apply_au() == 4)
-      bn_apply_bwd<T, YM_Y, 4><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act_k, mp, bs);
-    else
-      bn_apply_bwd<T, YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
-                                                  Cper, arows, act_k, mp, bs);
+    bn_apply_bwd<T, YM_Y><<<ag, BN_T, 0, stream>>>(dy, x, y, mean, invstd, ws, gs, dx, dres, M, C,
+                                                Cper, arows, act_k, mp, bs);
   }
   return (int)hipGetLastError();
 }

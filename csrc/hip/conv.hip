@@ -3820,23 +3820,18 @@ static void tile_dims(int v, int& bm, int& bn) {
   bn = t == 1 ? 128 : 64;
 }
 
-// split count for a fwd / dgrad GEMM: enough blocks for ~1.5 waves of 256 CUs,
-// >= 4 K tiles per split, within the registered workspace
-// (CER_SK_TARGET blocks, default 384; CER_SK_MAX splits, default 8)
-static int sk_env(const char* name, int dflt, int* cache) {
-  if (*cache <= 0) {
-    const char* e = getenv(name);
-    *cache = (e && atoi(e) > 0) ? atoi(e) : dflt;
-  }
-  return *cache;
-}
-static int g_sk_target = 0, g_sk_max = 0;
+// split count for a fwd / dgrad GEMM: enough blocks for ~1.5 waves of 256 CUs
+// (SK_TARGET), at most SK_MAX splits, >= 4 K tiles per split, within the
+// registered workspace (more, shorter splits lose at one config: each pays
+// the prologue, the partial-slot round trip and the last-arriver reduction;
+// r2_ab_kernel_knobs.md)
+constexpr int SK_TARGET = 384, SK_MAX = 8;
 
 static int nt_splits(const NTParams& p, int G, int bm, int bn, int ks) {
   const long tiles = ntiles(p.M, p.N, bm, bn) * G;
   const int KT = (p.K + ks - 1) / ks;
-  const int target = sk_env("CER_SK_TARGET", 384, &g_sk_target);
-  const int smax = sk_env("CER_SK_MAX", 8, &g_sk_max);
+  const int target = SK_TARGET;
+  const int smax = SK_MAX;
   int s = (int)((target + tiles - 1) / tiles);
   if (s > smax) s = smax;
   if (s > KT / 4) s = KT / 4;
