@@ -46,12 +46,6 @@ _BASIC = {18: [2, 2, 2, 2], 34: [3, 4, 6, 3]}
 
 
 class PackedResNet(PackedNet):
-    # every BN / bias parameter follows its own conv / dense weight in the
-    # layout, and its gradient is produced before that weight's wgrad is
-    # queued: the optimizer update may be split at a weight boundary
-    # (runtime/group.py _AdamSplit)
-    adam_split_ok = True
-
     def __init__(self, depth=50, num_classes=1000, input_hw=112):
         super(PackedResNet, self).__init__()
         self.depth = depth
