@@ -217,9 +217,24 @@ class MOPEngine(object):
         self.hop_watch = None        # parallel.health.HopWatch while a run is armed
         if ctx.initialized and not self.task_parallel:
             # the hop data plane: one communicator, used only by the hop
-            # service (async_mop.HopService / _hop_and_load), warmed here
+            # service (async_mop.HopService / _hop_and_load), warmed here --
+            # under the hop watchdog: the first point-to-point traffic of a
+            # multi-GPU job happens here, and a wedged peer connection would
+            # otherwise hang until the process group's 30-minute timeout
             from ..parallel.hop import hop_group
-            self._hop_group = hop_group(ctx.world, ctx.rank, self.device, ctx.backend)
+            watch = None
+            if ctx.world > 1 and self.o.hop_timeout:
+                from ..parallel.health import HopWatch
+                watch = HopWatch(ctx.rank, ctx.world, self.o.hop_timeout,
+                                 logs_root=self.o.logs_root).start()
+                tok = watch.begin("p2p warm-up", peers=[r for r in range(ctx.world)
+                                                        if r != ctx.rank])
+            try:
+                self._hop_group = hop_group(ctx.world, ctx.rank, self.device, ctx.backend)
+            finally:
+                if watch is not None:
+                    watch.end(tok)
+                    watch.stop()
         self.epoch = 0
         self.failures = []
         self._fired = set()

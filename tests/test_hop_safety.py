@@ -173,3 +173,35 @@ def test_watch_bound_tracks_longest_job():
     assert w.done == [3] and w.check() is None
     w.abort("test")
     assert fired and fired[0]["reason"] == "test"
+
+
+# ---------------------------------------------------------------------------
+def _warm_stall_worker(rank, world, port, outdir):
+    _env(rank, world, port)
+    from cerebro_ds_kpgi_amd.parallel import hop, init_distributed
+    from cerebro_ds_kpgi_amd.runtime.engine import EngineOptions, MOPEngine
+    from test_async_runtime import _cfgs
+    ctx = init_distributed(device_type="cpu")
+    if rank == 1:                      # a peer that never opens its connections
+        hop.warm_p2p = lambda *a, **k: time.sleep(600)
+    MOPEngine(_cfgs(world), ctx, EngineOptions(
+        n_train=16, n_valid=8, compute_dtype="fp32", slots_per_gpu=1, verbose=False,
+        ckpt_every="none", scheduler="rotation", runtime="async", hop_timeout=3.0,
+        logs_root=outdir))
+    with open(os.path.join(outdir, "built_{}.txt".format(rank)), "w") as f:
+        f.write("built")
+
+
+def test_stalled_p2p_warmup_ends_with_diagnostic(tmp_path):
+    """The hop communicator's warm-up (the first point-to-point traffic of a
+    multi-GPU job, in the engine's constructor) runs under the hop watchdog:
+    a peer that never answers ends the waiting rank with EXIT_HOP_STALL and
+    a record naming the warm-up, instead of a 30-minute hang."""
+    from cerebro_ds_kpgi_amd.parallel.health import EXIT_HOP_STALL
+    procs = _spawn(_warm_stall_worker, 2, str(tmp_path))
+    codes, dt = _join_all(procs, 90)
+    assert codes[0] == EXIT_HOP_STALL and codes[1] == EXIT_HOP_STALL, codes
+    assert not (tmp_path / "built_0.txt").exists()
+    d = json.load(open(tmp_path / "hop_stall_rank0.json"))
+    assert d["pending"] and d["pending"][0]["kind"] == "p2p warm-up", d
+    assert d["pending"][0]["peers"] == [1]
