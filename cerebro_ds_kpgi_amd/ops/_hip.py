@@ -41,7 +41,8 @@ IMPLEMENTED = {"adam", "loss", "gather"}
 # on MobileNetV2 (profiles/r4_bn_slabs.md).
 STAT_SLABS = int(os.environ.get("CER_BN_ATOMIC_SLABS", "2"))
 SLAB_F64 = 1 << 24     # conv.hip: a returned slab count with this flag is fp64 slabs
-_RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems"}
+_RET_I64 = {"cer_bn_part_floats", "cer_conv_stats_floats", "cer_stem_wpk_elems",
+            "cer_bn_bwd_f64_floats"}
 
 c_p = ctypes.c_void_p
 c_i64 = ctypes.c_int64
@@ -274,6 +275,8 @@ _SIGS.update({
     "cer_conv_set_addend_grid": [c_i],
     "cer_conv_set_addend_mask": [c_p],
     "cer_bn_set_dres_skip": [c_i],
+    "cer_bn_set_bwd_f64": [c_i],
+    "cer_bn_bwd_f64_floats": [c_i64, c_i, c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
     "cer_conv_dgrad_bnbwd": [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i64, c_i, c_i, c_p],
     "cer_conv_dgrad_babwd": [c_p, c_i64, c_p, c_i, c_p],
@@ -1264,10 +1267,26 @@ def bn_act_bwd(dy, x, y, mean, invstd, gref, bref, act, has_res, part=None, nsla
                                        M, C, Cper, _act_code(act), _stream())
             _check(rc, "cer_bn_bwd_part")
             return dx, dres
-        part = _bn_part(M, C, x.device)
-        rc = _fn("cer_bn_bwd", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd), c_p(gp),
-                              gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx), _ptr(dres),
-                              _ptr(ws), _ptr(part), M, C, Cper, _act_code(act), _stream())
+        # a layer with many row slabs: its partials go into STAT_SLABS fp64
+        # slabs of a zeroed buffer (fp64 atomics), so the apply folds the
+        # finalize as after a dgrad-epilogue link -- one launch less (+0.2 %
+        # at 8 configs, +0.6 % at one: profiles/r5_final.md)
+        L = lib()
+        nf = int(L.cer_bn_bwd_f64_floats(M, C, Cper, STAT_SLABS)) if STAT_SLABS > 0 else 0
+        if nf:
+            a = _ARENA[0]
+            part = (a.take(nf) if a is not None and torch.device(a.device) == x.device
+                    else torch.zeros(nf, dtype=torch.float32, device=x.device))
+        else:
+            part = _bn_part(M, C, x.device)
+        L.cer_bn_set_bwd_f64(STAT_SLABS if nf else 0)
+        try:
+            rc = _fn("cer_bn_bwd", dy)(_ptr(dy), _ptr(x), _ptr(y), _ptr(mean), _ptr(invstd),
+                                  c_p(gp), gs, c_p(bp), bs, c_p(dgp), c_p(dbp), dgs, _ptr(dx),
+                                  _ptr(dres), _ptr(ws), _ptr(part), M, C, Cper, _act_code(act),
+                                  _stream())
+        finally:
+            L.cer_bn_set_bwd_f64(0)
     _check(rc, "cer_bn_bwd")
     return dx, dres
 

@@ -140,7 +140,7 @@ __device__ __forceinline__ void partials_tile(
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
     int64_t M, int C, int rows_per_slab, int act, const Map& mp, int cbk, int slab, float* red,
     const Strided& gamma = Strided{nullptr, 0}, const Strided& beta = Strided{nullptr, 0},
-    int Cper = 1) {
+    int Cper = 1, int f64 = 0) {
   const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
   const int c0 = cbk * mp.cb + tc * V;
   const bool cok = c0 < C && tr < mp.tr_n;
@@ -218,6 +218,12 @@ __device__ __forceinline__ void partials_tile(
       a += rs[k * mp.cb + cl];
       b += rq[k * mp.cb + cl];
     }
+    if (f64) {        // fp64 atomics into slab (row slab % f64) of a zeroed buffer
+      double* dd = reinterpret_cast<double*>(part) + (int64_t)(slab % f64) * 2 * C;
+      atomicAdd(dd + c, (double)a);
+      atomicAdd(dd + C + c, (double)b);
+      continue;
+    }
     float* dst = part + (int64_t)slab * 2 * C;
     stf<SC>(dst + c, a);
     stf<SC>(dst + C + c, b);
@@ -230,10 +236,10 @@ __global__ __launch_bounds__(BN_T) void bn_partials(
     const T* __restrict__ x, const T* __restrict__ dy, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ part,
     int64_t M, int C, int rows_per_slab, int act, Map mp, Strided gamma = Strided{nullptr, 0},
-    Strided beta = Strided{nullptr, 0}, int Cper = 1) {
+    Strided beta = Strided{nullptr, 0}, int Cper = 1, int f64 = 0) {
   __shared__ float red[2 * BN_T * VEC];
   partials_tile<T, MODE, false, YM, V>(x, dy, y, mean, invstd, part, M, C, rows_per_slab, act, mp,
-                                 blockIdx.x, blockIdx.y, red, gamma, beta, Cper);
+                                 blockIdx.x, blockIdx.y, red, gamma, beta, Cper, f64);
 }
 
 // ---------------------------------------------------------------------------
@@ -806,6 +812,28 @@ CER_API void cer_bn_set_mask_in(int on) { g_mask_in = on ? 1 : 0; }
 static int g_dres_skip = 0;
 CER_API void cer_bn_set_dres_skip(int on) { g_dres_skip = on ? 1 : 0; }
 
+// The NEXT backward launches that compute their own partials (no dgrad-epilogue
+// link) may accumulate them by fp64 atomics into n slabs of their part buffer
+// (zeroed by the caller, n * 2 * C doubles), so the apply folds the finalize
+// for any layer size -- the conv epilogues' slab format (SLAB_F64) -- instead
+// of a separate finalize launch for layers with more than fold_max() row
+// slabs.  0 = off (one fp32 slab per row slab).
+static int g_bwd_f64 = 0;
+CER_API void cer_bn_set_bwd_f64(int nslabs) { g_bwd_f64 = nslabs > 0 ? nslabs : 0; }
+
+// floats of zeroed buffer a backward launch of this size would accumulate its
+// partials in with ``nslabs`` fp64 slabs (cer_bn_set_bwd_f64), or 0 when it
+// keeps the fp32 slab format (few row slabs, unaligned widths)
+CER_API int64_t cer_bn_bwd_f64_floats(int64_t M, int C, int Cper, int nslabs) {
+  if (nslabs <= 0 || C % VEC || Cper % VEC) return 0;
+  const Map mp = make_map(C);
+  dim3 rg;
+  int rrows;
+  make_grid(M, C, mp, RED_TARGET, RED_MIN_ROWS, &rg, &rrows);
+  if ((int)rg.y <= fold_max()) return 0;
+  return (int64_t)nslabs * 2 * C * 2;
+}
+
 int bn_mask_mode(int act, int has_res) {
   if (act == 0) return YM_NONE;
   if (act == 1 && !has_res && g_zmask) return YM_Z;
@@ -1030,20 +1058,23 @@ static int bn_bwd_impl(const T* dy, const T* x, const T* y, const float* mean,
   const int ym = bn_mask_mode(act, dres != nullptr || g_dres_skip);
   if (g_dres_skip) dres = nullptr;
   const Strided gs{gamma, gamma_stride}, bs{beta, beta_stride};
-  const int nslab = pre_nslab > 0 ? pre_nslab : (int)rg.y;
+  const int f64 = pre_nslab <= 0 && (int)rg.y > fold_max() ? g_bwd_f64 : 0;
+  const int nslab = pre_nslab > 0 ? pre_nslab
+                                  : f64 ? ((int)rg.y < f64 ? (int)rg.y : f64) | SLAB_F64
+                                        : (int)rg.y;
   if (pre_nslab <= 0) {
     if (ym == YM_NONE)
       bn_partials<T, 1, YM_NONE><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C,
-                                                       rrows, act, mp, gs, bs, Cper);
+                                                       rrows, act, mp, gs, bs, Cper, f64);
     else if (ym == YM_Z)
       bn_partials<T, 1, YM_Z><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                    act, mp, gs, bs, Cper);
+                                                    act, mp, gs, bs, Cper, f64);
     else if (ym == YM_M)
       bn_partials<T, 1, YM_M><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                    act, mp, gs, bs, Cper);
+                                                    act, mp, gs, bs, Cper, f64);
     else
       bn_partials<T, 1, YM_Y><<<rg, BN_T, 0, stream>>>(x, dy, y, mean, invstd, part, M, C, rrows,
-                                                    act, mp, gs, bs, Cper);
+                                                    act, mp, gs, bs, Cper, f64);
   }
   if ((nslab & SLAB_F64) || nslab <= fold_max()) {
     dim3 fg;

@@ -762,3 +762,51 @@ def test_resnext101_trains_on_hip_under_graph():
     assert w.graph is not None, "the step was not captured"
     assert torch.isfinite(w.arena.state).all()
     eng.close()
+
+
+@pytest.mark.parametrize("act,res", [(True, False), (False, False), (True, True)])
+@pytest.mark.parametrize("shape,G", [((8, 56, 56, 64), 1), ((16, 28, 28, 2 * 256), 2)])
+def test_bn_bwd_fp64_slabs_match_staged_fp32(act, res, shape, G, monkeypatch):
+    """BN backward of a layer with many row slabs (no dgrad-epilogue link):
+    partials by fp64 atomics into STAT_SLABS slabs, finalize folded into the
+    apply (bn.hip cer_bn_set_bwd_f64) == fp32 per-slab partials + separate
+    finalize, and both == an fp64 reference."""
+    from cerebro_ds_kpgi_amd.ops import _hip
+    C = shape[-1] // G
+    M = shape[0] * shape[1] * shape[2]
+    assert _hip.lib().cer_bn_bwd_f64_floats(M, shape[-1], C, _hip.STAT_SLABS) > 0
+    specs = [ParamSpec("g", (C,), "gamma"), ParamSpec("b", (C,), "beta"),
+             ParamSpec("rm", (C,), "running_mean"), ParamSpec("rv", (C,), "running_var")]
+    torch.manual_seed(17)
+    x = 2 * torch.randn(shape, device="cuda") + 0.3
+    r = torch.randn(shape, device="cuda") if res else None
+    gy = torch.randn(shape, device="cuda")
+    outs = []
+    for slabs in (_hip.STAT_SLABS, 0):
+        monkeypatch.setattr(_hip, "STAT_SLABS", slabs)
+        a, refs = _make(specs, G, seed=5)
+        a.grad_clean = True
+        a.grad.zero_()
+        xx = x.clone().requires_grad_(True)
+        rr = r.clone().requires_grad_(True) if res else None
+        y = P.bn_act(xx, refs["g"], refs["b"], refs["rm"], refs["rv"], True, act, rr)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xx.grad, rr.grad if res else None, a.grad.clone()))
+    # fp64 reference of the same op (training BN, act under OUR forward mask)
+    gam = refs["g"].master().double().reshape(-1)
+    bet = refs["b"].master().double().reshape(-1)
+    xd = x.double().reshape(-1, shape[-1]).requires_grad_(True)
+    mu = xd.mean(0)
+    var = xd.var(0, unbiased=False)
+    z = (xd - mu) / torch.sqrt(var + 1e-5) * gam + bet
+    if res:
+        z = z + r.double().reshape(-1, shape[-1])
+    mask = (outs[0][0].reshape(-1, shape[-1]) > 0).double() if act else 1.0
+    (z * mask * gy.double().reshape(-1, shape[-1])).sum().backward()
+    for u, v in zip(outs[0], outs[1]):
+        if u is not None:
+            assert _rel(u, v) < 1e-5, _rel(u, v)
+    e = _rel(outs[0][1].reshape(-1, shape[-1]), xd.grad)
+    print("fp64-slab BN backward dx rel vs fp64", e)
+    assert e < TOL
