@@ -275,6 +275,8 @@ _SIGS.update({
     "cer_conv_set_addend_grid": [c_i],
     "cer_conv_set_addend_mask": [c_p],
     "cer_bn_set_dres_skip": [c_i],
+    "cer_stem_set_wgrad_scratch": [c_p],
+    "cer_stem_set_wgrad_zeroed": [c_i],
     "cer_bn_set_bwd_f64": [c_i],
     "cer_bn_bwd_f64_floats": [c_i64, c_i, c_i, c_i],
     "cer_conv_set_splitk": [c_p, c_i64, c_p, c_i],
@@ -735,8 +737,10 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
         x4 = torch.empty((G, B, H, W, int(L.cer_stem_cp(mode))), dtype=x.dtype, device=dev)
         wpk = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=x.dtype,
                           device=dev)
+        x4._cer_dwp = _stem_dwp(G, cout, kh, kw, mode, dev)
 
         def launch():        # conv + BN statistics partials (no running-stat side effects)
+            L.cer_stem_set_wgrad_scratch(_ptr(x4._cer_dwp))
             _check(_fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw,
                                       stride, pad, _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo,
                                       _ptr(part), ctypes.byref(nslab), None, 0, 0, _stream()),
@@ -757,6 +761,13 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
     launch()
     return _bn_from_part(z, part, nslab.value, residual, gref, bref, rmref, rvref, act,
                          momentum, eps, hl_out=hl_out and hl_ok(z)) + (None,)
+
+
+def _stem_dwp(G, cout, kh, kw, mode, device):
+    """fp32 split-K scratch of the stem wgrad (packed layout), zeroed by the
+    stem forward's prep launch (conv.hip cer_stem_set_wgrad_scratch)."""
+    return torch.empty(int(lib().cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=torch.float32,
+                       device=device)
 
 
 def stem_mode(x, wref, stride, pad):
@@ -791,8 +802,12 @@ def stem_fwd_stats(x, wref, stride, pad, bref=None, act=0, stats=True):
     nslab = ctypes.c_int(0)
     wp, ws = wref.work_ptr()
     bp, bs = bref.work_ptr() if bref is not None else (0, 0)
+    dwp = _stem_dwp(G, cout, kh, kw, mode, x.device) if torch.is_grad_enabled() else None
+    if dwp is not None:
+        x4._cer_dwp = dwp
 
     def launch():
+        L.cer_stem_set_wgrad_scratch(_ptr(dwp))
         rc = _fn("cer_stem_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad,
                                 _ptr(x4), _ptr(wpk), _ptr(z), Ho, Wo, _ptr(part),
                                 ctypes.byref(nslab), c_p(bp), bs, _act_code(act), _stream())
@@ -811,15 +826,22 @@ def stem_wgrad(x4, dy, wref, pad, stride=2):
     cout, kh, kw, cin = wref.spec.shape
     L = lib()
     mode = int(L.cer_stem_ok(cin, W, kw, stride, pad))
-    dwp = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=torch.float32,
-                      device=dy.device)
+    # the forward's prep launch zeroed this step's scratch (cer_stem_set_wgrad_scratch)
+    dwp = getattr(x4, "_cer_dwp", None)
+    zeroed = dwp is not None
+    if dwp is None:
+        dwp = torch.empty(int(L.cer_stem_wpk_elems(G, cout, kh, kw, mode)), dtype=torch.float32,
+                          device=dy.device)
     gp, gs = wref.grad_ptr()
 
     def launch():
+        L.cer_stem_set_wgrad_zeroed(int(zeroed))
         rc = _fn("cer_stem_wgrad", x4)(_ptr(x4), B, H, W, cin, G, _ptr(dy), Ho, Wo, cout, kh, kw,
                                   stride, pad, _ptr(dwp), c_p(gp), gs, _stream())
         _check(rc, "cer_stem_wgrad")
-    _select(2, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, dy.dtype)
+    # (the timing launches of a first call accumulate into the scratch: re-zeroed after)
+    _select(2, ("stem", B, H, W, cin, cout, kh, kw, stride, pad, G), launch, dy.dtype,
+            after_tune=dwp.zero_ if zeroed else None)
     launch()
 
 

@@ -4866,11 +4866,10 @@ CER_API int cer_wgrad_splits(int Mred, int N, int K, int G) {
 // (K = kh*kw*8) at the price of 8/Cin x the MFMA work on a tiny layer.
 // ---------------------------------------------------------------------------
 enum { STEM_NONE = 0, STEM_PAD8 = 1, STEM_PAIR = 2 };
+// element i of the input repack: (pixel, config) -> [G][P][CP], channels >= C zero
 template <typename E>
-__global__ __launch_bounds__(256) void stem_repack_kernel(const E* __restrict__ x,
-                                                          E* __restrict__ x4, int64_t P,
-                                                          int G, int C, int CP) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (pixel, config)
+__device__ __forceinline__ void stem_repack_one(const E* __restrict__ x, E* __restrict__ x4,
+                                                int64_t i, int64_t P, int G, int C, int CP) {
   if (i >= P * G) return;
   const int64_t p = i / G;
   const int g = (int)(i - p * G);
@@ -4879,14 +4878,12 @@ __global__ __launch_bounds__(256) void stem_repack_kernel(const E* __restrict__ 
   for (int c = 0; c < CP; ++c) dst[c] = c < C ? src[c] : (E)0;
 }
 
+// element i of the weight re-layout [G][N][kh][kwp][8]
 template <typename E>
-__global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ w,
-                                                          int64_t w_gstride,
-                                                          E* __restrict__ wp, int N, int kh,
-                                                          int kw, int C, int kwp, int G,
-                                                          int pad8) {
+__device__ __forceinline__ void stem_pack_w_one(const E* __restrict__ w, int64_t w_gstride,
+                                                E* __restrict__ wp, int64_t i, int N, int kh,
+                                                int kw, int C, int kwp, int G, int pad8) {
   const int64_t per = (int64_t)N * kh * kwp * 8;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= per * G) return;
   const int g = (int)(i / per);
   int64_t t = i - g * per;
@@ -4901,6 +4898,30 @@ __global__ __launch_bounds__(256) void stem_pack_w_kernel(const E* __restrict__ 
   E v = 0;
   if (s >= 0 && s < kw && c < C) v = w[g * w_gstride + (((int64_t)n * kh + r) * kw + s) * C + c];
   wp[i] = v;
+}
+
+// The stem's per-step preparation in ONE launch: blocks [0, nbx) repack the
+// input, the next nbw blocks re-lay the weights, the rest zero the stem
+// wgrad's split-K scratch of this step (cer_stem_set_wgrad_scratch; nzero
+// floats, a multiple of 4) -- three small dependent launches became one
+template <typename E>
+__global__ __launch_bounds__(256) void stem_prep_kernel(
+    const E* __restrict__ x, E* __restrict__ x4, int64_t P, int G, int C, int CP, int nbx,
+    const E* __restrict__ w, int64_t w_gstride, E* __restrict__ wp, int N, int kh, int kw,
+    int kwp, int pad8, int nbw, float* __restrict__ zero, int64_t nzero) {
+  int b = blockIdx.x;
+  if (b < nbx) {
+    stem_repack_one(x, x4, (int64_t)b * 256 + threadIdx.x, P, G, C, CP);
+    return;
+  }
+  b -= nbx;
+  if (b < nbw) {
+    stem_pack_w_one(w, w_gstride, wp, (int64_t)b * 256 + threadIdx.x, N, kh, kw, C, kwp, G, pad8);
+    return;
+  }
+  b -= nbw;
+  const int64_t k = ((int64_t)b * 256 + threadIdx.x) * 4;
+  if (k < nzero) *reinterpret_cast<float4*>(zero + k) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __global__ __launch_bounds__(256) void stem_fold_grad_kernel(const float* __restrict__ dwp,
@@ -4968,29 +4989,39 @@ static GatherGeom stem_geom(const void* x4, int B, int H, int W, int Ho, int Wo,
   return g;
 }
 
+// the NEXT stem forward also zeroes this step's stem-wgrad scratch (fp32,
+// cer_stem_wpk_elems floats), and the NEXT stem wgrad takes its scratch as
+// already zeroed (cer_stem_set_wgrad_zeroed): ops._hip stem paths
+static float* g_stem_zero = nullptr;
+static int g_stem_zeroed = 0;
+CER_API void cer_stem_set_wgrad_scratch(float* dwp) { g_stem_zero = dwp; }
+CER_API void cer_stem_set_wgrad_zeroed(int on) { g_stem_zeroed = on ? 1 : 0; }
+
 static int stem_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, const void* w,
                          int64_t w_gstride, int Cout, int kh, int kw, int st, int pad,
                          void* x4, void* wpk, void* y, int Ho, int Wo, float* part,
                          int* nslab, const void* bias, int64_t bias_gstride, int act, bool f32,
                          hipStream_t stream) {
   const int mode = cer_stem_ok(Cin, W, kw, st, pad);
+  float* zero = g_stem_zero;
+  g_stem_zero = nullptr;
   if (mode == STEM_NONE) return (int)hipErrorInvalidValue;
   const int64_t P = (int64_t)B * H * W;
   const int kwp = stem_kwp(kw, mode), cp = stem_cp(mode);
-  const int64_t nw = (int64_t)G * Cout * kh * kwp * 8;
-  if (f32) {
-    stem_repack_kernel<float><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
-        reinterpret_cast<const float*>(x), reinterpret_cast<float*>(x4), P, G, Cin, cp);
-    stem_pack_w_kernel<float><<<cer_blocks(nw, 256), 256, 0, stream>>>(
+  const int64_t nw = (int64_t)G * Cout * kh * kwp * 8;       // (also the scratch's floats)
+  const int nbx = (int)cer_blocks(P * G, 256), nbw = (int)cer_blocks(nw, 256);
+  const int nbz = zero ? (int)cer_blocks(nw / 4, 256) : 0;   // nw % 8 == 0
+  const dim3 grid(nbx + nbw + nbz);
+  if (f32)
+    stem_prep_kernel<float><<<grid, 256, 0, stream>>>(
+        reinterpret_cast<const float*>(x), reinterpret_cast<float*>(x4), P, G, Cin, cp, nbx,
         reinterpret_cast<const float*>(w), w_gstride, reinterpret_cast<float*>(wpk), Cout, kh, kw,
-        Cin, kwp, G, mode == STEM_PAD8);
-  } else {
-    stem_repack_kernel<bf16_t><<<cer_blocks(P * G, 256), 256, 0, stream>>>(
-        reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(x4), P, G, Cin, cp);
-    stem_pack_w_kernel<bf16_t><<<cer_blocks(nw, 256), 256, 0, stream>>>(
+        kwp, mode == STEM_PAD8, nbw, zero, zero ? nw : 0);
+  else
+    stem_prep_kernel<bf16_t><<<grid, 256, 0, stream>>>(
+        reinterpret_cast<const bf16_t*>(x), reinterpret_cast<bf16_t*>(x4), P, G, Cin, cp, nbx,
         reinterpret_cast<const bf16_t*>(w), w_gstride, reinterpret_cast<bf16_t*>(wpk), Cout, kh,
-        kw, Cin, kwp, G, mode == STEM_PAD8);
-  }
+        kw, kwp, mode == STEM_PAD8, nbw, zero, zero ? nw : 0);
   NTParams p;
   p.a = stem_geom(x4, B, H, W, Ho, Wo, kh, kw, pad, mode);
   // the whole [G][B][H][W][cp] buffer is the buffer-load range
@@ -5057,7 +5088,10 @@ static int stem_wgrad_impl(const void* x4, int B, int H, int W, int Cin, int G, 
   const bool fast = f32 ? wg_fast32(8, Cout, p) : wg_fast(8, Cout, p);
   const int v = wg_variant(p.N, p.K, G, fast && !f32);
   const int splits = wg_splits(p.Mred, p.N, p.K, G, v);
-  if (splits > 1) cer_zero_async(dwp, sizeof(float) * (size_t)G * p.dw_gstride, stream);
+  const int zeroed = g_stem_zeroed;
+  g_stem_zeroed = 0;
+  if (splits > 1 && !zeroed)
+    cer_zero_async(dwp, sizeof(float) * (size_t)G * p.dw_gstride, stream);
   if (f32) {
     run_wg32(p, G, splits, fast, stream);
   } else {
