@@ -71,6 +71,11 @@ def main():
                     help="diagnostic: train only the first K configs (per-GPU work of N = 8/K "
                          "GPUs), or K > 8 configs packed (more learning rates); the headline "
                          "number always uses all 8")
+    ap.add_argument("--logs_root", default="",
+                    help="diagnostic: write the engine's metrics.jsonl (per-job and, at N > 1, "
+                         "per-hop records: bytes, post -> arrival, hold, peer) here")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="diagnostic: concurrency lanes per rank (0 = the engine default)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -129,7 +134,9 @@ def main():
         loader = da.da_partition_loader(da_root, ctx.device, stats=da_stats)
     opts = EngineOptions(slots_per_gpu=max(1, S // N), scheduler="rotation", n_train=n_train,
                          n_valid=n_valid, compute_dtype=args.dtype, use_graphs=not args.no_graphs,
-                         verbose=False, ckpt_every="none", store_loader=loader)
+                         verbose=False, ckpt_every="none", store_loader=loader,
+                         logs_root=args.logs_root,
+                         **({"lanes": args.lanes} if args.lanes else {}))
     t_etl = time.time()
     eng = MOPEngine(msts, ctx, opts)
     t_etl = time.time() - t_etl
@@ -150,7 +157,7 @@ def main():
     sync()
     ctx.barrier()
     sync()
-    img0, hop0, hopt0 = eng.train_images, eng.hop_bytes, eng.hop_time
+    img0, hop0, hopt0, hold0 = eng.train_images, eng.hop_bytes, eng.hop_time, eng.hop_hold_time
     t0 = time.time()
     eng.run_steps(args.steps, args.steps_per_round, epoch_start=2)
     sync()
@@ -160,7 +167,8 @@ def main():
     dt_max = ctx.allreduce_max(dt)
     per_rank = ctx.all_gather_object({"images": eng.train_images - img0,
                                       "hop_bytes": eng.hop_bytes - hop0,
-                                      "hop_s": eng.hop_time - hopt0})
+                                      "hop_s": eng.hop_time - hopt0,
+                                      "hold_s": eng.hop_hold_time - hold0})
     imgs = sum(r["images"] for r in per_rank)
     value = imgs / dt_max
     if ctx.rank == 0:
@@ -212,6 +220,9 @@ def main():
             "dist_backend": ctx.backend or "none",
             "hop_bytes": sum(r["hop_bytes"] for r in per_rank),
             "hop_ms_max": round(1000.0 * max(r["hop_s"] for r in per_rank), 3),
+            # the coordinator's hold of the hops a rank received (burst
+            # grouping, runtime/async_mop.py), summed over the timed window
+            "hold_ms_max": round(1000.0 * max(r["hold_s"] for r in per_rank), 3),
         }
         if da_stats is not None:
             st = da_stats

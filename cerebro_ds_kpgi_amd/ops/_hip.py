@@ -157,6 +157,8 @@ def softmax_ce_train(logits, labels, acc, G, head_bias=None):
     B, GN = logits.shape
     N = GN // G
     d = torch.empty((B, GN), dtype=torch.float32, device=logits.device)
+    if head_bias is not None and not head_bias.arena.grad_clean:
+        head_bias.grad().zero_()      # the kernel accumulates into it
     gp, gs = head_bias.grad_ptr() if head_bias is not None else (0, 0)
     rc = lib().cer_softmax_ce_f32_head(_ptr(logits), _ptr(labels.contiguous()), _ptr(acc),
                                        _ptr(d), c_p(gp), gs, B, G, N, _stream())

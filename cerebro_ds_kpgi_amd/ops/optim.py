@@ -27,6 +27,7 @@ def _aux(cursor, zero):
     if cursor is None and zero is None:
         return False
     if zero is not None and zero.numel() % 4:
+        zero.zero_()        # the kernel zeroes float4s only: clear it here, same stream point
         zero = None
     _hip.lib().cer_adam_set_aux(_hip._ptr(cursor), _hip._ptr(zero),
                                 _hip.c_i64(zero.numel() if zero is not None else 0))

@@ -155,6 +155,7 @@ class Heartbeat(object):
 # hop watchdog
 # ---------------------------------------------------------------------------
 EXIT_HOP_STALL = 18
+EXIT_HOP_ERROR = 19      # a hop that failed (mis-order, corruption, service error), not a stall
 
 
 class HopWatch(object):
@@ -181,7 +182,11 @@ class HopWatch(object):
        no waiting on the wedged communicator).
 
     ``abort(reason)`` is the same path for a hop error that would leave the
-    peers blocked in a group (e.g. ``HopOrderError`` on one endpoint)."""
+    peers blocked in a group (e.g. ``HopOrderError`` on one endpoint); it
+    ends every rank with ``EXIT_HOP_ERROR`` and a record whose ``kind`` is
+    ``"error"`` (a stall's is ``"stall"``), so the two are told apart.  Once
+    ``stop()`` has been called (the run is ending) an abort is ignored: the
+    caller's own exception and cleanup then run as usual."""
 
     def __init__(self, rank, world, timeout_s, store=None, key="cerebro_hopwatch",
                  logs_root="", interval=0.5, on_fire=None):
@@ -266,28 +271,33 @@ class HopWatch(object):
                 return
             why = self._remote_abort()
             if why is not None:
-                self._fire("abort raised by another rank: " + why, local=False)
+                code, _, text = why.partition("|")
+                code = int(code) if code.isdigit() else EXIT_HOP_STALL
+                self._fire("abort raised by another rank: " + text, local=False, code=code)
                 return
 
-    def abort(self, reason):
+    def abort(self, reason, code=EXIT_HOP_ERROR):
         """A hop error on this rank: stop every rank now (see class doc)."""
-        self._fire(reason, local=True)
+        if self._stop.is_set():
+            return
+        self._fire(reason, local=True, code=code)
 
-    def diagnostic(self, reason):
+    def diagnostic(self, reason, code=EXIT_HOP_STALL):
         now = time.time()
         with self.lock:
             pend = [dict(rec, age_s=round(now - rec["t0"], 3)) for rec in self.pending.values()]
             for p in pend:
                 p.pop("t0", None)
             return {"rank": self.rank, "world": self.world, "time": now, "reason": reason,
+                    "kind": "stall" if code == EXIT_HOP_STALL else "error", "exit_code": code,
                     "bound_s": self.bound(), "pending": pend, "groups_posted": self.groups,
                     "last_done": list(self.done)}
 
-    def _fire(self, reason, local):
+    def _fire(self, reason, local, code=EXIT_HOP_STALL):
         import sys
         if self.fired is not None:
             return
-        d = self.diagnostic(reason)
+        d = self.diagnostic(reason, code)
         self.fired = d
         msg = "HOP WATCHDOG rank {}: {}; pending {}; groups posted {}; last hops done {}".format(
             self.rank, reason, json.dumps(d["pending"]), d["groups_posted"], d["last_done"])
@@ -306,10 +316,10 @@ class HopWatch(object):
                 pass
         if local and self.store is not None:
             try:
-                self.store.set(self.key, "rank {}: {}".format(self.rank, reason))
+                self.store.set(self.key, "{}|rank {}: {}".format(code, self.rank, reason))
             except Exception:
                 pass
         self.on_fire(d)
 
     def _exit(self, diag):  # pragma: no cover - exercised in multi-process runs
-        os._exit(EXIT_HOP_STALL)
+        os._exit(diag.get("exit_code", EXIT_HOP_STALL))

@@ -203,9 +203,16 @@ def execute_moves(moves, rank, send_buf, recv_buf, group=None, check=False, watc
 
         def digest_of(m, buf):
             return checksum(send_buf(m))
-    recvs = post_transfers(items, rank, group, digest_of=digest_of, watch=watch)
-    if check:
-        verify_digests(recvs, rank)
+    try:
+        recvs = post_transfers(items, rank, group, digest_of=digest_of, watch=watch)
+        if check:
+            verify_digests(recvs, rank)
+    except (HopOrderError, HopChecksumError) as e:
+        if watch is not None:
+            # the peers that completed their side of the group would block in
+            # the next collective until the process group's timeout
+            watch.abort("{} on rank {}: {}".format(type(e).__name__, rank, e))
+        raise
     return len(items)
 
 

@@ -48,6 +48,7 @@ import contextlib
 import datetime
 import json
 import os
+import statistics
 import threading
 import time
 
@@ -212,7 +213,8 @@ class Coordinator(object):
         for p in range(eng.P):
             self.parts_of[eng.owner(p)].append(p)
         self.k = collections.defaultdict(int)          # next assignment slot per rank
-        self.nhop = 0
+        self.ntk = 0                                   # hop tickets (decided hops)
+        self.nseq = 0                                  # global hop sequence (published)
         self.nev = 0
         self.batch = {}                                # rank -> running batch record
         self.holder = dict(eng.holder)                 # committed state location
@@ -222,10 +224,12 @@ class Coordinator(object):
         self.round_base = 0                            # rotation rounds of earlier epochs
         self.rounds_done = 0
         self.nbatch = 0                                # batches finished (greedy subepoch id)
-        self._hop_buf = []                             # decided, not yet published hops
-        self._hop_buf_t0 = 0.0
-        self._train_s, self._train_n = 0.0, 0            # job training times (hold)
+        self._hop_buf = []                             # [ticket, record, t decided], unpublished
+        self._train_s, self._train_n = 0.0, 0            # job training times
+        self._train_recent = collections.deque(maxlen=32)  # recent job times (hold: median)
         self._train_max = 0.0                            # longest (hop watchdog bound)
+        self.hops = None                                 # this rank's HopService (measured T)
+        self.hold_log = []                               # (ticket, model, src, dst, held s, margin s)
         self.thread = None
 
     # -- plumbing ----------------------------------------------------------
@@ -260,64 +264,106 @@ class Coordinator(object):
             try:
                 self._flush_hops()
                 self._broadcast({"t": "stop", "error": self.error})
-                self.chan.hop(self.nhop, {"t": "stop"})
+                self.chan.hop(self.nseq, {"t": "stop"})
             except Exception:
                 pass
             return
         self._flush_hops()
         self._broadcast({"t": "stop", "error": None})
-        self.chan.hop(self.nhop, {"t": "stop"})
+        self.chan.hop(self.nseq, {"t": "stop"})
 
     # -- hop publication ---------------------------------------------------
-    # Hops are numbered when decided but published in bursts, so that every
-    # rank's hop service finds a whole boundary (a rotation's ring shift:
-    # each rank sends r -> r+1 and receives r-1 -> r) published at once and
-    # posts its send and its receive as ONE group on the one hop
-    # communicator.  Published one by one, a rank's receive from a late
+    # A hop gets a *ticket* when it is decided (the job records name their
+    # incoming hops by ticket) and a place in the global hop sequence only
+    # when it is published, so hops can be published in any order.  Hops
+    # published together form one burst: every rank's hop service finds them
+    # at once and posts its share as ONE group on the one hop communicator.
+    # A rotation's ring shift (each rank sends r -> r+1 and receives r-1 ->
+    # r) wants one burst: published one by one, a rank's receive from its
     # predecessor would sit in front of its own send (one communicator = one
-    # RCCL stream) and the shift would chain through the ring.
+    # RCCL stream) and, when the ranks finish within a transfer time of each
+    # other, the shift would chain through the ring (up to N transfer times
+    # instead of one).
     #
-    # A burst is held while further events are already waiting, and -- for
-    # rotation -- while a rank that is really computing (all its incoming
-    # hops published) has not finished training, for at most
-    # HOLD_FRAC x the mean training time of a job (at least HOLD_MIN_S, at
-    # most HOLD_MAX_S): a straggler delays its neighbours' hops by that much
-    # at worst, never indefinitely.
+    # Rotation therefore holds a decided hop back while a rank that is about
+    # to finish is still training -- "about to" meaning its job has run for
+    # the median job time give or take the hold margin (2 x the measured
+    # transfer time, at least HOLD_MIN_S): only those ranks' hops can still
+    # join the burst before a chain would cost more than the wait.  A rank
+    # past that window (a straggler) or far from it (it started late) holds
+    # nothing back, a hop to a rank that is still far from done is published
+    # at once (its transfer overlaps the receiver's compute), and no hop is
+    # held longer than the margin (or HOLD_MAX_S): the wait is bounded by what
+    # a receiver would lose to a chain, not by the slowest rank or the job
+    # length.
     HOLD_MIN_S = 0.002
     HOLD_MAX_S = 0.5
-    HOLD_FRAC = 0.2
+    HOP_GBPS = 50.0          # assumed per-hop rate until one is measured (xGMI, one link)
 
-    def _flush_hops(self):
-        n = len(self._hop_buf)
-        for i, (h, rec) in enumerate(self._hop_buf):
+    def _flush_hops(self, entries=None):
+        """Publish ``entries`` (default: every buffered hop) as one burst."""
+        if entries is None:
+            entries = self._hop_buf
+        if not entries:
+            return
+        pub = {id(e) for e in entries}
+        now = time.time()
+        margin = self._margin_s()
+        n = len(entries)
+        for i, e in enumerate(entries):
+            tk, rec, t_dec = e
+            held = now - t_dec
             rec["more"] = i + 1 < n          # the burst continues: read on
-            self.chan.hop(h, rec)
-        self._hop_buf = []
+            rec["hold"] = round(held, 6)
+            self.chan.hop(self.nseq, rec)
+            self.nseq += 1
+            self.hold_log.append((tk, rec["m"], rec["src"], rec["dst"], held, margin))
+        self._hop_buf = [e for e in self._hop_buf if id(e) not in pub]
 
-    def _hold_s(self):
-        mean = self._train_s / self._train_n if self._train_n else 0.0
-        return min(self.HOLD_MAX_S, max(self.HOLD_MIN_S, self.HOLD_FRAC * mean))
+    def _hop_est_s(self):
+        """One hop's transfer time: measured on this rank's hop service once
+        it has moved something, else the state row's bytes at HOP_GBPS."""
+        svc = self.hops
+        if svc is not None and svc.groups:
+            return svc.busy / svc.groups
+        return self.eng.hop_estimate_s(self.HOP_GBPS)
 
-    def _holding(self):
-        """Keep the buffered hops back a little longer?"""
-        if time.time() - self._hop_buf_t0 >= self._hold_s():
-            return False
+    def _margin_s(self):
+        return min(self.HOLD_MAX_S, max(self.HOLD_MIN_S, 2.0 * self._hop_est_s()))
+
+    def _about_to_finish(self, b, now, margin):
+        if not self._train_recent:
+            return True                           # nothing measured yet: every rank is
+        med = statistics.median(self._train_recent)
+        return abs((now - b["t0"]) - med) <= margin
+
+    def _releasable(self, now):
+        """The buffered hops to publish now (rotation hold, see above)."""
         if self.policy != "rotation":
-            return False
-        first = self._hop_buf[0][0]
-        return any(b["train_left"] and all(h is None or h < first for h in b["hops"])
-                   for b in self.batch.values())
+            return list(self._hop_buf)
+        margin = self._margin_s()
+        buffered = {e[0] for e in self._hop_buf}
+        # ranks really computing: training, with every incoming hop published
+        computing = {r: b for r, b in self.batch.items() if b["train_left"] and
+                     all(tk is None or tk not in buffered for tk in b["hops"])}
+        near = {r for r, b in computing.items() if self._about_to_finish(b, now, margin)}
+        out = []
+        for e in self._hop_buf:
+            if not near or now - e[2] >= margin:
+                out.append(e)
+            elif e[1]["dst"] in computing and e[1]["dst"] not in near:
+                out.append(e)                     # overlaps the receiver's compute
+        return out
 
     def _wait_event(self):
         """Next event; buffered hops are published before blocking on it."""
         while self._hop_buf:
-            if time.time() - self._hop_buf_t0 >= self._hold_s():
-                self._flush_hops()                     # never held past the cap
-                break
             if self.chan.has_event(self.nev):
                 break                                  # collect its hops too
-            if not self._holding():
-                self._flush_hops()
+            rel = self._releasable(time.time())
+            if rel:
+                self._flush_hops(rel)
+            if not self._hop_buf:
                 break
             time.sleep(0.0005)
         return self._next_event()
@@ -428,22 +474,20 @@ class Coordinator(object):
         return None
 
     def _pre_hop(self, m, dst):
-        """Publish m's hop to ``dst`` now (its state is final); returns the
-        hop's sequence number (None: no transfer needed)."""
+        """Decide m's hop to ``dst`` (its state is final; published by
+        ``_wait_event``); returns the hop's ticket (None: no transfer needed)."""
         src = self.holder.get(m)
         if src is None or src == dst:
             return None
         sent = self.hop_sent.get(m)
         if sent is not None and sent[0] == dst:
             return sent[1]
-        h = self.nhop
-        if not self._hop_buf:
-            self._hop_buf_t0 = time.time()
-        self._hop_buf.append((h, {"t": "hop", "m": m, "src": src, "dst": dst,
-                                  "jt": self._train_max}))
-        self.nhop += 1
-        self.hop_sent[m] = (dst, h)
-        return h
+        tk = self.ntk
+        self._hop_buf.append([tk, {"t": "hop", "tk": tk, "m": m, "src": src, "dst": dst,
+                                   "jt": self._train_max}, time.time()])
+        self.ntk += 1
+        self.hop_sent[m] = (dst, tk)
+        return tk
 
     def _prefetch_next_epoch(self, m):
         """Rotation, m's last visit of the epoch just ended: its first visit
@@ -483,9 +527,11 @@ class Coordinator(object):
         r = ev["rank"]
         b = self.batch.get(r)
         if t == "train_done":
-            self._train_s += time.time() - b["t0"]
+            jt = time.time() - b["t0"]
+            self._train_s += jt
             self._train_n += 1
-            self._train_max = max(self._train_max, time.time() - b["t0"])
+            self._train_recent.append(jt)
+            self._train_max = max(self._train_max, jt)
             for m in ev["models"]:
                 p = next(p for mm, p, _, _ in b["jobs"] if mm == m)
                 self.sched.release_model(m, p)
@@ -619,7 +665,7 @@ class HopService(object):
         self.cuda = eng.device.type == "cuda"
         self.stream = torch.cuda.Stream(device=eng.device) if self.cuda else None
         self.final = {}                       # model -> cuda event of its last parking
-        self.arrived = {}                     # hop id -> [threading.Event, cuda event]
+        self.arrived = {}                     # hop ticket -> [threading.Event, cuda event]
         self.lock = threading.Lock()
         self._cv = threading.Condition()      # in-flight group / pause (quiet)
         self._inflight = 0
@@ -627,10 +673,12 @@ class HopService(object):
         self.bytes = 0
         self.busy = 0.0
         self.groups = 0                       # batch_isend_irecv groups posted
-        self.spans = []                       # (t0, t1, "send"|"recv", model, peer)
+        self.spans = []                       # (t0, t1, "send"|"recv", model, peer, bytes, seq, hold)
+        self.hold = 0.0                       # coordinator hold of the hops received here
         self.error = None
+        self.stopping = False                     # the stop record has been read
         self.watch = eng.hop_watch                # parallel.health.HopWatch (or None)
-        self.seen = {}                            # hop id -> time its record was read
+        self.seen = {}                            # hop ticket -> time its record was read
         self.thread = None
 
     def start(self):
@@ -653,8 +701,8 @@ class HopService(object):
             self.final[m] = ev
 
     def wait_arrival(self, h):
-        """Main thread: block until hop ``h`` has landed (host side), then
-        order the compute stream after it (device side)."""
+        """Main thread: block until the hop with ticket ``h`` has landed
+        (host side), then order the compute stream after it (device side)."""
         with self.lock:
             slot = self.arrived.setdefault(h, [threading.Event(), None])
         tok = None
@@ -709,9 +757,12 @@ class HopService(object):
                 self._loop()
         except BaseException as e:
             self.error = "{}: {}".format(type(e).__name__, e)
-            if self.watch is not None:
+            if self.watch is not None and not self.stopping:
                 # peers may sit in a group with this rank: stop every rank
-                # with a diagnostic rather than leave them blocked
+                # with a diagnostic rather than leave them blocked (exit code
+                # EXIT_HOP_ERROR, not a stall; skipped once the stop record
+                # is in: the run is being torn down and the main thread's
+                # own error path reports)
                 self.watch.abort("hop service failed on rank {}: {}".format(
                     self.rank, self.error))
 
@@ -727,13 +778,14 @@ class HopService(object):
                 recs.append((h, self.chan.next_hop(h)))
                 h += 1
             stop = recs[-1][1]["t"] == "stop"
-            mine = [(hid, r["m"], r["src"], r["dst"]) for hid, r in recs
-                    if r["t"] == "hop" and self.rank in (r["src"], r["dst"])]
+            self.stopping = self.stopping or stop
+            mine = [(hid, r["m"], r["src"], r["dst"], r["tk"], r.get("hold", 0.0))
+                    for hid, r in recs if r["t"] == "hop" and self.rank in (r["src"], r["dst"])]
             now = time.time()
             with self.lock:
                 for hid, r in recs:
                     if r["t"] == "hop" and r["dst"] == self.rank:
-                        self.seen[hid] = now
+                        self.seen[r["tk"]] = now
             if self.watch is not None:
                 self.watch.note_job(max(r.get("jt", 0.0) for _, r in recs))
             if mine:
@@ -758,7 +810,8 @@ class HopService(object):
         eng = self.eng
         tx, nsend = [], 0
         t0 = time.time()
-        for hid, m, src, dst in items:
+        tk_of = {it[0]: it[4] for it in items}
+        for hid, m, src, dst, _, _ in items:
             grp = eng.group_of[m]
             row = grp.home.state[grp.home_row[m]]
             buf = row if eng.o.hop_optimizer_state else row[:grp.layout.n_master]
@@ -791,11 +844,14 @@ class HopService(object):
         t1 = time.time()
         with self.lock:
             self.busy += t1 - t0
-            for hid, m, src, dst in items:
+            for (hid, m, src, dst, _, hold), (_, _, _, _, buf) in zip(items, tx):
                 send = self.rank == src
-                self.spans.append((t0, t1, "send" if send else "recv", m, dst if send else src))
+                self.spans.append((t0, t1, "send" if send else "recv", m, dst if send else src,
+                                   buf.numel() * buf.element_size(), hid, hold))
+                if not send:
+                    self.hold += hold
             for hid, m, _, _ in recvs:
-                slot = self.arrived.setdefault(hid, [threading.Event(), None])
+                slot = self.arrived.setdefault(tk_of[hid], [threading.Event(), None])
                 slot[1] = done
                 slot[0].set()
 
@@ -886,7 +942,7 @@ def _run_batch(eng, chan, hops, rec):
     rank = eng.ctx.rank
     tr = eng.tracer
     t_start = time.time()
-    jobs = [tuple(j) for j in rec["jobs"]]         # (model, partition, holder, hop id)
+    jobs = [tuple(j) for j in rec["jobs"]]         # (model, partition, holder, hop ticket)
     models = [j[0] for j in jobs]
     error = None
     results, trained = [], 0
@@ -1000,7 +1056,9 @@ def run_session(eng, policy, first_epoch, num_epochs, mst_eval_fn=None, steps_of
     if ctx.rank == 0:
         eng.coord_begin()
         coord = Coordinator(eng, chan, eng.async_scheduler(policy), policy, first_epoch,
-                            num_epochs, mst_eval_fn, steps_of, round_budget).start()
+                            num_epochs, mst_eval_fn, steps_of, round_budget)
+        coord.hops = hops
+        coord.start()
     err = None
     try:
         err = run_worker(eng, chan, hops)
@@ -1017,6 +1075,7 @@ def run_session(eng, policy, first_epoch, num_epochs, mst_eval_fn=None, steps_of
         eng.hop_bytes += hops.bytes
         eng.hop_busy_time += hops.busy
         eng.hop_groups += hops.groups
+        eng.hop_hold_time += hops.hold
         eng.hop_spans.extend(hops.spans)
         if hops.error and not err:
             err = "hop service: " + hops.error
@@ -1031,6 +1090,12 @@ def run_session(eng, policy, first_epoch, num_epochs, mst_eval_fn=None, steps_of
             "failures": eng.failures, "round_idx": eng.round_idx, "error": err,
             "last_epoch": coord.last_epoch, "rounds_done": coord.rounds_done})
     fin = chan.get_final()
+    if hops is not None:
+        # per-hop telemetry of the session into rank 0's metrics.jsonl
+        # (bytes, post -> arrival, coordinator hold, peer)
+        spans = ctx.all_gather_object(hops.spans)
+        if ctx.rank == 0:
+            eng.log_hop_records(spans, coord.hold_log)
     ctx.barrier()
     eng.coord_end(fin)
     if fin["error"]:

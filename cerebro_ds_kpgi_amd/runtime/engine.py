@@ -135,10 +135,14 @@ RESUME_FILE = "resume.json"
 # one batch (different architectures / batch sizes, e.g. the hetero
 # drill-down or a TPE round) replay their step graphs on this many streams at
 # once (async_mop._run_batch); each lane has its own split-K workspace (64 MB).
-# Default 1 (one after another): lanes measured makespan-neutral on the
-# hetero jobs (profiles/r4_hetero.md) and every extra stream competes for the
-# 4 hardware queues (stream_budget, profiles/r5_stream_budget.md)
-LANES = 1
+# Default 4 on one GPU: the 16-config Criteo grid (4 batch sizes = 4 pack
+# groups of small, launch-bound MLP steps) runs 6.5 % faster with its groups
+# concurrent than one after another (same-lease A/B of the round-4 and round-5
+# builds, profiles/r6_r4_vs_r5.md; round 5 had set 1 after the lanes measured
+# neutral on the hetero jobs).  At world > 1 ``effective_lanes`` clamps them
+# to what leaves the hop's two streams within the hardware queues
+# (stream_budget, profiles/r5_stream_budget.md).
+LANES = 4
 # hardware queues per process (HIP's default GPU_MAX_HW_QUEUES)
 HW_QUEUES = 4
 
@@ -207,6 +211,7 @@ class MOPEngine(object):
         self.hop_bytes = 0
         self.hop_time = 0.0          # exposed: time a rank waited for a hop
         self.hop_busy_time = 0.0     # transfers themselves (async runtime)
+        self.hop_hold_time = 0.0     # coordinator hold of the hops this rank received
         self.hop_groups = 0          # batch_isend_irecv groups posted (async runtime)
         self.hop_spans = []
         self.coord_msts = None
@@ -223,6 +228,11 @@ class MOPEngine(object):
             # otherwise hang until the process group's 30-minute timeout
             from ..parallel.hop import hop_group
             watch = None
+            if ctx.world > 1:
+                # every rank has loaded its partitions before the watchdog
+                # starts: ranks finish their (DA) data loads tens of seconds
+                # apart, and that skew is not a stalled hop
+                ctx.barrier()
             if ctx.world > 1 and self.o.hop_timeout:
                 from ..parallel.health import HopWatch
                 watch = HopWatch(ctx.rank, ctx.world, self.o.hop_timeout,
@@ -477,7 +487,7 @@ class MOPEngine(object):
         self.jobs_info.setdefault(epoch, {})[(job["model_key"], r["dist_key"])] = job
         self.models_info[job["model_key"]].append(job)
         if self._metrics_path:
-            rec = {"epoch": epoch, "subepoch": sub, "cfg": job["model_key"],
+            rec = {"kind": "job", "epoch": epoch, "subepoch": sub, "cfg": job["model_key"],
                    "partition": r["dist_key"], "rank": g["rank"],
                    "loss": job["loss_train"], "top1": job["top1_train"],
                    "top5": job["metric_train"], "valid_loss": job["loss_valid"],
@@ -486,6 +496,43 @@ class MOPEngine(object):
                    "hop_ms": job["hop_time"] * 1e3}
             with open(self._metrics_path, "a") as f:
                 f.write(json.dumps(rec) + "\n")
+
+    def hop_estimate_s(self, gbps):
+        """Transfer time of the largest hop payload at ``gbps`` GB/s (plus the
+        test hook's forced link time): the coordinator's hold margin before
+        a hop has been measured."""
+        nbytes = 0
+        for grp in self.groups.values():
+            st = grp.home.state
+            n = st.shape[1] if self.o.hop_optimizer_state else grp.layout.n_master
+            nbytes = max(nbytes, n * st.element_size())
+        return nbytes / (gbps * 1e9) + (self.o.sim_hop_seconds or 0.0)
+
+    def log_hop_records(self, spans_per_rank, hold_log):
+        """Rank 0, asynchronous runtime: one ``metrics.jsonl`` record per hop
+        endpoint of the session -- sequence number, direction, model, peer,
+        bytes, post -> arrival (the group's span, us) and the coordinator's
+        hold before publishing it (us).  ``spans_per_rank``: every rank's
+        ``HopService.spans``; ``hold_log``: the coordinator's
+        ``(ticket, model, src, dst, seconds held, hold margin)``."""
+        if not self._metrics_path:
+            return
+        with open(self._metrics_path, "a") as f:
+            for r, spans in enumerate(spans_per_rank):
+                for sp in spans:
+                    t0, t1, d, m, peer = sp[:5]
+                    nbytes, seq, hold = (sp[5], sp[6], sp[7]) if len(sp) > 7 else (0, -1, 0.0)
+                    f.write(json.dumps({"kind": "hop", "seq": seq, "rank": r, "dir": d,
+                                        "model": m, "peer": peer, "bytes": nbytes,
+                                        "t_post": t0, "post_to_arrival_us": round((t1 - t0) * 1e6, 1),
+                                        "hold_us": round(hold * 1e6, 1)}) + "\n")
+            if hold_log:
+                holds = [h[4] for h in hold_log]
+                f.write(json.dumps({"kind": "hop_hold", "hops": len(holds),
+                                    "hold_us_max": round(max(holds) * 1e6, 1),
+                                    "hold_us_mean": round(sum(holds) / len(holds) * 1e6, 1),
+                                    "margin_us_max": round(max(h[5] for h in hold_log) * 1e6, 1)})
+                        + "\n")
 
     # ------------------------------------------------------------------
     def _epoch_summary(self, epoch):

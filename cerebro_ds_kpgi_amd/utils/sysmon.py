@@ -6,13 +6,20 @@ thread per node that samples
 
 * GPU: utilisation, HBM used, power — ``amd-smi metric --json`` (falls back
   to ``rocm-smi --json``, then to ``torch.cuda`` memory counters),
+* xGMI: per-link cumulative read / write KB between every GPU pair —
+  ``amd-smi xgmi --metric --json`` (the model-hop data plane's links; absent
+  on single-GPU boxes and when amd-smi cannot read them: the sample then
+  has no ``xgmi`` key),
 * CPU / memory: ``/proc/stat``, ``/proc/meminfo``,
 * disk: ``/proc/diskstats`` (sectors read / written),
 * network: ``/proc/net/dev`` (bytes rx / tx),
 
 and appends one JSON object per sample to ``{dir}/sysmon_{host}.jsonl``.
 ``summarize`` reproduces ``SystemLogAnalyzer``'s report (mean utilisation, GB
-read / written, GB over network; ``plots/data_analytics.py:200-477``).
+read / written, GB over network; ``plots/data_analytics.py:200-477``) and
+adds the GB moved over xGMI per GPU (the reference's per-node network
+logger, ``logs/bin/network_logger.sh:12-19``, is what attributes hop cost
+there).
 """
 
 import json
@@ -100,6 +107,51 @@ def gpu_metrics():
     return []
 
 
+def parse_xgmi(data):
+    """``amd-smi xgmi --metric --json`` output -> ``[{"gpu", "bit_rate",
+    "links": [{"peer", "read_kb", "write_kb"}]}]``.  The CLI's JSON nests
+    the per-GPU records differently across versions (a list, or a dict
+    holding one); every dict carrying ``link_metrics`` is one GPU."""
+    found = []
+
+    def walk(o):
+        if isinstance(o, dict):
+            if "link_metrics" in o:
+                found.append(o)
+                return
+            for v in o.values():
+                walk(v)
+        elif isinstance(o, list):
+            for v in o:
+                walk(v)
+    walk(data)
+    out = []
+    for g in found:
+        lm = g.get("link_metrics") or {}
+        links = []
+        for ln in lm.get("links") or []:
+            rd, wr = _num(ln.get("read")), _num(ln.get("write"))
+            if rd is None and wr is None:
+                continue                     # "N/A": no link to that GPU (itself)
+            links.append({"peer": ln.get("gpu"), "read_kb": rd, "write_kb": wr})
+        out.append({"gpu": g.get("gpu"), "bit_rate": _num(lm.get("bit_rate")), "links": links})
+    return out
+
+
+def xgmi_metrics():
+    """Per-GPU xGMI link counters (``parse_xgmi``), or [] when unavailable."""
+    if not shutil.which("amd-smi"):
+        return []
+    try:
+        r = subprocess.run(["amd-smi", "xgmi", "--metric", "--json"], capture_output=True,
+                           text=True, timeout=10)
+        if r.returncode != 0 or not r.stdout.strip():
+            return []
+        return [g for g in parse_xgmi(json.loads(r.stdout)) if g["links"]]
+    except (OSError, ValueError, subprocess.SubprocessError):
+        return []
+
+
 def _num(v):
     if isinstance(v, dict):
         v = v.get("value")
@@ -110,10 +162,11 @@ def _num(v):
 
 
 class SysMonitor(object):
-    def __init__(self, directory, interval=1.0, gpus=True):
+    def __init__(self, directory, interval=1.0, gpus=True, xgmi=True):
         self.dir = directory
         self.interval = interval
         self.gpus = gpus
+        self.xgmi = xgmi
         self.path = os.path.join(directory, "sysmon_{}.jsonl".format(socket.gethostname()))
         self._stop = threading.Event()
         self._t = None
@@ -126,6 +179,12 @@ class SysMonitor(object):
         d["net_rx"], d["net_tx"] = net_bytes()
         if self.gpus:
             d["gpus"] = gpu_metrics()
+        if self.xgmi:
+            x = xgmi_metrics()
+            if x:
+                d["xgmi"] = x
+            else:
+                self.xgmi = False            # not on this box: stop asking
         if prev:
             dt = max(tot - prev["cpu_total"], 1)
             d["cpu_util"] = 100.0 * (1 - (idle - prev["cpu_idle"]) / dt)
@@ -159,9 +218,28 @@ def summarize(path):
     a, b = rows[0], rows[-1]
     cpu = [r["cpu_util"] for r in rows if "cpu_util" in r]
     gutil = [g["util"] for r in rows for g in r.get("gpus", []) if g.get("util") is not None]
-    return {"seconds": b["ts"] - a["ts"],
-            "cpu_util_mean": sum(cpu) / len(cpu) if cpu else None,
-            "gpu_util_mean": sum(gutil) / len(gutil) if gutil else None,
-            "disk_read_gb": (b["disk_read"] - a["disk_read"]) / 1e9,
-            "disk_write_gb": (b["disk_write"] - a["disk_write"]) / 1e9,
-            "net_gb": ((b["net_rx"] - a["net_rx"]) + (b["net_tx"] - a["net_tx"])) / 1e9}
+    out = {"seconds": b["ts"] - a["ts"],
+           "cpu_util_mean": sum(cpu) / len(cpu) if cpu else None,
+           "gpu_util_mean": sum(gutil) / len(gutil) if gutil else None,
+           "disk_read_gb": (b["disk_read"] - a["disk_read"]) / 1e9,
+           "disk_write_gb": (b["disk_write"] - a["disk_write"]) / 1e9,
+           "net_gb": ((b["net_rx"] - a["net_rx"]) + (b["net_tx"] - a["net_tx"])) / 1e9}
+    xr = [r for r in rows if r.get("xgmi")]
+    if len(xr) >= 2:
+        out["xgmi_write_gb"] = _xgmi_delta(xr[0]["xgmi"], xr[-1]["xgmi"], "write_kb")
+        out["xgmi_read_gb"] = _xgmi_delta(xr[0]["xgmi"], xr[-1]["xgmi"], "read_kb")
+    return out
+
+
+def _xgmi_delta(first, last, field):
+    """{gpu: GB} of ``field`` moved between two samples, over all its links."""
+    def table(sample):
+        return {(g["gpu"], ln["peer"]): ln.get(field) for g in sample for ln in g["links"]}
+    t0, t1 = table(first), table(last)
+    out = {}
+    for (gpu, peer), v1 in t1.items():
+        v0 = t0.get((gpu, peer))
+        if v0 is None or v1 is None:
+            continue
+        out[str(gpu)] = out.get(str(gpu), 0.0) + max(0.0, v1 - v0) / 1e6
+    return out

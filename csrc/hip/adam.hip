@@ -104,7 +104,10 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
                           int zero_grad, bf16_t* work, int64_t work_stride, const float* lr,
                           const float* wd, int G, float b1, float b2, float eps, int l2,
                           hipStream_t stream) {
-  if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) return (int)hipErrorInvalidValue;
+  if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) {
+    cer_adam_set_aux(nullptr, nullptr, 0);   // a refused launch consumes its side jobs too
+    return (int)hipErrorInvalidValue;
+  }
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
                                                       g_aux_cursor);
   dim3 grid(cer_blocks(n_train / 8, 256), G);
@@ -175,8 +178,10 @@ CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int6
                          int64_t off_step, float* grad, int64_t grad_stride, int zero_grad,
                          bf16_t* work, int64_t work_stride, const float* lr, const float* wd,
                          int G, float momentum, int l2, hipStream_t stream) {
-  if (n_train % 8 != 0) return (int)hipErrorInvalidValue;
-  if (g_aux_zero_n % 4 != 0) return (int)hipErrorInvalidValue;
+  if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) {
+    cer_adam_set_aux(nullptr, nullptr, 0);
+    return (int)hipErrorInvalidValue;
+  }
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
                                                       g_aux_cursor);
   dim3 grid(cer_blocks(n_train / 8, 256), G);

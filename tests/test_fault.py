@@ -267,3 +267,43 @@ def test_sysmon_sampler(tmp_path):
     s = summarize(mon.path)
     assert s["seconds"] > 0 and s["cpu_util_mean"] is not None
     assert s["disk_read_gb"] >= 0 and s["net_gb"] >= 0
+
+
+def _xgmi_sample(kb):
+    # the shape `amd-smi xgmi --metric --json` prints (amdsmi_commands.py
+    # xgmi(): per source GPU a link_metrics dict, one link entry per GPU,
+    # "N/A" for itself), for two GPUs
+    return {"xgmi_metric": [
+        {"gpu": g, "bdf": "0000:0{}:00.0".format(g),
+         "link_metrics": {"bit_rate": {"value": 32, "unit": "Gb/s"},
+                          "max_bandwidth": {"value": 512, "unit": "Gb/s"},
+                          "link_type": "XGMI",
+                          "links": [{"gpu": p, "bdf": "0000:0{}:00.0".format(p),
+                                     "read": "N/A" if p == g else {"value": kb * (g + 1), "unit": "KB"},
+                                     "write": "N/A" if p == g else {"value": 2 * kb * (g + 1), "unit": "KB"}}
+                                    for p in range(2)]}}
+        for g in range(2)]}
+
+
+def test_sysmon_xgmi_schema(tmp_path):
+    """xGMI link counters: parsed per GPU and link from
+    the amd-smi JSON, written into the sysmon samples, and summarised as GB
+    moved per GPU; a box without them (this one) leaves the key out."""
+    from cerebro_ds_kpgi_amd.utils import sysmon
+    x0 = sysmon.parse_xgmi(_xgmi_sample(1000))
+    assert [g["gpu"] for g in x0] == [0, 1]
+    assert x0[0]["bit_rate"] == 32
+    assert x0[0]["links"] == [{"peer": 1, "read_kb": 1000.0, "write_kb": 2000.0}]
+    x1 = sysmon.parse_xgmi(_xgmi_sample(1000 + 5e6))
+    path = tmp_path / "sysmon_h.jsonl"
+    base = {"cpu_total": 1, "cpu_idle": 0, "disk_read": 0, "disk_write": 0, "net_rx": 0,
+            "net_tx": 0}
+    with open(path, "w") as f:
+        f.write(json.dumps(dict(base, ts=0.0, xgmi=x0)) + "\n")
+        f.write(json.dumps(dict(base, ts=1.0, xgmi=x1)) + "\n")
+    s = sysmon.summarize(str(path))
+    assert s["xgmi_read_gb"] == {"0": pytest.approx(5.0), "1": pytest.approx(10.0)}
+    assert s["xgmi_write_gb"] == {"0": pytest.approx(10.0), "1": pytest.approx(20.0)}
+    mon = sysmon.SysMonitor(str(tmp_path), interval=0.05, gpus=False)
+    d = mon.sample(None)
+    assert "xgmi" not in d and mon.xgmi is False        # no GPUs here: not sampled again

@@ -92,14 +92,22 @@ def _swap_worker(rank, world, port, outdir, sizes):
 
 def test_swapped_receives_raise_order_error(tmp_path):
     """Same-size transfers posted in swapped order complete (RCCL would pair
-    them the same way) and the headers expose the swap."""
+    them the same way) and the headers expose the swap: the receiving rank
+    raises ``HopOrderError``, which (under a hop watch) ends it with
+    EXIT_HOP_ERROR and an "error" record naming the swap, and raises the
+    job-wide abort so no peer blocks in its next collective."""
+    from cerebro_ds_kpgi_amd.parallel.health import EXIT_HOP_ERROR
     procs = _spawn(_swap_worker, 2, str(tmp_path), {0: 4096, 1: 4096})
     codes, dt = _join_all(procs, 120)
-    assert codes == [0, 0], codes
-    r0 = open(tmp_path / "swap_0.txt").read()
-    r1 = open(tmp_path / "swap_1.txt").read()
-    assert r0 == "ok"
-    assert r1.startswith("order:") and "different orders" in r1, r1
+    assert codes[1] == EXIT_HOP_ERROR, codes
+    # rank 0 completed its side; it then takes the abort (19) or sees its
+    # peer gone in its own teardown (gloo: 1) -- it does not hang
+    assert codes[0] is not None, codes
+    assert open(tmp_path / "swap_0.txt").read() == "ok"
+    assert not (tmp_path / "swap_1.txt").exists()     # ended before its own handler
+    d1 = json.load(open(tmp_path / "hop_stall_rank1.json"))
+    assert d1["kind"] == "error" and d1["exit_code"] == EXIT_HOP_ERROR
+    assert "HopOrderError" in d1["reason"] and "different orders" in d1["reason"], d1
 
 
 def test_swapped_receives_of_different_sizes_never_pass(tmp_path):
@@ -173,6 +181,30 @@ def test_watch_bound_tracks_longest_job():
     assert w.done == [3] and w.check() is None
     w.abort("test")
     assert fired and fired[0]["reason"] == "test"
+
+
+def test_watch_abort_is_an_error_not_a_stall_and_off_after_stop():
+    """a hop error (mis-order, corruption, service failure) ends
+    the ranks with EXIT_HOP_ERROR and kind "error"; a stall keeps
+    EXIT_HOP_STALL; an abort during teardown (after stop()) is ignored."""
+    from cerebro_ds_kpgi_amd.parallel.health import EXIT_HOP_ERROR, EXIT_HOP_STALL, HopWatch
+    fired = []
+    w = HopWatch(0, 2, 1.0, on_fire=fired.append)
+    w.abort("HopOrderError on rank 0: swapped")
+    assert fired[0]["kind"] == "error" and fired[0]["exit_code"] == EXIT_HOP_ERROR
+    fired.clear()
+    w2 = HopWatch(0, 2, 0.2, on_fire=fired.append, interval=0.05).start()
+    w2.begin("group", hops=[1], t0=time.time() - 5.0)
+    deadline = time.time() + 5
+    while not fired and time.time() < deadline:
+        time.sleep(0.05)
+    w2.stop()
+    assert fired and fired[0]["kind"] == "stall" and fired[0]["exit_code"] == EXIT_HOP_STALL
+    fired.clear()
+    w3 = HopWatch(0, 2, 1.0, on_fire=fired.append)
+    w3.stop()
+    w3.abort("late error during teardown")
+    assert not fired
 
 
 # ---------------------------------------------------------------------------

@@ -1,7 +1,7 @@
 """Stream / hardware-queue budget (profiles/r5_stream_budget.md).
 
 The headline engine's active streams per workload shape are counted by
-``MOPEngine.stream_budget``; lanes default to 1 and, at world > 1, never
+``MOPEngine.stream_budget``; lanes default to 4 (one GPU) and, at world > 1, never
 push the hop's streams out of the 4 hardware queues.  CPU: the engine is
 built on gloo ranks (the accounting does not depend on the device)."""
 
@@ -44,7 +44,8 @@ def test_headline_stream_budget_world2(tmp_path):
     world = 2
     mp.spawn(_budget_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     out = json.load(open(tmp_path / "budget.json"))
-    assert out["LANES"] == 1 and out["lanes_default"] == 1
+    # the default asks for 4 lanes (world 1); at world > 1 they are clamped
+    assert out["LANES"] == 4 and out["lanes_default"] == 1
     # 4 configs per GPU (N = 2): compute, branch, side wgrad, hop, RCCL
     assert out["headline"] == ["branch", "compute", "hop", "rccl_hop", "side_wgrad"]
     # one config per GPU (the N = 8 shape): no side batch -> 4 = the queues
