@@ -291,7 +291,6 @@ _SIGS.update({
     "cer_wgrad_batch_flush": [c_i, c_i, c_p],
     "cer_wgrad_batch_set_grid": [c_i],
     "cer_wgrad_batch_set_rows": [c_i],
-    "cer_wgrad_batch_set_ring": [c_i],
     "cer_wgrad_batch_set_narrow": [c_i],
     "cer_wgrad_batch_pending": [],
     "cer_bn_set_zmask": [c_i],
@@ -554,15 +553,9 @@ if os.environ.get("CER_FP32_WIDE", "1") != "0":
 _KSPLIT32 = (24, 26, 30, 32)
 if os.environ.get("CER_FP32_KSPLIT", "1") != "0":
     FP32_VARIANTS = {op: vs + (_KSPLIT32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
-# 36-47: wave-specialised twins of the wide register-staged fwd / dgrad
-# kernels (512 threads: 4 loader waves fill a 4-stage LDS ring, 4 MFMA waves
-# consume it; conv.hip kloop_ws), three tiles, with and without split-K.
-# Measured slower than the best of ids 0-35 on every ResNet-50 problem
-# (median 1.45x at 8 configs, profiles/r4_ws.md), so CER_FP32_WS=1 adds them
-# to the autotune for A/B runs only.
-_WS32 = (36, 37, 38, 42, 43, 44)
-if os.environ.get("CER_FP32_WS", "0") != "0":
-    FP32_VARIANTS = {op: vs + (_WS32 if op < 2 else ()) for op, vs in FP32_VARIANTS.items()}
+# (ids 36-47, the wave-specialised twins, and the LDS-DMA wgrad ring were
+# measured slower -- profiles/r4_ws.md, r5_wgring.md -- and removed in
+# round 6; their A/B evidence stays in those profiles and in git history)
 
 
 def _select(op, key, launch, dtype, after_tune=None):

@@ -157,6 +157,7 @@ def main(argv=None):
     ap.add_argument("--sweep", action="store_true", help="time every kernel variant per shape")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--ops", default="0,1,2", help="ops to sweep: 0 fwd, 1 dgrad, 2 wgrad")
+    ap.add_argument("--no_miopen", action="store_true", help="time our kernels only")
     a = ap.parse_args(argv)
     dtype = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     backend.set_backend("hip")
@@ -170,7 +171,10 @@ def main(argv=None):
     rows = []
     tot = collections.defaultdict(float)
     for shape, count in resnet50_shapes(a.B).items():
-        r = bench_shape(shape, a.G, a.iters, dtype)
+        r = bench_shape(shape, a.G, a.iters, dtype, miopen=not a.no_miopen)
+        for kk in ("miopen_fwd", "miopen_dgrad", "miopen_wgrad"):
+            r.setdefault(kk, float("nan"))
+            r["tflops"].setdefault(kk, float("nan"))
         r["shape"] = shape
         r["count"] = count
         rows.append(r)

@@ -2648,188 +2648,20 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
 
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
-constexpr int WS_THREADS = 512;
-constexpr int WS_S = 4;          // LDS ring stages
-constexpr int WS_P = 4;          // loader register sets (steps of global loads in flight)
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-
-__device__ __forceinline__ void ws_wait(unsigned* c, unsigned target) {
-  lds_u32* lc = (lds_u32*)c;
-  while (__hip_atomic_load(lc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-    __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-
-__device__ __forceinline__ void ws_post(unsigned* c) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_add((lds_u32*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-// f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>), unrolled
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Consumer side of the wave-specialised K loops (waves 0-3): ONE MFMA wave
-// per SIMD, so nothing else hides its LDS latency.  Each step's two 16-deep
-// substeps are software-pipelined: substep 1's fragments are read under
-// substep 0's MFMAs, the next step's substep 0 under substep 1's.  The
-// sched_barriers keep the reads ahead of the MFMAs and the counter waits
-// behind them (without them hipcc sinks the reads to their use and floats
-// the waits up: either way the reads are waited for in full).
-// The last step re-reads its own stage instead of a next one, so no read is
-// conditional (a conditionally live fragment set spills).
-template <int S, typename Frag, typename Read, typename Mma>
-__device__ __forceinline__ void ws_consume(int T, unsigned* cnt, Read&& read, Mma&& mma) {
-  unsigned* full = cnt;
-  unsigned* freed = cnt + S;
-  if (T <= 0) return;
-  Frag R0, R1;
-  ws_wait(&full[0], 4u);
-  read(0, 0, R0);
-  for (int t = 0; t < T; ++t) {
-    const int st = t % S;
-    read(st, 1, R1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(R0);
-    // the waits below are not memory operations to the scheduler: without
-    // this fence it hoists ws_post's lgkmcnt(0) above the MFMAs, right
-    // after the first one, and R1's reads are waited for in full there
-    __builtin_amdgcn_sched_barrier(0);
-    ws_post(&freed[st]);                        // every read of stage t has returned
-    const int tn = t + 1 < T ? t + 1 : t;
-    ws_wait(&full[tn % S], 4u * (unsigned)(tn / S + 1));
-    read(tn % S, 0, R0);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(R1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-// Loader side (waves 4-7): P register sets of global loads in flight; step t
-// waits for ring stage t % S to be released by all four consumers, splits and
-// stores register set t % P into it, refills that set with step t + P and
-// publishes the stage.  ``load`` is called in increasing step order (it may
-// keep an incremental im2col position) and past the last step (out-of-range
-// loads return zeros without memory traffic, as kloop32 does).
-template <int S, int P, typename Load, typename Store>
-__device__ __forceinline__ void ws_produce(int k0, int T, unsigned* cnt, Load&& load,
-                                           Store&& store) {
-  unsigned* full = cnt;
-  unsigned* freed = cnt + S;
-  static_for<P>([&](auto U) { load(k0 + decltype(U)::value, U); });
-  for (int t = 0; t < T; t += P) {
-    static_for<P>([&](auto U) {
-      const int tt = t + decltype(U)::value;
-      const int st = tt % S;
-      const bool live = tt < T;
-      if (live) {
-        if (tt >= S) ws_wait(&freed[st], 4u * (unsigned)(tt / S));
-        store(st, U);
-      }
-      // issued on every path: a load under a branch makes hipcc's vmcnt
-      // bookkeeping path-dependent, and it then drains every set (vmcnt(0))
-      // before each store instead of waiting for the one set it stores
-      load(k0 + tt + P, U);
-      if (live) ws_post(&full[st]);
-    });
-  }
-}
-
-// K loop of the wave-specialised fwd / dgrad twins (WS = 1): waves 4-7 run
-// the kernel's own load / store lambdas (register-staged global loads, WS_P
-// sets in flight, hi/lo split, ds_write into stage t % S), waves 0-3 read
-// fragments / issue MFMAs per stage (ws_consume); per-stage full / free LDS
-// counters as in wgrad_ws32.  The lambdas see tid = threadIdx.x & 255.
-template <int S, int P, typename Frag, typename Load, typename Store, typename Read, typename Mma>
-__device__ __forceinline__ void kloop_ws(int k0, int k1, unsigned* cnt, Load&& load, Store&& store,
-                                         Read&& read, Mma&& mma) {
-  if (threadIdx.x >= 256)
-    ws_produce<S, P>(k0, k1 - k0, cnt, load, store);
-  else
-    ws_consume<S, Frag>(k1 - k0, cnt, read, mma);
-}
-
-// fragments of one 16-deep substep of the wide (32x32x16) kernels' 64x64 wave tiles
-template <int BM, int BN>
-struct FragW {
-  bf16x8 ah[BM / 64], al[BM / 64], bh[BN / 64], bl[BN / 64];
-};
-
-// NT x NT images (fwd; mma3w_nt's reads)
-template <int BM, int BN>
-__device__ __forceinline__ void read_w_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
-                                          int lane, int s, FragW<BM, BN>& F) {
-  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    F.ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
-    F.al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    F.bh[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 2 * s + h));
-    F.bl[j] = *reinterpret_cast<const bf16x8*>(sb + nt_off(wn * TN + 32 * j + r, 4 + 2 * s + h));
-  }
-}
-
-// NT x TN images (dgrad; mma3w_nn's reads)
-template <int BM, int BN>
-__device__ __forceinline__ void read_w_nn(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
-                                          int lane, int s, FragW<BM, BN>& F) {
-  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    F.ah[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 2 * s + h));
-    F.al[i] = *reinterpret_cast<const bf16x8*>(sa + nt_off(wm * TM + 32 * i + r, 4 + 2 * s + h));
-  }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    F.bh[j] = tn_frag32<BN>(sb, 16 * s, wn * TN + 32 * j, lane);
-    F.bl[j] = tn_frag32<BN>(sb, KS + 16 * s, wn * TN + 32 * j, lane);
-  }
-}
-
-template <int BM, int BN>
-__device__ __forceinline__ void mma_w(const FragW<BM, BN>& F, f32x16 (&acc)[BM / 64][BN / 64]) {
-#pragma unroll
-  for (int i = 0; i < BM / 64; ++i)
-#pragma unroll
-    for (int j = 0; j < BN / 64; ++j) acc[i][j] = mfma3w(F.bh[j], F.bl[j], F.ah[i], F.al[i], acc[i][j]);
-}
-
-// WS = 1: the wave-specialised twin (512 threads: waves 4-7 load / split /
-// store into a WS_S-stage LDS ring, waves 0-3 run the MFMAs and, after the
-// loaders have exited, the split-K reduction and the epilogue; kloop_ws)
-template <int BM, int BN, int GM, bool WIDE = false, int WG = 1, int WS = 0>
-__global__ __launch_bounds__(NTHREADS * (WS ? 2 : WG),
-                             WS ? 2 : (WG == 1 ? 2 : 1))
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1)
 void igemm_nt32(NTParams p) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
-  static_assert(!WS || (WIDE && WG == 1 && GM != GM_SLOW), "WS: aligned wide kernels only");
-  constexpr int NST = WS ? WS_S : 2;                          // LDS stages
+  constexpr int NST = 2;                                       // LDS stages
   constexpr int CPR = KS / 8;                                  // 8-float chunks per row
   constexpr int A_CH = BM * CPR / NTHREADS, B_CH = BN * CPR / NTHREADS;
   constexpr int TILE_ELEMS = NST * (BM + BN) * BK;
-  constexpr int LDS_ELEMS = (TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN) + (WS ? 16 : 0);
+  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
   static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
                 "group hand-off must fit one group's LDS region");
   __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
   const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
   bf16_t* const lds = lds_all + grp * LDS_ELEMS;
-  unsigned* const wscnt = reinterpret_cast<unsigned*>(lds_all + LDS_ELEMS - 16);
-  if constexpr (WS != 0) {
-    if (threadIdx.x < 2 * WS_S) wscnt[threadIdx.x] = 0u;
-    __syncthreads();
-  }
 #define SA(buf) (lds + (buf) * (BM * BK))
 #define SB(buf) (lds + NST * BM * BK + (buf) * (BN * BK))
 
@@ -2861,7 +2693,7 @@ void igemm_nt32(NTParams p) {
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = WS ? WS_P : fp32_sets<BM, BN, WIDE>();
+  constexpr int SETS = fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -2920,16 +2752,7 @@ void igemm_nt32(NTParams p) {
   if constexpr (WIDE) {
     zero_accw<BM, BN>(acc);
     auto mma = [&](int cur) { mma3w_nt<BM, BN>(SA(cur), SB(cur), wm, wn, lane, acc); };
-    if constexpr (WS != 0) {
-      kloop_ws<WS_S, WS_P, FragW<BM, BN>>(
-          kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles,
-          [&](int st, int s, FragW<BM, BN>& F) { read_w_nt<BM, BN>(SA(st), SB(st), wm, wn, lane, s, F); },
-          [&](const FragW<BM, BN>& F) { mma_w<BM, BN>(F, acc); });
-      if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
-      __syncthreads();                           // every consumer is past its last ring read
-    } else {
-      kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
-    }
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   } else {
@@ -3073,28 +2896,21 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WIDE = false, int WG = 1, int WS = 0>
-__global__ __launch_bounds__(NTHREADS * (WS ? 2 : WG),
-                             WS ? 2 : (WG == 1 ? 2 : 1))
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1)
 void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
-  static_assert(!WS || (WIDE && WG == 1), "WS: wide kernels only");
-  constexpr int NST = WS ? WS_S : 2;
+  constexpr int NST = 2;
   constexpr int CPR = KS / 8;
   constexpr int A_CH = BM * CPR / NTHREADS;
   constexpr int B_CPR = BN / 8, B_CH = KS * B_CPR / NTHREADS, B_RSTEP = NTHREADS / B_CPR;
   constexpr int TILE_ELEMS = NST * (BM + BN) * BK;
-  constexpr int LDS_ELEMS = (TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN) + (WS ? 16 : 0);
+  constexpr int LDS_ELEMS = TILE_ELEMS > 8 * BN ? TILE_ELEMS : 8 * BN;
   static_assert(WG == 1 || LDS_ELEMS * 2 >= (BM / 32) * (BN / 32) * 16 * NTHREADS,
                 "group hand-off must fit one group's LDS region");
   __shared__ __attribute__((aligned(16))) bf16_t lds_all[LDS_ELEMS * WG];
   const int grp = WG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / NTHREADS);
   bf16_t* const lds = lds_all + grp * LDS_ELEMS;
-  unsigned* const wscnt = reinterpret_cast<unsigned*>(lds_all + LDS_ELEMS - 16);
-  if constexpr (WS != 0) {
-    if (threadIdx.x < 2 * WS_S) wscnt[threadIdx.x] = 0u;
-    __syncthreads();
-  }
 
   const int tiles_n = (p.N + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * tiles_n;
@@ -3120,7 +2936,7 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
-  constexpr int SETS = WS ? WS_P : fp32_sets<BM, BN>();
+  constexpr int SETS = fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
@@ -3180,19 +2996,7 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
       mma3w_nn<BM, BN>(lds + cur * (BM * BK), lds + NST * BM * BK + cur * (BK * BN), wm, wn, lane,
                        acc);
     };
-    if constexpr (WS != 0) {
-      bf16_t* const sb0 = lds + NST * BM * BK;
-      kloop_ws<WS_S, WS_P, FragW<BM, BN>>(
-          kr.kt0, kr.kt1, wscnt, load_tiles, store_tiles,
-          [&](int st, int s, FragW<BM, BN>& F) {
-            read_w_nn<BM, BN>(lds + st * (BM * BK), sb0 + st * (BK * BN), wm, wn, lane, s, F);
-          },
-          [&](const FragW<BM, BN>& F) { mma_w<BM, BN>(F, acc); });
-      if (threadIdx.x >= NTHREADS) return;        // loaders done; barriers below count waves 0-3
-      __syncthreads();                           // every consumer is past its last ring read
-    } else {
-      kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
-    }
+    kloop32<SETS>(kr.kt0, kr.kt1, load_tiles, store_tiles, mma);
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN, true>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   } else {
@@ -3372,102 +3176,6 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   }
 }
 
-// LDS-DMA ring wgrad body for HL operands (profiles/r4_ws.md
-// "what the measurements point to"): dy and x are both already split into
-// (hi, lo) bf16 pairs in HBM (HL format: per 8 channels 16 B of hi, then
-// 16 B of lo), so a stage needs no VGPR staging, no split VALU and no
-// ds_write -- every 16-B chunk goes global -> LDS by buffer_load ... lds
-// straight into the register body's LDS image ([64 rows][COLS]: rows 0-31
-// the hi halves of the stage's 32 reduction rows, rows 32-63 the lo halves,
-// tn_off swizzle), which mma3_tn reads unchanged.  Lane i of a DMA
-// instruction fills 16-B slot (i % 16) of image row (base + i / 16); the
-// slot's chunk is column group tn_col16(row, slot), half (row >> 5).  An
-// S-stage ring (ring_loop) keeps S - 1 stages in flight.  Padding taps and
-// rows past the split's range load from out-of-range offsets: zeros.
-template <int BM, int BN, int S>
-__device__ __forceinline__ void wgrad_ring_body32(const WGParams& p, int work, bf16_t* lds) {
-  constexpr int AJ = BM / 32, BJ = BN / 32, LPW = AJ + BJ;
-  constexpr int STAGE = (BM + BN) * BK;
-  constexpr int AROWS = 512 / BM, AC16 = BM / 8, BROWS = 512 / BN, BC16 = BN / 8;
-  const int tiles_k = (p.K + BN - 1) / BN;
-  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
-  const int cfg = work / (tiles * p.splits);
-  const int rem = work - cfg * tiles * p.splits;
-  const int split = rem / tiles, tile = rem - split * tiles;
-  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
-  const int n0 = tn_ * BM, k0 = tk * BN;
-  const int ms = split * p.m_per_split;
-  const int me = min(p.Mred, ms + p.m_per_split);
-  if (ms >= me) return;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wa = wid >> 1, wb = wid & 1;
-  const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
-  const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
-  const auto rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
-  const auto rX = make_rsrc(xb, p.x.bytes);
-  int arow[AJ];
-  uint32_t aoff[AJ];
-#pragma unroll
-  for (int j = 0; j < AJ; ++j) {
-    arow[j] = (wid * AJ + j) * AROWS + lane / AC16;          // image row 0..63
-    const int n = n0 + 8 * tn_col16<BM>(arow[j], lane % AC16);
-    aoff[j] = n < p.N ? ((uint32_t)((arow[j] & 31) * p.ldy + n) * 4u + 16u * (arow[j] >> 5))
-                      : OOB;
-  }
-  int brow[BJ];
-  KPos bk[BJ];
-  bool bok[BJ];
-#pragma unroll
-  for (int j = 0; j < BJ; ++j) {
-    brow[j] = (wid * BJ + j) * BROWS + lane / BC16;
-    const int k = k0 + 8 * tn_col16<BN>(brow[j], lane % BC16);
-    bok[j] = k < p.K;
-    bk[j] = kpos_init(p.x, bok[j] ? k : 0);
-  }
-  auto issue = [&](int mt, int st) {
-    bf16_t* sa = lds + st * STAGE;
-    bf16_t* sb = sa + BM * BK;
-    const int mbase = ms + mt * KS, lim = me - mbase;
-    const uint32_t so = (uint32_t)mbase * (uint32_t)p.ldy * 4u;
-#pragma unroll
-    for (int j = 0; j < AJ; ++j)
-      glds16(rDY, sa + (wid * AJ + j) * 512, (arow[j] & 31) < lim ? aoff[j] : OOB, so);
-#pragma unroll
-    for (int j = 0; j < BJ; ++j) {
-      const RowA ra = row_init<GM_FWD>(p.x, mbase + (brow[j] & 31), me);
-      const uint32_t off = a_off<GM_FWD, 4>(p.x, ra, bk[j].r, bk[j].s, bk[j].c);
-      glds16(rX, sb + (wid * BJ + j) * 512, bok[j] ? off + 16u * (uint32_t)(brow[j] >> 5) : OOB,
-             0);
-    }
-  };
-  f32x4 acc[BM / 32][BN / 32];
-  zero_acc<BM, BN>(acc);
-  ring_loop<S, LPW>((me - ms + KS - 1) / KS, issue, [&](int st) {
-    mma3_tn<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wa, wb, lane, acc);
-  });
-  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
-  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
-  const int fr = lane & 15, fc = lane >> 4;
-  const bool split_k = p.splits > 1;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = n0 + wa * TM + 16 * i + 4 * fc + e;
-        const int k = k0 + wb * TN + 16 * j + fr;
-        if (n < p.N && k < p.K) {
-          float* d = dwb + (int64_t)n * p.K + k;
-          if (split_k)
-            atomicAdd(d, acc[i][j][e]);
-          else
-            *d = acc[i][j][e];
-        }
-      }
-}
-
 template <int BM, int BN, int GM, bool WIDE = false>
 __global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
@@ -3491,236 +3199,6 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
     const WGParams p = b.p[i];
     wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
-  }
-}
-
-// batched fp32 weight gradients, LDS-DMA ring twin (CER_WGB_RING = S stages):
-// items whose dy and x are both HL take wgrad_ring_body32, the others the
-// register body (same LDS image, so one kernel serves a mixed batch)
-template <int BM, int BN, int S>
-__global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32r(WGBatch b) {
-  __shared__ __attribute__((aligned(16))) bf16_t lds[S * (BM + BN) * BK];
-  const int total = b.start[b.n];
-  const int nwg = (int)gridDim.x;
-  for (int w = blockIdx.x; w < total; w += nwg) {
-    const int work = nwg >= total ? xcd_remap(w, nwg) : w;
-    int i = 0;
-    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
-    const WGParams p = b.p[i];
-    if (p.x_hl && p.dy_hl)
-      wgrad_ring_body32<BM, BN, S>(p, work - b.start[i], lds);
-    else
-      wgrad_reg_body32<BM, BN, GM_FWD>(p, work - b.start[i], lds);
-    if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
-  }
-}
-
-// ===========================================================================
-// Wave-specialised fp32 weight gradient (wgrad_ws32)
-// ===========================================================================
-// The register-staged wgrad (wgrad_reg_body32) has every wave load, split,
-// store, wait at a block barrier and multiply in turn: one barrier per 32-deep
-// step, and one register set for the 128x128 tile (a second one spills), so
-// each step's L2 / HBM latency is covered by ONE step of MFMA work and about a
-// quarter of the wave time sits at barriers (profiles/r2_conv32_pmc_isa.md).
-// Here a 512-thread workgroup (one per CU) splits the roles:
-//  * waves 4-7 (loaders) keep WS_P steps of global loads in flight in
-//    registers, split fp32 -> (hi, lo) bf16 (HL operands are taken as they
-//    are) and write the TN images (tn_off_w, hi rows 0-31, lo rows 32-63)
-//    into an S-stage LDS ring;
-//  * waves 0-3 (consumers) read a stage's 32x32x16 fragments and issue its
-//    24 MFMAs (2 substeps x 3 passes x 2x2 tiles of a 64x64 wave tile),
-//    reading the NEXT stage's fragments under them.  They never wait at a
-//    block barrier.
-// Hand-off by two monotone LDS counters per stage: a loader wave adds 1 to
-// full[s] once its ds_writes of the stage have completed (lgkmcnt(0)); a
-// consumer wave adds 1 to free[s] once its fragment reads of the stage have
-// returned.  Step t (stage t % S) is readable when full[s] >= 4 (t / S + 1)
-// and writable when free[s] >= 4 (t / S).  Waves 0-3 and 4-7 land on the 4
-// SIMDs in the same order, so every SIMD holds one consumer and one loader:
-// the loader's split VALU and LDS writes issue in the 24 free cycles of each
-// 32-cycle 32x32x16 MFMA of its partner.  Counters and ring live in ONE
-// __shared__ array (a second LDS object can make hipcc drain vmcnt).
-template <int BM, int BN, int S>
-__device__ __forceinline__ void wgrad_ws_item(const WGParams& p, int work, bf16_t* lds,
-                                              unsigned* cnt) {
-  constexpr int STAGE = (BM + BN) * BK;            // [64 x BM] A image + [64 x BN] B image
-  const int tiles_k = (p.K + BN - 1) / BN;
-  const int tiles = ((p.N + BM - 1) / BM) * tiles_k;
-  const int cfg = work / (tiles * p.splits);
-  const int rem = work - cfg * tiles * p.splits;
-  const int split = rem / tiles, tile = rem - split * tiles;
-  const int tn_ = tile / tiles_k, tk = tile - tn_ * tiles_k;
-  const int n0 = tn_ * BM, k0 = tk * BN;
-  const int ms = split * p.m_per_split;
-  const int me = min(p.Mred, ms + p.m_per_split);
-  const int T = ms < me ? (me - ms + KS - 1) / KS : 0;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (wid >= 4) {
-    // ---------------- loaders ----------------
-    constexpr int A_CPR = BM / 8, B_CPR = BN / 8;
-    constexpr int A_CH = KS * A_CPR / 256, B_CH = KS * B_CPR / 256;
-    constexpr int A_RSTEP = 256 / A_CPR, B_RSTEP = 256 / B_CPR;
-    const int tl = tid - 256;
-    const int a_col = 8 * (tl % A_CPR), b_col = 8 * (tl % B_CPR);
-    const int a_row0 = tl / A_CPR, b_row0 = tl / B_CPR;
-    const int kk0 = k0 + b_col;
-    const bool b_kok = kk0 < p.K;
-    KPos bk{0, 0, 0};
-    if (b_kok) bk = kpos_init(p.x, kk0);
-    const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
-    const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
-    const __amdgpu_buffer_rsrc_t rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
-    const __amdgpu_buffer_rsrc_t rX = make_rsrc(xb, p.x.bytes);
-    const bool a_nok = n0 + a_col < p.N;
-    uint4 ra[WS_P][2 * A_CH], rb[WS_P][2 * B_CH];
-    auto load = [&](int t, auto U) {
-      constexpr int u = decltype(U)::value;
-      const int mbase = ms + t * KS;
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int m = mbase + a_row0 + A_RSTEP * i;
-        const uint32_t o = (m < me && a_nok) ? (uint32_t)(m * p.ldy + n0 + a_col) * 4u : OOB;
-        ra[u][2 * i] = bload(rDY, o);
-        ra[u][2 * i + 1] = bload(rDY, o + 16u);
-      }
-#pragma unroll
-      for (int i = 0; i < B_CH; ++i) {
-        const RowA rr = row_init<GM_FWD>(p.x, mbase + b_row0 + B_RSTEP * i, me);
-        const uint32_t off = a_off<GM_FWD, 4>(p.x, rr, bk.r, bk.s, bk.c);
-        const uint32_t o = b_kok ? off : OOB;
-        rb[u][2 * i] = bload(rX, o);
-        rb[u][2 * i + 1] = bload(rX, o + 16u);
-      }
-    };
-    auto store = [&](int st, auto U) {
-      constexpr int u = decltype(U)::value;
-      bf16_t* sa = lds + st * STAGE;
-      bf16_t* sb = sa + BK * BM;
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int row = a_row0 + A_RSTEP * i;
-        uint4 h, l;
-        take_hi_lo(p.dy_hl != 0, ra[u][2 * i], ra[u][2 * i + 1], h, l);
-        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row, a_col)) = h;
-        *reinterpret_cast<uint4*>(sa + tn_off_w<BM>(row + KS, a_col)) = l;
-      }
-#pragma unroll
-      for (int i = 0; i < B_CH; ++i) {
-        const int row = b_row0 + B_RSTEP * i;
-        uint4 h, l;
-        take_hi_lo(p.x_hl != 0, rb[u][2 * i], rb[u][2 * i + 1], h, l);
-        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
-        *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
-      }
-    };
-    // loads past the item's rows are issued anyway (out-of-range offsets:
-    // zeros, no memory traffic) so no branch guards a load and hipcc keeps
-    // counted vmcnt waits
-    ws_produce<S, WS_P>(0, T, cnt, load, store);
-    return;
-  }
-  // ---------------- consumers ----------------
-  constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
-  const int wa = wid >> 1, wb = wid & 1;
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  // tn_frag32 addresses, precomputed: for the 128-column images tn_off_w's
-  // swizzle XORs chunk bits 3-4 with row & 3 = q (every fragment row offset
-  // is a multiple of 4), so fragment i of wave column w starts at
-  // (8h + q) * 128 + 32 ((2w + i) ^ q) + 16g + 4pp; the substep / hi-lo row
-  // offsets are compile-time element offsets on top (one VGPR per i, not one
-  // per fragment read)
-  static_assert(BM == 128 && BN == 128, "wgrad_ws32: 128x128 tiles (tn_off_w<128>)");
-  const int fh = lane >> 5, fg = (lane >> 4) & 1, fq = (lane & 15) >> 2, fp = lane & 3;
-  int abase[FM], bbase[FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-    abase[i] = (8 * fh + fq) * BM + 32 * ((2 * wa + i) ^ fq) + 16 * fg + 4 * fp;
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-    bbase[j] = (8 * fh + fq) * BN + 32 * ((2 * wb + j) ^ fq) + 16 * fg + 4 * fp;
-  auto frag = [&](const bf16_t* tile, int base, int row0, int cols) {
-    const bf16_t* p0 = tile + base + row0 * cols;
-    s16x4 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    s16x4 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * cols));
-    s16x8 tt = __builtin_shufflevector(t0, t1, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_bit_cast(bf16x8, tt);
-  };
-  // one 16-deep substep's fragments of stage st (hi and lo of both operands)
-  struct Sub {
-    bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
-  };
-  auto read_sub = [&](int st, int sub, Sub& F) {
-    const bf16_t* sa = lds + st * STAGE;
-    const bf16_t* sb = sa + BK * BM;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      F.ah[i] = frag(sa, abase[i], 16 * sub, BM);
-      F.al[i] = frag(sa, abase[i], KS + 16 * sub, BM);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      F.bh[j] = frag(sb, bbase[j], 16 * sub, BN);
-      F.bl[j] = frag(sb, bbase[j], KS + 16 * sub, BN);
-    }
-  };
-  auto mma_sub = [&](const Sub& F) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        acc[i][j] = mfma3w(F.ah[i], F.al[i], F.bh[j], F.bl[j], acc[i][j]);
-  };
-  ws_consume<S, Sub>(T, cnt, read_sub, mma_sub);
-  // D[n][k]: k = lane & 31 (32 consecutive k per register: 128-B rows)
-  float* dwb = p.dw + (int64_t)cfg * p.dw_gstride;
-  const bool split_k = p.splits > 1;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int n = n0 + wa * TM + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
-        const int k = k0 + wb * TN + 32 * j + r;
-        if (n < p.N && k < p.K && T > 0) {
-          float* d = dwb + (int64_t)n * p.K + k;
-          if (split_k)
-            atomicAdd(d, acc[i][j][e]);
-          else
-            *d = acc[i][j][e];
-        }
-      }
-}
-
-// batched: one work item per block (XCD-ordered), or -- a grid capped below
-// the item count (the side-stream batch) -- items walked block-strided
-template <int BM, int BN>
-__global__ __launch_bounds__(WS_THREADS, 2) void wgrad_ws32(WGBatch b) {
-  constexpr int STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(16))) bf16_t lds[WS_S * STAGE + 4 * WS_S];
-  unsigned* cnt = reinterpret_cast<unsigned*>(lds + WS_S * STAGE);
-  const int total = b.start[b.n];
-  const int nwg = (int)gridDim.x;
-  if (threadIdx.x < 2 * WS_S) cnt[threadIdx.x] = 0u;
-  __syncthreads();
-  for (int w = blockIdx.x; w < total; w += nwg) {
-    const int work = nwg >= total ? xcd_remap(w, nwg) : w;
-    int i = 0;
-    while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
-    wgrad_ws_item<BM, BN, WS_S>(b.p[i], work - b.start[i], lds, cnt);
-    if (w + nwg < total) {              // the next item restarts the ring
-      __syncthreads();
-      if (threadIdx.x < 2 * WS_S) cnt[threadIdx.x] = 0u;
-      __syncthreads();
-    }
   }
 }
 
@@ -3792,10 +3270,10 @@ static long ntiles(long M, long N, int bm, int bn) { return ((M + bm - 1) / bm) 
 static int choose(int op, long M, long N, long K, int G, bool pipe_ok) {
   if (g_variant[op] >= 0) {
     int v = g_variant[op];
-    // fp32 twins: 12-23 wide, 24-35 intra-block K split, 36-47 wave-specialised
-    int wide = v >= 36 ? 36 : v >= 24 ? 24 : v >= 12 ? 12 : 0;
+    // fp32 twins: 12-23 wide, 24-35 intra-block K split
+    int wide = v >= 24 ? 24 : v >= 12 ? 12 : 0;
     v -= wide;
-    if (op == 2 && wide >= 24) wide = 0;            // wgrad: no K-split / ws twins here
+    if (op == 2 && wide >= 24) wide = 0;            // wgrad: no K-split twins here
     if (op == 2 && v >= 6) v -= 6;                  // wgrad has its own split-K
     v += wide;
     if (((v / 3) & 1) && !pipe_ok) v -= 3;
@@ -3897,12 +3375,8 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
-                          bool wide = false, int wg = 1, bool ws = false) {
+                          bool wide = false, int wg = 1) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
-  if (ws && fast) {                // wave-specialised 32x32x16 twin, 512 threads
-    igemm_nt32<BM, BN, GM_FWD, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p);
-    return;
-  }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
       igemm_nt32<BM, BN, GM_FWD, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
@@ -3954,14 +3428,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   if (p.a_hl && !fast) return (int)hipErrorInvalidValue;
   const bool ring_ok = fast && p.a.Cg % KS == 0;
   int v = choose(0, p.M, p.N, p.K, G, ring_ok);
-  bool wide = false, ws = false;
+  bool wide = false;
   int wg = 1;
-  if (v >= 36) {                                   // wave-specialised twins of 12-23
-    v -= 36;
-    if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
-    wide = p.bb.part == nullptr;
-    ws = wide && fast;
-  } else if (v >= 24) {
+  if (v >= 24) {
     wg = 2;
     v -= 24;
     if ((v / 3) & 1) v -= 3;                       // register-staged kernels only
@@ -3981,9 +3450,9 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg, ws); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide, 1, ws); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg, ws); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide, 1); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg); break;
   }
   return (int)hipGetLastError();
 }
@@ -4151,16 +3620,9 @@ CER_API void cer_conv_dgrad_babwd(float* dbias, int64_t dbstride, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
-                          bool wide = false, int wg = 1, bool ws = false) {
+                          bool wide = false, int wg = 1) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
-  if (ws) {                        // wave-specialised 32x32x16 twin, 512 threads
-    if (strided)
-      igemm_nn32<BM, BN, GM_DGS, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
-    else
-      igemm_nn32<BM, BN, GM_DG1, true, 1, 1><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
-    return;
-  }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && !wide) {                         // intra-block K split, 512 threads
       if (strided)
@@ -4246,12 +3708,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       strided = st > 1;
     }
     int v = choose(1, p.M, p.N, p.K, G, !f32 && Cout % 64 == 0);
-    bool wide = false, ws = false;
+    bool wide = false;
     int wg = 1;
-    if (v >= 36) {                        // fp32 wave-specialised twins of 12-23
-      v -= 36;
-      wide = ws = f32;
-    } else if (v >= 24) {                 // fp32 intra-block K-split twins
+    if (v >= 24) {                        // fp32 intra-block K-split twins
       wg = f32 ? 2 : 1;
       v -= 24;
     } else if (v >= 12) {                 // fp32 32x32x16-MFMA twins of 0-11
@@ -4277,9 +3736,9 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
     }
     if (f32) {
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg, ws); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1, ws); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg, ws); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg); break;
       }
       return (int)hipGetLastError();
     }
@@ -4701,29 +4160,6 @@ CER_API int cer_wgrad_batch_add_grouped_f32(const float* x, int B, int H, int W,
                            dw_gstride);
 }
 
-// the wave-specialised kernel for 128x128 fp32 batches (CER_WGB_WS, A/B)
-static int g_wgb_ws = -1;
-static bool wgb_ws() {
-  if (g_wgb_ws < 0) {
-    const char* e = getenv("CER_WGB_WS");
-    g_wgb_ws = e ? atoi(e) : 0;
-  }
-  return g_wgb_ws > 0;
-}
-CER_API void cer_wgrad_batch_set_ws(int on) { g_wgb_ws = on ? 1 : 0; }
-
-// LDS-DMA ring for the HL items of fp32 batches: stages (0 = off;
-// CER_WGB_RING; 3 stages only for tiles up to 128x64: 2 workgroups per CU)
-static int g_wgb_ring = -1;
-static int wgb_ring() {
-  if (g_wgb_ring < 0) {
-    const char* e = getenv("CER_WGB_RING");
-    g_wgb_ring = e ? atoi(e) : 0;
-  }
-  return g_wgb_ring;
-}
-CER_API void cer_wgrad_batch_set_ring(int stages) { g_wgb_ring = stages > 0 ? stages : 0; }
-
 // grid cap of the next fp32 batch flushes (0 = one block per work item)
 static int g_wgb_grid = 0;
 CER_API void cer_wgrad_batch_set_grid(int blocks) { g_wgb_grid = blocks > 0 ? blocks : 0; }
@@ -4743,14 +4179,7 @@ static void wgb32_launch_sel(hipStream_t stream, const int* idx, int n) {
     bt.start[bt.n] = tot;
     const int grid = g_wgb_grid > 0 && g_wgb_grid < tot ? g_wgb_grid : tot;
     if (tot <= 0) continue;
-    if (BM == 128 && BN == 128 && wgb_ws())
-      wgrad_ws32<128, 128><<<grid, WS_THREADS, 0, stream>>>(bt);
-    else if (!WIDE && wgb_ring() == 2)
-      wgrad_batch32r<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(bt);
-    else if (!WIDE && wgb_ring() == 3 && BM * BN <= 128 * 64)
-      wgrad_batch32r<BM, BN, 3><<<grid, NTHREADS, 0, stream>>>(bt);
-    else
-      wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
+    wgrad_batch32<BM, BN, WIDE><<<grid, NTHREADS, 0, stream>>>(bt);
   }
 }
 

@@ -69,7 +69,6 @@ def main(argv=None):
     ap.add_argument("--variants", default="0,1,2,12,13,14")
     ap.add_argument("--rows", default="0")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--ws", default="0", help="wave-specialised 128x128 kernel off / on (0,1)")
     a = ap.parse_args(argv)
     backend.set_backend("hip")
     layers, flops = _layers(a.G, a.B)
@@ -83,14 +82,11 @@ def main(argv=None):
     for rows in (int(r) for r in a.rows.split(",")):
         streams.set_batch_rows(rows)
         for v in (int(s) for s in a.variants.split(",")):
-            for ws in (int(w) for w in a.ws.split(",")):
-                _hip.lib().cer_wgrad_batch_set_ws(ws)
-                streams.set_batch_variant(v)
-                ms = _time(batched, a.reps)
-                print(json.dumps({"G": a.G, "mode": "batched", "variant": v, "ws": ws,
-                                  "rows": rows, "layers": len(layers), "ms": round(ms, 3),
-                                  "tflops": round(flops / (ms * 1e-3) / 1e12, 1)}), flush=True)
-    _hip.lib().cer_wgrad_batch_set_ws(0)
+            streams.set_batch_variant(v)
+            ms = _time(batched, a.reps)
+            print(json.dumps({"G": a.G, "mode": "batched", "variant": v,
+                              "rows": rows, "layers": len(layers), "ms": round(ms, 3),
+                              "tflops": round(flops / (ms * 1e-3) / 1e12, 1)}), flush=True)
     streams.set_batch_variant(keep)
     streams.set_batch_rows(0)
 

@@ -220,38 +220,6 @@ def test_conv_intra_block_ksplit_fp32_vs_fp64(case, v):
         _hip.conv_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("v", [36, 37, 38, 42, 43, 44])
-@pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_wave_specialised_fp32_vs_fp64(case, v):
-    """The wave-specialised twins (512-thread igemm_nt32 / igemm_nn32 with
-    WS = 1: loader waves -> 4-stage LDS ring -> MFMA waves, kloop_ws), fwd and
-    dgrad pinned, every tile, with and without split-K, on every conv case
-    (unaligned / generic-gather shapes fall back to the register kernels)."""
-    from cerebro_ds_kpgi_amd.ops import _hip
-    _hip.conv_set_variant(0, v)
-    _hip.conv_set_variant(1, v)
-    try:
-        test_conv_fp32_vs_fp64(case)
-    finally:
-        _hip.conv_set_variant(0, -1)
-        _hip.conv_set_variant(1, -1)
-
-
-@pytest.mark.parametrize("v", [36, 37, 42])
-def test_conv_bn_unit_wave_specialised_fp32_vs_fp64(v):
-    """BN statistics (fwd epilogue) and the BN-link dgrad epilogue run by the
-    MFMA waves of the wave-specialised twins after the loaders exited."""
-    from cerebro_ds_kpgi_amd.ops import _hip
-    _hip.conv_set_variant(0, v)
-    _hip.conv_set_variant(1, v)
-    try:
-        test_conv_bn_unit_fp32_vs_fp64(True, True, False)
-        test_bn_link_dgrad_epilogue_fp32()
-    finally:
-        _hip.conv_set_variant(0, -1)
-        _hip.conv_set_variant(1, -1)
-
-
 @pytest.mark.parametrize("v", [24, 26, 30])
 def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
     """BN statistics (fwd epilogue) and the BN-link dgrad epilogue from the
@@ -307,51 +275,6 @@ def test_wgrad_batch_wide_fp32_vs_fp64(vb, narrow):
         streams.set_batch_variant(keep)
         _hip.lib().cer_wgrad_batch_set_narrow(1)
     print("wgrad batch wide", vb, narrow, ["%.1e" % e for e in errs])
-    assert max(errs) < TOL, errs
-
-
-@pytest.mark.parametrize("grid", [0, 7])
-def test_wgrad_batch_ws_fp32_vs_fp64(grid):
-    """The wave-specialised batched wgrad (wgrad_ws32: loader waves -> LDS
-    ring -> MFMA waves, LDS-counter hand-off) over every aligned ResNet-50
-    shape at once, 8 configs and 1; grid = 7 walks the items persistently
-    (the side-stream batch's capped grid) and restarts the ring per item."""
-    from cerebro_ds_kpgi_amd.ops import _hip, streams
-    cases = [c for c in CONV_CASES if c[3] % 8 == 0 and c[4] % 8 == 0 and c[3] >= 8]
-    keep = streams._BATCH_VARIANT
-    L = _hip.lib()
-    streams.set_batch_variant(1)
-    L.cer_wgrad_batch_set_ws(1)
-    if grid:
-        L.cer_wgrad_batch_set_grid(grid)
-    try:
-        errs = []
-        made = []
-        for (B, H, W, cin, cout, k, s, p, G) in cases:
-            spec = ParamSpec("w", (cout, k, k, cin), "weight", fan_in=k * k * cin)
-            a, refs = _make([spec], G)
-            torch.manual_seed(1)
-            x = torch.randn(B, H, W, G * cin, device="cuda").requires_grad_(True)
-            made.append((a, refs, x, (B, H, W, cin, cout, k, s, p, G)))
-        with streams.deferred_wgrad():
-            for a, refs, x, c in made:
-                y = P.conv2d(x, refs["w"], c[6], c[7])
-                torch.manual_seed(3)
-                y.backward(torch.randn_like(y))
-        torch.cuda.synchronize()
-        for a, refs, x, (B, H, W, cin, cout, k, s, p, G) in made:
-            torch.manual_seed(3)
-            w64 = _w64(refs["w"]).requires_grad_(True)
-            y64 = F.conv2d(_nchw(x.detach().double()), w64, None, s, p, 1, G)
-            y64.backward(_nchw(torch.randn(y64.shape[0], y64.shape[2], y64.shape[3], y64.shape[1],
-                                           device="cuda").double()))
-            dw64 = w64.grad.view(G, cout, cin, k, k).permute(0, 1, 3, 4, 2)
-            errs.append(_rel(a.grad.view(G, -1)[:, :dw64[0].numel()], dw64.reshape(G, -1)))
-    finally:
-        L.cer_wgrad_batch_set_ws(0)
-        L.cer_wgrad_batch_set_grid(0)
-        streams.set_batch_variant(keep)
-    print("wgrad batch ws grid", grid, ["%.1e" % e for e in errs])
     assert max(errs) < TOL, errs
 
 
