@@ -102,10 +102,25 @@ def _check(rc, name):
 
 
 # ---------------------------------------------------------------------------
+def _opt_hl(arena):
+    """The optimizer launch also writes the arena's HL weight image."""
+    if arena.whl is not None:
+        lib().cer_adam_set_hl(_ptr(arena.whl), arena.whl.stride(0))
+
+
+def hl_image(src, dst):
+    """dst = HL image of the rows of ``src`` (fp32 [G, n], n % 8 == 0)."""
+    assert src.dtype == dst.dtype == torch.float32 and src.shape == dst.shape
+    rc = lib().cer_hl_image(_ptr(src), src.stride(0), _ptr(dst), dst.stride(0), src.shape[1],
+                            src.shape[0], _stream())
+    _check(rc, "cer_hl_image")
+
+
 def adam_step(arena, beta1, beta2, eps, l2):
     L = arena.layout
     st = arena.state
     work = arena.work if arena.work is not arena.params else None
+    _opt_hl(arena)
     rc = lib().cer_adam_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_v, L.off_step,
         _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
@@ -118,6 +133,7 @@ def sgd_step(arena, momentum, l2):
     L = arena.layout
     st = arena.state
     work = arena.work if arena.work is not arena.params else None
+    _opt_hl(arena)
     rc = lib().cer_sgd_step(
         _ptr(st), st.stride(0), L.n_train, L.off_m, L.off_step,
         _ptr(arena.grad), arena.grad.stride(0), int(bool(arena.grad_clean)),
@@ -331,6 +347,10 @@ _SIGS.update({
     "cer_softmax_ce_f32": [c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_p],
     "cer_softmax_ce_f32_head": [c_p, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p],
     "cer_adam_set_aux": [c_p, c_p, c_i64],
+    "cer_adam_set_hl": [c_p, c_i64],
+    "cer_hl_image": [c_p, c_i64, c_p, c_i64, c_i64, c_i, c_p],
+    "cer_conv_set_whl": [c_p, c_i64],
+    "cer_conv_set_uk": [c_i],
     "cer_conv_dgrad_bnbwd_f32": None,
 })
 _SIGS.pop("cer_conv_dgrad_bnbwd_f32")
@@ -622,13 +642,28 @@ def tune_times():
     return {k: dict(v) for k, v in _TUNE_T.items()}
 
 
+def _with_whl(wref, fn):
+    """Run ``fn()`` with ``wref``'s HL weight image registered for the fp32
+    GEMM it launches (conv.hip cer_conv_set_whl; the uniform-K kernels read
+    it instead of splitting the weights; nothing when the arena has none)."""
+    h, hs = wref.whl_ptr() if wref is not None else (0, 0)
+    if not h:
+        return fn()
+    L = lib()
+    L.cer_conv_set_whl(c_p(h), hs)
+    try:
+        return fn()
+    finally:
+        L.cer_conv_set_whl(None, 0)
+
+
 def _conv_fwd_launch(x, B, H, W, cin, G, wp, ws, cout, kh, kw, stride, pad, y, Ho, Wo, bp, bs,
                      act, wref=None):
     _splitk_ready(x.device)
     def launch():
-        rc = _fn("cer_conv_fwd", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
-                                    stride, pad, _ptr(y), Ho, Wo, c_p(bp), bs,
-                                    _act_code(act), _stream())
+        rc = _with_whl(wref, lambda: _fn("cer_conv_fwd", x)(
+            _ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad, _ptr(y), Ho, Wo,
+            c_p(bp), bs, _act_code(act), _stream()))
         _check(rc, "cer_conv_fwd")
     _select(0, (B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype)
     launch()
@@ -674,9 +709,9 @@ def conv2d_fwd_stats(x, wref, stride, pad):
     _splitk_ready(x.device)
 
     def launch():
-        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw,
-                                          stride, pad, _ptr(z), Ho, Wo, _ptr(part),
-                                          ctypes.byref(nslab), _stream())
+        rc = _with_whl(wref, lambda: _fn("cer_conv_fwd_stats", x)(
+            _ptr(x), B, H, W, cin, G, c_p(wp), ws, cout, kh, kw, stride, pad, _ptr(z), Ho, Wo,
+            _ptr(part), ctypes.byref(nslab), _stream()))
         _check(rc, "cer_conv_fwd_stats")
     # the autotune's timing launches accumulate into the (atomic) slabs
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo), launch, x.dtype,
@@ -747,9 +782,9 @@ def _conv_bn_fwd_train(x, wref, gref, bref, rmref, rvref, residual, act, momentu
                              momentum, eps) + (x4,)
 
     def launch():
-        rc = _fn("cer_conv_fwd_stats", x)(_ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout,
-                                          kh, kw, stride, pad, _ptr(z), Ho, Wo,
-                                          _ptr(part), ctypes.byref(nslab), _stream())
+        rc = _with_whl(wref, lambda: _fn("cer_conv_fwd_stats", x)(
+            _ptr(x), B, H, W, cin, G, c_p(wp), wstr, cout, kh, kw, stride, pad, _ptr(z), Ho, Wo,
+            _ptr(part), ctypes.byref(nslab), _stream()))
         _check(rc, "cer_conv_fwd_stats")
     _select(0, ("stats", B, H, W, cin, cout, kh, kw, stride, pad, G, Ho, Wo) + (("hl",) * x_hl),
             launch, x.dtype, after_tune=part.zero_)
@@ -848,9 +883,9 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
     wt = torch.empty(n_wt, dtype=dy.dtype, device=dy.device)
 
     def launch(out=dx):
-        rc = _fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
-                                       cin, kh, kw, stride, pad, _ptr(out), H, W,
-                                       _ptr(addend), _stream())
+        rc = _with_whl(wref, lambda: _fn("cer_conv_dgrad", dy)(
+            _ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh, kw, stride, pad,
+            _ptr(out), H, W, _ptr(addend), _stream()))
         _check(rc, "cer_conv_dgrad")
     # an in-place accumulation (dx IS the addend) must not be repeated by the
     # autotune's timing launches: they run in place too, on one scratch copy
@@ -864,9 +899,9 @@ def _conv_dgrad_launch(dy, B, Ho, Wo, cout, G, wp, ws, cin, kh, kw, stride, pad,
         def tune():
             if scratch[0] is None:
                 scratch[0] = addend.clone()
-            _check(_fn("cer_conv_dgrad", dy)(_ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt),
-                                             cin, kh, kw, stride, pad, _ptr(scratch[0]), H, W,
-                                             _ptr(scratch[0]), _stream()), "cer_conv_dgrad")
+            _check(_with_whl(wref, lambda: _fn("cer_conv_dgrad", dy)(
+                _ptr(dy), B, Ho, Wo, cout, G, c_p(wp), ws, _ptr(wt), cin, kh, kw, stride, pad,
+                _ptr(scratch[0]), H, W, _ptr(scratch[0]), _stream())), "cer_conv_dgrad")
     _select(1, (B, Ho, Wo, cout, cin, kh, kw, stride, pad, G, H, W, addend is not None, bnstats)
             + (("hl",) * bool(dy_hl)), tune, dy.dtype, after_tune=after_tune)
     launch()

@@ -13,6 +13,11 @@ checkpoint is one copy.  A GPU that trains G packed configurations owns a
   (bf16 by default), refreshed by the fused optimizer kernel,
 * ``grad``  ``[G, n_train]`` fp32 gradients, written *directly* by the
   weight-gradient kernels (no autograd AccumulateGrad pass),
+* ``whl``   ``[G, n_train]`` (fp32 mode, training working sets on the HIP
+  path: ``enable_whl``) the params in HL format -- every 8 as [8 x bf16 hi |
+  8 x bf16 lo], the operand split of the 3-pass fp32 conv kernels -- written
+  by the optimizer kernel next to the params and read by the conv / linear
+  GEMMs instead of splitting the weights in their K loops,
 * ``lr``/``wd`` ``[G]`` per-config hyper-parameters on device.
 
 The weight blob order follows the model's layer order and is the same as the
@@ -243,6 +248,7 @@ class Arena(object):
         # backward starts from zeros (split-K weight-gradient kernels then
         # accumulate without a per-layer memset)
         self.grad_clean = False
+        self.whl = None
         self.lr = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.wd = torch.zeros(G, dtype=torch.float32, device=self.device)
         self.model_ids = [None] * G
@@ -268,7 +274,21 @@ class Arena(object):
         self.step[row].zero_()
         self.sync_work(row)
 
+    def enable_whl(self):
+        """Keep an HL image of the params (fp32 working sets on the HIP
+        path): refreshed by ``sync_work`` and written by every optimizer
+        step; the uniform-K conv kernels read it (conv.hip cer_conv_set_whl)."""
+        if self.whl is None and self.compute_dtype == torch.float32 and self.grad is not None:
+            self.whl = torch.zeros(self.G, self.layout.n_train, dtype=torch.float32,
+                                   device=self.device)
+            self.sync_work()
+        return self.whl is not None
+
     def sync_work(self, row=None):
+        if self.whl is not None:
+            from ..ops import _hip
+            _hip.hl_image(self.params if row is None else self.params[row:row + 1],
+                          self.whl if row is None else self.whl[row:row + 1])
         if self.work is self.params:
             return
         if row is None:
@@ -326,6 +346,13 @@ class ParamRef(object):
     def work_ptr(self):
         w = self.arena.work
         return w.data_ptr() + self.spec.offset * w.element_size(), w.stride(0)
+
+    def whl_ptr(self):
+        """(pointer, per-config stride) of this param's HL image, or (0, 0)."""
+        h = self.arena.whl
+        if h is None:
+            return 0, 0
+        return h.data_ptr() + self.spec.offset * h.element_size(), h.stride(0)
 
     def grad_ptr(self):
         g = self.arena.grad

@@ -200,6 +200,9 @@ class _Working(object):
         g = group
         self.arena = Arena(g.layout, G, g.device, g.dtype, trainable=True)
         self.arena.grad_clean = True      # the optimizer clears the gradient it consumes
+        if (g.device.type == "cuda" and get_backend() == "hip" and g.dtype == torch.float32
+                and os.environ.get("CER_WHL", "1") != "0"):
+            self.arena.enable_whl()       # HL weight image for the conv GEMMs
         self.net = create_model_from_mst({"model": g.arch})
         self.net.bind(self.arena)
         B = g.batch_size

@@ -35,6 +35,39 @@ CER_API void cer_adam_set_aux(int* cursor, float* zero, int64_t zero_n) {
   g_aux_zero_n = zero ? zero_n : 0;
 }
 
+// HL image of the params (fp32 mode; runtime/arena.py Arena.whl) the NEXT
+// optimizer launch writes next to them: every 8 updated params as [8 x bf16
+// hi | 8 x bf16 lo] (common.h st8_hl), the operand format the fp32 conv
+// kernels read without splitting (conv.hip cer_conv_set_whl).  Cleared by
+// that launch.
+static float* g_hl_img = nullptr;
+static int64_t g_hl_stride = 0;
+CER_API void cer_adam_set_hl(float* img, int64_t stride) {
+  g_hl_img = img;
+  g_hl_stride = img ? stride : 0;
+}
+
+// the HL image of rows of an fp32 tensor: dst[g][i..] = HL(src[g][i..]),
+// n % 8 == 0 (Arena.sync_work after host / hop writes of the params)
+__global__ __launch_bounds__(256) void hl_image_kernel(const float* __restrict__ src,
+                                                       int64_t src_stride, float* __restrict__ dst,
+                                                       int64_t dst_stride, int64_t n) {
+  const int g = blockIdx.y;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  float v[8];
+  ld8(src + g * src_stride + i, v);
+  st8_hl(dst + g * dst_stride + i, v);
+}
+
+CER_API int cer_hl_image(const float* src, int64_t src_stride, float* dst, int64_t dst_stride,
+                         int64_t n, int G, hipStream_t stream) {
+  if (n % 8 != 0 || G <= 0) return (int)hipErrorInvalidValue;
+  dim3 grid(cer_blocks(n / 8, 256), G);
+  hl_image_kernel<<<grid, 256, 0, stream>>>(src, src_stride, dst, dst_stride, n);
+  return (int)hipGetLastError();
+}
+
 // grid-stride share of blocks (x, 0) in zeroing n floats (n % 4 == 0)
 __device__ __forceinline__ void aux_zero(float* z, int64_t n) {
   if (!z || blockIdx.y != 0) return;
@@ -51,7 +84,7 @@ __global__ __launch_bounds__(256) void adam_kernel(
     int64_t off_v, int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
     const float* __restrict__ wd, float b1, float b2, float eps, int l2, float* zero,
-    int64_t zero_n) {
+    int64_t zero_n, float* __restrict__ hl, int64_t hl_stride) {
   aux_zero(zero, zero_n);
   const int g = blockIdx.y;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
@@ -89,6 +122,7 @@ __global__ __launch_bounds__(256) void adam_kernel(
   pp[0] = p[0]; pp[1] = p[1];
   mp[0] = m[0]; mp[1] = m[1];
   vp[0] = v[0]; vp[1] = v[1];
+  if (hl) st8_hl(hl + g * hl_stride + i, pf);
   if (WRITE_BF16) {
     uint4 o;
     o.x = pack_bf2(pf[0], pf[1]);
@@ -106,6 +140,7 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
                           hipStream_t stream) {
   if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) {
     cer_adam_set_aux(nullptr, nullptr, 0);   // a refused launch consumes its side jobs too
+    cer_adam_set_hl(nullptr, 0);
     return (int)hipErrorInvalidValue;
   }
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
@@ -115,13 +150,14 @@ CER_API int cer_adam_step(float* state, int64_t row_stride, int64_t n_train, int
     adam_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
                                                  off_step, grad, grad_stride, zero_grad, work,
                                                  work_stride, lr, wd, b1, b2, eps, l2, g_aux_zero,
-                                                 g_aux_zero_n);
+                                                 g_aux_zero_n, g_hl_img, g_hl_stride);
   else
     adam_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_v,
                                                   off_step, grad, grad_stride, zero_grad, nullptr,
                                                   0, lr, wd, b1, b2, eps, l2, g_aux_zero,
-                                                  g_aux_zero_n);
+                                                  g_aux_zero_n, g_hl_img, g_hl_stride);
   cer_adam_set_aux(nullptr, nullptr, 0);
+  cer_adam_set_hl(nullptr, 0);
   return (int)hipGetLastError();
 }
 
@@ -135,7 +171,8 @@ __global__ __launch_bounds__(256) void sgd_kernel(
     float* __restrict__ state, int64_t row_stride, int64_t n_train, int64_t off_m,
     int64_t off_step, float* __restrict__ grad, int64_t grad_stride, int zero_grad,
     bf16_t* __restrict__ work, int64_t work_stride, const float* __restrict__ lr,
-    const float* __restrict__ wd, float mu, int l2, float* zero, int64_t zero_n) {
+    const float* __restrict__ wd, float mu, int l2, float* zero, int64_t zero_n,
+    float* __restrict__ hl, int64_t hl_stride) {
   aux_zero(zero, zero_n);
   const int g = blockIdx.y;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8;
@@ -164,6 +201,7 @@ __global__ __launch_bounds__(256) void sgd_kernel(
   }
   pp[0] = p[0]; pp[1] = p[1];
   mp[0] = m[0]; mp[1] = m[1];
+  if (hl) st8_hl(hl + g * hl_stride + i, pf);
   if (WRITE_BF16) {
     uint4 o;
     o.x = pack_bf2(pf[0], pf[1]);
@@ -180,6 +218,7 @@ CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int6
                          int G, float momentum, int l2, hipStream_t stream) {
   if (n_train % 8 != 0 || g_aux_zero_n % 4 != 0) {
     cer_adam_set_aux(nullptr, nullptr, 0);
+    cer_adam_set_hl(nullptr, 0);
     return (int)hipErrorInvalidValue;
   }
   adam_inc_step<<<cer_blocks(G, 64), 64, 0, stream>>>(state, row_stride, off_step, G,
@@ -188,11 +227,14 @@ CER_API int cer_sgd_step(float* state, int64_t row_stride, int64_t n_train, int6
   if (work)
     sgd_kernel<true><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step, grad,
                                                grad_stride, zero_grad, work, work_stride, lr, wd,
-                                               momentum, l2, g_aux_zero, g_aux_zero_n);
+                                               momentum, l2, g_aux_zero, g_aux_zero_n, g_hl_img,
+                                               g_hl_stride);
   else
     sgd_kernel<false><<<grid, 256, 0, stream>>>(state, row_stride, n_train, off_m, off_step,
                                                 grad, grad_stride, zero_grad, nullptr, 0, lr, wd,
-                                                momentum, l2, g_aux_zero, g_aux_zero_n);
+                                                momentum, l2, g_aux_zero, g_aux_zero_n, g_hl_img,
+                                                g_hl_stride);
   cer_adam_set_aux(nullptr, nullptr, 0);
+  cer_adam_set_hl(nullptr, 0);
   return (int)hipGetLastError();
 }

@@ -132,6 +132,8 @@ struct NTParams {
   int stat_slabs = 0;     // BN partials: 0 = one slab per M tile (plain stores); n > 0 = n
                           // slabs, tile t atomically adds into slab t % n (zeroed by the caller)
   int a_hl = 0;           // fp32 kernels: the A operand is in HL format (take_hi_lo)
+  int w_hl = 0;           // fp32 GM_GEMM / GM_TAP kernels: w is the HL image of the weights
+                          // (cer_conv_set_whl: written by the optimizer, no split in the K loop)
 };
 
 // Slab count for the BN partials of the next conv launches (cer_conv_set_stat_slabs):
@@ -223,6 +225,7 @@ struct WGParams {
   int m_per_split;
   int splits;
   int x_hl = 0, dy_hl = 0;  // HL-format operands (take_hi_lo)
+  int gemm = 0;             // fp32 batch items: 1x1 / stride 1 / pad 0 (GM_GEMM body)
 };
 
 // es: element size of the gathered tensor (2 = bf16, 4 = fp32)
@@ -247,10 +250,20 @@ static GatherGeom make_geom(const void* src, int B, int Ctot, int Cg, int Hs, in
 // every 16-B chunk is one buffer_load whose byte offset is set past the
 // descriptor's range for padding taps / out-of-range rows, so the hardware
 // returns zeros.
-enum { GM_SLOW = 0, GM_FWD = 1, GM_DG1 = 2, GM_DGS = 3 };
+enum { GM_SLOW = 0, GM_FWD = 1, GM_DG1 = 2, GM_DGS = 3, GM_GEMM = 4, GM_TAP = 5 };
 //  GM_FWD : hi = y*st - pad + r                (forward, wgrad, strided-1x1 dgrad)
 //  GM_DG1 : hi = y + pad - r                   (stride-1 dgrad)
 //  GM_DGS : hi = (y + pad - r) / st if exact   (strided k x k dgrad)
+// fp32 kernels only, "uniform K" modes: a 32-deep K step
+// lies inside ONE tap, so the step's tap / channel offset is wave-uniform
+// (scalar registers) and each thread keeps a per-row base offset computed
+// once -- the K loop does one add and one select per 16-B chunk pair instead
+// of the per-chunk im2col decode (FastDiv, bounds, the per-thread tap walk):
+//  GM_GEMM: 1x1 pad-0 convs and linear layers (fwd, any stride; dgrad on
+//           the 1x1 geometry, the strided one included; wgrad at stride 1):
+//           the operand rows are the GEMM rows, K walked as channels
+//  GM_TAP : k x k convs with Cg % 32 == 0 (fwd; stride-1 dgrad): a per-row
+//           bit mask of the in-range taps replaces the per-chunk bounds test
 constexpr uint32_t OOB = 0x80000000u;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -2680,26 +2693,95 @@ void igemm_nt32(NTParams p) {
   const float* wbase = reinterpret_cast<const float*>(p.w) + (int64_t)cfg * p.w_gstride;
   const float* abase = reinterpret_cast<const float*>(p.a.src) + (int64_t)cfg * p.a.cfg_off;
 
+  constexpr bool UK = GM == GM_GEMM || GM == GM_TAP;           // uniform-K modes
   RowPos rows[A_CH];
   RowA rowa[A_CH];
+  uint32_t abo[A_CH], amask[A_CH], bbo[B_CH];   // UK: per-row byte bases, tap masks
   __amdgpu_buffer_rsrc_t rA, rB;
   if constexpr (GM != GM_SLOW) {
     rA = make_rsrc(abase, p.a.bytes);
     rB = make_rsrc(wbase, (uint32_t)p.N * (uint32_t)p.K * 4u);
+  }
+  if constexpr (UK) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = m0 + (tid + NTHREADS * i) / CPR;
+      const RowA ra_ = row_init<GM_FWD>(p.a, m, p.M);
+      // tap (0, 0)'s pixel may lie in the padding (negative): the uint32
+      // arithmetic wraps and a valid tap's offset wraps back into range
+      abo[i] = ((uint32_t)ra_.pix * (uint32_t)p.a.Ctot + (uint32_t)(8 * my_chunk)) * 4u;
+      uint32_t mk = 0;
+      if constexpr (GM == GM_TAP) {
+        for (int r = 0; r < p.a.kh; ++r)
+          for (int s2 = 0; s2 < p.a.kw; ++s2)
+            if (((unsigned)(ra_.hy + r) < (unsigned)p.a.Hs) &
+                ((unsigned)(ra_.wx + s2) < (unsigned)p.a.Ws))
+              mk |= 1u << (r * p.a.kw + s2);
+      } else {
+        if (m < p.M) mk = 1u;
+      }
+      amask[i] = mk;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int n = n0 + (tid + NTHREADS * i) / CPR;
+      bbo[i] = n < p.N ? (uint32_t)(n * p.K + 8 * my_chunk) * 4u : OOB;
+    }
+  } else if constexpr (GM != GM_SLOW) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
   } else {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) rows[i] = decode_row(m0 + (tid + NTHREADS * i) / CPR, p.M, p.a);
   }
-  KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+  KPos kp{0, 0, 0};
+  if constexpr (!UK) kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+  // UK: tap (index, row, col) and channel offset of the next K step to load
+  // (wave-uniform: SGPRs); a step of KS channels never straddles a tap
+  int u_c = 0, u_t = 0, u_r = 0, u_s = 0;
+  if constexpr (GM == GM_TAP) {
+    u_t = (kr.kt0 * KS) / p.a.Cg;
+    u_c = kr.kt0 * KS - u_t * p.a.Cg;
+    u_r = u_t / p.a.kw;
+    u_s = u_t - u_r * p.a.kw;
+  }
   constexpr int SETS = fp32_sets<BM, BN, WIDE>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
   auto load_tiles = [&](int kt, auto S) {
     constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
-    if constexpr (GM != GM_SLOW) {
+    if constexpr (UK) {
+      const bool kok = kt * KS < kr.klim;
+      const uint32_t kb = (uint32_t)(kt * KS) * 4u;
+      uint32_t ko = kb;
+      if constexpr (GM == GM_TAP)
+        ko = ((uint32_t)(u_r * p.a.Ws + u_s) * (uint32_t)p.a.Ctot + (uint32_t)u_c) * 4u;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const uint32_t bit = GM == GM_TAP ? (amask[i] >> (u_t & 31)) & 1u : amask[i];
+        const uint32_t o = (kok && bit) ? abo[i] + ko : OOB;
+        ra[s][2 * i] = bload(rA, o);
+        ra[s][2 * i + 1] = bload(rA, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const uint32_t o = kok ? bbo[i] + kb : OOB;
+        rb[s][2 * i] = bload(rB, o);
+        rb[s][2 * i + 1] = bload(rB, o + 16u);
+      }
+      if constexpr (GM == GM_TAP) {
+        u_c += KS;
+        if (u_c == p.a.Cg) {
+          u_c = 0;
+          ++u_t;
+          if (++u_s == p.a.kw) {
+            u_s = 0;
+            ++u_r;
+          }
+        }
+      }
+    } else if constexpr (GM != GM_SLOW) {
       const bool kok = k0 < kr.klim;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -2742,7 +2824,7 @@ void igemm_nt32(NTParams p) {
     for (int i = 0; i < B_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
       uint4 h, l;
-      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      take_hi_lo(UK && p.w_hl != 0, rb[s][2 * i], rb[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk)) = h;
       *reinterpret_cast<uint4*>(SB(buf) + nt_off(row, my_chunk + 4)) = l;
     }
@@ -2932,10 +3014,49 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   const __amdgpu_buffer_rsrc_t rW =
       make_rsrc(wbase, (uint32_t)Cout * (uint32_t)T * (uint32_t)Cin * 4u);
 
+  // uniform-K modes (GM_GEMM: the 1x1 geometry, dy rows = GEMM rows; GM_TAP:
+  // stride-1 k x k, Cout % 32 == 0): per-row dy bases + tap masks, and per
+  // thread weight-row bases; a K step (32 output channels of one tap) adds
+  // a wave-uniform offset to each
+  constexpr bool UK = GM == GM_GEMM || GM == GM_TAP;
   RowA rowa[A_CH];
+  uint32_t abo[A_CH], amask[A_CH], bbo[B_CH];
+  if constexpr (UK) {
 #pragma unroll
-  for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
-  KPos kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = m0 + (tid + NTHREADS * i) / CPR;
+      const RowA ra_ = row_init<GM_DG1>(p.a, m, p.M);
+      abo[i] = ((uint32_t)ra_.pix * (uint32_t)p.a.Ctot + (uint32_t)(8 * my_chunk)) * 4u;
+      uint32_t mk = 0;
+      if constexpr (GM == GM_TAP) {
+        for (int r = 0; r < p.a.kh; ++r)
+          for (int s2 = 0; s2 < p.a.kw; ++s2)
+            if (((unsigned)(ra_.hy - r) < (unsigned)p.a.Hs) &
+                ((unsigned)(ra_.wx - s2) < (unsigned)p.a.Ws))
+              mk |= 1u << (r * p.a.kw + s2);
+      } else {
+        if (m < p.M) mk = 1u;
+      }
+      amask[i] = mk;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int c = n0 + b_col;
+      bbo[i] = c < Cin ? (uint32_t)((b_row0 + B_RSTEP * i) * T * Cin + c) * 4u : OOB;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) rowa[i] = row_init<GM>(p.a, m0 + (tid + NTHREADS * i) / CPR, p.M);
+  }
+  KPos kp{0, 0, 0};
+  if constexpr (!UK) kp = kpos_init(p.a, kr.kt0 * KS + 8 * my_chunk);
+  int u_c = 0, u_t = 0, u_r = 0, u_s = 0;     // UK: the next step's (channel, tap), uniform
+  if constexpr (GM == GM_TAP) {
+    u_t = (kr.kt0 * KS) / Cout;
+    u_c = kr.kt0 * KS - u_t * Cout;
+    u_r = u_t / p.a.kw;
+    u_s = u_t - u_r * p.a.kw;
+  }
   constexpr int SETS = fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
 
@@ -2943,6 +3064,42 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
     constexpr int s = decltype(S)::value;
     const int k0 = kt * KS + 8 * my_chunk;
     const bool kok = k0 < kr.klim;
+    if constexpr (UK) {
+      const bool kup = kt * KS < kr.klim;
+      uint32_t ko, wo;
+      if constexpr (GM == GM_TAP) {
+        ko = ((uint32_t)u_c - (uint32_t)(u_r * p.a.Ws + u_s) * (uint32_t)p.a.Ctot) * 4u;
+        wo = (uint32_t)((u_c * T + u_t) * Cin) * 4u;
+      } else {
+        ko = (uint32_t)(kt * KS) * 4u;
+        wo = (uint32_t)(kt * KS * Cin) * 4u;
+      }
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const uint32_t bit = GM == GM_TAP ? (amask[i] >> (u_t & 31)) & 1u : amask[i];
+        const uint32_t o = (kup && bit) ? abo[i] + ko : OOB;
+        ra[s][2 * i] = bload(rA, o);
+        ra[s][2 * i + 1] = bload(rA, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const uint32_t o = kup ? bbo[i] + wo : OOB;
+        rb[s][2 * i] = bload(rW, o);
+        rb[s][2 * i + 1] = bload(rW, o + 16u);
+      }
+      if constexpr (GM == GM_TAP) {
+        u_c += KS;
+        if (u_c == Cout) {
+          u_c = 0;
+          ++u_t;
+          if (++u_s == p.a.kw) {
+            u_s = 0;
+            ++u_r;
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const uint32_t off = a_off<GM, 4>(p.a, rowa[i], kp.r, kp.s, kp.c);
@@ -2978,7 +3135,7 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
     for (int i = 0; i < B_CH; ++i) {
       const int row = b_row0 + B_RSTEP * i;
       uint4 h, l;
-      split_hi_lo(rb[s][2 * i], rb[s][2 * i + 1], h, l);
+      take_hi_lo(UK && p.w_hl != 0, rb[s][2 * i], rb[s][2 * i + 1], h, l);
       if constexpr (WIDE) {
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row, b_col)) = h;
         *reinterpret_cast<uint4*>(sb + tn_off_w<BN>(row + KS, b_col)) = l;
@@ -3037,7 +3194,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   const int kk0 = k0 + b_col;
   const bool b_kok = kk0 < p.K;
   KPos bk{0, 0, 0};
-  if (b_kok) bk = kpos_init(p.x, kk0);
+  if (GM != GM_GEMM && b_kok) bk = kpos_init(p.x, kk0);
   constexpr int SETS = fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
   const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
@@ -3047,11 +3204,38 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
     rDY = make_rsrc(dyb, (uint32_t)p.Mred * (uint32_t)p.ldy * 4u);
     rX = make_rsrc(xb, p.x.bytes);
   }
+  // GM_GEMM (1x1, stride 1, pad 0: x rows = dy rows = the reduction index):
+  // per-thread row / column byte bases; a step adds the uniform row offset
+  uint32_t abo[A_CH], bbo[B_CH];
+  if constexpr (GM == GM_GEMM) {
+    const int n = n0 + a_col;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i)
+      abo[i] = n < p.N ? (uint32_t)((a_row0 + A_RSTEP * i) * p.ldy + n) * 4u : OOB;
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i)
+      bbo[i] = b_kok ? (uint32_t)((b_row0 + B_RSTEP * i) * p.x.Ctot + kk0) * 4u : OOB;
+  }
 
   auto load_tiles = [&](int mt, auto S) {
     constexpr int s = decltype(S)::value;
     const int mbase = ms + mt * KS;
-    if constexpr (GM != GM_SLOW) {
+    if constexpr (GM == GM_GEMM) {
+      const int left = me - mbase;                 // rows of this step inside the split
+      const uint32_t ao = (uint32_t)(mbase * p.ldy) * 4u, xo = (uint32_t)(mbase * p.x.Ctot) * 4u;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const uint32_t o = a_row0 + A_RSTEP * i < left ? abo[i] + ao : OOB;
+        ra[s][2 * i] = bload(rDY, o);
+        ra[s][2 * i + 1] = bload(rDY, o + 16u);
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const uint32_t o = b_row0 + B_RSTEP * i < left ? bbo[i] + xo : OOB;
+        rb[s][2 * i] = bload(rX, o);
+        rb[s][2 * i + 1] = bload(rX, o + 16u);
+      }
+    } else if constexpr (GM != GM_SLOW) {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const int m = mbase + a_row0 + A_RSTEP * i, n = n0 + a_col;
@@ -3197,7 +3381,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
     int i = 0;
     while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     const WGParams p = b.p[i];
-    wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
+    if (p.gemm)
+      wgrad_reg_body32<BM, BN, GM_GEMM, WIDE>(p, work - b.start[i], lds);
+    else
+      wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
   }
 }
@@ -3246,6 +3433,29 @@ static int g_variant[3] = {-1, -1, -1};
 
 CER_API void cer_conv_set_variant(int op, int v) {
   if (op >= 0 && op < 3) g_variant[op] = v;
+}
+
+// uniform-K fp32 kernels (GM_GEMM / GM_TAP: conv fwd, dgrad and the 1x1
+// wgrad).  CER_UK=0 (or cer_conv_set_uk(0)) keeps the
+// per-chunk im2col addressing for A/B runs.
+static int g_uk = -1;
+static bool uk_on() {
+  if (g_uk < 0) {
+    const char* e = getenv("CER_UK");
+    g_uk = e ? atoi(e) : 1;
+  }
+  return g_uk > 0;
+}
+CER_API void cer_conv_set_uk(int on) { g_uk = on ? 1 : 0; }
+
+// HL image of the weights for the NEXT fp32 fwd / dgrad launch (same layout
+// and per-config stride as w; the optimizer writes it, runtime/arena.py
+// Arena.whl); used by the uniform-K kernels only, null = split in the K loop
+static const void* g_whl = nullptr;
+static int64_t g_whl_gstride = 0;
+CER_API void cer_conv_set_whl(const void* whl, int64_t gstride) {
+  g_whl = whl;
+  g_whl_gstride = whl ? gstride : 0;
 }
 
 // split-K workspace (persistent; registered by the host before launches)
@@ -3373,13 +3583,27 @@ static int run_nt(NTParams p, int G, hipStream_t stream, int* nslab = nullptr) {
 
 // ---- fp32 (3-pass split-bf16) launches: register-staged variants only; an
 // LDS-DMA variant id maps to its register-staged twin (v - 3)
+// register-staged fp32 forward kernel of addressing mode gm (GM_FWD /
+// GM_GEMM / GM_TAP; GM_SLOW for unaligned operands)
+template <int BM, int BN, bool WIDE, int WG>
+static void nt32_go(int gm, dim3 grid, const NTParams& p, hipStream_t stream) {
+  const unsigned th = NTHREADS * WG;
+  switch (gm) {
+    case GM_GEMM: igemm_nt32<BM, BN, GM_GEMM, WIDE, WG><<<grid, th, 0, stream>>>(p); break;
+    case GM_TAP: igemm_nt32<BM, BN, GM_TAP, WIDE, WG><<<grid, th, 0, stream>>>(p); break;
+    case GM_SLOW: igemm_nt32<BM, BN, GM_SLOW, WIDE, WG><<<grid, th, 0, stream>>>(p); break;
+    default: igemm_nt32<BM, BN, GM_FWD, WIDE, WG><<<grid, th, 0, stream>>>(p); break;
+  }
+}
+
 template <int BM, int BN>
 static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStream_t stream,
-                          bool wide = false, int wg = 1) {
+                          bool wide = false, int wg = 1, int gm = GM_FWD) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
+  if (!fast) gm = GM_SLOW;
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && fast && kind == 0 && !wide) {    // intra-block K split, 512 threads
-      igemm_nt32<BM, BN, GM_FWD, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p);
+      nt32_go<BM, BN, false, 2>(gm, grid, p, stream);
       return;
     }
   }
@@ -3391,10 +3615,8 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStre
           return;
         }
       pipe_nt32<BM, BN, 2, true><<<grid, NTHREADS, 0, stream>>>(p);
-    } else if (!fast) {
-      igemm_nt32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
     } else {
-      igemm_nt32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
+      nt32_go<BM, BN, true, 1>(gm, grid, p, stream);
     }
     return;
   }
@@ -3406,10 +3628,17 @@ static void launch_nt32_t(const NTParams& p, int G, bool fast, int kind, hipStre
         return;
       }
     pipe_nt32<BM, BN, 2><<<grid, NTHREADS, 0, stream>>>(p);
-  } else if (!fast)
-    igemm_nt32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
-  else
-    igemm_nt32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
+  } else {
+    nt32_go<BM, BN, false, 1>(gm, grid, p, stream);
+  }
+}
+
+// uniform-K addressing mode of an fp32 forward GEMM (0 = none)
+static int nt_uk_mode(const NTParams& p, bool fast) {
+  const GatherGeom& g = p.a;
+  if (!fast || !uk_on() || p.dgrad || g.Cg % KS || p.K % KS) return 0;
+  if (g.kh == 1 && g.kw == 1 && g.pad == 0 && g.pad_w == 0) return GM_GEMM;
+  return g.kh * g.kw <= 32 ? GM_TAP : 0;
 }
 
 static bool nt_fast32(const NTParams& p) {
@@ -3449,10 +3678,19 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     tile_dims(v, bm, bn);
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
+  // register-staged kernels: uniform-K addressing and, with it, the HL
+  // weight image (the LDS-DMA ring kernels keep their own addressing)
+  const int gm = kind == 0 ? nt_uk_mode(p, fast) : 0;
+  if (gm && p.w_hl) {                // the caller allowed the HL image (not grouped)
+    p.w = reinterpret_cast<const bf16_t*>(g_whl);
+    p.w_gstride = g_whl_gstride;
+  } else {
+    p.w_hl = 0;
+  }
   switch (v % 3) {
-    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg); break;
-    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide, 1); break;
-    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg); break;
+    case 0: launch_nt32_t<64, 64>(p, G, fast, kind, stream, wide, wg, gm ? gm : GM_FWD); break;
+    case 1: launch_nt32_t<128, 128>(p, G, fast, kind, stream, wide, 1, gm ? gm : GM_FWD); break;
+    default: launch_nt32_t<128, 64>(p, G, fast, kind, stream, wide, wg, gm ? gm : GM_FWD); break;
   }
   return (int)hipGetLastError();
 }
@@ -3533,6 +3771,7 @@ static int conv_fwd_impl(const void* x, int B, int H, int W, int Cin, int G, con
   if (f32) {
     p.a_hl = g_hl_x;
     if (p.a_hl && (ctot || ldc)) return (int)hipErrorInvalidValue;   // grouped: no HL
+    p.w_hl = g_whl && !ctot && !ldc ? 1 : 0;    // run_nt32 decides whether to read it
   }
   return f32 ? run_nt32(p, G, stream, nslab) : run_nt(p, G, stream, nslab);
 }
@@ -3620,9 +3859,31 @@ CER_API void cer_conv_dgrad_babwd(float* dbias, int64_t dbstride, const void* y,
 
 template <int BM, int BN>
 static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStream_t stream,
-                          bool wide = false, int wg = 1) {
+                          bool wide = false, int wg = 1, int gm = 0) {
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
+  if (gm) {                        // uniform-K addressing (GM_GEMM / GM_TAP)
+    if constexpr (BM * BN <= 128 * 64) {
+      if (wg > 1 && !wide) {
+        if (gm == GM_GEMM)
+          igemm_nn32<BM, BN, GM_GEMM, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+        else
+          igemm_nn32<BM, BN, GM_TAP, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+        return;
+      }
+    }
+    if (wide) {
+      if (gm == GM_GEMM)
+        igemm_nn32<BM, BN, GM_GEMM, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else
+        igemm_nn32<BM, BN, GM_TAP, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    } else if (gm == GM_GEMM) {
+      igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    } else {
+      igemm_nn32<BM, BN, GM_TAP><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+    }
+    return;
+  }
   if constexpr (BM * BN <= 128 * 64) {
     if (wg > 1 && !wide) {                         // intra-block K split, 512 threads
       if (strided)
@@ -3735,10 +3996,25 @@ static int conv_dgrad_impl(const void* dy, int B, int Ho, int Wo, int Cout, int 
       *g_bb_nslab = 0;                    // not produced: the BN runs its own partials
     }
     if (f32) {
+      // uniform-K addressing: the 1x1 geometry (stride-1 1x1 and the
+      // strided 1x1's dy rows) and stride-1 k x k, a K step (32 output
+      // channels) inside one tap; with it the HL weight image (not grouped)
+      int gm = 0;
+      if (uk_on() && Cout % KS == 0) {
+        if (p.a.kh == 1 && p.a.kw == 1 && p.a.pad == 0 && p.a.Hm == p.a.Hs && p.a.Wm == p.a.Ws)
+          gm = GM_GEMM;
+        else if (!strided && T <= 32)
+          gm = GM_TAP;
+      }
+      if (gm && g_whl && !cout_tot && !cin_tot) {
+        p.w = reinterpret_cast<const bf16_t*>(g_whl);
+        p.w_gstride = g_whl_gstride;
+        p.w_hl = 1;
+      }
       switch (v % 3) {
-        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg); break;
-        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1); break;
-        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg); break;
+        case 0: launch_nn32_t<64, 64>(p, G, T, strided, stream, wide, wg, gm); break;
+        case 1: launch_nn32_t<128, 128>(p, G, T, strided, stream, wide, 1, gm); break;
+        default: launch_nn32_t<128, 64>(p, G, T, strided, stream, wide, wg, gm); break;
       }
       return (int)hipGetLastError();
     }
@@ -3857,14 +4133,26 @@ static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t 
   p.splits = splits;
   dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
   if (wide)   // 32x32x16-MFMA twins
-    if (fast)
+    if (fast && p.gemm)
+      igemm_wgrad32<BM, BN, GM_GEMM, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else if (fast)
       igemm_wgrad32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     else
       igemm_wgrad32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (fast && p.gemm)
+    igemm_wgrad32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p);
   else if (fast)
     igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
   else
     igemm_wgrad32<BM, BN, GM_SLOW><<<grid, NTHREADS, 0, stream>>>(p);
+}
+
+// the weight gradient of a 1x1 / stride-1 / pad-0 conv is a plain GEMM over
+// rows shared by x and dy (GM_GEMM body)
+static int wg_gemm(const WGParams& p) {
+  const GatherGeom& g = p.x;
+  return uk_on() && g.kh == 1 && g.kw == 1 && g.st == 1 && g.st_w == 1 && g.pad == 0 &&
+         g.pad_w == 0 && g.Hm == g.Hs && g.Wm == g.Ws;
 }
 
 static bool wg_fast32(int Cin, int Cout, const WGParams& p) {
@@ -3898,6 +4186,7 @@ CER_API int cer_conv_wgrad_f32(const float* x, int B, int H, int W, int Cin, int
   p.x_hl = g_hl_x;
   p.dy_hl = g_hl_dy;
   if ((p.x_hl || p.dy_hl) && !wg_fast32(Cin, Cout, p)) return (int)hipErrorInvalidValue;
+  p.gemm = wg_gemm(p);
   run_wg32(p, G, splits, wg_fast32(Cin, Cout, p), stream);
   return (int)hipGetLastError();
 }
@@ -4106,6 +4395,7 @@ CER_API int cer_wgrad_batch_add_f32(const float* x, int B, int H, int W, int Cin
   p.x_hl = g_hl_x;
   p.dy_hl = g_hl_dy;
   if (!wg_fast32(Cin, Cout, p)) return 0;     // HL operands: the direct launch refuses
+  p.gemm = wg_gemm(p);
   const int rows = wgb_rows();
   p.m_per_split = p.Mred < rows ? (p.Mred + BK - 1) / BK * BK : rows;
   p.splits = (p.Mred + p.m_per_split - 1) / p.m_per_split;
