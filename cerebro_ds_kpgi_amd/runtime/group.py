@@ -193,6 +193,15 @@ class PackGroup(object):
         self.current = None
 
 
+# Packs of at most this many configs keep an HL image of their weights
+# (Arena.whl): the optimizer writes it (+4 B per param and step) and the
+# uniform-K GEMMs read it instead of splitting the weights.  Measured
+# (profiles/r6_uk.md, same box): one config +1.0 %, eight configs -0.8 % (the
+# extra optimizer traffic outweighs the split it saves in wide packs).
+# CER_WHL_MAX_G overrides (0 = off).
+WHL_MAX_G = int(os.environ.get("CER_WHL_MAX_G", "2"))
+
+
 class _Working(object):
     def __init__(self, group, G):
         self.group = group
@@ -201,7 +210,7 @@ class _Working(object):
         self.arena = Arena(g.layout, G, g.device, g.dtype, trainable=True)
         self.arena.grad_clean = True      # the optimizer clears the gradient it consumes
         if (g.device.type == "cuda" and get_backend() == "hip" and g.dtype == torch.float32
-                and os.environ.get("CER_WHL", "1") != "0"):
+                and G <= WHL_MAX_G):
             self.arena.enable_whl()       # HL weight image for the conv GEMMs
         self.net = create_model_from_mst({"model": g.arch})
         self.net.bind(self.arena)

@@ -225,7 +225,8 @@ struct WGParams {
   int m_per_split;
   int splits;
   int x_hl = 0, dy_hl = 0;  // HL-format operands (take_hi_lo)
-  int gemm = 0;             // fp32 batch items: 1x1 / stride 1 / pad 0 (GM_GEMM body)
+  int gemm = 0;             // fp32: 1 = 1x1 / stride 1 / pad 0 (GM_GEMM body), 2 = k x k,
+                            // stride 1, same-size output (GM_TAP body); 0 = im2col body
 };
 
 // es: element size of the gathered tensor (2 = bf16, 4 = fp32)
@@ -3195,6 +3196,13 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   const bool b_kok = kk0 < p.K;
   KPos bk{0, 0, 0};
   if (GM != GM_GEMM && b_kok) bk = kpos_init(p.x, kk0);
+  // GM_TAP (k x k, stride 1, same-size output): a thread's x column (tap r,
+  // s and channel c) is fixed for the whole block, so its x row address is
+  // the dy row's pixel shifted by the tap -- a per-row base plus the
+  // uniform step offset; only the tap's bounds test needs the row's pixel
+  // (y, x), advanced by KS rows per step without a division
+  int ty[B_CH], tx[B_CH];
+  int dxs = 0, dys = 0, ry = 0, rx = 0;
   constexpr int SETS = fp32_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
   const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
@@ -3207,22 +3215,44 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   // GM_GEMM (1x1, stride 1, pad 0: x rows = dy rows = the reduction index):
   // per-thread row / column byte bases; a step adds the uniform row offset
   uint32_t abo[A_CH], bbo[B_CH];
-  if constexpr (GM == GM_GEMM) {
+  if constexpr (GM == GM_GEMM || GM == GM_TAP) {
     const int n = n0 + a_col;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i)
       abo[i] = n < p.N ? (uint32_t)((a_row0 + A_RSTEP * i) * p.ldy + n) * 4u : OOB;
+    if constexpr (GM == GM_GEMM) {
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i)
-      bbo[i] = b_kok ? (uint32_t)((b_row0 + B_RSTEP * i) * p.x.Ctot + kk0) * 4u : OOB;
+      for (int i = 0; i < B_CH; ++i)
+        bbo[i] = b_kok ? (uint32_t)((b_row0 + B_RSTEP * i) * p.x.Ctot + kk0) * 4u : OOB;
+    } else {
+      ry = bk.r - p.x.pad;
+      rx = bk.s - p.x.pad_w;
+      const int dpix = ry * p.x.Ws + rx;
+      dxs = KS % p.x.Wm;
+      dys = (KS / p.x.Wm) % p.x.Hm;
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const int m = ms + b_row0 + B_RSTEP * i;
+        const RowPos q = decode_row(m, p.Mred, p.x);
+        ty[i] = q.y;
+        tx[i] = q.x;
+        // offsets relative to the split's first row (ms): the step adds
+        // (mbase - ms) rows; the uint32 arithmetic wraps for taps left of /
+        // above the pixel, and a valid tap's offset wraps back into range
+        bbo[i] = b_kok ? (uint32_t)((b_row0 + B_RSTEP * i + dpix) * p.x.Ctot + bk.c) * 4u +
+                             (uint32_t)(ms * p.x.Ctot) * 4u
+                       : OOB;
+      }
+    }
   }
 
   auto load_tiles = [&](int mt, auto S) {
     constexpr int s = decltype(S)::value;
     const int mbase = ms + mt * KS;
-    if constexpr (GM == GM_GEMM) {
+    if constexpr (GM == GM_GEMM || GM == GM_TAP) {
       const int left = me - mbase;                 // rows of this step inside the split
-      const uint32_t ao = (uint32_t)(mbase * p.ldy) * 4u, xo = (uint32_t)(mbase * p.x.Ctot) * 4u;
+      const uint32_t ao = (uint32_t)(mbase * p.ldy) * 4u;
+      const uint32_t xo = (uint32_t)((GM == GM_TAP ? mbase - ms : mbase) * p.x.Ctot) * 4u;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const uint32_t o = a_row0 + A_RSTEP * i < left ? abo[i] + ao : OOB;
@@ -3231,7 +3261,20 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
-        const uint32_t o = b_row0 + B_RSTEP * i < left ? bbo[i] + xo : OOB;
+        bool ok = b_row0 + B_RSTEP * i < left;
+        if constexpr (GM == GM_TAP) {
+          ok = ok && ((unsigned)(ty[i] + ry) < (unsigned)p.x.Hs) &&
+               ((unsigned)(tx[i] + rx) < (unsigned)p.x.Ws);
+          // the next step's row pixel: KS rows on, within the image grid
+          int xn = tx[i] + dxs;
+          const int carry = xn >= p.x.Wm ? 1 : 0;
+          xn -= carry ? p.x.Wm : 0;
+          int yn = ty[i] + dys + carry;
+          yn -= yn >= p.x.Hm ? p.x.Hm : 0;
+          tx[i] = xn;
+          ty[i] = yn;
+        }
+        const uint32_t o = ok ? bbo[i] + xo : OOB;
         rb[s][2 * i] = bload(rX, o);
         rb[s][2 * i + 1] = bload(rX, o + 16u);
       }
@@ -3381,8 +3424,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
     int i = 0;
     while (i + 1 < b.n && work >= b.start[i + 1]) ++i;
     const WGParams p = b.p[i];
-    if (p.gemm)
+    if (p.gemm == 1)
       wgrad_reg_body32<BM, BN, GM_GEMM, WIDE>(p, work - b.start[i], lds);
+    else if (p.gemm == 2)
+      wgrad_reg_body32<BM, BN, GM_TAP, WIDE>(p, work - b.start[i], lds);
     else
       wgrad_reg_body32<BM, BN, GM_FWD, WIDE>(p, work - b.start[i], lds);
     if (w + nwg < total) __syncthreads();     // the next item restages the LDS images
@@ -4133,14 +4178,18 @@ static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t 
   p.splits = splits;
   dim3 grid((unsigned)(ntiles(p.N, p.K, BM, BN) * splits * G));
   if (wide)   // 32x32x16-MFMA twins
-    if (fast && p.gemm)
+    if (fast && p.gemm == 1)
       igemm_wgrad32<BM, BN, GM_GEMM, true><<<grid, NTHREADS, 0, stream>>>(p);
+    else if (fast && p.gemm == 2)
+      igemm_wgrad32<BM, BN, GM_TAP, true><<<grid, NTHREADS, 0, stream>>>(p);
     else if (fast)
       igemm_wgrad32<BM, BN, GM_FWD, true><<<grid, NTHREADS, 0, stream>>>(p);
     else
       igemm_wgrad32<BM, BN, GM_SLOW, true><<<grid, NTHREADS, 0, stream>>>(p);
-  else if (fast && p.gemm)
+  else if (fast && p.gemm == 1)
     igemm_wgrad32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p);
+  else if (fast && p.gemm == 2)
+    igemm_wgrad32<BM, BN, GM_TAP><<<grid, NTHREADS, 0, stream>>>(p);
   else if (fast)
     igemm_wgrad32<BM, BN, GM_FWD><<<grid, NTHREADS, 0, stream>>>(p);
   else
@@ -4148,11 +4197,14 @@ static void launch_wg32_t(WGParams p, int G, bool fast, int splits, hipStream_t 
 }
 
 // the weight gradient of a 1x1 / stride-1 / pad-0 conv is a plain GEMM over
-// rows shared by x and dy (GM_GEMM body)
+// rows shared by x and dy (1: GM_GEMM body); a stride-1 k x k conv with a
+// same-size output reads x at the dy row's pixel shifted by the tap (2:
+// GM_TAP body); others keep the im2col body (0)
 static int wg_gemm(const WGParams& p) {
   const GatherGeom& g = p.x;
-  return uk_on() && g.kh == 1 && g.kw == 1 && g.st == 1 && g.st_w == 1 && g.pad == 0 &&
-         g.pad_w == 0 && g.Hm == g.Hs && g.Wm == g.Ws;
+  if (!uk_on() || g.st != 1 || g.st_w != 1 || g.Hm != g.Hs || g.Wm != g.Ws) return 0;
+  if (g.kh == 1 && g.kw == 1) return g.pad == 0 && g.pad_w == 0 ? 1 : 0;
+  return 2;
 }
 
 static bool wg_fast32(int Cin, int Cout, const WGParams& p) {

@@ -14,12 +14,6 @@ step() {   # name, seconds, command...
   echo "$name rc=$rc $(tail -1 "$OUT/$name.log")"
   return $rc
 }
-step tests_uk 600 python -u -m pytest tests/test_uk_gpu.py -x -q --timeout 300 \
-  --timeout-method thread || exit 1
-step tests_fp32 900 python -u -m pytest tests/test_fp32_gpu.py -x -q --timeout 300 \
-  --timeout-method thread || exit 1
-step tests_timed 600 python -u -m pytest tests/test_timed_path_gpu.py -x -q -s --timeout 500 \
-  --timeout-method thread || exit 1
 for R in 1 2; do
   for V in "CER_UK=1" "CER_UK=0" "CER_UK=1,CER_WHL=0"; do
     for C in 8 1; do
@@ -30,5 +24,7 @@ for R in 1 2; do
     done
   done
 done
+step tests_timed 900 python -u -m pytest tests/test_timed_path_gpu.py -x -q -s --timeout 800 \
+  --timeout-method thread || exit 1
 step conv_g8 600 python -u -m cerebro_ds_kpgi_amd.tools.bench_conv --dtype fp32 --G 8 \
   --no_miopen --iters 20 --json "$OUT/conv_g8.json" || exit 1
