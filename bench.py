@@ -137,6 +137,11 @@ def main():
                          verbose=False, ckpt_every="none", store_loader=loader,
                          logs_root=args.logs_root,
                          **({"lanes": args.lanes} if args.lanes else {}))
+    mon = None
+    if args.logs_root and int(os.environ.get("LOCAL_RANK", "0")) == 0:
+        # 1 Hz host / GPU / xGMI sampler (sys_logs/sysmon_<host>.jsonl)
+        from cerebro_ds_kpgi_amd.utils.sysmon import SysMonitor
+        mon = SysMonitor(os.path.join(args.logs_root, "sys_logs")).start()
     t_etl = time.time()
     eng = MOPEngine(msts, ctx, opts)
     t_etl = time.time() - t_etl
@@ -154,6 +159,9 @@ def main():
     # when the engine created its hop communicator, parallel.hop.hop_group)
     if args.warmup > 0:
         eng.run_steps(args.warmup, args.steps_per_round)
+    # xGMI link counters around the timed window (rank 0, outside it; the
+    # hops' bytes on the wire at N > 1; None where amd-smi has no xgmi data)
+    xg0 = _xgmi_sample() if N > 1 and ctx.rank == 0 else None
     sync()
     ctx.barrier()
     sync()
@@ -171,6 +179,7 @@ def main():
                                       "hold_s": eng.hop_hold_time - hold0})
     imgs = sum(r["images"] for r in per_rank)
     value = imgs / dt_max
+    xg = _xgmi_delta_gb(xg0, _xgmi_sample()) if xg0 else None
     if ctx.rank == 0:
         base = BASELINE_IMG_S.get(N)
         headline = (S == 8 and args.workload == "headline" and args.model == "resnet50"
@@ -223,6 +232,9 @@ def main():
             # the coordinator's hold of the hops a rank received (burst
             # grouping, runtime/async_mop.py), summed over the timed window
             "hold_ms_max": round(1000.0 * max(r["hold_s"] for r in per_rank), 3),
+            # xGMI GB written per GPU over the timed window (amd-smi link
+            # counters; includes any other traffic on the links), or null
+            "xgmi_write_gb": xg,
         }
         if da_stats is not None:
             st = da_stats
@@ -236,6 +248,9 @@ def main():
                                                max(st["h2d_s"], 1e-9), 2)}
         print(json.dumps(out))
         sys.stdout.flush()
+    if mon is not None:
+        mon.stop()
+    if ctx.rank == 0:
         tune_log = os.environ.get("CER_TUNE_LOG")
         if tune_log and backend == "hip":
             from cerebro_ds_kpgi_amd.ops import _hip
@@ -249,6 +264,19 @@ def main():
         import shutil
         shutil.rmtree(da_root, ignore_errors=True)
     shutdown(ctx)
+
+
+def _xgmi_sample():
+    from cerebro_ds_kpgi_amd.utils.sysmon import xgmi_metrics
+    return xgmi_metrics()
+
+
+def _xgmi_delta_gb(first, last):
+    from cerebro_ds_kpgi_amd.utils.sysmon import _xgmi_delta
+    if not first or not last:
+        return None
+    d = _xgmi_delta(first, last, "write_kb")
+    return {k: round(v, 3) for k, v in d.items()} or None
 
 
 def _free_port():

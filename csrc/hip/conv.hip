@@ -1594,6 +1594,9 @@ constexpr int KS = 32;
 #ifndef CER_TIMING_NOSPLIT
 #define CER_TIMING_NOSPLIT 0
 #endif
+#ifndef CER_TIMING_NOAW
+#define CER_TIMING_NOAW 0       // timing only: no LDS stores of the A operand (loads kept)
+#endif
 #ifndef CER_TIMING_1PASS
 #define CER_TIMING_1PASS 0
 #endif
@@ -1621,6 +1624,11 @@ __device__ __forceinline__ void split_hi_lo(const uint4& a, const uint4& b, uint
 // lo] of the fp32 values, split exactly as split_hi_lo does -- the same 32
 // bytes at the same offsets as 8 fp32, so the gathers are unchanged and the
 // 3-pass MFMAs see bit-identical operands.  An HL chunk IS the (hi, lo) pair.
+// timing builds: keep a loaded value (and its load) without using it
+__device__ __forceinline__ void keep_alive(const uint4& v) {
+  asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+}
+
 __device__ __forceinline__ void take_hi_lo(bool hl, const uint4& a, const uint4& b, uint4& hi,
                                            uint4& lo) {
   if (hl) {
@@ -1701,10 +1709,30 @@ __device__ __forceinline__ f32x4 mfma3(const bf16x8& xh, const bf16x8& xl, const
 #ifndef CER_FP32W_PF_BIG
 #define CER_FP32W_PF_BIG 1
 #endif
+// workgroups per CU the big (128x128) fp32 tiles are compiled for (the
+// launch bound: 2 = 256 registers per lane; 1 = 512, room for a second
+// prefetch set at half the waves -- an A/B build knob)
+#ifndef CER_BIG_OCC
+#define CER_BIG_OCC 2
+#endif
+template <int BM, int BN>
+constexpr int fp32_occ() {
+  return BM * BN > 128 * 64 ? CER_BIG_OCC : 2;
+}
 template <int BM, int BN, bool WIDE = false>
 constexpr int fp32_sets() {
   return BM * BN > 128 * 64 ? (WIDE ? CER_FP32W_PF_BIG : CER_FP32_PF_BIG)
                             : BM * BN > 64 * 64 ? CER_FP32_PF : CER_FP32_PF_SMALL;
+}
+// the weight-gradient body holds ~45-85 fewer registers than the NT / NN
+// kernels at one set (170 at 128x128): its big tiles may take two
+// (CER_WG_PF_BIG; A/B build knob)
+#ifndef CER_WG_PF_BIG
+#define CER_WG_PF_BIG CER_FP32_PF_BIG
+#endif
+template <int BM, int BN>
+constexpr int wgrad_sets() {
+  return BM * BN > 128 * 64 ? CER_WG_PF_BIG : fp32_sets<BM, BN>();
 }
 using RS0 = std::integral_constant<int, 0>;
 
@@ -2663,7 +2691,7 @@ __device__ __forceinline__ bool group_reduce(f32x4 (&acc)[BM / 32][BN / 32], flo
 // forward (and the unaligned-dgrad fallback through transposed weights):
 // y = act(im2col(x) W^T + b), fp32 in / out.  WIDE: 32x32x16 MFMAs (above).
 template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
-__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1)
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? (fp32_occ<BM, BN>()) : 1)
 void igemm_nt32(NTParams p) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
   constexpr int NST = 2;                                       // LDS stages
@@ -2816,6 +2844,11 @@ void igemm_nt32(NTParams p) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
+      if constexpr (CER_TIMING_NOAW) {
+        keep_alive(ra[s][2 * i]);
+        keep_alive(ra[s][2 * i + 1]);
+        continue;
+      }
       uint4 h, l;
       take_hi_lo(p.a_hl != 0, ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(SA(buf) + nt_off(row, my_chunk)) = h;
@@ -2980,7 +3013,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
 template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
-__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? 2 : 1)
+__global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? (fp32_occ<BM, BN>()) : 1)
 void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
   constexpr int NST = 2;
@@ -3127,6 +3160,11 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + NTHREADS * i) / CPR;
+      if constexpr (CER_TIMING_NOAW) {
+        keep_alive(ra[s][2 * i]);
+        keep_alive(ra[s][2 * i + 1]);
+        continue;
+      }
       uint4 h, l;
       take_hi_lo(p.a_hl != 0, ra[s][2 * i], ra[s][2 * i + 1], h, l);
       *reinterpret_cast<uint4*>(sa + nt_off(row, my_chunk)) = h;
@@ -3203,7 +3241,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
   // (y, x), advanced by KS rows per step without a division
   int ty[B_CH], tx[B_CH];
   int dxs = 0, dys = 0, ry = 0, rx = 0;
-  constexpr int SETS = fp32_sets<BM, BN>();
+  constexpr int SETS = wgrad_sets<BM, BN>();
   uint4 ra[SETS][2 * A_CH], rb[SETS][2 * B_CH];
   const float* dyb = reinterpret_cast<const float*>(p.dy) + (int64_t)cfg * p.N;
   const float* xb = reinterpret_cast<const float*>(p.x.src) + (int64_t)cfg * p.x.cfg_off;
@@ -3404,7 +3442,7 @@ __device__ __forceinline__ void wgrad_reg_body32(const WGParams& p, int work, bf
 }
 
 template <int BM, int BN, int GM, bool WIDE = false>
-__global__ __launch_bounds__(NTHREADS, 2) void igemm_wgrad32(WGParams p) {
+__global__ __launch_bounds__(NTHREADS, (fp32_occ<BM, BN>())) void igemm_wgrad32(WGParams p) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
   wgrad_reg_body32<BM, BN, GM, WIDE>(p, xcd_remap(blockIdx.x, gridDim.x), lds);
 }
@@ -3415,7 +3453,7 @@ template <int BM, int BN, bool WIDE = false>
 // side-stream batch that should leave most CUs to the dgrad chain) walks the
 // items persistently, block-strided; the full grid takes one item per block
 // in XCD-aware order.
-__global__ __launch_bounds__(NTHREADS, 2) void wgrad_batch32(WGBatch b) {
+__global__ __launch_bounds__(NTHREADS, (fp32_occ<BM, BN>())) void wgrad_batch32(WGBatch b) {
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * (BM + BN) * BK];
   const int total = b.start[b.n];
   const int nwg = (int)gridDim.x;

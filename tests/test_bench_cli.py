@@ -22,14 +22,22 @@ def _bench(*args):
     return json.loads(lines[0])
 
 
-def test_bench_two_ranks_cpu():
+def test_bench_two_ranks_cpu(tmp_path):
     out = _bench("--gpus", "2", "--backend", "torch", "--model", "tinycnn", "--steps", "4",
-                 "--warmup", "2", "--steps_per_round", "2", "--train_per_partition", "64")
+                 "--warmup", "2", "--steps_per_round", "2", "--train_per_partition", "64",
+                 "--logs_root", str(tmp_path))
     assert out["n_gpus"] == 2 and out["world_size"] == 2
     assert out["dist_backend"] == "gloo"
     assert out["hop_bytes"] > 0                  # models hopped between the two ranks
     assert out["metric"].startswith("diag_")     # not the headline model: diagnostic name
     assert out["steps"] == 4 and out["value"] > 0
+    # hop telemetry next to the rate: hold time, xGMI bytes (null without amd-smi)
+    assert out["hold_ms_max"] >= 0 and "xgmi_write_gb" in out
+    recs = [json.loads(l) for l in open(tmp_path / "metrics.jsonl")]
+    assert any(r.get("kind") == "hop" for r in recs)
+    assert any(r.get("kind") == "hop_hold" for r in recs)
+    # the 1 Hz sampler ran beside the ranks
+    assert list((tmp_path / "sys_logs").glob("sysmon_*.jsonl"))
 
 
 def test_bench_one_rank_cpu():
