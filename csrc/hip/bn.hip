@@ -622,10 +622,6 @@ __device__ __forceinline__ void fold_any(const float* __restrict__ part, int nsl
 
 constexpr int FOLD_LDS = 2 * BN_T * VEC + 2 * 32 * VEC;   // partial tree + [2][cb], cb <= 256
 
-// The first row chunk of every thread is loaded BEFORE the partial-sum fold
-// (its values do not depend on it): on the small late-stage layers a block
-// has one chunk, and the fold's dependent slab reads then overlap the
-// activation reads instead of preceding them.
 template <typename T>
 __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
     const float* __restrict__ part, int nslab, float* mean_out, float* invstd_out, float* rmean,
@@ -636,28 +632,11 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  const bool live = c0 < C && tr < mp.tr_n;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
-  const int64_t r1 = min(M, r0 + rows_per_slab);
-  constexpr int AU = 2;
-  float v[AU][VEC], rv[AU][VEC];
-  auto load = [&](int64_t r) {
-#pragma unroll
-    for (int u = 0; u < AU; ++u) {
-      const int64_t rr = r + (int64_t)u * mp.tr_n;
-      if (rr < r1) {
-        ld8(x + rr * C + c0, v[u]);
-        if (res) ld8(res + rr * C + c0, rv[u]);
-      }
-    }
-  };
-  int64_t r = r0 + tr;
-  if (live) load(r);
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
-  if (!live) return;
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const float inv_m = 1.f / (float)M;
   float mu[VEC], is[VEC], var[VEC];
 #pragma unroll
@@ -673,15 +652,27 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
       mean_out[c0 + i] = mu[i];
       invstd_out[c0 + i] = is[i];
       float* rm = rmean + g * rstat_stride + cc + i;
-      float* rvp = rvar + g * rstat_stride + cc + i;
+      float* rv = rvar + g * rstat_stride + cc + i;
       const float unb = M > 1 ? var[i] * (float)M / (float)(M - 1) : var[i];
       *rm = (1.f - momentum) * *rm + momentum * mu[i];
-      *rvp = (1.f - momentum) * *rvp + momentum * unb;
+      *rv = (1.f - momentum) * *rv + momentum * unb;
     }
   }
   float sc[VEC], sh[VEC];
   bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
-  while (r < r1) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float v[AU][VEC], rv[AU][VEC];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        ld8(x + rr * C + c0, v[u]);
+        if (res) ld8(res + rr * C + c0, rv[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
@@ -696,8 +687,6 @@ __global__ __launch_bounds__(BN_T) void bn_apply_fwd_fold(
         st8(y + rr * C + c0, o);
       if (mask_out) mask_out[rr * (C / VEC) + (c0 >> 3)] = (uint8_t)act_bits8(o, act);
     }
-    r += AU * mp.tr_n;
-    if (r < r1) load(r);
   }
 }
 
@@ -711,31 +700,11 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
   const bool hl = (act >> 8) & 1;          // HL-format output (cer_bn_set_hl_out)
   act &= 0xff;
   __shared__ float red[FOLD_LDS];
-  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
-  const int c0 = blockIdx.x * mp.cb + tc * VEC;
-  const bool live = c0 < C && tr < mp.tr_n;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
-  const int64_t r1 = min(M, r0 + rows_per_slab);
-  constexpr int AU = 2;
-  float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
-  auto load = [&](int64_t r) {
-#pragma unroll
-    for (int u = 0; u < AU; ++u) {
-      const int64_t rr = r + (int64_t)u * mp.tr_n;
-      if (rr < r1) {
-        ld8(dy + rr * C + c0, d[u]);
-        ld8(x + rr * C + c0, xv[u]);
-        if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
-        if constexpr (YM == YM_M)
-          mask_to_y8(reinterpret_cast<const uint8_t*>(y) + rr * (C / 8), c0, yv[u]);
-      }
-    }
-  };
-  int64_t r = r0 + tr;
-  if (live) load(r);
   float a[VEC], b[VEC];
   fold_any(part, nslab, C, mp, blockIdx.x, red, a, b);
-  if (!live) return;
+  const int tc = threadIdx.x % mp.tc_n, tr = threadIdx.x / mp.tc_n;
+  const int c0 = blockIdx.x * mp.cb + tc * VEC;
+  if (c0 >= C || tr >= mp.tr_n) return;
   const int g = c0 / Cper, cc = c0 - g * Cper;
   if (blockIdx.y == 0 && tr == 0) {
 #pragma unroll
@@ -756,7 +725,22 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
     sdz[i] = a[i] * inv_m;
   }
   if (YM == YM_Z) bn_scale_shift<T>(gamma, beta, g, cc, mu, is, sc, sh);
-  while (r < r1) {
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r1 = min(M, r0 + rows_per_slab);
+  constexpr int AU = 2;
+  for (int64_t r = r0 + tr; r < r1; r += AU * mp.tr_n) {
+    float d[AU][VEC], xv[AU][VEC], yv[AU][VEC];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t rr = r + (int64_t)u * mp.tr_n;
+      if (rr < r1) {
+        ld8(dy + rr * C + c0, d[u]);
+        ld8(x + rr * C + c0, xv[u]);
+        if (YM == YM_Y) ld8(y + rr * C + c0, yv[u]);
+        if constexpr (YM == YM_M)
+          mask_to_y8(reinterpret_cast<const uint8_t*>(y) + rr * (C / 8), c0, yv[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       const int64_t rr = r + (int64_t)u * mp.tr_n;
@@ -774,8 +758,6 @@ __global__ __launch_bounds__(BN_T) void bn_apply_bwd_fold(
         st8(dx + rr * C + c0, o);
       if (dres) st8(dres + rr * C + c0, dz);
     }
-    r += AU * mp.tr_n;
-    if (r < r1) load(r);
   }
 }
 
