@@ -2054,8 +2054,12 @@ __device__ __forceinline__ bool epi_fits(const NTParams& p) {
 // second, double-buffered group spills the 128x128 kernels and costs the
 // 128x64 ones a wave per SIMD).
 // Unaligned channels, the y-form BN link (ym 1) and > 2 GB tensors take
-// epi32_ref.  xch: LDS scratch of 4*BN floats.
-template <int BM, int BN>
+// epi32_ref.  xch: LDS scratch of 4*BN floats.  FULL = false (the
+// uniform-K forward kernels, which never carry an addend or BN-backward
+// operands): bias + activation + forward statistics only, none of the
+// other operands' loads issued (through empty descriptors they still cost
+// instructions and registers in every tile).
+template <int BM, int BN, bool FULL = true>
 __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
                                       int lane, int tid) {
@@ -2072,6 +2076,65 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   }
   const int fr = lane & 15, fc = lane >> 4;
   float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
+  if constexpr (!FULL) {
+    const auto rB = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
+    float bl[FN][4], sl[FN][4], ql[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+        const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
+        bl[j][e] = bload_f32(rB, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
+        sl[j][e] = ql[j][e] = 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * TM + 16 * i + fr;
+      if (m >= p.M) continue;
+      int64_t orow = m;
+      if (p.o_st > 1) {
+        const RowPos r = decode_row(m, p.M, p.a);
+        orow = ((int64_t)r.b * p.o_H + (int64_t)r.y * p.o_st) * p.o_W + (int64_t)r.x * p.o_st;
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * TN + 16 * j + 4 * fc;
+        if (n >= p.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] + bl[j][e];
+          v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
+          sl[j][e] += v[e];
+          ql[j][e] += v[e] * v[e];
+        }
+        *reinterpret_cast<float4*>(obase + orow * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    if (!fstat) return;
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float sm = row16_sum(sl[j][e]);
+        const float sq = row16_sum(ql[j][e]);
+        if (fr == 0) {
+          const int nl = wn * TN + 16 * j + 4 * fc + e;
+          xch[(wm * 2) * BN + nl] = sm;
+          xch[(wm * 2 + 1) * BN + nl] = sq;
+        }
+      }
+    __syncthreads();
+    const int64_t sb = stat_base(m0 / BM, p.stat_slabs, p.ldc, cfg, p.N);
+    for (int t = tid; t < 2 * BN; t += NTHREADS) {
+      const int qd = t / BN, nl = t - qd * BN, n = n0 + nl;
+      if (n < p.N)
+        stat_store(p.stats, sb + (int64_t)qd * p.ldc + n, xch[qd * BN + nl] + xch[(2 + qd) * BN + nl],
+                   p.stat_slabs);
+    }
+    return;
+  }
   const bool ymz = bstat && bb.ym == 2, ymm = bstat && bb.ym == 3;
   const bool ymb = bstat && bb.ym == YM_BIAS;
   const auto rBias = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
@@ -2879,7 +2942,7 @@ void igemm_nt32(NTParams p) {
                                   tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+    epi32<BM, BN, !UK>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
 #undef SA
 #undef SB
@@ -3763,7 +3826,10 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   }
   // register-staged kernels: uniform-K addressing and, with it, the HL
   // weight image (the LDS-DMA ring kernels keep their own addressing)
-  const int gm = kind == 0 ? nt_uk_mode(p, fast) : 0;
+  // (a launch carrying an addend or BN-backward operands -- the unaligned
+  // dgrad fallback -- never reaches them: their epilogue is the lean one)
+  const bool epi_plain = p.addend == nullptr && p.addend_mask == nullptr && p.bb.part == nullptr;
+  const int gm = kind == 0 && epi_plain ? nt_uk_mode(p, fast) : 0;
   if (gm && p.w_hl) {                // the caller allowed the HL image (not grouped)
     p.w = reinterpret_cast<const bf16_t*>(g_whl);
     p.w_gstride = g_whl_gstride;
