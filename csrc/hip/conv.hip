@@ -2030,6 +2030,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
 // such branches between stores, paid ~20 dependent memory round trips per
 // tile, which dominated the small-K (K = 64) dgrad / forward kernels.
 constexpr uint32_t EPI_BIG = 0x7ffffff0u;
+constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2;   // epi32 MODE
 __device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -2054,12 +2055,16 @@ __device__ __forceinline__ bool epi_fits(const NTParams& p) {
 // second, double-buffered group spills the 128x128 kernels and costs the
 // 128x64 ones a wave per SIMD).
 // Unaligned channels, the y-form BN link (ym 1) and > 2 GB tensors take
-// epi32_ref.  xch: LDS scratch of 4*BN floats.  FULL = false (the
-// uniform-K forward kernels, which never carry an addend or BN-backward
-// operands): bias + activation + forward statistics only, none of the
-// other operands' loads issued (through empty descriptors they still cost
-// instructions and registers in every tile).
-template <int BM, int BN, bool FULL = true>
+// epi32_ref.  xch: LDS scratch of 4*BN floats.  MODE (compile time) drops
+// the operands a launch class never has -- through empty descriptors their
+// loads still cost instructions and registers in every tile:
+//   EPI_FULL  everything above (run-time flags);
+//   EPI_FWD   the uniform-K forward kernels: bias + activation + forward
+//             statistics only;
+//   EPI_ZLINK a uniform-K dgrad whose only extra is a BN link with the mask
+//             recomputed from z (ym 2): no bias, addend, addend mask or
+//             stored mask.
+template <int BM, int BN, int MODE = EPI_FULL>
 __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
                                       int lane, int tid) {
@@ -2076,7 +2081,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   }
   const int fr = lane & 15, fc = lane >> 4;
   float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
-  if constexpr (!FULL) {
+  if constexpr (MODE == EPI_FWD) {
     const auto rB = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
     float bl[FN][4], sl[FN][4], ql[FN][4];
 #pragma unroll
@@ -2135,9 +2140,10 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
     }
     return;
   }
-  const bool ymz = bstat && bb.ym == 2, ymm = bstat && bb.ym == 3;
-  const bool ymb = bstat && bb.ym == YM_BIAS;
-  const auto rBias = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
+  constexpr bool ZL = MODE == EPI_ZLINK;       // host-gated: bstat, ym 2, nothing else
+  const bool ymz = ZL || (bstat && bb.ym == 2), ymm = !ZL && bstat && bb.ym == 3;
+  const bool ymb = !ZL && bstat && bb.ym == YM_BIAS;
+  const auto rBias = make_rsrc(p.bias, !ZL && p.bias ? EPI_BIG : 0u);
   const auto rMean = make_rsrc(bb.mean, bstat && !ymb ? EPI_BIG : 0u);
   const auto rInv = make_rsrc(bb.invstd, bstat && !ymb ? EPI_BIG : 0u);
   const auto rGa = make_rsrc(bb.gamma, ymz ? EPI_BIG : 0u);
@@ -2155,7 +2161,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
       const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
       const uint32_t c = (uint32_t)cfg * (uint32_t)p.N + nn;
-      bc[j][e] = bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
+      bc[j][e] = ZL ? 0.f : bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
       mu[j][e] = bload_f32(rMean, c * 4u);
       is[j][e] = bload_f32(rInv, c * 4u);
       ga[j][e] = bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
@@ -2186,10 +2192,15 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         const bool ok = i < FM && rok[i < FM ? i : 0] && n < p.N;
         const int64_t el = orow[i < FM ? i : 0] * p.ldc + (int64_t)cfg * p.N + n;
         const uint32_t off = ok ? (uint32_t)el * 4u : OOB;
-        ad[ii][j] = bload(rAd, off);
         zz[ii][j] = bload(rZ, off);
-        mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
-        amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+        if constexpr (!ZL) {
+          ad[ii][j] = bload(rAd, off);
+          mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+          amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+        } else {
+          ad[ii][j] = make_uint4(0u, 0u, 0u, 0u);
+          mk[ii][j] = amk[ii][j] = 0u;
+        }
       }
     }
   };
@@ -2221,7 +2232,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         for (int e = 0; e < 4; ++e) {
           v[e] = acc[i][j][e] + bc[j][e];
           v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
-          v[e] += !amask || ((amk[ii][j] >> e) & 1u) ? av[e] : 0.f;
+          if constexpr (!ZL) v[e] += !amask || ((amk[ii][j] >> e) & 1u) ? av[e] : 0.f;
         }
         if (ymb) {                   // bias-act link: dz = act'(y) * dx, written
           const float yv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
@@ -2942,7 +2953,7 @@ void igemm_nt32(NTParams p) {
                                   tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-    epi32<BM, BN, !UK>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+    epi32<BM, BN, UK ? EPI_FWD : EPI_FULL>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
 #undef SA
 #undef SB
@@ -3075,7 +3086,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
 
 // dgrad: dx = col2im(dy) * W with W read in place ([k = (tap, cout)] x [cin]
 // rows, TN image), fp32 in / out; Cout % 8 == 0, Cin % 8 == 0
-template <int BM, int BN, int GM, bool WIDE = false, int WG = 1>
+template <int BM, int BN, int GM, bool WIDE = false, int WG = 1, int EPI = EPI_FULL>
 __global__ __launch_bounds__(NTHREADS * WG, WG == 1 ? (fp32_occ<BM, BN>()) : 1)
 void igemm_nn32(NTParams p, int T, FastDiv dCout) {
   static_assert(WG == 1 || !WIDE, "intra-block K split: 16x16x16 kernels only");
@@ -3268,7 +3279,7 @@ void igemm_nn32(NTParams p, int T, FastDiv dCout) {
                                   tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+    epi32<BM, BN, EPI>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
 }
 
@@ -4012,12 +4023,23 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
   dim3 grid((unsigned)(ntiles(p.M, p.N, BM, BN) * G * p.splits));
   const FastDiv dc = make_div((uint32_t)p.a.Cg);
   if (gm) {                        // uniform-K addressing (GM_GEMM / GM_TAP)
+    // a BN link with the mask from z and nothing else (the c2 / c3 dgrads of
+    // a bottleneck) takes the lean epilogue (epi32 EPI_ZLINK)
+    const bool zl = p.bb.part != nullptr && p.bb.ym == 2 && p.addend == nullptr &&
+                    p.addend_mask == nullptr && p.bias == nullptr;
     if constexpr (BM * BN <= 128 * 64) {
       if (wg > 1 && !wide) {
-        if (gm == GM_GEMM)
-          igemm_nn32<BM, BN, GM_GEMM, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
-        else
-          igemm_nn32<BM, BN, GM_TAP, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+        if (gm == GM_GEMM) {
+          if (zl)
+            igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_ZLINK><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+          else
+            igemm_nn32<BM, BN, GM_GEMM, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+        } else {
+          if (zl)
+            igemm_nn32<BM, BN, GM_TAP, false, 2, EPI_ZLINK><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+          else
+            igemm_nn32<BM, BN, GM_TAP, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+        }
         return;
       }
     }
@@ -4027,9 +4049,15 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
       else
         igemm_nn32<BM, BN, GM_TAP, true><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     } else if (gm == GM_GEMM) {
-      igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      if (zl)
+        igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_ZLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else
+        igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     } else {
-      igemm_nn32<BM, BN, GM_TAP><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      if (zl)
+        igemm_nn32<BM, BN, GM_TAP, false, 1, EPI_ZLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else
+        igemm_nn32<BM, BN, GM_TAP><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     }
     return;
   }
