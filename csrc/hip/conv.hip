@@ -2030,7 +2030,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
 // such branches between stores, paid ~20 dependent memory round trips per
 // tile, which dominated the small-K (K = 64) dgrad / forward kernels.
 constexpr uint32_t EPI_BIG = 0x7ffffff0u;
-constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2;   // epi32 MODE
+constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2, EPI_JOIN = 3;   // epi32 MODE
 __device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -2063,7 +2063,10 @@ __device__ __forceinline__ bool epi_fits(const NTParams& p) {
 //             statistics only;
 //   EPI_ZLINK a uniform-K dgrad whose only extra is a BN link with the mask
 //             recomputed from z (ym 2): no bias, addend, addend mask or
-//             stored mask.
+//             stored mask;
+//   EPI_JOIN  a uniform-K dgrad into a residual join: BN link with the
+//             stored activation bits (ym 3), any addend / addend mask, no
+//             bias, no scale / shift.
 template <int BM, int BN, int MODE = EPI_FULL>
 __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
@@ -2141,9 +2144,12 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
     return;
   }
   constexpr bool ZL = MODE == EPI_ZLINK;       // host-gated: bstat, ym 2, nothing else
-  const bool ymz = ZL || (bstat && bb.ym == 2), ymm = !ZL && bstat && bb.ym == 3;
-  const bool ymb = !ZL && bstat && bb.ym == YM_BIAS;
-  const auto rBias = make_rsrc(p.bias, !ZL && p.bias ? EPI_BIG : 0u);
+  constexpr bool JN = MODE == EPI_JOIN;        // host-gated: bstat, ym 3, no bias
+  constexpr bool NOBIAS = ZL || JN;
+  const bool ymz = ZL || (!JN && bstat && bb.ym == 2);
+  const bool ymm = JN || (!ZL && bstat && bb.ym == 3);
+  const bool ymb = !ZL && !JN && bstat && bb.ym == YM_BIAS;
+  const auto rBias = make_rsrc(p.bias, !NOBIAS && p.bias ? EPI_BIG : 0u);
   const auto rMean = make_rsrc(bb.mean, bstat && !ymb ? EPI_BIG : 0u);
   const auto rInv = make_rsrc(bb.invstd, bstat && !ymb ? EPI_BIG : 0u);
   const auto rGa = make_rsrc(bb.gamma, ymz ? EPI_BIG : 0u);
@@ -2161,11 +2167,11 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
       const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
       const uint32_t c = (uint32_t)cfg * (uint32_t)p.N + nn;
-      bc[j][e] = ZL ? 0.f : bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
+      bc[j][e] = NOBIAS ? 0.f : bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
       mu[j][e] = bload_f32(rMean, c * 4u);
       is[j][e] = bload_f32(rInv, c * 4u);
-      ga[j][e] = bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
-      be[j][e] = bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
+      ga[j][e] = JN ? 0.f : bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
+      be[j][e] = JN ? 0.f : bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
     }
   // one row group's operands: [row in group][j]
   uint4 ad[CH][FN], zz[CH][FN];
@@ -4027,11 +4033,15 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
     // a bottleneck) takes the lean epilogue (epi32 EPI_ZLINK)
     const bool zl = p.bb.part != nullptr && p.bb.ym == 2 && p.addend == nullptr &&
                     p.addend_mask == nullptr && p.bias == nullptr;
+    // a residual join's BN link (stored activation bits), any addend
+    const bool jn = p.bb.part != nullptr && p.bb.ym == 3 && p.bias == nullptr;
     if constexpr (BM * BN <= 128 * 64) {
       if (wg > 1 && !wide) {
         if (gm == GM_GEMM) {
           if (zl)
             igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_ZLINK><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+          else if (jn)
+            igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_JOIN><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
           else
             igemm_nn32<BM, BN, GM_GEMM, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
         } else {
@@ -4051,6 +4061,8 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
     } else if (gm == GM_GEMM) {
       if (zl)
         igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_ZLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else if (jn)
+        igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_JOIN><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else
         igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     } else {
