@@ -233,7 +233,16 @@ def warm_p2p(world, rank, device, group=None):
         bufs.append((s, r, peer))
         ops.append(p2p(dist.isend, s, peer, group, tag=900000 + rank))
         ops.append(p2p(dist.irecv, r, peer, group, tag=900000 + peer))
+    # gloo with device tensors (the one-GPU rehearsal) stages them through
+    # the host outside the stream order: the fills must have landed before
+    # it reads them and its copies before the check reads them (RCCL orders
+    # both on its own; the syncs cost nothing at warm-up)
+    cuda = torch.device(device).type == "cuda"
+    if cuda:
+        torch.cuda.synchronize(device)
     _run_group(ops)
+    if cuda:
+        torch.cuda.synchronize(device)
     for s, r, peer in bufs:
         if float(r[0]) != float(peer):
             raise RuntimeError("p2p warm-up: rank {} got {} from {}".format(rank, float(r[0]), peer))
