@@ -2376,7 +2376,7 @@ __device__ __forceinline__ void mma3w_nt(const bf16_t* sa, const bf16_t* sb, int
 template <int BM, int BN>
 __device__ __forceinline__ void mma3w_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
                                               int lane, f32x16 (&acc)[BM / 64][BN / 64],
-                                              bool ahl) {
+                                              bool ahl, bool bhl = false) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 32, FN = TN / 32;
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -2388,7 +2388,7 @@ __device__ __forceinline__ void mma3w_ring_nt(const bf16_t* sa, const bf16_t* sb
       const uint4 x0 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 4 * s + 2 * h));
       const uint4 x1 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 4 * s + 2 * h + 1));
       uint4 hh, ll;
-      split_hi_lo(x0, x1, hh, ll);
+      take_hi_lo(bhl, x0, x1, hh, ll);
       bh[j] = __builtin_bit_cast(bf16x8, hh);
       bl[j] = __builtin_bit_cast(bf16x8, ll);
     }
@@ -2976,7 +2976,8 @@ void igemm_nt32(NTParams p) {
 // costs 2.5x a read per byte on the VGPR -> LDS path.  Requires Cg % 32 == 0.
 template <int BM, int BN>
 __device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb, int wm, int wn,
-                                             int lane, f32x4 (&acc)[BM / 32][BN / 32], bool ahl) {
+                                             int lane, f32x4 (&acc)[BM / 32][BN / 32], bool ahl,
+                                             bool bhl = false) {
   constexpr int TM = BM / 2, TN = BN / 2, FM = TM / 16, FN = TN / 16;
   const int fr = lane & 15, fc = lane >> 4;
   bf16x8 ah[FM], al[FM], bh[FN], bl[FN];
@@ -2986,7 +2987,7 @@ __device__ __forceinline__ void mma3_ring_nt(const bf16_t* sa, const bf16_t* sb,
     const uint4 x0 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 2 * fc));
     const uint4 x1 = *reinterpret_cast<const uint4*>(sb + nt_off(row, 2 * fc + 1));
     uint4 h, l;
-    split_hi_lo(x0, x1, h, l);
+    take_hi_lo(bhl, x0, x1, h, l);
     bh[j] = __builtin_bit_cast(bf16x8, h);
     bl[j] = __builtin_bit_cast(bf16x8, l);
   }
@@ -3075,7 +3076,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
     zero_accw<BM, BN>(acc);
     ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
       mma3w_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc,
-                            p.a_hl != 0);
+                            p.a_hl != 0, p.w_hl != 0);
     });
     if (p.splits > 1 && !splitk_reduce_w<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
     epi32w<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
@@ -3083,10 +3084,11 @@ __global__ __launch_bounds__(NTHREADS, 2) void pipe_nt32(NTParams p) {
     zero_acc<BM, BN>(acc);
     ring_loop<S, LPW>(kr.kt1 - kr.kt0, [&](int t, int st) { issue(kr.kt0 + t, st); }, [&](int st) {
       mma3_ring_nt<BM, BN>(lds + st * STAGE, lds + st * STAGE + BM * BK, wm, wn, lane, acc,
-                           p.a_hl != 0);
+                           p.a_hl != 0, p.w_hl != 0);
     });
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-    epi32<BM, BN>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+    // host-gated (run_nt32): ring launches are plain forwards
+    epi32<BM, BN, EPI_FWD>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
 }
 
@@ -3834,6 +3836,11 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     if (((v / 3) & 1) && !ring_ok) v -= 3;
   }
   if (!fast) v = fp32_variant(v);
+  // a launch carrying an addend or BN-backward operands (the unaligned dgrad
+  // fallback) never reaches the uniform-K or ring kernels, whose epilogue is
+  // the lean forward one (epi32 EPI_FWD)
+  const bool epi_plain = p.addend == nullptr && p.addend_mask == nullptr && p.bb.part == nullptr;
+  if (((v / 3) & 1) && !epi_plain) v -= 3;
   const int kind = (v / 3) & 1;
   set_splits(p, G, v, KS);
   if (nslab) {
@@ -3841,13 +3848,10 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
     tile_dims(v, bm, bn);
     *nslab = stat_nslab((int)((p.M + bm - 1) / bm), p.stat_slabs);
   }
-  // register-staged kernels: uniform-K addressing and, with it, the HL
-  // weight image (the LDS-DMA ring kernels keep their own addressing)
-  // (a launch carrying an addend or BN-backward operands -- the unaligned
-  // dgrad fallback -- never reaches them: their epilogue is the lean one)
-  const bool epi_plain = p.addend == nullptr && p.addend_mask == nullptr && p.bb.part == nullptr;
+  // register-staged kernels: uniform-K addressing; with it, and in the
+  // LDS-DMA ring kernels (their own addressing), the HL weight image
   const int gm = kind == 0 && epi_plain ? nt_uk_mode(p, fast) : 0;
-  if (gm && p.w_hl) {                // the caller allowed the HL image (not grouped)
+  if ((gm || kind == 1) && p.w_hl) {   // the caller allowed the HL image (not grouped)
     p.w = reinterpret_cast<const bf16_t*>(g_whl);
     p.w_gstride = g_whl_gstride;
   } else {

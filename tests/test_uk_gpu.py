@@ -82,7 +82,7 @@ def _run(case, whl, uk, v=None):
     return a, ref, x, y.detach(), gy, x.grad.detach(), a.grad.clone()
 
 
-@pytest.mark.parametrize("v", [0, 1, 2, 12, 13, 14, 24, 26])
+@pytest.mark.parametrize("v", [0, 1, 2, 3, 5, 12, 13, 14, 15, 17, 24, 26])
 @pytest.mark.parametrize("case", CASES)
 def test_uk_bitwise_equals_im2col(case, v):
     """Pinned variant (no split-K): y and dx of the uniform-K kernels, with
