@@ -2085,17 +2085,25 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   const int fr = lane & 15, fc = lane >> 4;
   float* obase = reinterpret_cast<float*>(p.out) + (int64_t)cfg * p.N;
   if constexpr (MODE == EPI_FWD) {
-    const auto rB = make_rsrc(p.bias, p.bias ? EPI_BIG : 0u);
+    // the bias loads only when there is a bias (a uniform branch: nothing
+    // else is in flight here, so its vmcnt drain costs nothing, while 16
+    // loads through an empty descriptor would still be issued and waited on)
     float bl[FN][4], sl[FN][4], ql[FN][4];
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
-        const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
-        bl[j][e] = bload_f32(rB, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
-        sl[j][e] = ql[j][e] = 0.f;
-      }
+      for (int e = 0; e < 4; ++e) bl[j][e] = sl[j][e] = ql[j][e] = 0.f;
+    if (p.bias) {
+      const auto rB = make_rsrc(p.bias, EPI_BIG);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = n0 + wn * TN + 16 * j + 4 * fc + e;
+          const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
+          bl[j][e] = bload_f32(rB, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = m0 + wm * TM + 16 * i + fr;
