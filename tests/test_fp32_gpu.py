@@ -235,19 +235,20 @@ def test_conv_bn_unit_ksplit_fp32_vs_fp64(v):
         _hip.conv_set_variant(1, -1)
 
 
-@pytest.mark.parametrize("narrow", [True, False])
+@pytest.mark.parametrize("narrow", [1, 0, 2])
 @pytest.mark.parametrize("vb", [1, 12, 13, 14])
 def test_wgrad_batch_wide_fp32_vs_fp64(vb, narrow):
     """Batched (deferred) fp32 weight gradients on the register 128x128 and
     the wide kernels (cer_wgrad_batch_flush with ids 1, 12-14) over three
     layers at once; ``narrow``: the 64-output-channel layer goes to its own
-    64x64-tile launch (CER_WGB_NARROW, the default) or stays in the batch."""
+    64x128-tile launch (CER_WGB_NARROW=2, the default), to a 64x64-tile one
+    (1) or stays in the batch (0)."""
     from cerebro_ds_kpgi_amd.ops import _hip, streams
     # N = 64 (its own 64x64 launch), a K = 64 1x1 layer and two wide layers
     cases = [CONV_CASES[0], CONV_CASES[1], CONV_CASES[5], (8, 14, 14, 64, 256, 1, 1, 0, 4)]
     keep = streams._BATCH_VARIANT
     streams.set_batch_variant(vb)
-    _hip.lib().cer_wgrad_batch_set_narrow(1 if narrow else 0)
+    _hip.lib().cer_wgrad_batch_set_narrow(narrow)
     try:
         errs = []
         made = []
@@ -273,7 +274,7 @@ def test_wgrad_batch_wide_fp32_vs_fp64(vb, narrow):
             errs.append(_rel(a.grad.view(G, -1)[:, :dw64[0].numel()], dw64.reshape(G, -1)))
     finally:
         streams.set_batch_variant(keep)
-        _hip.lib().cer_wgrad_batch_set_narrow(1)
+        _hip.lib().cer_wgrad_batch_set_narrow(2)
     print("wgrad batch wide", vb, narrow, ["%.1e" % e for e in errs])
     assert max(errs) < TOL, errs
 
