@@ -2030,7 +2030,7 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
 // such branches between stores, paid ~20 dependent memory round trips per
 // tile, which dominated the small-K (K = 64) dgrad / forward kernels.
 constexpr uint32_t EPI_BIG = 0x7ffffff0u;
-constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2, EPI_JOIN = 3;   // epi32 MODE
+constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2, EPI_JOIN = 3, EPI_ADD = 4;   // epi32 MODE
 __device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -2066,7 +2066,9 @@ __device__ __forceinline__ bool epi_fits(const NTParams& p) {
 //             stored mask;
 //   EPI_JOIN  a uniform-K dgrad into a residual join: BN link with the
 //             stored activation bits (ym 3), any addend / addend mask, no
-//             bias, no scale / shift.
+//             bias, no scale / shift;
+//   EPI_ADD   a uniform-K dgrad with no BN link (its input is not a BN
+//             output, e.g. the max pool's): any addend / addend mask only.
 template <int BM, int BN, int MODE = EPI_FULL>
 __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
@@ -2076,7 +2078,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   constexpr int NG = (FM + CH - 1) / CH;
   const BNBwdEpi& bb = p.bb;
   const bool fstat = p.stats != nullptr;
-  const bool bstat = bb.part != nullptr;
+  const bool bstat = MODE != EPI_ADD && bb.part != nullptr;   // EPI_ADD: host-gated none
   const bool vec = ((p.N | p.ldc) & 3) == 0;
   if (!vec || (bstat && bb.ym == 1) || !epi_fits(p)) {
     epi32_ref<BM, BN>(p, acc, xch, cfg, m0, n0, wm, wn, lane, tid);
@@ -2153,7 +2155,8 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   }
   constexpr bool ZL = MODE == EPI_ZLINK;       // host-gated: bstat, ym 2, nothing else
   constexpr bool JN = MODE == EPI_JOIN;        // host-gated: bstat, ym 3, no bias
-  constexpr bool NOBIAS = ZL || JN;
+  constexpr bool AD = MODE == EPI_ADD;        // host-gated: no BN link, no bias
+  constexpr bool NOBIAS = ZL || JN || AD;
   const bool ymz = ZL || (!JN && bstat && bb.ym == 2);
   const bool ymm = JN || (!ZL && bstat && bb.ym == 3);
   const bool ymb = !ZL && !JN && bstat && bb.ym == YM_BIAS;
@@ -2176,10 +2179,10 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
       const uint32_t c = (uint32_t)cfg * (uint32_t)p.N + nn;
       bc[j][e] = NOBIAS ? 0.f : bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
-      mu[j][e] = bload_f32(rMean, c * 4u);
-      is[j][e] = bload_f32(rInv, c * 4u);
-      ga[j][e] = JN ? 0.f : bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
-      be[j][e] = JN ? 0.f : bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
+      mu[j][e] = AD ? 0.f : bload_f32(rMean, c * 4u);
+      is[j][e] = AD ? 0.f : bload_f32(rInv, c * 4u);
+      ga[j][e] = JN || AD ? 0.f : bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
+      be[j][e] = JN || AD ? 0.f : bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
     }
   // one row group's operands: [row in group][j]
   uint4 ad[CH][FN], zz[CH][FN];
@@ -2206,8 +2209,12 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         const bool ok = i < FM && rok[i < FM ? i : 0] && n < p.N;
         const int64_t el = orow[i < FM ? i : 0] * p.ldc + (int64_t)cfg * p.N + n;
         const uint32_t off = ok ? (uint32_t)el * 4u : OOB;
-        zz[ii][j] = bload(rZ, off);
-        if constexpr (!ZL) {
+        zz[ii][j] = AD ? make_uint4(0u, 0u, 0u, 0u) : bload(rZ, off);
+        if constexpr (AD) {
+          ad[ii][j] = bload(rAd, off);
+          amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
+          mk[ii][j] = 0u;
+        } else if constexpr (!ZL) {
           ad[ii][j] = bload(rAd, off);
           mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
           amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
@@ -4047,6 +4054,8 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
                     p.addend_mask == nullptr && p.bias == nullptr;
     // a residual join's BN link (stored activation bits), any addend
     const bool jn = p.bb.part != nullptr && p.bb.ym == 3 && p.bias == nullptr;
+    // no BN link at all (the input is not a BN output), addend only
+    const bool ad = p.bb.part == nullptr && p.bias == nullptr && p.stats == nullptr;
     if constexpr (BM * BN <= 128 * 64) {
       if (wg > 1 && !wide) {
         if (gm == GM_GEMM) {
@@ -4054,6 +4063,8 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
             igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_ZLINK><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
           else if (jn)
             igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_JOIN><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
+          else if (ad)
+            igemm_nn32<BM, BN, GM_GEMM, false, 2, EPI_ADD><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
           else
             igemm_nn32<BM, BN, GM_GEMM, false, 2><<<grid, 2 * NTHREADS, 0, stream>>>(p, T, dc);
         } else {
@@ -4075,6 +4086,8 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
         igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_ZLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else if (jn)
         igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_JOIN><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else if (ad)
+        igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_ADD><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else
         igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     } else {
