@@ -2030,7 +2030,8 @@ __device__ __forceinline__ void epi32_ref(const NTParams& p, const f32x4 (&acc)[
 // such branches between stores, paid ~20 dependent memory round trips per
 // tile, which dominated the small-K (K = 64) dgrad / forward kernels.
 constexpr uint32_t EPI_BIG = 0x7ffffff0u;
-constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2, EPI_JOIN = 3, EPI_ADD = 4;   // epi32 MODE
+constexpr int EPI_FULL = 0, EPI_FWD = 1, EPI_ZLINK = 2, EPI_JOIN = 3, EPI_ADD = 4,
+              EPI_BLINK = 5;   // epi32 MODE
 __device__ __forceinline__ float bload_f32(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
 }
@@ -2068,7 +2069,9 @@ __device__ __forceinline__ bool epi_fits(const NTParams& p) {
 //             stored activation bits (ym 3), any addend / addend mask, no
 //             bias, no scale / shift;
 //   EPI_ADD   a uniform-K dgrad with no BN link (its input is not a BN
-//             output, e.g. the max pool's): any addend / addend mask only.
+//             output, e.g. the max pool's): any addend / addend mask only;
+//   EPI_BLINK a uniform-K dgrad with the bias-act link (ym YM_BIAS, VGG's
+//             conv -> conv) and nothing else.
 template <int BM, int BN, int MODE = EPI_FULL>
 __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM / 32][BN / 32],
                                       float* xch, int cfg, int m0, int n0, int wm, int wn,
@@ -2156,10 +2159,11 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
   constexpr bool ZL = MODE == EPI_ZLINK;       // host-gated: bstat, ym 2, nothing else
   constexpr bool JN = MODE == EPI_JOIN;        // host-gated: bstat, ym 3, no bias
   constexpr bool AD = MODE == EPI_ADD;        // host-gated: no BN link, no bias
-  constexpr bool NOBIAS = ZL || JN || AD;
-  const bool ymz = ZL || (!JN && bstat && bb.ym == 2);
-  const bool ymm = JN || (!ZL && bstat && bb.ym == 3);
-  const bool ymb = !ZL && !JN && bstat && bb.ym == YM_BIAS;
+  constexpr bool BL = MODE == EPI_BLINK;      // host-gated: bias link, nothing else
+  constexpr bool NOBIAS = ZL || JN || AD || BL;
+  const bool ymz = ZL || (!JN && !BL && bstat && bb.ym == 2);
+  const bool ymm = JN || (!ZL && !BL && bstat && bb.ym == 3);
+  const bool ymb = BL || (!ZL && !JN && bstat && bb.ym == YM_BIAS);
   const auto rBias = make_rsrc(p.bias, !NOBIAS && p.bias ? EPI_BIG : 0u);
   const auto rMean = make_rsrc(bb.mean, bstat && !ymb ? EPI_BIG : 0u);
   const auto rInv = make_rsrc(bb.invstd, bstat && !ymb ? EPI_BIG : 0u);
@@ -2179,10 +2183,10 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
       const uint32_t nn = (uint32_t)(n < p.N ? n : p.N - 1);
       const uint32_t c = (uint32_t)cfg * (uint32_t)p.N + nn;
       bc[j][e] = NOBIAS ? 0.f : bload_f32(rBias, ((uint32_t)cfg * (uint32_t)p.bias_gstride + nn) * 4u);
-      mu[j][e] = AD ? 0.f : bload_f32(rMean, c * 4u);
-      is[j][e] = AD ? 0.f : bload_f32(rInv, c * 4u);
-      ga[j][e] = JN || AD ? 0.f : bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
-      be[j][e] = JN || AD ? 0.f : bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
+      mu[j][e] = AD || BL ? 0.f : bload_f32(rMean, c * 4u);
+      is[j][e] = AD || BL ? 0.f : bload_f32(rInv, c * 4u);
+      ga[j][e] = JN || AD || BL ? 0.f : bload_f32(rGa, ((uint32_t)cfg * (uint32_t)bb.gstride + nn) * 4u);
+      be[j][e] = JN || AD || BL ? 0.f : bload_f32(rBe, ((uint32_t)cfg * (uint32_t)bb.bstride + nn) * 4u);
     }
   // one row group's operands: [row in group][j]
   uint4 ad[CH][FN], zz[CH][FN];
@@ -2214,6 +2218,9 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
           ad[ii][j] = bload(rAd, off);
           amk[ii][j] = bload_u8(rAm, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
           mk[ii][j] = 0u;
+        } else if constexpr (BL) {
+          ad[ii][j] = make_uint4(0u, 0u, 0u, 0u);
+          mk[ii][j] = amk[ii][j] = 0u;
         } else if constexpr (!ZL) {
           ad[ii][j] = bload(rAd, off);
           mk[ii][j] = bload_u8(rMk, ok ? (uint32_t)(el >> 3) : OOB) >> (uint32_t)(el & 7);
@@ -2253,7 +2260,7 @@ __device__ __forceinline__ void epi32(const NTParams& p, const f32x4 (&acc)[BM /
         for (int e = 0; e < 4; ++e) {
           v[e] = acc[i][j][e] + bc[j][e];
           v[e] = p.act == 6 ? fminf(fmaxf(v[e], 0.f), 6.f) : (p.act ? fmaxf(v[e], 0.f) : v[e]);
-          if constexpr (!ZL) v[e] += !amask || ((amk[ii][j] >> e) & 1u) ? av[e] : 0.f;
+          if constexpr (!ZL && !BL) v[e] += !amask || ((amk[ii][j] >> e) & 1u) ? av[e] : 0.f;
         }
         if (ymb) {                   // bias-act link: dz = act'(y) * dx, written
           const float yv[4] = {__uint_as_float(zz[ii][j].x), __uint_as_float(zz[ii][j].y),
@@ -4056,6 +4063,9 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
     const bool jn = p.bb.part != nullptr && p.bb.ym == 3 && p.bias == nullptr;
     // no BN link at all (the input is not a BN output), addend only
     const bool ad = p.bb.part == nullptr && p.bias == nullptr && p.stats == nullptr;
+    // the bias-act link (VGG's conv -> conv) and nothing else
+    const bool bl = p.bb.part != nullptr && p.bb.ym == YM_BIAS && p.addend == nullptr &&
+                    p.addend_mask == nullptr && p.bias == nullptr;
     if constexpr (BM * BN <= 128 * 64) {
       if (wg > 1 && !wide) {
         if (gm == GM_GEMM) {
@@ -4088,11 +4098,15 @@ static void launch_nn32_t(const NTParams& p, int G, int T, bool strided, hipStre
         igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_JOIN><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else if (ad)
         igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_ADD><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else if (bl)
+        igemm_nn32<BM, BN, GM_GEMM, false, 1, EPI_BLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else
         igemm_nn32<BM, BN, GM_GEMM><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     } else {
       if (zl)
         igemm_nn32<BM, BN, GM_TAP, false, 1, EPI_ZLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
+      else if (bl)
+        igemm_nn32<BM, BN, GM_TAP, false, 1, EPI_BLINK><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
       else
         igemm_nn32<BM, BN, GM_TAP><<<grid, NTHREADS, 0, stream>>>(p, T, dc);
     }
