@@ -2981,7 +2981,7 @@ void igemm_nt32(NTParams p) {
                                   tid))
       return;
     if (p.splits > 1 && !splitk_reduce<BM, BN>(p, acc, cfg * tiles + tile, split, tid)) return;
-    epi32<BM, BN, UK ? EPI_FWD : EPI_FULL>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
+    epi32<BM, BN, (UK || GM == GM_FWD) ? EPI_FWD : EPI_FULL>(p, acc, reinterpret_cast<float*>(lds), cfg, m0, n0, wm, wn, lane, tid);
   }
 #undef SA
 #undef SB
@@ -3873,6 +3873,10 @@ static int run_nt32(NTParams p, int G, hipStream_t stream, int* nslab = nullptr)
   // register-staged kernels: uniform-K addressing; with it, and in the
   // LDS-DMA ring kernels (their own addressing), the HL weight image
   const int gm = kind == 0 && epi_plain ? nt_uk_mode(p, fast) : 0;
+  // the aligned gather (GM_FWD) kernels carry the lean forward epilogue too:
+  // an addend / BN-backward launch only ever comes through the unaligned
+  // dgrad fallback (p.dgrad = 1, GM_SLOW); refuse anything else loudly
+  if (fast && !epi_plain) return (int)hipErrorInvalidValue;
   if ((gm || kind == 1) && p.w_hl) {   // the caller allowed the HL image (not grouped)
     p.w = reinterpret_cast<const bf16_t*>(g_whl);
     p.w_gstride = g_whl_gstride;
